@@ -1,0 +1,154 @@
+/*
+ * dsplat_hip.h — C ABI of libdsplat_hip.so, the MI355X (gfx950) hot path of
+ * yuehuarulian/my_depthsplat: the differentiable 3D-Gaussian tile rasterizer behind
+ * src/model/decoder/cuda_splatting.py and the plane-sweep cost volume behind
+ * src/model/encoder/unimatch/matching.py + mv_unimatch.py.
+ *
+ * Conventions (every entry point):
+ *   - all array arguments are DEVICE pointers (HBM), fp32 unless typed otherwise,
+ *     C-contiguous in the layout written next to them;
+ *   - the library never allocates or frees: the caller owns every buffer
+ *     (the Python layer allocates from the PyTorch-ROCm caching allocator);
+ *   - all work is enqueued on `stream` (hipStream_t passed as void*); no host sync,
+ *     no hipMalloc, so every call is hipGraph-capturable;
+ *   - return 0 on success, non-zero on a bad argument or HIP error; the message is
+ *     in dsplat_last_error() (thread-local). No exception crosses the ABI.
+ *
+ * Reference interfaces replaced (file:line in yuehuarulian/my_depthsplat):
+ *   rasterizer  : diff_gaussian_rasterization.GaussianRasterizer.forward/backward,
+ *                 called at src/model/decoder/cuda_splatting.py:112-123 (one call per
+ *                 view there; here one call sequence renders a whole batch of views)
+ *   cost volume : warp_with_pose_depth_candidates  src/model/encoder/unimatch/matching.py:24-90
+ *                 fused with the correlation at   src/model/encoder/unimatch/mv_unimatch.py:494-505
+ */
+#ifndef DSPLAT_HIP_H
+#define DSPLAT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSR_TILE 16          /* 16x16 pixel screen tiles (upstream BLOCK_X/BLOCK_Y) */
+#define DSR_GEOM_STRIDE 12   /* floats per (view, gaussian) geometry record        */
+
+/* One camera/view. Mirrors GaussianRasterizationSettings (cuda_splatting.py:98-111):
+ * viewmatrix/projmatrix are the row-major storage of the TRANSPOSED torch matrices
+ * (i.e. column-major world->camera and world->clip), campos = c2w[:3, 3]. `scene`
+ * selects which Gaussian set [S] this view renders, replacing the per-view
+ * `repeat(...)` of decoder_splatting_cuda.py:53-56; viewmatrix/projmatrix/campos are
+ * those of the RESCALED camera when scale != 1. 176 bytes, device-resident. */
+typedef struct dsr_camera {
+    float viewmatrix[16];
+    float projmatrix[16];
+    float campos[3];
+    float tanfovx;
+    float tanfovy;
+    float bg[3];
+    int32_t scene;
+    float scale;            /* scale-invariant rescale 1/near (cuda_splatting.py:63-70): the
+                               kernel uses means*scale and cov*(scale*scale); 1 = off */
+    int32_t _pad[2];
+} dsr_camera;
+
+/* Geometry record per (view, gaussian), DSR_GEOM_STRIDE floats:
+ *   [0..1] pixel-space mean xy   [2..4] conic (a, b, c)   [5] opacity
+ *   [6..8] rgb                   [9] view-space depth     [10] radius (int32 bits)
+ *   [11] SH clamp mask (uint32 bits 0..2). radius == 0 <=> culled / not rendered. */
+
+/* ---- rasterizer forward ------------------------------------------------------------
+ * Replaces preprocessCUDA + tiles_touched (upstream K1). Per view v and gaussian g of
+ * scene cams[v].scene: cull, EWA projection, conic, radius, SH->RGB (or colors), and
+ * the per-(view, tile) entry count seg_count[v*T + t] (T = tiles per view).
+ *   means [S,G,3]  shs [S,G,M,3] (M = (sh_degree+1)^2) xor colors [S,G,3]
+ *   opacities [S,G]  cov6 [S,G,6] (xx,xy,xz,yy,yz,zz = cuda_splatting.py:114,122)
+ *   out: geom [V,G,12], radii [V,G] int32, seg_count [V*T] (zeroed by this call).  */
+int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
+                       const float* means, const float* shs, const float* colors,
+                       const float* opacities, const float* cov6, const dsr_camera* cams,
+                       float* geom, int32_t* radii, uint32_t* seg_count, void* stream);
+
+/* Exclusive scan of seg_count[V*T] -> seg_start[V*T+1], seg_cursor[V*T] (= seg_start),
+ * totals[0] = N (num_rendered over all views), totals[1] = max entries in one tile. */
+int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_start,
+                 uint32_t* seg_cursor, uint32_t* totals, void* stream);
+
+/* Emit one 64-bit key per (gaussian, touched tile): key = float_bits(depth) << 32 | id,
+ * grouped by segment (v, t) at seg_start; order inside a segment is arbitrary here and
+ * fixed by dsr_bin_sort. keys must hold N entries. Replaces duplicateWithKeys (K3). */
+int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor,
+                    uint64_t* keys, void* stream);
+
+/* Sort every segment by (depth, id) ascending — identical to upstream's stable radix
+ * sort of (tile << 32 | depth) with emission-order ties (K4/K5). Segments up to
+ * dsr_sort_lds_capacity() entries sort in LDS; larger ones use `scratch` (N entries,
+ * may be NULL when max_count <= capacity). id_bits = bits needed for G-1. */
+int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, uint64_t* keys,
+                 uint64_t* scratch, uint32_t max_count, void* stream);
+uint32_t dsr_sort_lds_capacity(void);
+
+/* Front-to-back compositing per 16x16 tile (K6). out_color [V,3,H,W], final_T [V,H,W],
+ * n_contrib [V,H,W] (uint32). Background from cams[v].bg. */
+int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
+                   const uint32_t* seg_start, const uint64_t* keys, float* out_color,
+                   float* final_T, uint32_t* n_contrib, void* stream);
+
+/* ---- rasterizer backward -----------------------------------------------------------
+ * Back-to-front per tile (K7). dL_dpix [V,3,H,W]. Accumulates into dgeom [V,G,12]
+ * (caller zeroes): [0..1] dL/dxy (ndc scale, as upstream dL_dmean2D), [2..4] dL/dconic,
+ * [5] dL/dopacity, [6..8] dL/drgb. */
+int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
+                   const uint32_t* seg_start, const uint64_t* keys, const float* final_T,
+                   const uint32_t* n_contrib, const float* dL_dpix, float* dgeom, void* stream);
+
+/* Preprocess backward (K8 + K9), reduced over all views of each scene without atomics.
+ * scene_view_start [S+1], scene_views [V] list the views of each scene.
+ * out (overwritten): dmeans [S,G,3], dshs [S,G,M,3] or NULL, dcolors [S,G,3] or NULL,
+ * dopac [S,G], dcov6 [S,G,6]; dmean2D [V,G,3] optional (NULL to skip). */
+int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
+                       const float* means, const float* shs, const float* cov6,
+                       const dsr_camera* cams, const float* geom, const float* dgeom,
+                       const int32_t* scene_view_start, const int32_t* scene_views,
+                       float* dmeans, float* dshs, float* dcolors, float* dopac, float* dcov6,
+                       float* dmean2D, void* stream);
+
+/* ---- plane-sweep cost volume -------------------------------------------------------
+ * Fused warp_with_pose_depth_candidates (matching.py:24-90) + correlation
+ * (mv_unimatch.py:494-505):
+ *   cost[b,d,y,x] = mean_j ( sum_c ref[b,c,y,x] * warp_j[b,c,d,y,x] ) / sqrt(C)
+ * where warp_j bilinearly samples tgt[b,j] (zeros padding, align_corners=True) at the
+ * projection of pixel (x,y) at depth[b,d,y,x] through K[b,j] and pose[b,j].
+ *   ref [B,C,H,W]  tgt [B,J,C,H,W]  intr [B,J,3,3] (pixel units)  pose [B,J,4,4]
+ *   depth [B,D,H,W] when depth_per_pixel else [B,D]   ->   cost [B,D,H,W]
+ * tgt_hwc: workspace [B,J,H,W,C] (filled here: channel-last copy of tgt).          */
+int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel,
+                        const float* ref, const float* tgt, const float* intr, const float* pose,
+                        const float* depth, float clamp_min_depth, float* tgt_hwc, float* cost,
+                        void* stream);
+
+/* Backward of dcv_cost_volume_fwd w.r.t. both feature maps (geometry gets no grad,
+ * matching.py:46). dcost [B,D,H,W] -> dref [B,C,H,W] (overwritten), dtgt [B,J,C,H,W]
+ * (overwritten). Needs the tgt_hwc workspace from the forward and dtgt_hwc [B,J,H,W,C]
+ * scratch (zeroed here). */
+int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel,
+                        const float* ref, const float* tgt_hwc, const float* intr,
+                        const float* pose, const float* depth, float clamp_min_depth,
+                        const float* dcost, float* dref, float* dtgt, float* dtgt_hwc,
+                        void* stream);
+
+/* Materialising warp with the exact matching.py:24-90 signature semantics:
+ * feature [B,C,H,W], intr [B,3,3], pose [B,4,4], depth [B,D,H,W] -> out [B,C,D,H,W]. */
+int dcv_warp_fwd(int B, int C, int H, int W, int D, const float* feature, const float* intr,
+                 const float* pose, const float* depth, float clamp_min_depth, float* out,
+                 void* stream);
+
+/* ---- misc ------------------------------------------------------------------------- */
+const char* dsplat_last_error(void);
+int dsplat_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSPLAT_HIP_H */

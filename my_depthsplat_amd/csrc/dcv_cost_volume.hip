@@ -1,0 +1,338 @@
+// dcv_cost_volume.hip — fused plane-sweep warp + correlation for gfx950 (wave64).
+//
+// Replaces, in one pass and without materialising the [B, C, D, H, W] warped tensor,
+//   warp_with_pose_depth_candidates   src/model/encoder/unimatch/matching.py:24-90
+//   cost = mean_j(sum_c ref * warped_j) / sqrt(C)   src/model/encoder/unimatch/mv_unimatch.py:494-505
+//
+// Layout: target features are first copied channel-last ([B,J,H,W,C]) so every bilinear
+// tap is one contiguous C-float row; a wave owns one reference pixel with its 64 lanes
+// over channels (coalesced 256-B tap reads), accumulates the per-depth partial dot
+// products of 64 depth hypotheses in registers and finishes them with a transpose
+// reduction (63 shuffles for 64 outputs) instead of 64 full wave reductions.
+// Geometry per (pixel, depth, view) is wave-uniform and follows the reference's
+// operation order: p_rot = R K^-1 [x, y, 1]; X = p_rot * depth + t; x = K X;
+// uv = x.xy / max(x.z, clamp); grid = 2 uv / (size - 1) - 1; grid_sample unnormalise
+// ((g + 1) / 2) * (size - 1), bilinear, zeros padding (align_corners=True).
+
+#include "dsplat_common.h"
+
+namespace {
+
+constexpr int DG = 16;  // depth hypotheses per register group
+
+struct Cam {
+  float Kinv[9], R[9], t[3], K[9];
+};
+
+__device__ __forceinline__ void load_cam(const float* intr, const float* pose, Cam& c) {
+  // intr: 3x3 row-major K; pose: 4x4 row-major [R | t].
+  const float* k = intr;
+  for (int i = 0; i < 9; ++i) c.K[i] = k[i];
+  // explicit 3x3 inverse (adjugate / det), row-major
+  const float a = k[0], b = k[1], cc = k[2], d = k[3], e = k[4], f = k[5], g = k[6], h = k[7], i = k[8];
+  const float A = e * i - f * h, Bc = -(d * i - f * g), C = d * h - e * g;
+  const float det = a * A + b * Bc + cc * C;
+  const float id = 1.0f / det;
+  c.Kinv[0] = A * id;
+  c.Kinv[1] = -(b * i - cc * h) * id;
+  c.Kinv[2] = (b * f - cc * e) * id;
+  c.Kinv[3] = Bc * id;
+  c.Kinv[4] = (a * i - cc * g) * id;
+  c.Kinv[5] = -(a * f - cc * d) * id;
+  c.Kinv[6] = C * id;
+  c.Kinv[7] = -(a * h - b * g) * id;
+  c.Kinv[8] = (a * e - b * d) * id;
+  for (int r = 0; r < 3; ++r) {
+    for (int q = 0; q < 3; ++q) c.R[r * 3 + q] = pose[r * 4 + q];
+    c.t[r] = pose[r * 4 + 3];
+  }
+}
+
+struct Taps {
+  int idx[4];   // flattened y*W + x of nw, ne, sw, se (or -1 when outside)
+  float w[4];
+};
+
+__device__ __forceinline__ void taps_at(const Cam& c, float prx, float pry, float prz, float depth,
+                                        float clampz, int H, int W, Taps& tp) {
+  const float X = prx * depth + c.t[0];
+  const float Y = pry * depth + c.t[1];
+  const float Z = prz * depth + c.t[2];
+  const float x = c.K[0] * X + c.K[1] * Y + c.K[2] * Z;
+  const float y = c.K[3] * X + c.K[4] * Y + c.K[5] * Z;
+  const float z = fmaxf(c.K[6] * X + c.K[7] * Y + c.K[8] * Z, clampz);
+  const float u = x / z, v = y / z;
+  const float gxn = 2 * u / (W - 1) - 1;
+  const float gyn = 2 * v / (H - 1) - 1;
+  const float ix = ((gxn + 1) / 2) * (W - 1);
+  const float iy = ((gyn + 1) / 2) * (H - 1);
+  if (!(ix > -2.f && ix < (float)W + 1.f && iy > -2.f && iy < (float)H + 1.f)) {  // also NaN
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      tp.idx[k] = -1;
+      tp.w[k] = 0.f;
+    }
+    return;
+  }
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const int x0 = (int)fx0, y0 = (int)fy0, x1 = x0 + 1, y1 = y0 + 1;
+  // weights in grid_sample's form: nw = (x1 - ix)(y1 - iy) etc.
+  const float wx0 = (float)x1 - ix, wx1 = ix - fx0, wy0 = (float)y1 - iy, wy1 = iy - fy0;
+  const bool vx0 = x0 >= 0 && x0 < W, vx1 = x1 >= 0 && x1 < W;
+  const bool vy0 = y0 >= 0 && y0 < H, vy1 = y1 >= 0 && y1 < H;
+  // out-of-range sample positions (e.g. inf/nan) fall outside every tap
+  tp.idx[0] = (vx0 && vy0) ? y0 * W + x0 : -1;
+  tp.idx[1] = (vx1 && vy0) ? y0 * W + x1 : -1;
+  tp.idx[2] = (vx0 && vy1) ? y1 * W + x0 : -1;
+  tp.idx[3] = (vx1 && vy1) ? y1 * W + x1 : -1;
+  tp.w[0] = wx0 * wy0;
+  tp.w[1] = wx1 * wy0;
+  tp.w[2] = wx0 * wy1;
+  tp.w[3] = wx1 * wy1;
+}
+
+// [B,J,C,H,W] -> [B,J,H,W,C] through a 64x64 LDS tile.
+__global__ __launch_bounds__(256) void k_to_hwc(int C, int HW, const float* __restrict__ src,
+                                                float* __restrict__ dst) {
+  __shared__ float tile[64][65];
+  const int bj = blockIdx.z;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const float* s = src + (size_t)bj * C * HW;
+  float* d = dst + (size_t)bj * C * HW;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, p = p0 + tx;
+    tile[r][tx] = (c < C && p < HW) ? s[(size_t)c * HW + p] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int p = p0 + r, c = c0 + tx;
+    if (p < HW && c < C) d[(size_t)p * C + c] = tile[tx][r];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_to_chw(int C, int HW, const float* __restrict__ src,
+                                                float* __restrict__ dst) {
+  __shared__ float tile[64][65];
+  const int bj = blockIdx.z;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const float* s = src + (size_t)bj * C * HW;
+  float* d = dst + (size_t)bj * C * HW;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int p = p0 + r, c = c0 + tx;
+    tile[r][tx] = (p < HW && c < C) ? s[(size_t)p * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, p = p0 + tx;
+    if (c < C && p < HW) d[(size_t)c * HW + p] = tile[tx][r];
+  }
+}
+
+// Transpose-reduce of DG=16 per-lane partials over the wave: 4 halving exchange stages
+// (lane bits 32, 16, 8, 4) then a butterfly over lane bits 2, 1 -> 17 shuffles for 16
+// sums; lane l ends with the total of partial index (l >> 2) & 15.
+template <int NV, int LB>
+__device__ __forceinline__ void treduce_step(float (&part)[DG], int lane) {
+  constexpr int HALF = NV / 2;
+  const bool upper = (lane & LB) != 0;
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) {
+    const float send = upper ? part[i] : part[i + HALF];
+    const float keep = upper ? part[i + HALF] : part[i];
+    part[i] = keep + __shfl_xor(send, LB, 64);
+  }
+}
+__device__ __forceinline__ float transpose_reduce16(float (&part)[DG], int lane) {
+  treduce_step<16, 32>(part, lane);
+  treduce_step<8, 16>(part, lane);
+  treduce_step<4, 8>(part, lane);
+  treduce_step<2, 4>(part, lane);
+  float v = part[0];
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 1, 64);
+  return v;
+}
+
+// One wave per (b, pixel). grid = (ceil(HW / 4), B), block = 256 (4 pixels).
+__global__ __launch_bounds__(256) void k_cost_fwd(int J, int C, int H, int W, int D, int depth_per_pixel,
+                                                  const float* __restrict__ ref, const float* __restrict__ tgt_hwc,
+                                                  const float* __restrict__ intr, const float* __restrict__ pose,
+                                                  const float* __restrict__ depth, float clampz,
+                                                  float* __restrict__ cost) {
+  const int HW = H * W;
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= HW) return;
+  const float px = (float)(p % W), py = (float)(p / W);
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  for (int d0 = 0; d0 < D; d0 += DG) {
+    float part[DG];
+#pragma unroll
+    for (int i = 0; i < DG; ++i) part[i] = 0.f;
+    for (int j = 0; j < J; ++j) {
+      Cam cam;
+      load_cam(intr + ((size_t)b * J + j) * 9, pose + ((size_t)b * J + j) * 16, cam);
+      const float qx = cam.Kinv[0] * px + cam.Kinv[1] * py + cam.Kinv[2];
+      const float qy = cam.Kinv[3] * px + cam.Kinv[4] * py + cam.Kinv[5];
+      const float qz = cam.Kinv[6] * px + cam.Kinv[7] * py + cam.Kinv[8];
+      const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
+      const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
+      const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
+      const float* tg = tgt_hwc + ((size_t)b * J + j) * HW * C;
+      for (int c0 = 0; c0 < C; c0 += 64) {
+        const int c = c0 + lane;
+        const bool cv = c < C;
+        const float r = cv ? ref[((size_t)b * C + c) * HW + p] : 0.f;
+#pragma unroll
+        for (int i = 0; i < DG; ++i) {
+          const int d = d0 + i;
+          if (d >= D) continue;
+          const float dep = depth_per_pixel ? depth[((size_t)b * D + d) * HW + p] : depth[(size_t)b * D + d];
+          Taps tp;
+          taps_at(cam, prx, pry, prz, dep, clampz, H, W, tp);
+          float s = 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (tp.idx[k] >= 0 && cv) s += tp.w[k] * tg[(size_t)tp.idx[k] * C + c];
+          part[i] += r * s;
+        }
+      }
+    }
+    const float tot = transpose_reduce16(part, lane);
+    const int d = d0 + (lane >> 2);
+    if ((lane & 3) == 0 && d < D) cost[((size_t)b * D + d) * HW + p] = tot * scale;
+  }
+}
+
+// Backward: one wave per (b, pixel); lanes over channels.
+//   dref[c,p]   += sum_{j,d} g(d) * warp_j[c,d,p]
+//   dtgt[q,c]   += g(d) * w_k * ref[c,p] for each tap (atomics into channel-last scratch)
+__global__ __launch_bounds__(256) void k_cost_bwd(int J, int C, int H, int W, int D, int depth_per_pixel,
+                                                  const float* __restrict__ ref, const float* __restrict__ tgt_hwc,
+                                                  const float* __restrict__ intr, const float* __restrict__ pose,
+                                                  const float* __restrict__ depth, float clampz,
+                                                  const float* __restrict__ dcost, float* __restrict__ dref,
+                                                  float* __restrict__ dtgt_hwc) {
+  const int HW = H * W;
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= HW) return;
+  const float px = (float)(p % W), py = (float)(p / W);
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int c = c0 + lane;
+    const bool cv = c < C;
+    const float r = cv ? ref[((size_t)b * C + c) * HW + p] : 0.f;
+    float dr = 0.f;
+    for (int j = 0; j < J; ++j) {
+      Cam cam;
+      load_cam(intr + ((size_t)b * J + j) * 9, pose + ((size_t)b * J + j) * 16, cam);
+      const float qx = cam.Kinv[0] * px + cam.Kinv[1] * py + cam.Kinv[2];
+      const float qy = cam.Kinv[3] * px + cam.Kinv[4] * py + cam.Kinv[5];
+      const float qz = cam.Kinv[6] * px + cam.Kinv[7] * py + cam.Kinv[8];
+      const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
+      const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
+      const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
+      const float* tg = tgt_hwc + ((size_t)b * J + j) * HW * C;
+      float* dtg = dtgt_hwc + ((size_t)b * J + j) * HW * C;
+      for (int d = 0; d < D; ++d) {
+        const float g = dcost[((size_t)b * D + d) * HW + p] * scale;
+        if (g == 0.f) continue;
+        const float dep = depth_per_pixel ? depth[((size_t)b * D + d) * HW + p] : depth[(size_t)b * D + d];
+        Taps tp;
+        taps_at(cam, prx, pry, prz, dep, clampz, H, W, tp);
+        const float gr = g * r;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (tp.idx[k] >= 0 && cv) {
+            dr += g * tp.w[k] * tg[(size_t)tp.idx[k] * C + c];
+            atomicAdd(&dtg[(size_t)tp.idx[k] * C + c], gr * tp.w[k]);
+          }
+        }
+      }
+    }
+    if (cv) dref[((size_t)b * C + c) * HW + p] = dr;
+  }
+}
+
+// Materialising warp: out[b, c, d, y, x]. Thread per (b, d, pixel), loop over channels
+// (feature in [B,C,H,W]; out written coalesced across pixels).
+__global__ __launch_bounds__(256) void k_warp(int C, int H, int W, int D, const float* __restrict__ feat,
+                                              const float* __restrict__ intr, const float* __restrict__ pose,
+                                              const float* __restrict__ depth, float clampz,
+                                              float* __restrict__ out) {
+  const int HW = H * W;
+  const int b = blockIdx.z, d = blockIdx.y;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= HW) return;
+  Cam cam;
+  load_cam(intr + (size_t)b * 9, pose + (size_t)b * 16, cam);
+  const float px = (float)(p % W), py = (float)(p / W);
+  const float qx = cam.Kinv[0] * px + cam.Kinv[1] * py + cam.Kinv[2];
+  const float qy = cam.Kinv[3] * px + cam.Kinv[4] * py + cam.Kinv[5];
+  const float qz = cam.Kinv[6] * px + cam.Kinv[7] * py + cam.Kinv[8];
+  const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
+  const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
+  const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
+  Taps tp;
+  taps_at(cam, prx, pry, prz, depth[((size_t)b * D + d) * HW + p], clampz, H, W, tp);
+  const float* f = feat + (size_t)b * C * HW;
+  for (int c = 0; c < C; ++c) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tp.idx[k] >= 0) s += tp.w[k] * f[(size_t)c * HW + tp.idx[k]];
+    out[(((size_t)b * C + c) * D + d) * HW + p] = s;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref,
+                        const float* tgt, const float* intr, const float* pose, const float* depth,
+                        float clamp_min_depth, float* tgt_hwc, float* cost, void* stream) {
+  DSPLAT_REQUIRE(B > 0 && J > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_cost_volume_fwd: bad sizes B=%d J=%d C=%d H=%d W=%d D=%d", B, J, C, H, W, D);
+  DSPLAT_REQUIRE(ref && tgt && intr && pose && depth && tgt_hwc && cost, "dcv_cost_volume_fwd: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int HW = H * W;
+  k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, tgt, tgt_hwc);
+  if (int e = dsplat::check_launch("k_to_hwc")) return e;
+  k_cost_fwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
+                                                   depth, clamp_min_depth, cost);
+  return dsplat::check_launch("k_cost_fwd");
+}
+
+int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref,
+                        const float* tgt_hwc, const float* intr, const float* pose, const float* depth,
+                        float clamp_min_depth, const float* dcost, float* dref, float* dtgt, float* dtgt_hwc,
+                        void* stream) {
+  DSPLAT_REQUIRE(B > 0 && J > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_cost_volume_bwd: bad sizes");
+  DSPLAT_REQUIRE(ref && tgt_hwc && intr && pose && depth && dcost && dref && dtgt && dtgt_hwc,
+                 "dcv_cost_volume_bwd: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int HW = H * W;
+  if (int e = dsplat::check_hip(hipMemsetAsync(dtgt_hwc, 0, (size_t)B * J * HW * C * 4, st), "memset dtgt_hwc")) return e;
+  k_cost_bwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
+                                                   depth, clamp_min_depth, dcost, dref, dtgt_hwc);
+  if (int e = dsplat::check_launch("k_cost_bwd")) return e;
+  k_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, dtgt_hwc, dtgt);
+  return dsplat::check_launch("k_to_chw");
+}
+
+int dcv_warp_fwd(int B, int C, int H, int W, int D, const float* feature, const float* intr, const float* pose,
+                 const float* depth, float clamp_min_depth, float* out, void* stream) {
+  DSPLAT_REQUIRE(B > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_warp_fwd: bad sizes");
+  DSPLAT_REQUIRE(feature && intr && pose && depth && out, "dcv_warp_fwd: null pointer");
+  const int HW = H * W;
+  k_warp<<<dim3((HW + 255) / 256, D, B), 256, 0, (hipStream_t)stream>>>(C, H, W, D, feature, intr, pose, depth,
+                                                                        clamp_min_depth, out);
+  return dsplat::check_launch("k_warp");
+}
+
+}  // extern "C"

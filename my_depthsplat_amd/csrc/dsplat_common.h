@@ -1,0 +1,56 @@
+// Shared helpers for the libdsplat_hip.so translation units (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/dsplat_hip.h"
+
+namespace dsplat {
+
+void set_error(const char* fmt, ...);
+
+// Check the last launch / API status and convert it to the ABI status code.
+inline int check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return 2;
+  }
+  return 0;
+}
+inline int check_launch(const char* what) { return check_hip(hipGetLastError(), what); }
+
+#define DSPLAT_REQUIRE(cond, ...)       \
+  do {                                  \
+    if (!(cond)) {                      \
+      ::dsplat::set_error(__VA_ARGS__); \
+      return 1;                         \
+    }                                   \
+  } while (0)
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Inclusive scan over one wave64.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(v, off, 64);
+    if (lane >= off) v += t;
+  }
+  return v;
+}
+
+inline int tiles_x(int W) { return (W + DSR_TILE - 1) / DSR_TILE; }
+inline int tiles_y(int H) { return (H + DSR_TILE - 1) / DSR_TILE; }
+
+}  // namespace dsplat

@@ -1,0 +1,109 @@
+"""Decoder plugin: drop-in for src/model/decoder/{decoder.py, decoder_splatting_cuda.py,
+__init__.py} (Decoder ABC, DecoderOutput, DECODERS registry, get_decoder).
+
+`DecoderSplattingCUDA.forward` keeps the reference signature and outputs
+(decoder_splatting_cuda.py:35-67) but renders all B*v views in one batched rasterizer
+call over the B scenes' Gaussians: the `repeat(gaussians, "b g ... -> (b v) g ...")`
+materialisation of decoder_splatting_cuda.py:53-56 and the per-view loop of
+cuda_splatting.py:90-125 are gone.
+"""
+from __future__ import annotations
+
+from abc import ABC, abstractmethod
+from dataclasses import dataclass
+from typing import Generic, Literal, TypeVar
+
+import torch
+from torch import nn
+
+from .cuda_splatting import DepthRenderingMode, render_depth_cuda, render_views
+
+
+@dataclass
+class Gaussians:
+    """src/model/types.py:7-12."""
+    means: torch.Tensor        # [b, g, 3]
+    covariances: torch.Tensor  # [b, g, 3, 3]
+    harmonics: torch.Tensor    # [b, g, 3, d_sh]
+    opacities: torch.Tensor    # [b, g]
+
+
+@dataclass
+class DecoderOutput:
+    """src/model/decoder/decoder.py:19-22."""
+    color: torch.Tensor              # [b, v, 3, h, w]
+    depth: torch.Tensor | None       # [b, v, h, w]
+
+
+T = TypeVar("T")
+
+
+class Decoder(nn.Module, ABC, Generic[T]):
+    """src/model/decoder/decoder.py:28-48."""
+
+    def __init__(self, cfg: T, dataset_cfg) -> None:
+        super().__init__()
+        self.cfg = cfg
+        self.dataset_cfg = dataset_cfg
+
+    @abstractmethod
+    def forward(self, gaussians: Gaussians, extrinsics: torch.Tensor, intrinsics: torch.Tensor,
+                near: torch.Tensor, far: torch.Tensor, image_shape: tuple[int, int],
+                depth_mode: DepthRenderingMode | None = None) -> DecoderOutput:
+        ...
+
+
+@dataclass
+class DecoderSplattingCUDACfg:
+    name: Literal["splatting_cuda"]
+
+
+def _background(dataset_cfg) -> list[float]:
+    if isinstance(dataset_cfg, dict):
+        return list(dataset_cfg["background_color"])
+    return list(dataset_cfg.background_color)
+
+
+class DecoderSplattingCUDA(Decoder[DecoderSplattingCUDACfg]):
+    """decoder_splatting_cuda.py:19-91 on libdsplat_hip.so."""
+
+    def __init__(self, cfg: DecoderSplattingCUDACfg, dataset_cfg) -> None:
+        super().__init__(cfg, dataset_cfg)
+        self.register_buffer("background_color", torch.tensor(_background(dataset_cfg), dtype=torch.float32),
+                             persistent=False)
+
+    def forward(self, gaussians: Gaussians, extrinsics: torch.Tensor, intrinsics: torch.Tensor,
+                near: torch.Tensor, far: torch.Tensor, image_shape: tuple[int, int],
+                depth_mode: DepthRenderingMode | None = None) -> DecoderOutput:
+        b, v = extrinsics.shape[:2]
+        h, w = image_shape
+        color = render_views(
+            extrinsics.reshape(b * v, 4, 4), intrinsics.reshape(b * v, 3, 3), near.reshape(b * v),
+            far.reshape(b * v), image_shape, self.background_color.expand(b * v, 3), gaussians.means,
+            gaussians.covariances, gaussians.harmonics, gaussians.opacities,
+            view_scene=[i // v for i in range(b * v)])
+        color = color.reshape(b, v, 3, h, w)
+        depth = None if depth_mode is None else self.render_depth(
+            gaussians, extrinsics, intrinsics, near, far, image_shape, depth_mode)
+        return DecoderOutput(color, depth)
+
+    def render_depth(self, gaussians: Gaussians, extrinsics: torch.Tensor, intrinsics: torch.Tensor,
+                     near: torch.Tensor, far: torch.Tensor, image_shape: tuple[int, int],
+                     mode: DepthRenderingMode = "depth") -> torch.Tensor:
+        """decoder_splatting_cuda.py:69-91 (depth colours differ per view, so the
+        Gaussians are expanded per view here as in the reference)."""
+        b, v = extrinsics.shape[:2]
+        rep = lambda t: t[:, None].expand(b, v, *t.shape[1:]).reshape(b * v, *t.shape[1:])  # noqa: E731
+        out = render_depth_cuda(extrinsics.reshape(b * v, 4, 4), intrinsics.reshape(b * v, 3, 3),
+                                near.reshape(b * v), far.reshape(b * v), image_shape, rep(gaussians.means),
+                                rep(gaussians.covariances), rep(gaussians.opacities), mode=mode)
+        return out.reshape(b, v, *image_shape)
+
+
+DECODERS = {"splatting_cuda": DecoderSplattingCUDA}
+DecoderCfg = DecoderSplattingCUDACfg
+
+
+def get_decoder(decoder_cfg: DecoderCfg, dataset_cfg) -> Decoder:
+    """src/model/decoder/__init__.py:12-13."""
+    return DECODERS[decoder_cfg.name](decoder_cfg, dataset_cfg)

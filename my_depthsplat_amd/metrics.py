@@ -1,0 +1,13 @@
+"""PSNR as defined by the reference (src/evaluation/metrics.py:12-19)."""
+from __future__ import annotations
+
+import torch
+
+
+@torch.no_grad()
+def compute_psnr(ground_truth: torch.Tensor, predicted: torch.Tensor) -> torch.Tensor:
+    """[b, c, h, w] x2 -> [b]: clip both to [0, 1], -10 log10(mean squared error)."""
+    gt = ground_truth.clip(min=0, max=1)
+    pr = predicted.clip(min=0, max=1)
+    mse = ((gt - pr) ** 2).flatten(1).mean(dim=1)
+    return -10 * mse.log10()

@@ -1,0 +1,192 @@
+"""Batched differentiable rasterization through libdsplat_hip.so.
+
+`rasterize_views` is the single entry the drop-in shims (rasterizer.py, cuda_splatting.py,
+decoder.py) call: it renders V views of S Gaussian scenes in ONE launch sequence
+(preprocess -> bucket scan -> scatter -> per-tile LDS sort -> composite), replacing the
+per-view Python loop, the two `.item()` syncs per view and the Gaussian x views repeat
+of the reference (cuda_splatting.py:90-125, decoder_splatting_cuda.py:53-56).
+The only host sync is one 8-byte read of (num_rendered, max tile count) per batch,
+needed to size the key buffer.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+TILE = 16
+GEOM_STRIDE = 12
+CAM_FLOATS = 44  # sizeof(dsr_camera) / 4
+
+
+def tiles(h: int, w: int) -> tuple[int, int]:
+    return (w + TILE - 1) // TILE, (h + TILE - 1) // TILE
+
+
+def pack_cameras(viewmatrix: torch.Tensor, projmatrix: torch.Tensor, campos: torch.Tensor,
+                 tanfovx: torch.Tensor, tanfovy: torch.Tensor, bg: torch.Tensor,
+                 scene: torch.Tensor, scale: torch.Tensor | None = None) -> torch.Tensor:
+    """Build the device array of `dsr_camera` structs ([V, 44] float32, 176 B each).
+
+    viewmatrix / projmatrix: [V, 4, 4] exactly as handed to GaussianRasterizationSettings
+    (transposed torch matrices, cuda_splatting.py:83-86); campos [V, 3]; tanfov [V];
+    bg [V, 3]; scene [V] int (which Gaussian set); scale [V] (1/near when the reference's
+    scale-invariant rescale applies, else 1).
+    """
+    V = viewmatrix.shape[0]
+    dev = viewmatrix.device
+    f32 = torch.float32
+    if scale is None:
+        scale = torch.ones(V, dtype=f32, device=dev)
+    scene_bits = scene.to(device=dev, dtype=torch.int32).view(f32).reshape(V, 1)
+    cam = torch.cat([
+        viewmatrix.reshape(V, 16).to(f32), projmatrix.reshape(V, 16).to(f32),
+        campos.reshape(V, 3).to(f32), tanfovx.reshape(V, 1).to(f32), tanfovy.reshape(V, 1).to(f32),
+        bg.reshape(V, 3).to(f32), scene_bits, scale.reshape(V, 1).to(f32),
+        torch.zeros(V, 2, dtype=f32, device=dev),
+    ], dim=1).contiguous()
+    assert cam.shape[1] == CAM_FLOATS
+    return cam
+
+
+@dataclass
+class RasterState:
+    """Everything the backward needs (all device tensors)."""
+    geom: torch.Tensor        # [V, G, 12]
+    radii: torch.Tensor       # [V, G] int32
+    seg_start: torch.Tensor   # [V*T + 1] int32 (uint32)
+    keys: torch.Tensor        # [N] int64 (uint64 keys, sorted per segment)
+    final_T: torch.Tensor     # [V, H, W]
+    n_contrib: torch.Tensor   # [V, H, W] int32
+    num_rendered: int
+    max_count: int
+
+
+def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W):
+    """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh) or [S,G,3]; opacities
+    [S,G]; cov6 [S,G,6]; cams [V,44]. Returns (color [V,3,H,W], RasterState)."""
+    lib = _lib.load()
+    _lib.require_gpu(means, feats, opacities, cov6, cams)
+    S, G = means.shape[0], means.shape[1]
+    M = feats.shape[2] if use_sh else 0
+    dev = means.device
+    gx, gy = tiles(H, W)
+    T = gx * gy
+    st = _lib.stream_of(dev)
+    geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
+    radii = torch.empty((V, G), dtype=torch.int32, device=dev)
+    seg_count = torch.empty(V * T, dtype=torch.int32, device=dev)
+    _lib.check(lib.dsr_preprocess_fwd(
+        S, G, V, H, W, sh_degree if use_sh else -1, M, means.data_ptr(),
+        feats.data_ptr() if use_sh else None, None if use_sh else feats.data_ptr(),
+        opacities.data_ptr(), cov6.data_ptr(), cams.data_ptr(), geom.data_ptr(), radii.data_ptr(),
+        seg_count.data_ptr(), st), "dsr_preprocess_fwd")
+    seg_start = torch.empty(V * T + 1, dtype=torch.int32, device=dev)
+    cursor = torch.empty(V * T, dtype=torch.int32, device=dev)
+    totals = torch.empty(4, dtype=torch.int32, device=dev)
+    _lib.check(lib.dsr_bin_scan(V, H, W, seg_count.data_ptr(), seg_start.data_ptr(), cursor.data_ptr(),
+                                totals.data_ptr(), st), "dsr_bin_scan")
+    tot = totals[:2].cpu()  # the one host sync: sizes the key buffer
+    N, maxc = int(tot[0]), int(tot[1])
+    keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
+    if N > 0:
+        _lib.check(lib.dsr_bin_scatter(G, V, H, W, geom.data_ptr(), cursor.data_ptr(), keys.data_ptr(), st),
+                   "dsr_bin_scatter")
+        cap = lib.dsr_sort_lds_capacity()
+        scratch = torch.empty(N, dtype=torch.int64, device=dev) if maxc > cap else None
+        _lib.check(lib.dsr_bin_sort(G, V, H, W, seg_start.data_ptr(), keys.data_ptr(),
+                                    None if scratch is None else scratch.data_ptr(), maxc, st), "dsr_bin_sort")
+    color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
+    final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
+    n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
+    _lib.check(lib.dsr_render_fwd(G, V, H, W, cams.data_ptr(), geom.data_ptr(), seg_start.data_ptr(),
+                                  keys.data_ptr(), color.data_ptr(), final_T.data_ptr(), n_contrib.data_ptr(), st),
+               "dsr_render_fwd")
+    return color, RasterState(geom, radii, seg_start, keys, final_T, n_contrib, N, maxc)
+
+
+def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, state: RasterState,
+                 dcolor, want_mean2d: bool):
+    lib = _lib.load()
+    S, G = means.shape[0], means.shape[1]
+    V, _, H, W = dcolor.shape
+    M = feats.shape[2] if use_sh else 0
+    dev = means.device
+    st = _lib.stream_of(dev)
+    dcolor = dcolor.contiguous().float()
+    dgeom = torch.zeros((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
+    _lib.check(lib.dsr_render_bwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), state.seg_start.data_ptr(),
+                                  state.keys.data_ptr(), state.final_T.data_ptr(), state.n_contrib.data_ptr(),
+                                  dcolor.data_ptr(), dgeom.data_ptr(), st), "dsr_render_bwd")
+    # views of each scene, in view order (fixed summation order -> deterministic reduce)
+    order = sorted(range(V), key=lambda v: (view_scene[v], v))
+    starts = [0] * (S + 1)
+    for v in range(V):
+        starts[view_scene[v] + 1] += 1
+    for s in range(S):
+        starts[s + 1] += starts[s]
+    idx = torch.tensor(starts + order, dtype=torch.int32).to(dev, non_blocking=True)
+    dmeans = torch.empty((S, G, 3), dtype=torch.float32, device=dev)
+    dfeat = torch.empty_like(feats, dtype=torch.float32)
+    dopac = torch.empty((S, G), dtype=torch.float32, device=dev)
+    dcov6 = torch.empty((S, G, 6), dtype=torch.float32, device=dev)
+    dmean2d = torch.empty((V, G, 3), dtype=torch.float32, device=dev) if want_mean2d else None
+    _lib.check(lib.dsr_preprocess_bwd(
+        S, G, V, H, W, sh_degree if use_sh else -1, M, means.data_ptr(), feats.data_ptr() if use_sh else None,
+        cov6.data_ptr(), cams.data_ptr(), state.geom.data_ptr(), dgeom.data_ptr(), idx.data_ptr(),
+        idx[S + 1:].data_ptr(), dmeans.data_ptr(), dfeat.data_ptr() if use_sh else None,
+        None if use_sh else dfeat.data_ptr(), dopac.data_ptr(), dcov6.data_ptr(),
+        None if dmean2d is None else dmean2d.data_ptr(), st), "dsr_preprocess_bwd")
+    return dmeans, dfeat, dopac, dcov6, dmean2d, dgeom
+
+
+class _RasterizeViews(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means, feats, opacities, cov6, means2d, cams, view_scene, use_sh, sh_degree, H, W):
+        V = len(view_scene)
+        color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W)
+        ctx.save_for_backward(means, feats, opacities, cov6, cams)
+        ctx.state = state
+        ctx.meta = (view_scene, use_sh, sh_degree, None if means2d is None else means2d.shape)
+        ctx.mark_non_differentiable(state.radii)
+        return color, state.radii
+
+    @staticmethod
+    def backward(ctx, dcolor, _dradii):
+        means, feats, opacities, cov6, cams = ctx.saved_tensors
+        view_scene, use_sh, sh_degree, m2d_shape = ctx.meta
+        want_m2d = m2d_shape is not None and ctx.needs_input_grad[4]
+        dmeans, dfeat, dopac, dcov6, dmean2d, _ = backward_raw(
+            means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, ctx.state, dcolor,
+            want_mean2d=want_m2d)
+        if dmean2d is not None:
+            dmean2d = dmean2d.view(m2d_shape)
+        return dmeans, dfeat, dopac, dcov6, dmean2d, None, None, None, None, None, None
+
+
+def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.Tensor, cov6: torch.Tensor,
+                    cams: torch.Tensor, view_scene: list[int], *, use_sh: bool, sh_degree: int,
+                    image_height: int, image_width: int, means2d: torch.Tensor | None = None):
+    """Differentiable render of V views. means [S,G,3], feats [S,G,M,3] (SH, coefficient-major
+    like the rasterizer's `shs`) or [S,G,3] (colors_precomp), opacities [S,G], cov6 [S,G,6],
+    cams [V,44] from pack_cameras, view_scene[v] = scene index of view v.
+    Returns color [V,3,H,W] and radii [V,G] (int32)."""
+    S = means.shape[0]
+    if len(view_scene) != cams.shape[0]:
+        raise ValueError(f"view_scene has {len(view_scene)} entries for {cams.shape[0]} cameras")
+    if any(not (0 <= s < S) for s in view_scene):
+        raise ValueError(f"view_scene entries must be in [0, {S})")
+    if use_sh and not (0 <= sh_degree <= 3 and feats.shape[2] >= (sh_degree + 1) ** 2):
+        raise ValueError(f"unsupported sh_degree={sh_degree} for {feats.shape[2]} coefficients")
+    if image_height <= 0 or image_width <= 0:
+        raise ValueError("image size must be positive")
+    f = lambda t: t.contiguous().float()  # noqa: E731
+    return _RasterizeViews.apply(f(means), f(feats), f(opacities), f(cov6), means2d, cams.contiguous(),
+                                 list(view_scene), use_sh, int(sh_degree), int(image_height), int(image_width))
+
+
+def sh_degree_of(n_coeffs: int) -> int:
+    return math.isqrt(n_coeffs) - 1
