@@ -1,0 +1,182 @@
+#!/usr/bin/env python
+"""Benchmark: rendered target views/sec on the reference's headline workload.
+
+Workload (BASELINE.json configs[1]): RE10K-shaped 2-view 256x256 context -> 1 Gaussian
+per pixel (G = 131,072), fp32, rendered into v = 3 target views (the RE10K evaluation
+index: 2 context, 3 target views per scene). One "step" = one DecoderSplattingCUDA
+forward of one scene batch (B scenes x v views) with the Gaussians already resident in
+HBM — the `decoder` timer of the reference test loop (model_wrapper.py:432-484).
+Synthetic inputs through the Gaussian adapter (my_depthsplat_amd.synthetic).
+
+N GPUs: one process per GPU (torchrun), each rank renders its own scenes (per-scene data
+parallel, no collective on the data path) -> scaling "weak"; value = all views / max time.
+
+Extra fields: roofline of the dominant kernel (HIP events around its launches on the
+stream it runs on; algorithmic bytes per launch in DESIGN.md §4), cpu_baseline (the CPU
+oracle on the host, rank 0, bounded sample), psnr_vs_oracle_db (parity PSNR of one view).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec); 6.29 TB/s measured copy
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=1, help="scenes per step per GPU (reference test loop: 1)")
+    p.add_argument("--views", type=int, default=3, help="target views per scene (RE10K eval: 3)")
+    p.add_argument("--size", type=int, default=256)
+    p.add_argument("--context", type=int, default=2)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from my_depthsplat_amd import _lib, raster
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.synthetic import make_scene
+
+    _lib.load()
+    H = W = args.size
+    sc = make_scene(batch=args.batch, n_context=args.context, n_targets=args.views, height=H, width=W,
+                    seed=1000 + rank, device=dev)
+    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]})
+    dec = dec.to(dev)
+
+    def step():
+        with torch.no_grad():
+            return dec(sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near, sc.far, (H, W))
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+
+    # live per-kernel timing with HIP events on the launch stream (torch's current stream,
+    # which is the stream every C-ABI call is enqueued on)
+    ev = raster.KernelTimer()
+    raster.set_timer(ev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    raster.set_timer(None)
+    ktimes = ev.summary()  # name -> (launches, avg_ms)
+    n_rendered = raster.last_stats()["num_rendered"]
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    views_per_step = args.batch * args.views
+    total_views = views_per_step * args.steps * world
+    value = total_views / elapsed
+
+    if rank == 0:
+        G = sc.gaussians.means.shape[1]
+        V = views_per_step
+        HW = H * W
+        # dominant kernel + its algorithmic bytes per launch
+        name, (launches, avg_ms) = max(ktimes.items(), key=lambda kv: kv[1][0] * kv[1][1])
+        alg = raster.algorithmic_bytes(name, G=G, V=V, N=n_rendered, HW=HW)
+        achieved = alg / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "avg_ms": round(avg_ms, 5), "algorithmic_bytes_per_launch": alg,
+                "per_kernel_avg_ms": {k: round(v[1], 5) for k, v in sorted(ktimes.items())}}
+        psnr, l1, cpu = None, None, None
+        if not args.no_cpu_baseline:
+            psnr, l1, cpu = cpu_leg(sc, out, args, H, W)
+        line = {
+            "metric": "rendered views/sec + PSNR, 2-view 256x256 RE10K, 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "views/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.context}-view {H}x{W} RE10K feed-forward render, 1 Gaussian/pixel "
+                                   f"(G={G}), {args.views} target views/scene, fp32",
+                       "global_batch": args.batch * world, "views_per_scene": args.views, "gaussians": G,
+                       "num_rendered_per_step": n_rendered, "parallelism": f"dp{world} (per-scene, no collective)"},
+            "psnr_vs_oracle_db": psnr, "l1_vs_oracle": l1,
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_leg(sc, out, args, H, W):
+    """CPU oracle on the host: parity PSNR/L1 of view 0 + a bounded throughput sample."""
+    import numpy as np
+    import torch
+
+    from my_depthsplat_amd.cuda_splatting import _cov6, camera_settings
+    from oracle import raster as orc
+
+    g = sc.gaussians
+    st = camera_settings(sc.target_extrinsics[0].cpu(), sc.target_intrinsics[0].cpu(), sc.near[0].cpu(),
+                         sc.far[0].cpu())
+    npst = {k: t.numpy() for k, t in st.items()}
+    means = g.means[0].cpu().numpy()
+    shs = g.harmonics[0].transpose(-1, -2).contiguous().cpu().numpy()
+    opac = g.opacities[0].cpu().numpy()
+    cov6 = _cov6(g.covariances[0]).contiguous().cpu().numpy()
+    bg = np.zeros(3, np.float32)
+    deg = int(round(shs.shape[1] ** 0.5)) - 1
+
+    def one(i):
+        return orc.render_settings(means, shs, None, opac, cov6, npst, i, bg, H, W, deg)
+
+    o = one(0)
+    ref, _, _ = o.image()
+    o.close()
+    hip = out.color[0, 0].float().cpu().numpy()
+    l1 = float(np.abs(hip - ref).mean())
+    mse = float(np.mean((np.clip(hip, 0, 1) - np.clip(ref, 0, 1)) ** 2))
+    psnr = None if mse == 0 else round(-10 * np.log10(mse), 3)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        o = one(n % args.views)
+        o.close()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds and n >= 2:
+            break
+    return psnr, l1, {"value": round(n / el, 3), "unit": "views/s", "cores": threads, "kind": "port",
+                      "sample": f"{n} target views of the same {H}x{W} scene (G={means.shape[0]}) rendered by "
+                                f"oracle/dsr_oracle.cpp (OpenMP, {threads} threads) in {el:.1f}s"}
+
+
+if __name__ == "__main__":
+    main()

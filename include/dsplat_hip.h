@@ -144,6 +144,12 @@ int dcv_warp_fwd(int B, int C, int H, int W, int D, const float* feature, const 
                  const float* pose, const float* depth, float clamp_min_depth, float* out,
                  void* stream);
 
+/* Gradient of dcv_warp_fwd w.r.t. `feature`: dout [B,C,D,H,W] -> dfeature [B,C,H,W]
+ * (overwritten). Geometry receives no gradient (matching.py:46, torch.no_grad). */
+int dcv_warp_bwd(int B, int C, int H, int W, int D, const float* dout, const float* intr,
+                 const float* pose, const float* depth, float clamp_min_depth, float* dfeature,
+                 void* stream);
+
 /* ---- misc ------------------------------------------------------------------------- */
 const char* dsplat_last_error(void);
 int dsplat_abi_version(void);

@@ -32,6 +32,7 @@ SIGNATURES: dict[str, tuple] = {
     "dcv_cost_volume_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P,
                                  _P, _P, _P]),
     "dcv_warp_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, _P, _P]),
+    "dcv_warp_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, _P, _P]),
     "dsplat_last_error": (ctypes.c_char_p, []),
     "dsplat_abi_version": (_I, []),
 }

@@ -290,9 +290,51 @@ __global__ __launch_bounds__(256) void k_warp(int C, int H, int W, int D, const 
   }
 }
 
+// Backward of k_warp w.r.t. the feature map: scatter-add through the same bilinear taps.
+__global__ __launch_bounds__(256) void k_warp_bwd(int C, int H, int W, int D, const float* __restrict__ dout,
+                                                  const float* __restrict__ intr, const float* __restrict__ pose,
+                                                  const float* __restrict__ depth, float clampz,
+                                                  float* __restrict__ dfeat) {
+  const int HW = H * W;
+  const int b = blockIdx.z, d = blockIdx.y;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= HW) return;
+  Cam cam;
+  load_cam(intr + (size_t)b * 9, pose + (size_t)b * 16, cam);
+  const float px = (float)(p % W), py = (float)(p / W);
+  const float qx = cam.Kinv[0] * px + cam.Kinv[1] * py + cam.Kinv[2];
+  const float qy = cam.Kinv[3] * px + cam.Kinv[4] * py + cam.Kinv[5];
+  const float qz = cam.Kinv[6] * px + cam.Kinv[7] * py + cam.Kinv[8];
+  const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
+  const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
+  const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
+  Taps tp;
+  taps_at(cam, prx, pry, prz, depth[((size_t)b * D + d) * HW + p], clampz, H, W, tp);
+  float* f = dfeat + (size_t)b * C * HW;
+  for (int c = 0; c < C; ++c) {
+    const float g = dout[(((size_t)b * C + c) * D + d) * HW + p];
+    if (g == 0.f) continue;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tp.idx[k] >= 0) atomicAdd(&f[(size_t)c * HW + tp.idx[k]], g * tp.w[k]);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int dcv_warp_bwd(int B, int C, int H, int W, int D, const float* dout, const float* intr, const float* pose,
+                 const float* depth, float clamp_min_depth, float* dfeature, void* stream) {
+  DSPLAT_REQUIRE(B > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_warp_bwd: bad sizes");
+  DSPLAT_REQUIRE(dout && intr && pose && depth && dfeature, "dcv_warp_bwd: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int HW = H * W;
+  if (int e = dsplat::check_hip(hipMemsetAsync(dfeature, 0, (size_t)B * C * HW * 4, st), "memset dfeature")) return e;
+  k_warp_bwd<<<dim3((HW + 255) / 256, D, B), 256, 0, st>>>(C, H, W, D, dout, intr, pose, depth, clamp_min_depth,
+                                                           dfeature);
+  return dsplat::check_launch("k_warp_bwd");
+}
 
 int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref,
                         const float* tgt, const float* intr, const float* pose, const float* depth,

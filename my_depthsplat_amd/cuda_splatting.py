@@ -121,19 +121,11 @@ def render_cuda(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch.
                         scale_invariant=scale_invariant, use_sh=use_sh)
 
 
-def render_cuda_orthographic(extrinsics: torch.Tensor, width: torch.Tensor, height: torch.Tensor,
-                             near: torch.Tensor, far: torch.Tensor, image_shape: tuple[int, int],
-                             background_color: torch.Tensor, gaussian_means: torch.Tensor,
-                             gaussian_covariances: torch.Tensor, gaussian_sh_coefficients: torch.Tensor,
-                             gaussian_opacities: torch.Tensor, fov_degrees: float = 0.1, use_sh: bool = True,
-                             dump: dict | None = None) -> torch.Tensor:
-    """Pseudo-orthographic render: tiny fov, camera pulled back (cuda_splatting.py:129-219)."""
+def orthographic_settings(extrinsics: torch.Tensor, width: torch.Tensor, height: torch.Tensor, near: torch.Tensor,
+                          far: torch.Tensor, fov_degrees: float = 0.1, dump: dict | None = None) -> dict:
+    """Pseudo-orthographic camera: tiny fov, camera pulled back by 0.5 width / tan(fov/2)
+    (cuda_splatting.py:146-175). Returns the rasterizer settings per view."""
     b = extrinsics.shape[0]
-    h, w = image_shape
-    if not (use_sh or gaussian_sh_coefficients.shape[-1] == 1):
-        raise ValueError("use_sh=False needs harmonics with d_sh == 1")
-    n = gaussian_sh_coefficients.shape[-1]
-    degree = math.isqrt(n) - 1
     dev = extrinsics.device
     fov_x = torch.tensor(fov_degrees, device=dev).deg2rad()
     tan_x = (0.5 * fov_x).tan()
@@ -143,16 +135,33 @@ def render_cuda_orthographic(extrinsics: torch.Tensor, width: torch.Tensor, heig
     near = near + dist
     far = far + dist
     move_back = torch.eye(4, dtype=torch.float32, device=dev)
-    move_back[2, 3] = -dist
+    move_back[2, 3] = -dist  # as in the reference: one shared pull-back (b = 1 in practice)
     extrinsics = extrinsics @ move_back
     if dump is not None:
         dump.update(extrinsics=extrinsics, fov_x=fov_x, fov_y=fov_y, near=near, far=far)
     proj = get_projection_matrix(near, far, fov_x.expand(b), fov_y).transpose(1, 2)
     view = extrinsics.inverse().transpose(1, 2)
-    full = view @ proj
-    scene = torch.arange(b, dtype=torch.int32, device=dev)
-    cams = raster.pack_cameras(view, full, extrinsics[:, :3, 3], tan_x.expand(b), tan_y.expand(b) if tan_y.dim() == 0
-                               else tan_y, background_color, scene)
+    return {"viewmatrix": view, "projmatrix": view @ proj, "campos": extrinsics[:, :3, 3],
+            "tanfovx": tan_x.expand(b), "tanfovy": tan_y.expand(b) if tan_y.dim() == 0 else tan_y,
+            "scale": torch.ones(b, dtype=torch.float32, device=dev)}
+
+
+def render_cuda_orthographic(extrinsics: torch.Tensor, width: torch.Tensor, height: torch.Tensor,
+                             near: torch.Tensor, far: torch.Tensor, image_shape: tuple[int, int],
+                             background_color: torch.Tensor, gaussian_means: torch.Tensor,
+                             gaussian_covariances: torch.Tensor, gaussian_sh_coefficients: torch.Tensor,
+                             gaussian_opacities: torch.Tensor, fov_degrees: float = 0.1, use_sh: bool = True,
+                             dump: dict | None = None) -> torch.Tensor:
+    """cuda_splatting.py:129-219. -> [b,3,H,W]."""
+    b = extrinsics.shape[0]
+    h, w = image_shape
+    if not (use_sh or gaussian_sh_coefficients.shape[-1] == 1):
+        raise ValueError("use_sh=False needs harmonics with d_sh == 1")
+    degree = math.isqrt(gaussian_sh_coefficients.shape[-1]) - 1
+    st = orthographic_settings(extrinsics, width, height, near, far, fov_degrees, dump)
+    scene = torch.arange(b, dtype=torch.int32, device=extrinsics.device)
+    cams = raster.pack_cameras(st["viewmatrix"], st["projmatrix"], st["campos"], st["tanfovx"], st["tanfovy"],
+                               background_color, scene)
     shs = gaussian_sh_coefficients.transpose(-1, -2)
     feats = shs if use_sh else shs[:, :, 0, :]
     color, _ = raster.rasterize_views(gaussian_means, feats, gaussian_opacities, _cov6(gaussian_covariances), cams,
@@ -161,18 +170,25 @@ def render_cuda_orthographic(extrinsics: torch.Tensor, width: torch.Tensor, heig
     return color
 
 
-def render_depth_cuda(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch.Tensor, far: torch.Tensor,
-                      image_shape: tuple[int, int], gaussian_means: torch.Tensor,
-                      gaussian_covariances: torch.Tensor, gaussian_opacities: torch.Tensor,
-                      scale_invariant: bool = True, mode: DepthRenderingMode = "depth") -> torch.Tensor:
-    """Depth / disparity / log-depth as colour (cuda_splatting.py:225-264). -> [b,H,W]."""
+def depth_colors(extrinsics: torch.Tensor, gaussian_means: torch.Tensor, near: torch.Tensor, far: torch.Tensor,
+                 mode: DepthRenderingMode = "depth") -> torch.Tensor:
+    """Per-view Gaussian colour used by render_depth_cuda (cuda_splatting.py:237-246): camera-
+    space z, 1/z, or log(z.minimum(near).maximum(far)) (order as written). -> [b, g]."""
     cam_pts = torch.einsum("bij,bgj->bgi", extrinsics.inverse(), homogenize_points(gaussian_means))
     fake = cam_pts[..., 2]
     if mode == "disparity":
         fake = 1 / fake
     elif mode == "log":
-        # order as written in the reference (:246): minimum(near) then maximum(far)
         fake = fake.minimum(near[:, None]).maximum(far[:, None]).log()
+    return fake
+
+
+def render_depth_cuda(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch.Tensor, far: torch.Tensor,
+                      image_shape: tuple[int, int], gaussian_means: torch.Tensor,
+                      gaussian_covariances: torch.Tensor, gaussian_opacities: torch.Tensor,
+                      scale_invariant: bool = True, mode: DepthRenderingMode = "depth") -> torch.Tensor:
+    """Depth / disparity / log-depth as colour (cuda_splatting.py:225-264). -> [b,H,W]."""
+    fake = depth_colors(extrinsics, gaussian_means, near, far, mode)
     b = fake.shape[0]
     out = render_cuda(extrinsics, intrinsics, near, far, image_shape,
                       torch.zeros((b, 3), dtype=fake.dtype, device=fake.device), gaussian_means,

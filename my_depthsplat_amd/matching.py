@@ -1,0 +1,174 @@
+"""Plane-sweep cost volume on MI355X: drop-in for the cost-volume block of
+src/model/encoder/unimatch/ (SURVEY.md §8a rows A17-A20).
+
+  coords_grid                        matching.py:5-21
+  warp_with_pose_depth_candidates    matching.py:24-90 (same signature; HIP dcv_warp_fwd/bwd)
+  batch_features_camera_parameters   mv_transformer.py:653-747
+  depth_candidates                   mv_unimatch.py:416-475
+  plane_sweep_cost_volume            NEW fused op = warp + correlation (mv_unimatch.py:484-505)
+                                     without materialising [B, C, D, H, W] (HIP dcv_cost_volume_*)
+"""
+from __future__ import annotations
+
+import torch
+from einops import repeat
+
+from . import _lib
+
+
+def coords_grid(b, h, w, homogeneous=False, device=None):
+    """[b, 2 or 3, h, w] integer pixel coordinates (x, y[, 1]) (matching.py:5-21)."""
+    ys, xs = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+    parts = [xs, ys] + ([torch.ones_like(xs)] if homogeneous else [])
+    g = torch.stack(parts, dim=0).float()[None].repeat(b, 1, 1, 1)
+    return g if device is None else g.to(device)
+
+
+def _f(t):
+    return t.contiguous().float()
+
+
+class _Warp(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feature, intrinsics, pose, depth, clamp):
+        lib = _lib.load()
+        B, C, H, W = feature.shape
+        D = depth.shape[1]
+        out = torch.empty((B, C, D, H, W), dtype=torch.float32, device=feature.device)
+        _lib.check(lib.dcv_warp_fwd(B, C, H, W, D, feature.data_ptr(), intrinsics.data_ptr(), pose.data_ptr(),
+                                    depth.data_ptr(), clamp, out.data_ptr(), _lib.stream_of(feature.device)),
+                   "dcv_warp_fwd")
+        ctx.save_for_backward(intrinsics, pose, depth)
+        ctx.meta = (B, C, H, W, D, clamp)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        intrinsics, pose, depth = ctx.saved_tensors
+        B, C, H, W, D, clamp = ctx.meta
+        dout = _f(dout)
+        dfeat = torch.empty((B, C, H, W), dtype=torch.float32, device=dout.device)
+        _lib.check(_lib.load().dcv_warp_bwd(B, C, H, W, D, dout.data_ptr(), intrinsics.data_ptr(), pose.data_ptr(),
+                                            depth.data_ptr(), clamp, dfeat.data_ptr(), _lib.stream_of(dout.device)),
+                   "dcv_warp_bwd")
+        return dfeat, None, None, None, None
+
+
+def warp_with_pose_depth_candidates(feature1, intrinsics, pose, depth, clamp_min_depth=1e-3,
+                                    grid_sample_disable_cudnn=False):
+    """feature1 [B,C,H,W], intrinsics [B,3,3], pose [B,4,4], depth [B,D,H,W] -> [B,C,D,H,W]
+    (matching.py:24-90). Geometry gets no gradient; feature1 does."""
+    if not (intrinsics.size(1) == intrinsics.size(2) == 3):
+        raise ValueError("intrinsics must be [B, 3, 3]")
+    if not (pose.size(1) == pose.size(2) == 4):
+        raise ValueError("pose must be [B, 4, 4]")
+    if depth.dim() != 4:
+        raise ValueError("depth must be [B, D, H, W]")
+    _lib.require_gpu(feature1, intrinsics, pose, depth)
+    return _Warp.apply(_f(feature1), _f(intrinsics).detach(), _f(pose).detach(), _f(depth).detach(),
+                       float(clamp_min_depth))
+
+
+class _CostVolume(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ref, tgt, intrinsics, pose, depth, per_pixel, clamp):
+        lib = _lib.load()
+        B, J, C, H, W = tgt.shape
+        D = depth.shape[1]
+        dev = ref.device
+        st = _lib.stream_of(dev)
+        tgt_hwc = torch.empty((B, J, H, W, C), dtype=torch.float32, device=dev)
+        cost = torch.empty((B, D, H, W), dtype=torch.float32, device=dev)
+        _lib.check(lib.dcv_cost_volume_fwd(B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), tgt.data_ptr(),
+                                           intrinsics.data_ptr(), pose.data_ptr(), depth.data_ptr(), clamp,
+                                           tgt_hwc.data_ptr(), cost.data_ptr(), st), "dcv_cost_volume_fwd")
+        ctx.save_for_backward(ref, tgt_hwc, intrinsics, pose, depth)
+        ctx.meta = (B, J, C, H, W, D, per_pixel, clamp)
+        return cost
+
+    @staticmethod
+    def backward(ctx, dcost):
+        ref, tgt_hwc, intrinsics, pose, depth = ctx.saved_tensors
+        B, J, C, H, W, D, per_pixel, clamp = ctx.meta
+        dev = ref.device
+        dcost = _f(dcost)
+        dref = torch.empty_like(ref)
+        dtgt = torch.empty((B, J, C, H, W), dtype=torch.float32, device=dev)
+        scratch = torch.empty((B, J, H, W, C), dtype=torch.float32, device=dev)
+        _lib.check(_lib.load().dcv_cost_volume_bwd(
+            B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), tgt_hwc.data_ptr(), intrinsics.data_ptr(),
+            pose.data_ptr(), depth.data_ptr(), clamp, dcost.data_ptr(), dref.data_ptr(), dtgt.data_ptr(),
+            scratch.data_ptr(), _lib.stream_of(dev)), "dcv_cost_volume_bwd")
+        return dref, dtgt, None, None, None, None, None
+
+
+def plane_sweep_cost_volume(ref: torch.Tensor, tgt: torch.Tensor, intrinsics: torch.Tensor, pose: torch.Tensor,
+                            depth: torch.Tensor, clamp_min_depth: float = 1e-3) -> torch.Tensor:
+    """Fused warp + correlation (mv_unimatch.py:484-505):
+    cost[b,d,y,x] = mean_j( sum_c ref[b,c,y,x] * warp(tgt[b,j])[c,d,y,x] ) / sqrt(C).
+    ref [B,C,H,W]; tgt [B,J,C,H,W]; intrinsics [B,3,3] or [B,J,3,3] (pixel units at this
+    scale, the reference uses the ref-view K for every source view); pose [B,J,4,4]
+    (= tgt_c2w^-1 ref_c2w); depth [B,D] (per-image candidates, scale 0) or [B,D,H,W]
+    (per-pixel candidates, scale > 0) -- DEPTH values, not inverse depth. -> [B,D,H,W]."""
+    B, J, C, H, W = tgt.shape
+    if ref.shape != (B, C, H, W):
+        raise ValueError(f"ref {tuple(ref.shape)} does not match tgt {tuple(tgt.shape)}")
+    if intrinsics.dim() == 3:
+        intrinsics = intrinsics[:, None].expand(B, J, 3, 3)
+    if depth.dim() not in (2, 4):
+        raise ValueError("depth must be [B, D] or [B, D, H, W]")
+    _lib.require_gpu(ref, tgt, intrinsics, pose, depth)
+    per_pixel = depth.dim() == 4
+    return _CostVolume.apply(_f(ref), _f(tgt), _f(intrinsics).detach(), _f(pose).detach(), _f(depth).detach(),
+                             per_pixel, float(clamp_min_depth))
+
+
+def batch_features_camera_parameters(features, intrinsics, extrinsics, nn_matrix=None, no_batch=False):
+    """Reference view + its source views for every view (mv_transformer.py:653-747).
+    features/intrinsics/extrinsics: lists over views of [B,C,H,W] / [B,3,3] / [B,4,4].
+    Returns ref [BV,C,H,W], ref K, ref c2w, tgt [BV,V-1,C,H,W], tgt K, tgt c2w."""
+    V = len(features)
+    if nn_matrix is not None:
+        F_ = torch.stack(features, 1)
+        K_ = torch.stack(intrinsics, 1)
+        E_ = torch.stack(extrinsics, 1)
+        n_sel = nn_matrix.size(-1) - 1
+    else:
+        n_sel = V - 1
+    q, qk, qe, kv, kvk, kve = [], [], [], [], [], []
+    for i in range(V):
+        q.append(features[i])
+        qk.append(intrinsics[i])
+        qe.append(extrinsics[i])
+        if nn_matrix is not None:
+            sel = nn_matrix[:, i, 1:]
+            c, h, w = F_.shape[-3:]
+            kv.append(torch.gather(F_, 1, repeat(sel, "b v -> b v c h w", c=c, h=h, w=w)))
+            kvk.append(torch.gather(K_, 1, repeat(sel, "b v -> b v i j", i=3, j=3)))
+            kve.append(torch.gather(E_, 1, repeat(sel, "b v -> b v i j", i=4, j=4)))
+        else:
+            others = [j for j in range(V) if j != i]
+            kv.append(torch.stack([features[j] for j in others], 1))
+            kvk.append(torch.stack([intrinsics[j] for j in others], 1))
+            kve.append(torch.stack([extrinsics[j] for j in others], 1))
+    if no_batch:
+        return q, qk, qe, kv, kvk, kve
+    c, h, w = q[0].shape[1:]
+    return (torch.stack(q, 1).reshape(-1, c, h, w), torch.stack(qk, 1).reshape(-1, 3, 3),
+            torch.stack(qe, 1).reshape(-1, 4, 4), torch.stack(kv, 1).reshape(-1, n_sel, c, h, w),
+            torch.stack(kvk, 1).reshape(-1, n_sel, 3, 3), torch.stack(kve, 1).reshape(-1, n_sel, 4, 4))
+
+
+def depth_candidates(min_depth: torch.Tensor, max_depth: torch.Tensor, num_candidates: int, scale_idx: int = 0,
+                     depth: torch.Tensor | None = None) -> torch.Tensor:
+    """Inverse-depth hypotheses (mv_unimatch.py:416-461). min/max_depth are INVERSE depths [BV].
+    scale 0: [BV, D, 1, 1] linspace per image; scale s > 0: [BV, D/4^s, H, W] per-pixel window
+    around the (inverse) `depth` [BV, 1, H, W] of the previous scale, clamped to [min, max]."""
+    D = num_candidates // (4 ** scale_idx)
+    lin = torch.linspace(0, 1, D, dtype=min_depth.dtype, device=min_depth.device).view(1, D, 1, 1)
+    if scale_idx == 0:
+        return min_depth.view(-1, 1, 1, 1) + lin * (max_depth - min_depth).view(-1, 1, 1, 1)
+    interval = ((max_depth - min_depth) / (num_candidates - 1) / (2 ** scale_idx)).view(-1, 1, 1, 1)
+    lo = (depth - interval * (D // 2)).clamp(min=min_depth.view(-1, 1, 1, 1))
+    hi = (depth + interval * (D // 2 - 1)).clamp(max=max_depth.view(-1, 1, 1, 1))
+    return lo + lin * (hi - lo)

@@ -52,6 +52,65 @@ def pack_cameras(viewmatrix: torch.Tensor, projmatrix: torch.Tensor, campos: tor
     return cam
 
 
+class KernelTimer:
+    """HIP-event timing of each C-ABI launch on the stream it is enqueued on (bench.py)."""
+
+    def __init__(self):
+        self.events: dict[str, list] = {}
+
+    def start(self, name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return name, e
+
+    def stop(self, tok):
+        name, e0 = tok
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.events.setdefault(name, []).append((e0, e1))
+
+    def summary(self) -> dict[str, tuple[int, float]]:
+        torch.cuda.synchronize()
+        return {k: (len(v), sum(a.elapsed_time(b) for a, b in v) / len(v)) for k, v in self.events.items()}
+
+
+_timer: KernelTimer | None = None
+_last = {"num_rendered": 0, "max_count": 0}
+
+
+def set_timer(t: KernelTimer | None) -> None:
+    global _timer
+    _timer = t
+
+
+def last_stats() -> dict:
+    return dict(_last)
+
+
+def _timed(name, fn, *args):
+    tok = _timer.start(name) if _timer is not None else None
+    r = fn(*args)
+    if tok is not None:
+        _timer.stop(tok)
+    return r
+
+
+def algorithmic_bytes(kernel: str, *, G: int, V: int, N: int, HW: int, T: int | None = None) -> int:
+    """Minimum HBM bytes one launch must move. G Gaussians per scene, V views,
+    N (view, tile, Gaussian) entries, HW pixels per view."""
+    if kernel == "k_preprocess":   # 148 B of Gaussian params in, 48 B record + 4 B radius out
+        return V * G * (148 + 52)
+    if kernel == "k_scan":
+        return 8 * V * (T or 0)
+    if kernel == "k_scatter":      # xy, depth, radius in; one 8-B key out per entry
+        return V * G * 16 + 8 * N
+    if kernel == "k_sort":         # keys in + out
+        return 16 * N
+    if kernel == "k_render_fwd":   # key + 36-B record per entry; RGB + T + n_contrib out
+        return 44 * N + 20 * V * HW
+    raise KeyError(kernel)
+
+
 @dataclass
 class RasterState:
     """Everything the backward needs (all device tensors)."""
@@ -79,7 +138,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W)
     geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
     radii = torch.empty((V, G), dtype=torch.int32, device=dev)
     seg_count = torch.empty(V * T, dtype=torch.int32, device=dev)
-    _lib.check(lib.dsr_preprocess_fwd(
+    _lib.check(_timed("k_preprocess", lib.dsr_preprocess_fwd,
         S, G, V, H, W, sh_degree if use_sh else -1, M, means.data_ptr(),
         feats.data_ptr() if use_sh else None, None if use_sh else feats.data_ptr(),
         opacities.data_ptr(), cov6.data_ptr(), cams.data_ptr(), geom.data_ptr(), radii.data_ptr(),
@@ -87,24 +146,25 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W)
     seg_start = torch.empty(V * T + 1, dtype=torch.int32, device=dev)
     cursor = torch.empty(V * T, dtype=torch.int32, device=dev)
     totals = torch.empty(4, dtype=torch.int32, device=dev)
-    _lib.check(lib.dsr_bin_scan(V, H, W, seg_count.data_ptr(), seg_start.data_ptr(), cursor.data_ptr(),
+    _lib.check(_timed("k_scan", lib.dsr_bin_scan, V, H, W, seg_count.data_ptr(), seg_start.data_ptr(), cursor.data_ptr(),
                                 totals.data_ptr(), st), "dsr_bin_scan")
     tot = totals[:2].cpu()  # the one host sync: sizes the key buffer
     N, maxc = int(tot[0]), int(tot[1])
     keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
     if N > 0:
-        _lib.check(lib.dsr_bin_scatter(G, V, H, W, geom.data_ptr(), cursor.data_ptr(), keys.data_ptr(), st),
+        _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(), keys.data_ptr(), st),
                    "dsr_bin_scatter")
         cap = lib.dsr_sort_lds_capacity()
         scratch = torch.empty(N, dtype=torch.int64, device=dev) if maxc > cap else None
-        _lib.check(lib.dsr_bin_sort(G, V, H, W, seg_start.data_ptr(), keys.data_ptr(),
+        _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), keys.data_ptr(),
                                     None if scratch is None else scratch.data_ptr(), maxc, st), "dsr_bin_sort")
     color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
-    _lib.check(lib.dsr_render_fwd(G, V, H, W, cams.data_ptr(), geom.data_ptr(), seg_start.data_ptr(),
+    _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(), seg_start.data_ptr(),
                                   keys.data_ptr(), color.data_ptr(), final_T.data_ptr(), n_contrib.data_ptr(), st),
                "dsr_render_fwd")
+    _last["num_rendered"], _last["max_count"] = N, maxc
     return color, RasterState(geom, radii, seg_start, keys, final_T, n_contrib, N, maxc)
 
 
