@@ -58,6 +58,15 @@ typedef struct dsr_camera {
  *   [6..8] rgb                   [9] view-space depth     [10] radius (int32 bits)
  *   [11] SH clamp mask (uint32 bits 0..2). radius == 0 <=> culled / not rendered. */
 
+/* Build the camera array on the device from the reference's render_cuda inputs
+ * (cuda_splatting.py:62-86 + projection.py:233-247 get_fov + :16-43 projection matrix):
+ *   extrinsics [V,4,4] c2w, intrinsics [V,3,3] normalised, near/far [V], bg [V,3],
+ *   view_scene [V] int32; scale_invariant != 0 applies the 1/near rescale.
+ * Computed in double per view (torch does it in float32: agreement ~1e-7 relative). */
+int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, const float* near,
+                      const float* far, const float* bg, const int32_t* view_scene,
+                      int scale_invariant, dsr_camera* cams, void* stream);
+
 /* ---- rasterizer forward ------------------------------------------------------------
  * Replaces preprocessCUDA + tiles_touched (upstream K1). Per view v and gaussian g of
  * scene cams[v].scene: cull, EWA projection, conic, radius, SH->RGB (or colors), and
@@ -82,9 +91,10 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
                     uint64_t* keys, void* stream);
 
 /* Sort every segment by (depth, id) ascending — identical to upstream's stable radix
- * sort of (tile << 32 | depth) with emission-order ties (K4/K5). Segments up to
- * dsr_sort_lds_capacity() entries sort in LDS; larger ones use `scratch` (N entries,
- * may be NULL when max_count <= capacity). id_bits = bits needed for G-1. */
+ * sort of (tile << 32 | depth) with emission-order ties (K4/K5). max_count sizes the LDS
+ * sort (0 = unknown): segments that fit sort in LDS, larger ones sort through HBM using
+ * `scratch` (same size as keys). scratch may be NULL only when max_count is an exact
+ * bound <= dsr_sort_lds_capacity(). */
 int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, uint64_t* keys,
                  uint64_t* scratch, uint32_t max_count, void* stream);
 uint32_t dsr_sort_lds_capacity(void);

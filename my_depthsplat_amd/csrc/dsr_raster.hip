@@ -405,9 +405,73 @@ __device__ bool radix_pass(const uint64_t* src, uint64_t* dst, uint32_t n, int s
   return true;
 }
 
+// Sort one segment by its 64-bit (depth << 32 | id) keys. Common case: 4 stable LSD
+// passes over the depth bits only, then a tie check; pairs of equal depth (rare: random
+// float depths) are put in id order by an insertion sort of each short run; segments with
+// many ties (e.g. fronto-parallel planes) redo the full id-then-depth LSD (7 passes).
+// Either way the result is the unique ascending order of the keys.
+template <int NTH>
+__device__ void sort_segment(uint64_t* A, uint64_t* B, uint32_t n, int id_bits, uint32_t* hist, uint32_t* wsum,
+                             uint32_t* flag, uint64_t* home) {
+  uint64_t* src = A;
+  uint64_t* dst = B;
+  for (int sh = 32; sh < 64; sh += 8)
+    if (radix_pass<NTH>(src, dst, n, sh, hist, wsum, flag)) {
+      uint64_t* t = src;
+      src = dst;
+      dst = t;
+    }
+  // tie check (flag reused as a counter)
+  if (threadIdx.x == 0) *flag = 0;
+  __syncthreads();
+  uint32_t ties = 0;
+  for (uint32_t i = threadIdx.x; i + 1 < n; i += NTH) ties += (uint32_t)((src[i] >> 32) == (src[i + 1] >> 32));
+  if (ties) atomicAdd(flag, ties);
+  __syncthreads();
+  ties = *flag;
+  __syncthreads();
+  if (ties != 0 && ties <= 32) {
+    // one thread per run of equal depth: insertion sort by the full key (= by id)
+    for (uint32_t i = threadIdx.x; i + 1 < n; i += NTH) {
+      const uint64_t d = src[i] >> 32;
+      if ((src[i + 1] >> 32) != d || (i > 0 && (src[i - 1] >> 32) == d)) continue;
+      uint32_t e = i + 1;
+      while (e < n && (src[e] >> 32) == d) ++e;
+      for (uint32_t k = i + 1; k < e; ++k) {
+        const uint64_t x = src[k];
+        uint32_t m = k;
+        while (m > i && src[m - 1] > x) {
+          src[m] = src[m - 1];
+          --m;
+        }
+        src[m] = x;
+      }
+    }
+    __syncthreads();
+  } else if (ties > 32) {
+    for (int sh = 0; sh < id_bits; sh += 8)
+      if (radix_pass<NTH>(src, dst, n, sh, hist, wsum, flag)) {
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+      }
+    for (int sh = 32; sh < 64; sh += 8)
+      if (radix_pass<NTH>(src, dst, n, sh, hist, wsum, flag)) {
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+      }
+  }
+  if (src != home)
+    for (uint32_t i = threadIdx.x; i < n; i += NTH) home[i] = src[i];
+}
+
+// One workgroup per (view, tile) segment. n <= cap: sort in LDS. n > cap: when big_here,
+// sort through HBM (keys <-> scratch) with the same 4 waves; otherwise leave it to
+// k_sort_global.
 __global__ __launch_bounds__(NT) void k_sort_lds(const uint32_t* __restrict__ seg_start,
-                                                 uint64_t* __restrict__ keys, int id_bits,
-                                                 uint32_t cap) {
+                                                 uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
+                                                 int id_bits, uint32_t cap, int big_here) {
   extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
   uint64_t* A = s_keys;
   uint64_t* B = s_keys + cap;
@@ -417,24 +481,16 @@ __global__ __launch_bounds__(NT) void k_sort_lds(const uint32_t* __restrict__ se
   const int seg = blockIdx.x;
   const uint32_t b = seg_start[seg];
   const uint32_t n = seg_start[seg + 1] - b;
-  if (n <= 1 || n > cap) return;
+  if (n <= 1) return;
+  if (n > cap) {
+    if (big_here) sort_segment<NT>(keys + b, scratch + b, n, id_bits, hist, wsum, flag, keys + b);
+    return;
+  }
   for (uint32_t i = threadIdx.x; i < n; i += NT) A[i] = keys[b + i];
   __syncthreads();
-  uint64_t* src = A;
-  uint64_t* dst = B;
-  for (int sh = 0; sh < id_bits; sh += 8)
-    if (radix_pass<NT>(src, dst, n, sh, hist, wsum, flag)) {
-      uint64_t* t = src;
-      src = dst;
-      dst = t;
-    }
-  for (int sh = 32; sh < 64; sh += 8)
-    if (radix_pass<NT>(src, dst, n, sh, hist, wsum, flag)) {
-      uint64_t* t = src;
-      src = dst;
-      dst = t;
-    }
-  for (uint32_t i = threadIdx.x; i < n; i += NT) keys[b + i] = src[i];
+  sort_segment<NT>(A, B, n, id_bits, hist, wsum, flag, A);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += NT) keys[b + i] = A[i];
 }
 
 // Segments larger than the LDS capacity: same passes through HBM, 16 waves.
@@ -449,26 +505,44 @@ __global__ __launch_bounds__(1024) void k_sort_global(const uint32_t* __restrict
   const uint32_t b = seg_start[seg];
   const uint32_t n = seg_start[seg + 1] - b;
   if (n <= cap) return;
-  uint64_t* src = keys + b;
-  uint64_t* dst = scratch + b;
-  for (int sh = 0; sh < id_bits; sh += 8)
-    if (radix_pass<1024>(src, dst, n, sh, hist, wsum, &flag)) {
-      uint64_t* t = src;
-      src = dst;
-      dst = t;
-    }
-  for (int sh = 32; sh < 64; sh += 8)
-    if (radix_pass<1024>(src, dst, n, sh, hist, wsum, &flag)) {
-      uint64_t* t = src;
-      src = dst;
-      dst = t;
-    }
-  if (src != keys + b)
-    for (uint32_t i = threadIdx.x; i < n; i += 1024) keys[b + i] = src[i];
+  sort_segment<1024>(keys + b, scratch + b, n, id_bits, hist, wsum, &flag, keys + b);
 }
 
 // ------------------------------------------------------------------------------------
-// K6: front-to-back compositing. grid = (gx, gy, V), block = 16x16 (4 waves).
+// K6/K7 shared structure. A 16x16 tile = 4 waves; wave w owns the 8x8 sub-tile
+// (w & 1, w >> 1), lane l its pixel (l & 7, l >> 3). The workgroup stages 256 list
+// entries at a time in LDS (one coalesced key + record read per entry); every entry gets a
+// 4-bit mask of the sub-tiles its alpha >= 1/255 ellipse can reach (conservative bounding
+// box of {d : d^T Q d <= 2 ln(255 o)}, Q = conic), and each wave composites only the entries
+// of its mask, in list order. Culled entries would have been skipped by the per-pixel test
+// (power > 0 or alpha < 1/255) for every pixel of that sub-tile, so outputs are those of the
+// uncull loop; positions in the list are kept so n_contrib keeps its meaning.
+constexpr int SUB = 8;
+
+__device__ __forceinline__ float gauss_weight(float power) { return __expf(power); }
+
+__device__ __forceinline__ uint32_t subtile_mask(float4 q, float4 r, int tx0, int ty0) {
+  // q = (x, y, conic a, conic b), r = (conic c, opacity, ...); tile origin (tx0, ty0)
+  const float op = r.y;
+  if (!(op >= 1.0f / 255.0f)) return 0u;  // alpha = min(.99, o G) <= o < 1/255 everywhere
+  const float t2 = 2.0f * __logf(255.0f * op);
+  const float det = q.z * r.x - q.w * q.w;
+  // half extents of the ellipse's bounding box, padded against rounding
+  const float hx = sqrtf(fmaxf(t2 * r.x / det, 0.f)) * 1.002f + 0.05f;
+  const float hy = sqrtf(fmaxf(t2 * q.z / det, 0.f)) * 1.002f + 0.05f;
+  uint32_t m = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const float x0 = (float)(tx0 + (w & 1) * SUB), y0 = (float)(ty0 + (w >> 1) * SUB);
+    const bool out = (q.x + hx < x0) || (q.x - hx > x0 + (SUB - 1)) || (q.y + hy < y0) || (q.y - hy > y0 + (SUB - 1));
+    m |= (out ? 0u : 1u) << w;
+  }
+  // NaN / degenerate conic: keep (never cull what cannot be proven irrelevant)
+  if (!(det > 0.f) || !(hx == hx) || !(hy == hy)) m = 0xFu;
+  return m;
+}
+
+// K6: front-to-back compositing. grid = (gx, gy, V), block = 256 (4 waves x 8x8 pixels).
 __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, int T,
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
@@ -476,41 +550,58 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
                                                    const uint64_t* __restrict__ keys,
                                                    float* __restrict__ out, float* __restrict__ finalT,
                                                    uint32_t* __restrict__ ncontrib) {
-  __shared__ float4 s_q[NT];   // x, y, conic a, conic b
-  __shared__ float4 s_r[NT];   // conic c, opacity, r, g
-  __shared__ float s_bl[NT];   // b
+  __shared__ float4 s_q[NT];       // x, y, conic a, conic b
+  __shared__ float4 s_r[NT];       // conic c, opacity, r, g
+  __shared__ float s_bl[NT];       // b
+  __shared__ uint32_t s_mask[NT];  // sub-tile mask per staged entry
+  __shared__ uint16_t s_list[4][NT];
   const int v = blockIdx.z;
-  const int tid = threadIdx.x;
-  const int px = blockIdx.x * BX + (tid & (BX - 1));
-  const int py = blockIdx.y * BY + (tid / BX);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int tx0 = blockIdx.x * BX, ty0 = blockIdx.y * BY;
+  const int px = tx0 + (w & 1) * SUB + (lane & (SUB - 1));
+  const int py = ty0 + (w >> 1) * SUB + (lane >> 3);
   const bool inside = px < W && py < H;
   const int seg = v * T + blockIdx.y * gx + blockIdx.x;
   const uint32_t start = seg_start[seg], end = seg_start[seg + 1];
   const float pfx = (float)px, pfy = (float)py;
   const float* gv = geom + (size_t)v * G * GS;
+  const uint64_t lt = dsplat::lanemask_lt(lane);
   bool done = !inside;
   float Tr = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
-  uint32_t contributor = 0, last = 0;
+  uint32_t last = 0;
   for (uint32_t base = start; base < end; base += NT) {
     if (__syncthreads_count(done) == NT) break;
     const uint32_t i = base + tid;
+    uint32_t m = 0;
     if (i < end) {
       const uint32_t id = (uint32_t)keys[i];
       const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
-      s_q[tid] = rec[0];
-      s_r[tid] = rec[1];
+      const float4 q = rec[0], r = rec[1];
+      s_q[tid] = q;
+      s_r[tid] = r;
       s_bl[tid] = rec[2].x;
+      m = subtile_mask(q, r, tx0, ty0);
     }
+    s_mask[tid] = m;
     __syncthreads();
-    const int cnt = (int)min((uint32_t)NT, end - base);
-    for (int j = 0; j < cnt && !done; ++j) {
-      contributor++;
+    // this wave's entries, in list order (4 chunks of 64, ballot compaction)
+    int cnt = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bool mine = (s_mask[c * 64 + lane] >> w) & 1u;
+      const uint64_t bal = __ballot(mine);
+      if (mine) s_list[w][cnt + __popcll(bal & lt)] = (uint16_t)(c * 64 + lane);
+      cnt += __popcll(bal);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int k = 0; k < cnt && !done; ++k) {
+      const int j = s_list[w][k];
       const float4 q = s_q[j];
       const float4 r = s_r[j];
       const float dx = q.x - pfx, dy = q.y - pfy;
       const float power = -0.5f * (q.z * dx * dx + r.x * dy * dy) - q.w * dx * dy;
       if (power > 0.0f) continue;
-      const float alpha = fminf(0.99f, r.y * expf(power));
+      const float alpha = fminf(0.99f, r.y * gauss_weight(power));
       if (alpha < 1.0f / 255.0f) continue;
       const float testT = Tr * (1 - alpha);
       if (testT < 0.0001f) {
@@ -521,7 +612,7 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
       C1 += r.w * alpha * Tr;
       C2 += s_bl[j] * alpha * Tr;
       Tr = testT;
-      last = contributor;
+      last = base - start + (uint32_t)j + 1u;
     }
   }
   if (inside) {
@@ -537,9 +628,10 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
 }
 
 // ------------------------------------------------------------------------------------
-// K7: back-to-front gradient of the compositing. Per Gaussian of the tile list, the 256
-// pixel contributions are summed across each wave (shuffles) and the 4 waves (LDS float
-// atomics), then flushed with one global atomic per (Gaussian, component) per tile.
+// K7: back-to-front gradient of the compositing (same 4 x 8x8 sub-tile culling). Per
+// entry, the 64 pixel contributions of a wave are summed with shuffles, the 4 waves
+// combine through LDS float atomics, and each staged batch is flushed with one global
+// atomic per (Gaussian, component) per tile instead of one per pixel.
 __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, int T,
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
@@ -553,12 +645,15 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
   __shared__ float4 s_r[NT];
   __shared__ float s_bl[NT];
   __shared__ uint32_t s_id[NT];
+  __shared__ uint32_t s_mask[NT];
+  __shared__ uint16_t s_list[4][NT];
   __shared__ float s_acc[NT * 9];
   __shared__ uint32_t s_max;
   const int v = blockIdx.z;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int px = blockIdx.x * BX + (tid & (BX - 1));
-  const int py = blockIdx.y * BY + (tid / BX);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int tx0 = blockIdx.x * BX, ty0 = blockIdx.y * BY;
+  const int px = tx0 + (w & 1) * SUB + (lane & (SUB - 1));
+  const int py = ty0 + (w >> 1) * SUB + (lane >> 3);
   const bool inside = px < W && py < H;
   const int seg = v * T + blockIdx.y * gx + blockIdx.x;
   const uint32_t start = seg_start[seg], end = seg_start[seg + 1];
@@ -568,6 +663,7 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
   const float* gv = geom + (size_t)v * G * GS;
   float* dgv = dgeom + (size_t)v * G * GS;
   const float* bg = cams[v].bg;
+  const uint64_t lt = dsplat::lanemask_lt(lane);
   const float Tfin = inside ? finalT[v * HW + pix] : 0.f;
   const uint32_t lastc = inside ? ncontrib[v * HW + pix] : 0u;
   float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
@@ -589,17 +685,31 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
   for (int hi = (int)nproc; hi > 0; hi -= NT) {
     const int lo = max(0, hi - NT);
     const int cnt = hi - lo;
+    uint32_t m = 0;
     if (tid < cnt) {
       const uint32_t id = (uint32_t)keys[start + lo + tid];
       const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
-      s_q[tid] = rec[0];
-      s_r[tid] = rec[1];
+      const float4 q = rec[0], r = rec[1];
+      s_q[tid] = q;
+      s_r[tid] = r;
       s_bl[tid] = rec[2].x;
       s_id[tid] = id;
+      m = subtile_mask(q, r, tx0, ty0);
     }
+    s_mask[tid] = m;
     for (int k = tid; k < cnt * 9; k += NT) s_acc[k] = 0.f;
     __syncthreads();
-    for (int j = cnt - 1; j >= 0; --j) {
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bool mine = (s_mask[c * 64 + lane] >> w) & 1u;
+      const uint64_t bal = __ballot(mine);
+      if (mine) s_list[w][n + __popcll(bal & lt)] = (uint16_t)(c * 64 + lane);
+      n += __popcll(bal);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int k = n - 1; k >= 0; --k) {
+      const int j = s_list[w][k];
       const uint32_t pos = (uint32_t)(lo + j);
       float g[9];
 #pragma unroll
@@ -611,7 +721,7 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
         const float dx = q.x - pfx, dy = q.y - pfy;
         const float power = -0.5f * (q.z * dx * dx + r.x * dy * dy) - q.w * dx * dy;
         if (power <= 0.0f) {
-          const float Gs = expf(power);
+          const float Gs = gauss_weight(power);
           const float alpha = fminf(0.99f, r.y * Gs);
           if (alpha >= 1.0f / 255.0f) {
             act = true;
@@ -649,8 +759,8 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
       if (__ballot(act) != 0ull) {
 #pragma unroll
         for (int c = 0; c < 9; ++c) {
-          const float s = dsplat::wave_sum(g[c]);
-          if (lane == 0) atomicAdd(&s_acc[j * 9 + c], s);
+          const float sum = dsplat::wave_sum(g[c]);
+          if (lane == 0) atomicAdd(&s_acc[j * 9 + c], sum);
         }
       }
     }
@@ -932,17 +1042,17 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
 int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, uint64_t* keys, uint64_t* scratch,
                  uint32_t max_count, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_sort: bad sizes");
-  DSPLAT_REQUIRE(seg_start != nullptr, "dsr_bin_sort: null seg_start");
-  if (max_count <= 1) return 0;
-  DSPLAT_REQUIRE(keys != nullptr, "dsr_bin_sort: null keys");
-  DSPLAT_REQUIRE(max_count <= kSortCap || scratch != nullptr,
-                 "dsr_bin_sort: max_count=%u exceeds LDS capacity %u and no scratch given", max_count, kSortCap);
+  DSPLAT_REQUIRE(seg_start != nullptr && keys != nullptr, "dsr_bin_sort: null pointer");
+  DSPLAT_REQUIRE(scratch != nullptr || (max_count > 0 && max_count <= kSortCap),
+                 "dsr_bin_sort: without scratch, max_count (%u) must bound every segment and be <= %u", max_count,
+                 kSortCap);
   hipStream_t st = (hipStream_t)stream;
   const int nseg = V * dsplat::tiles_x(W) * dsplat::tiles_y(H);
   int id_bits = 0;
   while (id_bits < 32 && ((uint64_t)1 << id_bits) < (uint64_t)G) ++id_bits;
+  const uint32_t want = max_count ? max_count : kSortCap;
   uint32_t cap = 256;
-  while (cap < max_count && cap < kSortCap) cap <<= 1;
+  while (cap < want && cap < kSortCap) cap <<= 1;
   const size_t lds = (size_t)cap * 16 + (4 * 256 + 8) * 4;
   static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted into once
   if (!attr_set) {
@@ -953,9 +1063,12 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, uint64_t
       return e;
     attr_set = true;
   }
-  k_sort_lds<<<nseg, NT, lds, st>>>(seg_start, keys, id_bits, cap);
+  // segments above cap: in this launch through HBM unless they are known to be large
+  // (max_count > kSortCap), in which case the 16-wave k_sort_global takes them
+  const bool big_known = scratch != nullptr && max_count > kSortCap;
+  k_sort_lds<<<nseg, NT, lds, st>>>(seg_start, keys, scratch, id_bits, cap, scratch != nullptr && !big_known);
   if (int e = dsplat::check_launch("k_sort_lds")) return e;
-  if (max_count > cap) {
+  if (big_known) {
     k_sort_global<<<nseg, 1024, 0, st>>>(seg_start, keys, scratch, id_bits, cap);
     if (int e = dsplat::check_launch("k_sort_global")) return e;
   }
@@ -1016,3 +1129,121 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
 }
 
 }  // extern "C"
+
+// =====================================================================================
+// Camera set-up on the device: replaces ~40 small torch ops per render call
+// (scale-invariant rescale, get_fov, get_projection_matrix, inverse/transposes;
+// cuda_splatting.py:62-86, projection.py:233-247). One thread per view, double internally.
+// =====================================================================================
+namespace {
+
+__device__ void inv4(const double* m, double* o) {  // row-major 4x4 inverse (cofactors)
+  double inv[16];
+  inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+  inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+  inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+  inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+  inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+  inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+  inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+  inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+  inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+  inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+  inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+  inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+  inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+  inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+  inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+  inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+  const double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
+  for (int i = 0; i < 16; ++i) o[i] = inv[i] / det;
+}
+
+__device__ void inv3(const double* k, double* o) {
+  const double a = k[0], b = k[1], c = k[2], d = k[3], e = k[4], f = k[5], g = k[6], h = k[7], i = k[8];
+  const double A = e * i - f * h, B = -(d * i - f * g), C = d * h - e * g;
+  const double det = a * A + b * B + c * C;
+  o[0] = A / det; o[1] = -(b * i - c * h) / det; o[2] = (b * f - c * e) / det;
+  o[3] = B / det; o[4] = (a * i - c * g) / det; o[5] = -(a * f - c * d) / det;
+  o[6] = C / det; o[7] = -(a * h - b * g) / det; o[8] = (a * e - b * d) / det;
+}
+
+__device__ double edge_angle(const double* ki, double x0, double y0, double x1, double y1) {
+  double u[3], w[3];
+  for (int r = 0; r < 3; ++r) {
+    u[r] = ki[3 * r] * x0 + ki[3 * r + 1] * y0 + ki[3 * r + 2];
+    w[r] = ki[3 * r] * x1 + ki[3 * r + 1] * y1 + ki[3 * r + 2];
+  }
+  const double nu = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+  const double nw = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+  double dot = (u[0] * w[0] + u[1] * w[1] + u[2] * w[2]) / (nu * nw);
+  dot = fmin(1.0, fmax(-1.0, dot));
+  return acos(dot);
+}
+
+__global__ void k_cameras(int V, const float* __restrict__ ext, const float* __restrict__ intr,
+                          const float* __restrict__ near, const float* __restrict__ far,
+                          const float* __restrict__ bg, const int32_t* __restrict__ view_scene,
+                          int scale_invariant, dsr_camera* __restrict__ cams) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= V) return;
+  double E[16], K[9], Ki[9], Wc[16];
+  for (int i = 0; i < 16; ++i) E[i] = ext[16 * v + i];
+  for (int i = 0; i < 9; ++i) K[i] = intr[9 * v + i];
+  double n = near[v], f = far[v];
+  float sc = 1.f;
+  if (scale_invariant) {
+    sc = 1.0f / near[v];  // float, as the reference's `scale = 1 / near`
+    for (int r = 0; r < 3; ++r) E[4 * r + 3] *= (double)sc;
+    n *= (double)sc;
+    f *= (double)sc;
+  }
+  inv3(K, Ki);
+  const double fovx = edge_angle(Ki, 0.0, 0.5, 1.0, 0.5);
+  const double fovy = edge_angle(Ki, 0.5, 0.0, 0.5, 1.0);
+  const double tx = tan(0.5 * fovx), ty = tan(0.5 * fovy);
+  // P (row-major) = get_projection_matrix
+  double P[16] = {0};
+  const double top = ty * n, right = tx * n;
+  P[0] = 2 * n / (2 * right);
+  P[5] = 2 * n / (2 * top);
+  P[14] = 1.0;  // [3][2]
+  P[10] = f / (f - n);
+  P[11] = -(f * n) / (f - n);
+  inv4(E, Wc);  // world -> camera, row-major
+  dsr_camera& c = cams[v];
+  // viewmatrix storage = (W2C)^T row-major  -> element [r*4 + c] = Wc[c*4 + r]
+  for (int r = 0; r < 4; ++r)
+    for (int q = 0; q < 4; ++q) c.viewmatrix[r * 4 + q] = (float)Wc[q * 4 + r];
+  // projmatrix storage = (P W2C)^T
+  for (int r = 0; r < 4; ++r)
+    for (int q = 0; q < 4; ++q) {
+      double s = 0;
+      for (int k = 0; k < 4; ++k) s += P[r * 4 + k] * Wc[k * 4 + q];
+      c.projmatrix[q * 4 + r] = (float)s;
+    }
+  c.campos[0] = (float)E[3];
+  c.campos[1] = (float)E[7];
+  c.campos[2] = (float)E[11];
+  c.tanfovx = (float)tx;
+  c.tanfovy = (float)ty;
+  c.bg[0] = bg[3 * v];
+  c.bg[1] = bg[3 * v + 1];
+  c.bg[2] = bg[3 * v + 2];
+  c.scene = view_scene[v];
+  c.scale = sc;
+  c._pad[0] = 0;
+  c._pad[1] = 0;
+}
+
+}  // namespace
+
+extern "C" int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, const float* near,
+                                 const float* far, const float* bg, const int32_t* view_scene,
+                                 int scale_invariant, dsr_camera* cams, void* stream) {
+  DSPLAT_REQUIRE(V > 0, "dsr_build_cameras: V=%d", V);
+  DSPLAT_REQUIRE(extrinsics && intrinsics && near && far && bg && view_scene && cams, "dsr_build_cameras: null pointer");
+  k_cameras<<<(V + 63) / 64, 64, 0, (hipStream_t)stream>>>(V, extrinsics, intrinsics, near, far, bg, view_scene,
+                                                         scale_invariant, cams);
+  return dsplat::check_launch("k_cameras");
+}

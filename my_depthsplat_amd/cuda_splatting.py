@@ -97,10 +97,9 @@ def render_views(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch
     h, w = image_shape
     n = gaussian_sh_coefficients.shape[-1]
     degree = math.isqrt(n) - 1
-    st = camera_settings(extrinsics, intrinsics, near, far, scale_invariant)
-    scene = torch.tensor(view_scene, dtype=torch.int32, device=extrinsics.device)
-    cams = raster.pack_cameras(st["viewmatrix"], st["projmatrix"], st["campos"], st["tanfovx"], st["tanfovy"],
-                               background_color, scene, st["scale"])
+    # the camera_settings() math, as one device kernel (no torch op chain, no host sync)
+    cams = raster.build_cameras(extrinsics, intrinsics, near, far, background_color.expand(V, 3), view_scene,
+                                scale_invariant)
     shs = gaussian_sh_coefficients.transpose(-1, -2)  # b g xyz n -> b g n xyz
     feats = shs if use_sh else shs[:, :, 0, :]
     color, radii = raster.rasterize_views(

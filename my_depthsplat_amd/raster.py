@@ -75,7 +75,7 @@ class KernelTimer:
 
 
 _timer: KernelTimer | None = None
-_last = {"num_rendered": 0, "max_count": 0}
+_last: dict = {"totals": None}
 
 
 def set_timer(t: KernelTimer | None) -> None:
@@ -84,7 +84,13 @@ def set_timer(t: KernelTimer | None) -> None:
 
 
 def last_stats() -> dict:
-    return dict(_last)
+    """(num_rendered, max tile count) of the last forward (reads the device: syncs)."""
+    t = _last["totals"]
+    if t is None:
+        return {"num_rendered": 0, "max_count": 0}
+    n, m = (int(x) for x in t[:2].cpu())
+    _spec["max_count"] = m
+    return {"num_rendered": n, "max_count": m}
 
 
 def _timed(name, fn, *args):
@@ -120,8 +126,78 @@ class RasterState:
     keys: torch.Tensor        # [N] int64 (uint64 keys, sorted per segment)
     final_T: torch.Tensor     # [V, H, W]
     n_contrib: torch.Tensor   # [V, H, W] int32
-    num_rendered: int
-    max_count: int
+    totals: torch.Tensor      # [4] int32 on device: (num_rendered, max entries per tile, ...)
+
+    @property
+    def num_rendered(self) -> int:  # host read: syncs
+        return int(self.totals[0].item())
+
+    @property
+    def max_count(self) -> int:
+        return int(self.totals[1].item())
+
+
+# Key-buffer sizing. N (the number of (view, tile, Gaussian) entries) is only known on the
+# device after the scan. Instead of reading it back mid-pipeline (the reference's per-view
+# D2H + .item() syncs), the key buffers are sized by the exact worst case V*G*tiles when
+# that fits KEY_BUDGET_BYTES (1.6 GB at 2x256^2 x 3 views: cheap on a 288 GB part, and
+# untouched pages cost no bandwidth); the whole forward then runs with NO host sync.
+# Larger problems fall back to one 8-byte read of (N, max tile count) after the scan.
+KEY_BUDGET_BYTES = 8 << 30
+_spec = {"max_count": 0}
+_inflight: list = []  # (pinned int32[4], event) read-backs of totals, consumed without blocking
+
+
+def _note_totals(totals: torch.Tensor) -> None:
+    """Queue a non-blocking copy of (N, max count) to pinned memory; completed copies from
+    earlier calls update the LDS-sort size hint. Never waits on the device."""
+    while _inflight and _inflight[0][1].query():
+        host, _ = _inflight.pop(0)
+        _spec["max_count"] = int(host[1])
+    if len(_inflight) < 4:
+        host = torch.empty(4, dtype=torch.int32, pin_memory=True)
+        host.copy_(totals, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        _inflight.append((host, ev))
+
+
+def _key_capacity(V, G, T):
+    worst = V * G * T
+    return worst if worst * 16 <= KEY_BUDGET_BYTES else None
+
+
+_index_cache: dict = {}
+
+
+def device_index(values, device) -> torch.Tensor:
+    """Small int32 index arrays (view -> scene maps) cached on the device, so steady-state
+    calls do no pageable H2D copy (which would serialise the host with the stream)."""
+    key = (tuple(int(v) for v in values), str(device))
+    t = _index_cache.get(key)
+    if t is None:
+        if len(_index_cache) > 256:
+            _index_cache.clear()
+        t = torch.tensor(key[0], dtype=torch.int32).to(device)
+        _index_cache[key] = t
+    return t
+
+
+def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True) -> torch.Tensor:
+    """Device-side camera set-up (dsr_build_cameras) -> [V, 44] float32 dsr_camera array."""
+    lib = _lib.load()
+    V = extrinsics.shape[0]
+    dev = extrinsics.device
+    _lib.require_gpu(extrinsics, intrinsics, near, far, bg)
+    cams = torch.empty((V, CAM_FLOATS), dtype=torch.float32, device=dev)
+    vs = view_scene.to(device=dev, dtype=torch.int32) if isinstance(view_scene, torch.Tensor) \
+        else device_index(view_scene, dev)
+    f = lambda t: t.detach().contiguous().float()  # noqa: E731
+    ext, K, n, fa, b = f(extrinsics), f(intrinsics), f(near), f(far), f(bg)
+    _lib.check(lib.dsr_build_cameras(V, ext.data_ptr(), K.data_ptr(), n.data_ptr(), fa.data_ptr(), b.data_ptr(),
+                                     vs.data_ptr(), int(bool(scale_invariant)), cams.data_ptr(),
+                                     _lib.stream_of(dev)), "dsr_build_cameras")
+    return cams
 
 
 def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W):
@@ -146,26 +222,37 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W)
     seg_start = torch.empty(V * T + 1, dtype=torch.int32, device=dev)
     cursor = torch.empty(V * T, dtype=torch.int32, device=dev)
     totals = torch.empty(4, dtype=torch.int32, device=dev)
-    _lib.check(_timed("k_scan", lib.dsr_bin_scan, V, H, W, seg_count.data_ptr(), seg_start.data_ptr(), cursor.data_ptr(),
-                                totals.data_ptr(), st), "dsr_bin_scan")
-    tot = totals[:2].cpu()  # the one host sync: sizes the key buffer
-    N, maxc = int(tot[0]), int(tot[1])
-    keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
-    if N > 0:
-        _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(), keys.data_ptr(), st),
-                   "dsr_bin_scatter")
-        cap = lib.dsr_sort_lds_capacity()
-        scratch = torch.empty(N, dtype=torch.int64, device=dev) if maxc > cap else None
-        _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), keys.data_ptr(),
-                                    None if scratch is None else scratch.data_ptr(), maxc, st), "dsr_bin_sort")
+    _lib.check(_timed("k_scan", lib.dsr_bin_scan, V, H, W, seg_count.data_ptr(), seg_start.data_ptr(),
+                      cursor.data_ptr(), totals.data_ptr(), st), "dsr_bin_scan")
+    cap = _key_capacity(V, G, T)
+    lds_cap = lib.dsr_sort_lds_capacity()
+    if cap is None:  # too large for the worst-case buffer: one small read-back
+        tot = totals[:2].cpu()
+        N, maxc = int(tot[0]), int(tot[1])
+        cap = max(N, 1)
+    else:
+        N = maxc = None
+        # LDS-sort launch size from earlier calls (any value is correct: segments above it
+        # take the HBM path inside the same launch); first call assumes the full capacity
+        _note_totals(totals)
+        maxc_hint = min(lds_cap, _spec["max_count"]) if _spec["max_count"] else lds_cap
+    keys = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+    # scratch: only for segments that may exceed the LDS sort (always possible when N is unknown)
+    need_scratch = maxc is None or maxc > lds_cap
+    scratch = torch.empty(max(cap, 1), dtype=torch.int64, device=dev) if need_scratch else None
+    _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
+                      keys.data_ptr(), st), "dsr_bin_scatter")
+    _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), keys.data_ptr(),
+                      None if scratch is None else scratch.data_ptr(), maxc_hint if maxc is None else maxc, st),
+               "dsr_bin_sort")
     color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
-    _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(), seg_start.data_ptr(),
-                                  keys.data_ptr(), color.data_ptr(), final_T.data_ptr(), n_contrib.data_ptr(), st),
-               "dsr_render_fwd")
-    _last["num_rendered"], _last["max_count"] = N, maxc
-    return color, RasterState(geom, radii, seg_start, keys, final_T, n_contrib, N, maxc)
+    _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
+                      seg_start.data_ptr(), keys.data_ptr(), color.data_ptr(), final_T.data_ptr(),
+                      n_contrib.data_ptr(), st), "dsr_render_fwd")
+    _last["totals"] = totals
+    return color, RasterState(geom, radii, seg_start, keys, final_T, n_contrib, totals)
 
 
 def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, state: RasterState,
@@ -188,7 +275,7 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
         starts[view_scene[v] + 1] += 1
     for s in range(S):
         starts[s + 1] += starts[s]
-    idx = torch.tensor(starts + order, dtype=torch.int32).to(dev, non_blocking=True)
+    idx = device_index(starts + order, dev)
     dmeans = torch.empty((S, G, 3), dtype=torch.float32, device=dev)
     dfeat = torch.empty_like(feats, dtype=torch.float32)
     dopac = torch.empty((S, G), dtype=torch.float32, device=dev)

@@ -182,3 +182,92 @@ def test_empty_and_culled(gpu):
     assert state.num_rendered == 0
     ref = torch.tensor([0.25, 0.5, 0.75])[None, :, None, None].expand_as(color.cpu())
     assert torch.equal(color.cpu(), ref)
+
+
+def test_device_cameras_match_reference_settings(gpu):
+    """dsr_build_cameras vs the settings the REFERENCE wrapper handed to its rasterizer
+    (tests/golden/cuda_splatting_settings.npz)."""
+    from pathlib import Path
+
+    from my_depthsplat_amd import raster
+    G = np.load(Path(__file__).parent / "golden" / "cuda_splatting_settings.npz")
+    T = lambda k: torch.from_numpy(G[k]).to(gpu)  # noqa: E731
+    b = G["extrinsics"].shape[0]
+    for tag, si in (("si", True), ("ns", False)):
+        cams = raster.build_cameras(T("extrinsics"), T("intrinsics"), T("near"), T("far"), T("bg"), list(range(b)),
+                                    si).cpu().numpy()
+        for i in range(b):
+            np.testing.assert_allclose(cams[i, 0:16], G[f"{tag}_view{i}_viewmatrix"].reshape(16), rtol=1e-5, atol=1e-6)
+            np.testing.assert_allclose(cams[i, 16:32], G[f"{tag}_view{i}_projmatrix"].reshape(16), rtol=1e-5,
+                                       atol=1e-5)
+            np.testing.assert_allclose(cams[i, 32:35], G[f"{tag}_view{i}_campos"], rtol=1e-6, atol=1e-7)
+            if tag == "si":
+                np.testing.assert_allclose(cams[i, 35:37], G["si_view%d_tanfov" % i], rtol=1e-6)
+                assert cams[i, 41] == np.float32(1) / G["near"][i]
+            assert cams[i, 40:41].view(np.int32)[0] == i
+
+
+def test_render_cuda_end_to_end_vs_oracle(gpu):
+    """Reference-signature render_cuda (device cameras, scale-invariant) vs the oracle fed
+    the reference wrapper's float32 settings."""
+    from my_depthsplat_amd.cuda_splatting import render_cuda
+    sc = scene_inputs(h=64, w=96, seed=8, n_tgt=3)
+    st = settings_for(sc)
+    g = sc.gaussians
+    v = sc.target_extrinsics.shape[1]
+    rep = lambda t: t.expand(v, *t.shape[1:]).to(gpu)  # noqa: E731
+    out = render_cuda(sc.target_extrinsics[0].to(gpu), sc.target_intrinsics[0].to(gpu), sc.near[0].to(gpu),
+                      sc.far[0].to(gpu), (64, 96), torch.zeros(v, 3, device=gpu), rep(g.means), rep(g.covariances),
+                      rep(g.harmonics), rep(g.opacities)).cpu().numpy()
+    for i, o in enumerate(oracle_views(sc, st)):
+        ref, _, _ = o.image()
+        assert float(np.abs(out[i] - ref).mean()) < 1e-4
+        assert abs(_psnr(out[i], ref * 0 + 0.5) - _psnr(ref, ref * 0 + 0.5)) < 0.01
+        o.close()
+
+
+def test_decoder_batched_views(gpu):
+    """DecoderSplattingCUDA (B scenes x v views in one call, no repeat) == per-view render_cuda."""
+    from my_depthsplat_amd.cuda_splatting import render_cuda
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.synthetic import make_scene
+    sc = make_scene(batch=2, n_context=2, n_targets=3, height=48, width=64, seed=9, device=gpu)
+    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.1, 0.2, 0.3]}).to(gpu)
+    out = dec(sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near, sc.far, (48, 64))
+    g = sc.gaussians
+    for b in range(2):
+        rep = lambda t: t[b:b + 1].expand(3, *t.shape[1:])  # noqa: E731
+        want = render_cuda(sc.target_extrinsics[b], sc.target_intrinsics[b], sc.near[b], sc.far[b], (48, 64),
+                           dec.background_color.expand(3, 3), rep(g.means), rep(g.covariances), rep(g.harmonics),
+                           rep(g.opacities))
+        assert torch.equal(out.color[b], want)
+
+
+@pytest.mark.parametrize("n_ties", [6, 100000])
+def test_equal_depth_ties_sorted_by_id(gpu, n_ties):
+    """Equal view-space depths: a few tie pairs (insertion fix-up) and a fronto-parallel
+    plane where every Gaussian shares one depth (full id-then-depth radix path). Order
+    must match the oracle's stable sort (ties in Gaussian-id order) exactly."""
+    sc = scene_inputs(h=64, w=64, seed=12)
+    m = sc.gaussians.means.clone()
+    if n_ties >= m.shape[1]:
+        m[..., 2] = 3.0
+    else:
+        g = torch.Generator().manual_seed(1)
+        src = torch.randint(0, m.shape[1], (n_ties,), generator=g)
+        dst = torch.randint(0, m.shape[1], (n_ties,), generator=g)
+        m[0, dst, 2] = m[0, src, 2]
+    sc.gaussians.means = m
+    st = settings_for(sc)
+    color, state, _ = hip_forward(sc, st, gpu)
+    orcs = oracle_views(sc, st)
+    start, keys = _segments(state, 2, 16)
+    for v, o in enumerate(orcs):
+        okeys, ovals, ranges = o.binning()
+        for t in range(16):
+            hk = keys[start[v * 16 + t]:start[v * 16 + t + 1]]
+            ob, oe = ranges[t]
+            np.testing.assert_array_equal((hk & np.uint64(0xFFFFFFFF)).astype(np.uint32), ovals[ob:oe])
+        oc, _, _ = o.image()
+        assert float(np.abs(color[v].cpu().numpy() - oc).mean()) < 1e-4
+        o.close()
