@@ -466,31 +466,173 @@ __device__ void sort_segment(uint64_t* A, uint64_t* B, uint32_t n, int id_bits, 
     for (uint32_t i = threadIdx.x; i < n; i += NTH) home[i] = src[i];
 }
 
-// One workgroup per (view, tile) segment. n <= cap: sort in LDS. n > cap: when big_here,
-// sort through HBM (keys <-> scratch) with the same 4 waves; otherwise leave it to
-// k_sort_global.
+// ---- in-LDS segment sort (n <= 256 * KMAX) -------------------------------------------
+// Keys live in LDS; each pass every thread loads its KMAX contiguous keys into registers,
+// ranks them with per-thread packed 8-bit counters for a 4-bit digit (no ballots, no
+// atomics, no serial dependency across threads), one block-wide scan of the 16 x 256
+// counters (u16, digit-major) gives every (digit, thread) its output base, and keys are
+// scattered to the other LDS buffer. Contiguous ownership + digit-major scan = stable.
+// LDS index padding i + i / KMAX makes the per-thread row reads bank-conflict free.
+template <int KMAX>
+__device__ __forceinline__ uint32_t padi(uint32_t i) { return i + i / KMAX; }
+
+template <int KMAX>
+__device__ bool reg_pass(uint64_t* buf, uint32_t n, int shift, uint16_t* cnt, uint32_t* wsum) {
+  // in place: every key of the pass is in registers before the first barrier, so the
+  // scatter can overwrite the same LDS buffer (one buffer -> more workgroups per CU)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t base = (uint32_t)tid * KMAX;
+  uint64_t k[KMAX];
+  uint32_t dg[KMAX], loc[KMAX];
+  uint64_t c_lo = 0, c_hi = 0;
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const uint32_t idx = base + i;
+    const bool valid = idx < n;
+    k[i] = valid ? buf[padi<KMAX>(idx)] : 0ull;
+    const uint32_t d = valid ? (uint32_t)(k[i] >> shift) & 15u : 16u;
+    dg[i] = d;
+    const uint32_t sh8 = 8u * (d & 7u);
+    if (d < 8u) {
+      loc[i] = (uint32_t)(c_lo >> sh8) & 255u;
+      c_lo += 1ull << sh8;
+    } else {
+      loc[i] = (uint32_t)(c_hi >> sh8) & 255u;
+      if (d < 16u) c_hi += 1ull << sh8;
+    }
+  }
+  const uint32_t d0 = (uint32_t)(buf[0] >> shift) & 15u;  // digit of key 0 (broadcast read)
+#pragma unroll
+  for (int d = 0; d < 16; ++d) cnt[d * NT + tid] = (uint16_t)(((d < 8 ? c_lo : c_hi) >> (8 * (d & 7))) & 255u);
+  __syncthreads();
+  // exclusive scan of the 4096 counters in (digit, thread) order; thread t owns [16t, 16t+16)
+  uint32_t v[16];
+  {
+    const uint4* p = reinterpret_cast<const uint4*>(cnt + 16 * tid);
+    const uint4 x = p[0], y = p[1];
+    const uint32_t wds[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      v[2 * q] = wds[q] & 0xFFFFu;
+      v[2 * q + 1] = wds[q] >> 16;
+    }
+  }
+  uint32_t tot = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const uint32_t c = v[q];
+    v[q] = tot;
+    tot += c;
+  }
+  const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t off = incl - tot;
+  for (int ww = 0; ww < w; ++ww) off += wsum[ww];
+  {
+    uint32_t wds[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) wds[q] = (v[2 * q] + off) | ((v[2 * q + 1] + off) << 16);
+    uint4* p = reinterpret_cast<uint4*>(cnt + 16 * tid);
+    p[0] = make_uint4(wds[0], wds[1], wds[2], wds[3]);
+    p[1] = make_uint4(wds[4], wds[5], wds[6], wds[7]);
+  }
+  __syncthreads();
+  // a digit holding every key makes the pass the identity (same decision in every thread)
+  const uint32_t s0 = cnt[d0 * NT];
+  const uint32_t s1 = d0 < 15 ? (uint32_t)cnt[(d0 + 1) * NT] : n;
+  if (s1 - s0 == n) return false;  // nothing written; the next pass re-reads buf
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i)
+    if (dg[i] < 16u) buf[padi<KMAX>((uint32_t)cnt[dg[i] * NT + tid] + loc[i])] = k[i];
+  __syncthreads();
+  return true;
+}
+
+template <int KMAX>
+__device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, uint32_t* wsum, uint32_t* flag) {
+  for (int sh = 32; sh < 64; sh += 4) reg_pass<KMAX>(A, n, sh, cnt, wsum);
+  if (threadIdx.x == 0) *flag = 0;
+  __syncthreads();
+  uint32_t ties = 0;
+  for (uint32_t i = threadIdx.x; i + 1 < n; i += NT)
+    ties += (uint32_t)((A[padi<KMAX>(i)] >> 32) == (A[padi<KMAX>(i + 1)] >> 32));
+  if (ties) atomicAdd(flag, ties);
+  __syncthreads();
+  ties = *flag;
+  __syncthreads();
+  if (ties != 0 && ties <= 32) {
+    for (uint32_t i = threadIdx.x; i + 1 < n; i += NT) {
+      const uint64_t d = A[padi<KMAX>(i)] >> 32;
+      if ((A[padi<KMAX>(i + 1)] >> 32) != d || (i > 0 && (A[padi<KMAX>(i - 1)] >> 32) == d)) continue;
+      uint32_t e = i + 1;
+      while (e < n && (A[padi<KMAX>(e)] >> 32) == d) ++e;
+      for (uint32_t k = i + 1; k < e; ++k) {
+        const uint64_t x = A[padi<KMAX>(k)];
+        uint32_t m = k;
+        while (m > i && A[padi<KMAX>(m - 1)] > x) {
+          A[padi<KMAX>(m)] = A[padi<KMAX>(m - 1)];
+          --m;
+        }
+        A[padi<KMAX>(m)] = x;
+      }
+    }
+    __syncthreads();
+  } else if (ties > 32) {
+    for (int sh = 0; sh < id_bits; sh += 4) reg_pass<KMAX>(A, n, sh, cnt, wsum);
+    for (int sh = 32; sh < 64; sh += 4) reg_pass<KMAX>(A, n, sh, cnt, wsum);
+  }
+}
+
+// One workgroup per (view, tile) segment. n <= 256*KMAX: sort in LDS. Larger: when
+// big_here, sort through HBM (keys <-> scratch) with the ballot-ranked passes; otherwise
+// leave it to k_sort_global.
+template <int KMAX>
 __global__ __launch_bounds__(NT) void k_sort_lds(const uint32_t* __restrict__ seg_start,
                                                  uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
-                                                 int id_bits, uint32_t cap, int big_here) {
+                                                 int id_bits, int big_here) {
+  constexpr uint32_t cap = NT * KMAX;
+  constexpr uint32_t padded = cap + cap / KMAX;
   extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
   uint64_t* A = s_keys;
-  uint64_t* B = s_keys + cap;
-  uint32_t* hist = reinterpret_cast<uint32_t*>(B + cap);
-  uint32_t* wsum = hist + 4 * 256;
-  uint32_t* flag = wsum + 4;
+  uint32_t* aux = reinterpret_cast<uint32_t*>(A + padded);  // 8 KiB counters (u16) / HBM-path histogram
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(aux);
+  uint32_t* wsum = aux + 2048;
+  uint32_t* flag = wsum + 16;
   const int seg = blockIdx.x;
   const uint32_t b = seg_start[seg];
   const uint32_t n = seg_start[seg + 1] - b;
   if (n <= 1) return;
   if (n > cap) {
-    if (big_here) sort_segment<NT>(keys + b, scratch + b, n, id_bits, hist, wsum, flag, keys + b);
+    if (big_here) sort_segment<NT>(keys + b, scratch + b, n, id_bits, aux, wsum, flag, keys + b);
     return;
   }
-  for (uint32_t i = threadIdx.x; i < n; i += NT) A[i] = keys[b + i];
+  // all KMAX global loads of a thread in flight at once (coalesced across the workgroup)
+  {
+    uint64_t tmp[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      const uint32_t idx = threadIdx.x + (uint32_t)i * NT;
+      tmp[i] = idx < n ? keys[b + idx] : 0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      const uint32_t idx = threadIdx.x + (uint32_t)i * NT;
+      if (idx < n) A[padi<KMAX>(idx)] = tmp[i];
+    }
+  }
   __syncthreads();
-  sort_segment<NT>(A, B, n, id_bits, hist, wsum, flag, A);
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += NT) keys[b + i] = A[i];
+  reg_sort<KMAX>(A, n, id_bits, cnt, wsum, flag);
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const uint32_t idx = threadIdx.x + (uint32_t)i * NT;
+    if (idx < n) keys[b + idx] = A[padi<KMAX>(idx)];
+  }
+}
+
+template <int KMAX>
+constexpr size_t sort_lds_bytes() {
+  return (size_t)(NT * KMAX + NT) * 8 + 8192 + 64 * 4;
 }
 
 // Segments larger than the LDS capacity: same passes through HBM, 16 waves.
@@ -521,6 +663,18 @@ constexpr int SUB = 8;
 
 __device__ __forceinline__ float gauss_weight(float power) { return __expf(power); }
 
+// The compositing loops evaluate the Gaussian falloff in base 2 with the conic pre-scaled
+// once per staged entry: p2 = log2(e) * power = A dx^2 + C dy^2 + B dx dy with
+// A = -0.5 log2(e) a, C = -0.5 log2(e) c, B = -log2(e) b, and G = 2^p2 (one v_exp_f32).
+// Forward and backward use this exact sequence, so their skip decisions agree.
+constexpr float kLog2e = 1.4426950408889634f;
+__device__ __forceinline__ float4 scaled_conic_q(float4 q) {  // (x, y, a, b) -> (x, y, A, B)
+  return make_float4(q.x, q.y, -0.5f * kLog2e * q.z, -kLog2e * q.w);
+}
+__device__ __forceinline__ float falloff_p2(float A, float B, float C, float dx, float dy) {
+  return fmaf(A * dx, dx, fmaf(C * dy, dy, B * dx * dy));
+}
+
 __device__ __forceinline__ uint32_t subtile_mask(float4 q, float4 r, int tx0, int ty0) {
   // q = (x, y, conic a, conic b), r = (conic c, opacity, ...); tile origin (tx0, ty0)
   const float op = r.y;
@@ -543,6 +697,9 @@ __device__ __forceinline__ uint32_t subtile_mask(float4 q, float4 r, int tx0, in
 }
 
 // K6: front-to-back compositing. grid = (gx, gy, V), block = 256 (4 waves x 8x8 pixels).
+// Each wave copies the records of the entries its sub-tile needs into its own contiguous
+// LDS list (no index indirection in the hot loop); every lane then walks that list with
+// branch-free compositing, reading the next record before compositing the current one.
 __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, int T,
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
@@ -550,11 +707,13 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
                                                    const uint64_t* __restrict__ keys,
                                                    float* __restrict__ out, float* __restrict__ finalT,
                                                    uint32_t* __restrict__ ncontrib) {
-  __shared__ float4 s_q[NT];       // x, y, conic a, conic b
-  __shared__ float4 s_r[NT];       // conic c, opacity, r, g
-  __shared__ float s_bl[NT];       // b
-  __shared__ uint32_t s_mask[NT];  // sub-tile mask per staged entry
-  __shared__ uint16_t s_list[4][NT];
+  __shared__ float4 s_q[NT];        // staged: x, y, conic a, conic b
+  __shared__ float4 s_r[NT];        // staged: conic c, opacity, r, g
+  __shared__ float s_bl[NT];        // staged: b
+  __shared__ uint32_t s_mask[NT];   // staged: sub-tile mask
+  __shared__ float4 w_q[4][NT];     // per-wave lists
+  __shared__ float4 w_r[4][NT];
+  __shared__ float2 w_bp[4][NT];    // (b, list position bits)
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int tx0 = blockIdx.x * BX, ty0 = blockIdx.y * BY;
@@ -569,50 +728,83 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   bool done = !inside;
   float Tr = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
   uint32_t last = 0;
+  // software pipeline over 256-entry batches: the record of batch b+1 and the key of
+  // batch b+2 are in flight while batch b is composited (two dependent HBM/L2 round
+  // trips per batch otherwise dominate: ~3000 entries per tile at 256x256)
+  auto load_rec = [&](uint32_t e, float4& q, float4& r, float& bb) {
+    if (e < end) {
+      const uint32_t id = (uint32_t)keys[e];
+      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
+      q = rec[0];
+      r = rec[1];
+      bb = rec[2].x;
+    }
+  };
+  float4 cq = make_float4(0.f, 0.f, 0.f, 0.f), cr = cq;
+  float cb = 0.f;
+  load_rec(start + tid, cq, cr, cb);
   for (uint32_t base = start; base < end; base += NT) {
     if (__syncthreads_count(done) == NT) break;
     const uint32_t i = base + tid;
-    uint32_t m = 0;
-    if (i < end) {
-      const uint32_t id = (uint32_t)keys[i];
-      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
-      const float4 q = rec[0], r = rec[1];
-      s_q[tid] = q;
-      s_r[tid] = r;
-      s_bl[tid] = rec[2].x;
-      m = subtile_mask(q, r, tx0, ty0);
-    }
+    float4 nq = make_float4(0.f, 0.f, 0.f, 0.f), nr = nq;
+    float nb = 0.f;
+    load_rec(i + NT, nq, nr, nb);  // next batch, consumed next iteration
+    const uint32_t m = i < end ? subtile_mask(cq, cr, tx0, ty0) : 0u;
+    s_q[tid] = cq;
+    s_r[tid] = cr;
+    s_bl[tid] = cb;
     s_mask[tid] = m;
+    cq = nq;
+    cr = nr;
+    cb = nb;
     __syncthreads();
-    // this wave's entries, in list order (4 chunks of 64, ballot compaction)
     int cnt = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const bool mine = (s_mask[c * 64 + lane] >> w) & 1u;
+      const int e = c * 64 + lane;
+      const bool mine = (s_mask[e] >> w) & 1u;
       const uint64_t bal = __ballot(mine);
-      if (mine) s_list[w][cnt + __popcll(bal & lt)] = (uint16_t)(c * 64 + lane);
+      if (mine) {
+        const int slot = cnt + __popcll(bal & lt);
+        const float4 rr = s_r[e];
+        w_q[w][slot] = scaled_conic_q(s_q[e]);
+        w_r[w][slot] = make_float4(-0.5f * kLog2e * rr.x, rr.y, rr.z, rr.w);
+        w_bp[w][slot] = make_float2(s_bl[e], __uint_as_float(base - start + (uint32_t)e + 1u));
+      }
       cnt += __popcll(bal);
     }
     __builtin_amdgcn_wave_barrier();
-    for (int k = 0; k < cnt && !done; ++k) {
-      const int j = s_list[w][k];
-      const float4 q = s_q[j];
-      const float4 r = s_r[j];
-      const float dx = q.x - pfx, dy = q.y - pfy;
-      const float power = -0.5f * (q.z * dx * dx + r.x * dy * dy) - q.w * dx * dy;
-      if (power > 0.0f) continue;
-      const float alpha = fminf(0.99f, r.y * gauss_weight(power));
-      if (alpha < 1.0f / 255.0f) continue;
-      const float testT = Tr * (1 - alpha);
-      if (testT < 0.0001f) {
-        done = true;
-        continue;
+    if (cnt > 0 && !__all(done)) {
+      // two entries per step: both records are read before either is composited
+      for (int k = 0; k < cnt; k += 2) {
+        const float4 qa = w_q[w][k], ra = w_r[w][k];
+        const float2 ba = w_bp[w][k];
+        const int k1 = min(k + 1, NT - 1);
+        const float4 qb = w_q[w][k1], rb = w_r[w][k1];
+        const float2 bb = w_bp[w][k1];
+        const bool has_b = k + 1 < cnt;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const float4 q = u ? qb : qa;
+          const float4 r = u ? rb : ra;
+          const float2 bp = u ? bb : ba;
+          const float dx = q.x - pfx, dy = q.y - pfy;
+          const float p2 = falloff_p2(q.z, q.w, r.x, dx, dy);
+          const float alpha = fminf(0.99f, r.y * __builtin_amdgcn_exp2f(p2));
+          const bool ok = (u == 0 || has_b) && !done && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+          const float testT = Tr * (1 - alpha);
+          const bool stop = ok && testT < 0.0001f;
+          const bool blend = ok && !stop;
+          done = done || stop;
+          const float wgt = blend ? alpha * Tr : 0.f;
+          C0 = fmaf(r.z, wgt, C0);
+          C1 = fmaf(r.w, wgt, C1);
+          C2 = fmaf(bp.x, wgt, C2);
+          Tr = blend ? testT : Tr;
+          last = blend ? __float_as_uint(bp.y) : last;
+        }
+        if (__all(done)) break;
       }
-      C0 += r.z * alpha * Tr;
-      C1 += r.w * alpha * Tr;
-      C2 += s_bl[j] * alpha * Tr;
-      Tr = testT;
-      last = base - start + (uint32_t)j + 1u;
     }
   }
   if (inside) {
@@ -719,9 +911,10 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
         const float4 q = s_q[j];
         const float4 r = s_r[j];
         const float dx = q.x - pfx, dy = q.y - pfy;
-        const float power = -0.5f * (q.z * dx * dx + r.x * dy * dy) - q.w * dx * dy;
-        if (power <= 0.0f) {
-          const float Gs = gauss_weight(power);
+        // same falloff sequence as k_render_fwd (decisions must agree with the forward)
+        const float p2 = falloff_p2(-0.5f * kLog2e * q.z, -kLog2e * q.w, -0.5f * kLog2e * r.x, dx, dy);
+        if (p2 <= 0.0f) {
+          const float Gs = __builtin_amdgcn_exp2f(p2);
           const float alpha = fminf(0.99f, r.y * Gs);
           if (alpha >= 1.0f / 255.0f) {
             act = true;
@@ -1051,22 +1244,38 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, uint64_t
   int id_bits = 0;
   while (id_bits < 32 && ((uint64_t)1 << id_bits) < (uint64_t)G) ++id_bits;
   const uint32_t want = max_count ? max_count : kSortCap;
-  uint32_t cap = 256;
-  while (cap < want && cap < kSortCap) cap <<= 1;
-  const size_t lds = (size_t)cap * 16 + (4 * 256 + 8) * 4;
+  // segments above the LDS capacity: sorted in this launch through HBM unless they are
+  // known to be large (max_count > kSortCap): then the 16-wave k_sort_global takes them
+  const bool big_known = scratch != nullptr && max_count > kSortCap;
+  const int big_here = scratch != nullptr && !big_known;
   static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted into once
   if (!attr_set) {
-    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds,
+    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds<32>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)((size_t)kSortCap * 16 + (4 * 256 + 8) * 4)),
+                                                      (int)sort_lds_bytes<32>()),
+                                  "hipFuncSetAttribute(k_sort_lds)"))
+      return e;
+    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds<16>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      (int)sort_lds_bytes<16>()),
                                   "hipFuncSetAttribute(k_sort_lds)"))
       return e;
     attr_set = true;
   }
-  // segments above cap: in this launch through HBM unless they are known to be large
-  // (max_count > kSortCap), in which case the 16-wave k_sort_global takes them
-  const bool big_known = scratch != nullptr && max_count > kSortCap;
-  k_sort_lds<<<nseg, NT, lds, st>>>(seg_start, keys, scratch, id_bits, cap, scratch != nullptr && !big_known);
+  uint32_t cap;
+  if (want <= 256 * 4) {
+    cap = 256 * 4;
+    k_sort_lds<4><<<nseg, NT, sort_lds_bytes<4>(), st>>>(seg_start, keys, scratch, id_bits, big_here);
+  } else if (want <= 256 * 8) {
+    cap = 256 * 8;
+    k_sort_lds<8><<<nseg, NT, sort_lds_bytes<8>(), st>>>(seg_start, keys, scratch, id_bits, big_here);
+  } else if (want <= 256 * 16) {
+    cap = 256 * 16;
+    k_sort_lds<16><<<nseg, NT, sort_lds_bytes<16>(), st>>>(seg_start, keys, scratch, id_bits, big_here);
+  } else {
+    cap = 256 * 32;
+    k_sort_lds<32><<<nseg, NT, sort_lds_bytes<32>(), st>>>(seg_start, keys, scratch, id_bits, big_here);
+  }
   if (int e = dsplat::check_launch("k_sort_lds")) return e;
   if (big_known) {
     k_sort_global<<<nseg, 1024, 0, st>>>(seg_start, keys, scratch, id_bits, cap);
