@@ -71,13 +71,17 @@ int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, c
  * Replaces preprocessCUDA + tiles_touched (upstream K1). Per view v and gaussian g of
  * scene cams[v].scene: cull, EWA projection, conic, radius, SH->RGB (or colors), and
  * the per-(view, tile) entry count seg_count[v*T + t] (T = tiles per view).
- *   means [S,G,3]  shs [S,G,M,3] (M = (sh_degree+1)^2) xor colors [S,G,3]
+ *   means [S,G,3]  shs [S,G,M,3] (M >= (sh_degree+1)^2) xor colors [S,G,3]
  *   opacities [S,G]  cov6 [S,G,6] (xx,xy,xz,yy,yz,zz = cuda_splatting.py:114,122)
+ *   layout: DSR_LAYOUT_* bits for the shs / covariance arrays (0 = as above)
  *   out: geom [V,G,12], radii [V,G] int32, seg_count [V*T] (zeroed by this call).  */
+#define DSR_LAYOUT_SH_CHANNEL_MAJOR 1  /* shs given as [S,G,3,M] (Gaussians.harmonics)      */
+#define DSR_LAYOUT_COV_FULL 2          /* covariance given as [S,G,3,3]; grads: upper triangle */
 int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,
-                       float* geom, int32_t* radii, uint32_t* seg_count, void* stream);
+                       float* geom, int32_t* radii, uint32_t* seg_count, int layout,
+                       void* stream);
 
 /* Exclusive scan of seg_count[V*T] -> seg_start[V*T+1], seg_cursor[V*T] (= seg_start),
  * totals[0] = N (num_rendered over all views), totals[1] = max entries in one tile. */
@@ -116,13 +120,15 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
 /* Preprocess backward (K8 + K9), reduced over all views of each scene without atomics.
  * scene_view_start [S+1], scene_views [V] list the views of each scene.
  * out (overwritten): dmeans [S,G,3], dshs [S,G,M,3] or NULL, dcolors [S,G,3] or NULL,
- * dopac [S,G], dcov6 [S,G,6]; dmean2D [V,G,3] optional (NULL to skip). */
+ * dopac [S,G], dcov6 [S,G,6]; dmean2D [V,G,3] optional (NULL to skip). `layout` as in
+ * the forward; dshs / dcov6 are written in that layout (full covariance: upper triangle,
+ * zeros below, as the reference's triu-gather backward produces). */
 int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* cov6,
                        const dsr_camera* cams, const float* geom, const float* dgeom,
                        const int32_t* scene_view_start, const int32_t* scene_views,
                        float* dmeans, float* dshs, float* dcolors, float* dopac, float* dcov6,
-                       float* dmean2D, void* stream);
+                       float* dmean2D, int layout, void* stream);
 
 /* ---- plane-sweep cost volume -------------------------------------------------------
  * Fused warp_with_pose_depth_candidates (matching.py:24-90) + correlation

@@ -20,7 +20,7 @@ _P = c_void_p
 _I = c_int
 SIGNATURES: dict[str, tuple] = {
     "dsr_build_cameras": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),
-    "dsr_preprocess_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dsr_preprocess_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dsr_bin_scan": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
     "dsr_bin_scatter": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
     "dsr_bin_sort": (_I, [_I, _I, _I, _I, _P, _P, _P, c_uint32, _P]),
@@ -28,7 +28,7 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_render_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dsr_render_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dsr_preprocess_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
-                                _P, _P, _P, _P, _P, _P, _P]),
+                                _P, _P, _P, _P, _P, _P, _I, _P]),
     "dcv_cost_volume_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P, _P]),
     "dcv_cost_volume_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P,
                                  _P, _P, _P]),

@@ -134,6 +134,32 @@ __device__ __forceinline__ float sh_eval(const float* sh, int ch, float x, float
   return v;
 }
 
+// Input layouts (dsr_preprocess_* `layout` bits). bit 0: SH channel-major [S,G,3,M] (the
+// decoder's Gaussians.harmonics) instead of the rasterizer's coefficient-major [S,G,M,3];
+// bit 1: full covariance [S,G,3,3] instead of cov6 — the upper triangle is read, exactly
+// what cuda_splatting.py:114,122's triu gather hands the rasterizer.
+constexpr int kLayoutShChannelMajor = 1, kLayoutCovFull = 2;
+__device__ __forceinline__ float load_cov(const float* cov, size_t sg, int k, int layout) {
+  if (layout & kLayoutCovFull) {
+    constexpr int idx[6] = {0, 1, 2, 4, 5, 8};
+    return cov[9 * sg + idx[k]];
+  }
+  return cov[6 * sg + k];
+}
+template <int NC>
+__device__ __forceinline__ void load_sh(const float* shs, size_t sg, int M, int layout, float* out) {
+  const float* p = shs + sg * (size_t)M * 3;
+  if (layout & kLayoutShChannelMajor) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) out[k * 3 + ch] = p[ch * M + k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < NC * 3; ++k) out[k] = p[k];
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // K1: preprocess + per-(view, tile) entry counts.
 // grid = (ceil(G/256), V), block = 256. DEG = -1 -> colors_precomp path.
@@ -146,7 +172,7 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
                                                    const float* __restrict__ cov6,
                                                    const dsr_camera* __restrict__ cams,
                                                    float* __restrict__ geom, int32_t* __restrict__ radii,
-                                                   uint32_t* __restrict__ seg_count, int lds_hist) {
+                                                   uint32_t* __restrict__ seg_count, int lds_hist, int layout) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
   const int v = blockIdx.y;
   const int T = gx * gy;
@@ -175,7 +201,7 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
       float c6[6];
       const float gsc2 = gsc * gsc;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) c6[k] = cov6[6 * sg + k] * gsc2;
+      for (int k = 0; k < 6; ++k) c6[k] = load_cov(cov6, sg, k, layout) * gsc2;
       const float fx = W / (2.0f * cam->tanfovx);
       const float fy = H / (2.0f * cam->tanfovy);
       Cov2D w;
@@ -193,7 +219,9 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
           r = rr;
           uint32_t clamp_bits = 0;
           if constexpr (DEG >= 0) {
-            const float* sh = shs + sg * (size_t)M * 3;
+            constexpr int NC = (DEG + 1) * (DEG + 1);
+            float sh[NC * 3];
+            load_sh<NC>(shs, sg, M, layout, sh);
             float dx = p.x - cam->campos[0], dy = p.y - cam->campos[1], dz = p.z - cam->campos[2];
             const float len = sqrtf(dx * dx + dy * dy + dz * dz);
             dx = dx / len;
@@ -975,7 +1003,7 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     const float* __restrict__ geom, const float* __restrict__ dgeom,
     const int32_t* __restrict__ scene_view_start, const int32_t* __restrict__ scene_views,
     float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
-    float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D) {
+    float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D, int layout) {
   constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
   const int s = blockIdx.y;
   const int g = blockIdx.x * NT + threadIdx.x;
@@ -984,14 +1012,15 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
   const F3 m0 = {means[3 * sg], means[3 * sg + 1], means[3 * sg + 2]};
   float c60[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) c60[k] = cov6[6 * sg + k];
+  for (int k = 0; k < 6; ++k) c60[k] = load_cov(cov6, sg, k, layout);
   float sh[NC * 3];
   float dsh[NC * 3];
 #pragma unroll
   for (int k = 0; k < NC * 3; ++k) {
-    sh[k] = (DEG >= 0) ? shs[sg * (size_t)M * 3 + k] : 0.f;
+    sh[k] = 0.f;
     dsh[k] = 0.f;
   }
+  if constexpr (DEG >= 0) load_sh<NC>(shs, sg, M, layout, sh);
   float dm0 = 0.f, dm1 = 0.f, dm2 = 0.f, dop = 0.f, dcol0 = 0.f, dcol1 = 0.f, dcol2 = 0.f;
   float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int vb = scene_view_start[s], ve = scene_view_start[s + 1];
@@ -1157,8 +1186,15 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
   dmeans[3 * sg] = dm0;
   dmeans[3 * sg + 1] = dm1;
   dmeans[3 * sg + 2] = dm2;
+  if (layout & kLayoutCovFull) {  // gradient lands on the upper triangle only (triu gather)
+    float* o = dcov6 + 9 * sg;
+    o[0] = dc[0]; o[1] = dc[1]; o[2] = dc[2];
+    o[3] = 0.f;   o[4] = dc[3]; o[5] = dc[4];
+    o[6] = 0.f;   o[7] = 0.f;   o[8] = dc[5];
+  } else {
 #pragma unroll
-  for (int k = 0; k < 6; ++k) dcov6[6 * sg + k] = dc[k];
+    for (int k = 0; k < 6; ++k) dcov6[6 * sg + k] = dc[k];
+  }
   dopac[sg] = dop;
   if constexpr (DEG < 0) {
     dcolors[3 * sg] = dcol0;
@@ -1166,9 +1202,18 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     dcolors[3 * sg + 2] = dcol2;
   } else {
     float* o = dshs + sg * (size_t)M * 3;
+    if (layout & kLayoutShChannelMajor) {
 #pragma unroll
-    for (int k = 0; k < NC * 3; ++k) o[k] = dsh[k];
-    for (int k = NC * 3; k < M * 3; ++k) o[k] = 0.f;
+      for (int k = 0; k < NC; ++k)
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) o[ch * M + k] = dsh[k * 3 + ch];
+      for (int k = NC; k < M; ++k)
+        for (int ch = 0; ch < 3; ++ch) o[ch * M + k] = 0.f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < NC * 3; ++k) o[k] = dsh[k];
+      for (int k = NC * 3; k < M * 3; ++k) o[k] = 0.f;
+    }
   }
 }
 
@@ -1186,7 +1231,7 @@ uint32_t dsr_sort_lds_capacity(void) { return kSortCap; }
 int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                        const float* shs, const float* colors, const float* opacities,
                        const float* cov6, const dsr_camera* cams, float* geom, int32_t* radii,
-                       uint32_t* seg_count, void* stream) {
+                       uint32_t* seg_count, int layout, void* stream) {
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_preprocess_fwd: bad sizes S=%d G=%d V=%d H=%d W=%d", S, G, V, H, W);
   DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "dsr_preprocess_fwd: exactly one of shs/colors must be given");
   DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
@@ -1200,7 +1245,7 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   const int deg = shs ? sh_degree : -1;
 #define DSR_PRE(D)                                                                                     \
   k_preprocess<D><<<grid, NT, lds, st>>>(G, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, \
-                                         geom, radii, seg_count, lds > 0)
+                                         geom, radii, seg_count, lds > 0, layout)
   switch (deg) {
     case -1: DSR_PRE(-1); break;
     case 0: DSR_PRE(0); break;
@@ -1312,7 +1357,7 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
                        const float* shs, const float* cov6, const dsr_camera* cams, const float* geom,
                        const float* dgeom, const int32_t* scene_view_start, const int32_t* scene_views,
                        float* dmeans, float* dshs, float* dcolors, float* dopac, float* dcov6, float* dmean2D,
-                       void* stream) {
+                       int layout, void* stream) {
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_preprocess_bwd: bad sizes");
   DSPLAT_REQUIRE((shs != nullptr) == (dshs != nullptr), "dsr_preprocess_bwd: shs and dshs must both be given or both NULL");
   DSPLAT_REQUIRE(shs != nullptr || dcolors != nullptr, "dsr_preprocess_bwd: colors path needs dcolors");
@@ -1325,7 +1370,7 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   const int deg = shs ? sh_degree : -1;
 #define DSR_PREB(D)                                                                                              \
   k_preprocess_bwd<D><<<grid, NT, 0, st>>>(G, H, W, M, means, shs, cov6, cams, geom, dgeom, scene_view_start, \
-                                           scene_views, dmeans, dshs, dcolors, dopac, dcov6, dmean2D)
+                                           scene_views, dmeans, dshs, dcolors, dopac, dcov6, dmean2D, layout)
   switch (deg) {
     case -1: DSR_PREB(-1); break;
     case 0: DSR_PREB(0); break;

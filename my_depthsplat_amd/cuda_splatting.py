@@ -100,11 +100,13 @@ def render_views(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch
     # the camera_settings() math, as one device kernel (no torch op chain, no host sync)
     cams = raster.build_cameras(extrinsics, intrinsics, near, far, background_color.expand(V, 3), view_scene,
                                 scale_invariant)
-    shs = gaussian_sh_coefficients.transpose(-1, -2)  # b g xyz n -> b g n xyz
-    feats = shs if use_sh else shs[:, :, 0, :]
+    # The kernels read the decoder's layouts directly: harmonics [S,G,3,d_sh] (no
+    # "b g xyz n -> b g n xyz" copy) and full covariances through the triu gather (no
+    # [S,G,6] copy); gradients come back in the same layouts (upper triangle for cov).
+    feats = gaussian_sh_coefficients if use_sh else gaussian_sh_coefficients[..., 0]
     color, radii = raster.rasterize_views(
-        gaussian_means, feats, gaussian_opacities, _cov6(gaussian_covariances), cams, view_scene,
-        use_sh=use_sh, sh_degree=degree, image_height=h, image_width=w)
+        gaussian_means, feats, gaussian_opacities, gaussian_covariances, cams, view_scene,
+        use_sh=use_sh, sh_degree=degree, image_height=h, image_width=w, channel_major_sh=True)
     return (color, radii) if return_radii else color
 
 

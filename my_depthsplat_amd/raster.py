@@ -200,13 +200,25 @@ def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invar
     return cams
 
 
-def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W):
-    """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh) or [S,G,3]; opacities
-    [S,G]; cov6 [S,G,6]; cams [V,44]. Returns (color [V,3,H,W], RasterState)."""
+LAYOUT_SH_CHANNEL_MAJOR = 1  # feats [S,G,3,M] (Gaussians.harmonics) instead of [S,G,M,3]
+LAYOUT_COV_FULL = 2          # covariance [S,G,3,3] instead of cov6 [S,G,6]
+
+
+def input_layout(feats, cov6, use_sh, channel_major_sh):
+    lay = LAYOUT_COV_FULL if cov6.dim() >= 2 and tuple(cov6.shape[-2:]) == (3, 3) else 0
+    if use_sh and channel_major_sh:
+        lay |= LAYOUT_SH_CHANNEL_MAJOR
+    return lay
+
+
+def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0):
+    """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh; [S,G,3,M] with
+    LAYOUT_SH_CHANNEL_MAJOR) or [S,G,3]; opacities [S,G]; cov6 [S,G,6] (or [S,G,3,3] with
+    LAYOUT_COV_FULL); cams [V,44]. Returns (color [V,3,H,W], RasterState)."""
     lib = _lib.load()
     _lib.require_gpu(means, feats, opacities, cov6, cams)
     S, G = means.shape[0], means.shape[1]
-    M = feats.shape[2] if use_sh else 0
+    M = (feats.shape[3] if layout & LAYOUT_SH_CHANNEL_MAJOR else feats.shape[2]) if use_sh else 0
     dev = means.device
     gx, gy = tiles(H, W)
     T = gx * gy
@@ -218,7 +230,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W)
         S, G, V, H, W, sh_degree if use_sh else -1, M, means.data_ptr(),
         feats.data_ptr() if use_sh else None, None if use_sh else feats.data_ptr(),
         opacities.data_ptr(), cov6.data_ptr(), cams.data_ptr(), geom.data_ptr(), radii.data_ptr(),
-        seg_count.data_ptr(), st), "dsr_preprocess_fwd")
+        seg_count.data_ptr(), layout, st), "dsr_preprocess_fwd")
     seg_start = torch.empty(V * T + 1, dtype=torch.int32, device=dev)
     cursor = torch.empty(V * T, dtype=torch.int32, device=dev)
     totals = torch.empty(4, dtype=torch.int32, device=dev)
@@ -256,11 +268,11 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W)
 
 
 def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, state: RasterState,
-                 dcolor, want_mean2d: bool):
+                 dcolor, want_mean2d: bool, layout=0):
     lib = _lib.load()
     S, G = means.shape[0], means.shape[1]
     V, _, H, W = dcolor.shape
-    M = feats.shape[2] if use_sh else 0
+    M = (feats.shape[3] if layout & LAYOUT_SH_CHANNEL_MAJOR else feats.shape[2]) if use_sh else 0
     dev = means.device
     st = _lib.stream_of(dev)
     dcolor = dcolor.contiguous().float()
@@ -279,60 +291,65 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     dmeans = torch.empty((S, G, 3), dtype=torch.float32, device=dev)
     dfeat = torch.empty_like(feats, dtype=torch.float32)
     dopac = torch.empty((S, G), dtype=torch.float32, device=dev)
-    dcov6 = torch.empty((S, G, 6), dtype=torch.float32, device=dev)
+    dcov6 = torch.empty_like(cov6, dtype=torch.float32)
     dmean2d = torch.empty((V, G, 3), dtype=torch.float32, device=dev) if want_mean2d else None
     _lib.check(lib.dsr_preprocess_bwd(
         S, G, V, H, W, sh_degree if use_sh else -1, M, means.data_ptr(), feats.data_ptr() if use_sh else None,
         cov6.data_ptr(), cams.data_ptr(), state.geom.data_ptr(), dgeom.data_ptr(), idx.data_ptr(),
         idx[S + 1:].data_ptr(), dmeans.data_ptr(), dfeat.data_ptr() if use_sh else None,
         None if use_sh else dfeat.data_ptr(), dopac.data_ptr(), dcov6.data_ptr(),
-        None if dmean2d is None else dmean2d.data_ptr(), st), "dsr_preprocess_bwd")
+        None if dmean2d is None else dmean2d.data_ptr(), layout, st), "dsr_preprocess_bwd")
     return dmeans, dfeat, dopac, dcov6, dmean2d, dgeom
 
 
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, means, feats, opacities, cov6, means2d, cams, view_scene, use_sh, sh_degree, H, W):
+    def forward(ctx, means, feats, opacities, cov6, means2d, cams, view_scene, use_sh, sh_degree, H, W, layout):
         V = len(view_scene)
-        color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W)
+        color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout)
         ctx.save_for_backward(means, feats, opacities, cov6, cams)
         ctx.state = state
-        ctx.meta = (view_scene, use_sh, sh_degree, None if means2d is None else means2d.shape)
+        ctx.meta = (view_scene, use_sh, sh_degree, None if means2d is None else means2d.shape, layout)
         ctx.mark_non_differentiable(state.radii)
         return color, state.radii
 
     @staticmethod
     def backward(ctx, dcolor, _dradii):
         means, feats, opacities, cov6, cams = ctx.saved_tensors
-        view_scene, use_sh, sh_degree, m2d_shape = ctx.meta
+        view_scene, use_sh, sh_degree, m2d_shape, layout = ctx.meta
         want_m2d = m2d_shape is not None and ctx.needs_input_grad[4]
         dmeans, dfeat, dopac, dcov6, dmean2d, _ = backward_raw(
             means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, ctx.state, dcolor,
-            want_mean2d=want_m2d)
+            want_mean2d=want_m2d, layout=layout)
         if dmean2d is not None:
             dmean2d = dmean2d.view(m2d_shape)
-        return dmeans, dfeat, dopac, dcov6, dmean2d, None, None, None, None, None, None
+        return dmeans, dfeat, dopac, dcov6, dmean2d, None, None, None, None, None, None, None
 
 
 def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.Tensor, cov6: torch.Tensor,
                     cams: torch.Tensor, view_scene: list[int], *, use_sh: bool, sh_degree: int,
-                    image_height: int, image_width: int, means2d: torch.Tensor | None = None):
-    """Differentiable render of V views. means [S,G,3], feats [S,G,M,3] (SH, coefficient-major
-    like the rasterizer's `shs`) or [S,G,3] (colors_precomp), opacities [S,G], cov6 [S,G,6],
-    cams [V,44] from pack_cameras, view_scene[v] = scene index of view v.
-    Returns color [V,3,H,W] and radii [V,G] (int32)."""
+                    image_height: int, image_width: int, means2d: torch.Tensor | None = None,
+                    channel_major_sh: bool = False):
+    """Differentiable render of V views. means [S,G,3]; feats [S,G,M,3] (SH, coefficient-major
+    like the rasterizer's `shs`; [S,G,3,M] = Gaussians.harmonics with channel_major_sh) or
+    [S,G,3] (colors_precomp); opacities [S,G]; cov6 [S,G,6] or the full [S,G,3,3] matrices
+    (read through the reference's triu gather); cams [V,44] (pack_cameras / build_cameras);
+    view_scene[v] = scene index of view v. Returns color [V,3,H,W] and radii [V,G] (int32)."""
     S = means.shape[0]
     if len(view_scene) != cams.shape[0]:
         raise ValueError(f"view_scene has {len(view_scene)} entries for {cams.shape[0]} cameras")
     if any(not (0 <= s < S) for s in view_scene):
         raise ValueError(f"view_scene entries must be in [0, {S})")
-    if use_sh and not (0 <= sh_degree <= 3 and feats.shape[2] >= (sh_degree + 1) ** 2):
-        raise ValueError(f"unsupported sh_degree={sh_degree} for {feats.shape[2]} coefficients")
+    n_coef = (feats.shape[3] if channel_major_sh else feats.shape[2]) if use_sh else 0
+    if use_sh and not (0 <= sh_degree <= 3 and n_coef >= (sh_degree + 1) ** 2):
+        raise ValueError(f"unsupported sh_degree={sh_degree} for {n_coef} coefficients")
     if image_height <= 0 or image_width <= 0:
         raise ValueError("image size must be positive")
     f = lambda t: t.contiguous().float()  # noqa: E731
+    layout = input_layout(feats, cov6, use_sh, channel_major_sh)
     return _RasterizeViews.apply(f(means), f(feats), f(opacities), f(cov6), means2d, cams.contiguous(),
-                                 list(view_scene), use_sh, int(sh_degree), int(image_height), int(image_width))
+                                 list(view_scene), use_sh, int(sh_degree), int(image_height), int(image_width),
+                                 layout)
 
 
 def sh_degree_of(n_coeffs: int) -> int:

@@ -271,3 +271,39 @@ def test_equal_depth_ties_sorted_by_id(gpu, n_ties):
         oc, _, _ = o.image()
         assert float(np.abs(color[v].cpu().numpy() - oc).mean()) < 1e-4
         o.close()
+
+
+def test_reference_layout_gradients(gpu):
+    """render_views reads harmonics [S,G,3,d_sh] and full covariances in place; its
+    gradients must equal the reference path (transpose + triu gather, autograd)."""
+    from my_depthsplat_amd import raster
+    from my_depthsplat_amd.cuda_splatting import _cov6, render_views
+    from my_depthsplat_amd.synthetic import make_scene
+    sc = make_scene(batch=1, n_context=2, n_targets=2, height=48, width=64, seed=13, device=gpu)
+    g = sc.gaussians
+    v = 2
+    ext, K = sc.target_extrinsics[0], sc.target_intrinsics[0]
+    bg = torch.zeros(v, 3, device=gpu)
+    gp = torch.Generator(device=gpu).manual_seed(5)
+    dcol = torch.randn(v, 3, 48, 64, device=gpu, generator=gp)
+
+    def grads(fast):
+        m = g.means.clone().requires_grad_(True)
+        c = g.covariances.clone().requires_grad_(True)
+        h = g.harmonics.clone().requires_grad_(True)
+        o = g.opacities.clone().requires_grad_(True)
+        if fast:
+            img = render_views(ext, K, sc.near[0], sc.far[0], (48, 64), bg, m, c, h, o, [0, 0])
+        else:
+            cams = raster.build_cameras(ext, K, sc.near[0], sc.far[0], bg, [0, 0], True)
+            img, _ = raster.rasterize_views(m, h.transpose(-1, -2), o, _cov6(c), cams, [0, 0], use_sh=True,
+                                            sh_degree=2, image_height=48, image_width=64)
+        (img * dcol).sum().backward()
+        return img.detach(), m.grad, c.grad, h.grad, o.grad
+
+    a, b = grads(True), grads(False)
+    assert torch.equal(a[0], b[0])
+    for x, y, name in zip(a[1:], b[1:], ("means", "cov", "harmonics", "opacities")):
+        err = float((x - y).abs().max() / (y.abs().max() + 1e-12))
+        assert err < 1e-5, (name, err)
+    assert float(a[2][..., 1, 0].abs().max()) == 0.0  # lower triangle gets no gradient
