@@ -330,7 +330,7 @@ int dcv_warp_bwd(int B, int C, int H, int W, int D, const float* dout, const flo
   DSPLAT_REQUIRE(dout && intr && pose && depth && dfeature, "dcv_warp_bwd: null pointer");
   hipStream_t st = (hipStream_t)stream;
   const int HW = H * W;
-  if (int e = dsplat::check_hip(hipMemsetAsync(dfeature, 0, (size_t)B * C * HW * 4, st), "memset dfeature")) return e;
+  if (int e = dsplat::zero_async(dfeature, (size_t)B * C * HW * 4, st, "zero dfeature")) return e;
   k_warp_bwd<<<dim3((HW + 255) / 256, D, B), 256, 0, st>>>(C, H, W, D, dout, intr, pose, depth, clamp_min_depth,
                                                            dfeature);
   return dsplat::check_launch("k_warp_bwd");
@@ -359,7 +359,7 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
                  "dcv_cost_volume_bwd: null pointer");
   hipStream_t st = (hipStream_t)stream;
   const int HW = H * W;
-  if (int e = dsplat::check_hip(hipMemsetAsync(dtgt_hwc, 0, (size_t)B * J * HW * C * 4, st), "memset dtgt_hwc")) return e;
+  if (int e = dsplat::zero_async(dtgt_hwc, (size_t)B * J * HW * C * 4, st, "zero dtgt_hwc")) return e;
   k_cost_bwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
                                                    depth, clamp_min_depth, dcost, dref, dtgt_hwc);
   if (int e = dsplat::check_launch("k_cost_bwd")) return e;

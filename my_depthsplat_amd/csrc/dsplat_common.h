@@ -50,6 +50,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
   return v;
 }
 
+// Zero a buffer with a plain kernel rather than hipMemsetAsync: the fill must be an
+// ordinary kernel node when callers capture the stream into a hipGraph (a captured
+// small hipMemsetAsync was observed not to re-run on replays 2+, leaving stale counts).
+__global__ void k_zero_u32(uint32_t* __restrict__ p, size_t n);
+int zero_async(void* p, size_t bytes, hipStream_t st, const char* what);
+
 inline int tiles_x(int W) { return (W + DSR_TILE - 1) / DSR_TILE; }
 inline int tiles_y(int H) { return (H + DSR_TILE - 1) / DSR_TILE; }
 

@@ -12,6 +12,22 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+
+__global__ void k_zero_u32(uint32_t* __restrict__ p, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = 0u;
+}
+
+int zero_async(void* p, size_t bytes, hipStream_t st, const char* what) {
+  if (bytes == 0) return 0;
+  if (bytes % 4 != 0) {
+    set_error("%s: zero_async needs a multiple of 4 bytes (%zu)", what, bytes);
+    return 1;
+  }
+  const size_t n = bytes / 4;
+  const unsigned blocks = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  k_zero_u32<<<blocks, 256, 0, st>>>(static_cast<uint32_t*>(p), n);
+  return check_launch(what);
+}
 }  // namespace dsplat
 
 extern "C" {

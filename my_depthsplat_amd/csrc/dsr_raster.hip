@@ -824,10 +824,12 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
           const bool stop = ok && testT < 0.0001f;
           const bool blend = ok && !stop;
           done = done || stop;
-          const float wgt = blend ? alpha * Tr : 0.f;
-          C0 = fmaf(r.z, wgt, C0);
-          C1 = fmaf(r.w, wgt, C1);
-          C2 = fmaf(bp.x, wgt, C2);
+          // select the result, not the weight: a lane reading past the list end (u = 1,
+          // k + 1 == cnt) sees stale LDS that may hold NaN, and NaN * 0 is NaN
+          const float wgt = alpha * Tr;
+          C0 = blend ? fmaf(r.z, wgt, C0) : C0;
+          C1 = blend ? fmaf(r.w, wgt, C1) : C1;
+          C2 = blend ? fmaf(bp.x, wgt, C2) : C2;
           Tr = blend ? testT : Tr;
           last = blend ? __float_as_uint(bp.y) : last;
         }
@@ -1239,7 +1241,7 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   DSPLAT_REQUIRE(means && opacities && cov6 && cams && geom && radii && seg_count, "dsr_preprocess_fwd: null pointer");
   hipStream_t st = (hipStream_t)stream;
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H), T = gx * gy;
-  if (int e = dsplat::check_hip(hipMemsetAsync(seg_count, 0, (size_t)V * T * 4, st), "memset seg_count")) return e;
+  if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
   const int lds = lds_hist_bytes(T);
   dim3 grid((G + NT - 1) / NT, V);
   const int deg = shs ? sh_degree : -1;

@@ -53,12 +53,16 @@ def pack_cameras(viewmatrix: torch.Tensor, projmatrix: torch.Tensor, campos: tor
 
 
 class KernelTimer:
-    """HIP-event timing of each C-ABI launch on the stream it is enqueued on (bench.py)."""
+    """HIP-event timing of C-ABI launches on the stream they are enqueued on (bench.py).
+    `only`: restrict to these launch names (events perturb the timeline least)."""
 
-    def __init__(self):
+    def __init__(self, only=None):
         self.events: dict[str, list] = {}
+        self.only = None if only is None else set(only)
 
     def start(self, name):
+        if self.only is not None and name not in self.only:
+            return None
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         return name, e
@@ -94,7 +98,7 @@ def last_stats() -> dict:
 
 
 def _timed(name, fn, *args):
-    tok = _timer.start(name) if _timer is not None else None
+    tok = _timer.start(name) if _timer is not None and not torch.cuda.is_current_stream_capturing() else None
     r = fn(*args)
     if tok is not None:
         _timer.stop(tok)
@@ -151,6 +155,8 @@ _inflight: list = []  # (pinned int32[4], event) read-backs of totals, consumed 
 def _note_totals(totals: torch.Tensor) -> None:
     """Queue a non-blocking copy of (N, max count) to pinned memory; completed copies from
     earlier calls update the LDS-sort size hint. Never waits on the device."""
+    if torch.cuda.is_current_stream_capturing():
+        return  # inside a hipGraph capture: no host-side bookkeeping (hint stays fixed)
     while _inflight and _inflight[0][1].query():
         host, _ = _inflight.pop(0)
         _spec["max_count"] = int(host[1])
@@ -239,6 +245,9 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     cap = _key_capacity(V, G, T)
     lds_cap = lib.dsr_sort_lds_capacity()
     if cap is None:  # too large for the worst-case buffer: one small read-back
+        if torch.cuda.is_current_stream_capturing():
+            raise _lib.DsplatError(f"V*G*tiles = {V * G * T} key slots exceed KEY_BUDGET_BYTES: this size needs a "
+                                   "host read-back and cannot be captured into a graph")
         tot = totals[:2].cpu()
         N, maxc = int(tot[0]), int(tot[1])
         cap = max(N, 1)
