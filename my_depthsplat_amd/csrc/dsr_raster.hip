@@ -724,10 +724,82 @@ __device__ __forceinline__ uint32_t subtile_mask(float4 q, float4 r, int tx0, in
   return m;
 }
 
-// K6: front-to-back compositing. grid = (gx, gy, V), block = 256 (4 waves x 8x8 pixels).
-// Each wave copies the records of the entries its sub-tile needs into its own contiguous
-// LDS list (no index indirection in the hot loop); every lane then walks that list with
-// branch-free compositing, reading the next record before compositing the current one.
+// Can the alpha >= 1/255 region of a Gaussian reach any pixel centre of the 8x8 sub-tile
+// [x0, x0 + 7] x [y0, y0 + 7]? Exact for the continuous box (conservative for the pixel
+// centres in it): with Q(d) = a dx^2 + 2b dx dy + c dy^2 (the conic; power = -Q/2) and
+// alpha = min(.99, o e^power), alpha >= 1/255 needs Q(d) <= t2 = 2 ln(255 o). Q is convex,
+// so its minimum over the box is 0 when the centre is inside, else on one of the 4 edges,
+// where it is a clamped 1-D quadratic. The margin absorbs the rounding of the compositing
+// arithmetic, so the entries dropped here are exactly ones the per-pixel test would skip.
+// Degenerate / NaN conics are kept.
+__device__ __forceinline__ bool subtile_hit(float4 q, float4 r, float x0, float y0) {
+  const float op = r.y;
+  if (!(op >= 1.0f / 255.0f)) return false;
+  const float a = q.z, b = q.w, c = r.x;
+  const float t2 = 2.0f * __logf(255.0f * op) * 1.002f + 0.02f;
+  const float lx = x0 - q.x, hx = x0 + (SUB - 1) - q.x;  // box relative to the centre
+  const float ly = y0 - q.y, hy = y0 + (SUB - 1) - q.y;
+  if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;
+  if (lx <= 0.f && hx >= 0.f && ly <= 0.f && hy >= 0.f) return true;
+  const float ia = 1.0f / a, ic = 1.0f / c;
+  float m = 3.4e38f;
+  // edges x = const
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float dx = k ? hx : lx;
+    const float dy = fminf(fmaxf(-b * dx * ic, ly), hy);
+    m = fminf(m, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
+  }
+  // edges y = const
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float dy = k ? hy : ly;
+    const float dx = fminf(fmaxf(-b * dy * ia, lx), hx);
+    m = fminf(m, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
+  }
+  return !(m > t2);
+}
+
+#ifndef RF_EPL
+#define RF_EPL 1
+#endif
+constexpr int EPL = RF_EPL;      // list entries per lane per chunk
+constexpr int CH = 64 * EPL;     // entries per chunk
+// one compacted list entry: q = (x, y, A, C), r = (B, opacity, red, green), bp = (blue, pos)
+struct __align__(16) ListRec {
+  float4 q;
+  float4 r;
+  float2 bp;
+  float2 pad;
+};
+
+// One compositing step (upstream renderCUDA semantics). A pixel that has stopped keeps a
+// negative T (its magnitude is the final T): for it testT <= 0, so nothing blends again.
+__device__ __forceinline__ void composite_step(const ListRec& e, float pfx, float pfy, float& Tr, float& C0,
+                                               float& C1, float& C2, uint32_t& last) {
+  const float dx = e.q.x - pfx, dy = e.q.y - pfy;
+  const float p2 = falloff_p2(e.q.z, e.r.x, e.q.w, dx, dy);
+  const float alpha = fminf(0.99f, e.r.y * __builtin_amdgcn_exp2f(p2));
+  const bool ok = p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+  const float testT = Tr * (1 - alpha);
+  const bool stop = ok && testT < 0.0001f;
+  const bool blend = ok && !stop;
+  const float wgt = blend ? alpha * Tr : 0.0f;
+  C0 = fmaf(e.r.z, wgt, C0);
+  C1 = fmaf(e.r.w, wgt, C1);
+  C2 = fmaf(e.bp.x, wgt, C2);
+  Tr = blend ? testT : (stop ? -fabsf(Tr) : Tr);
+  last = blend ? __float_as_uint(e.bp.y) : last;
+}
+
+// K6: front-to-back compositing. grid = (gx, gy, V), block = 256 = 4 independent waves;
+// wave w owns the 8x8 sub-tile (w & 1, w >> 1) of the tile. There is no workgroup barrier:
+// each wave walks the tile's list CH entries at a time (EPL keys + records per lane, the
+// next chunk's records and the chunk after's keys already in flight), keeps the entries that
+// can reach its sub-tile in a wave-private LDS list (ballot compaction, list order kept, 4
+// zero-opacity pad records after the end), and composites that list four entries per step
+// with the next four records read ahead. A wave retires as soon as its own 64 pixels have
+// terminated; the waves of a workgroup share the tile's keys/records through L1.
 __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, int T,
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
@@ -735,117 +807,112 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
                                                    const uint64_t* __restrict__ keys,
                                                    float* __restrict__ out, float* __restrict__ finalT,
                                                    uint32_t* __restrict__ ncontrib) {
-  __shared__ float4 s_q[NT];        // staged: x, y, conic a, conic b
-  __shared__ float4 s_r[NT];        // staged: conic c, opacity, r, g
-  __shared__ float s_bl[NT];        // staged: b
-  __shared__ uint32_t s_mask[NT];   // staged: sub-tile mask
-  __shared__ float4 w_q[4][NT];     // per-wave lists
-  __shared__ float4 w_r[4][NT];
-  __shared__ float2 w_bp[4][NT];    // (b, list position bits)
+  __shared__ ListRec l_rec[4][CH + 4];
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int tx0 = blockIdx.x * BX, ty0 = blockIdx.y * BY;
-  const int px = tx0 + (w & 1) * SUB + (lane & (SUB - 1));
-  const int py = ty0 + (w >> 1) * SUB + (lane >> 3);
+  const int sx0 = blockIdx.x * BX + (w & 1) * SUB, sy0 = blockIdx.y * BY + (w >> 1) * SUB;
+  const int px = sx0 + (lane & (SUB - 1));
+  const int py = sy0 + (lane >> 3);
   const bool inside = px < W && py < H;
   const int seg = v * T + blockIdx.y * gx + blockIdx.x;
   const uint32_t start = seg_start[seg], end = seg_start[seg + 1];
   const float pfx = (float)px, pfy = (float)py;
+  const float fx0 = (float)sx0, fy0 = (float)sy0;
   const float* gv = geom + (size_t)v * G * GS;
   const uint64_t lt = dsplat::lanemask_lt(lane);
-  bool done = !inside;
-  float Tr = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
+  ListRec* list = l_rec[w];
+  float Tr = inside ? 1.0f : -1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
   uint32_t last = 0;
-  // software pipeline over 256-entry batches: the record of batch b+1 and the key of
-  // batch b+2 are in flight while batch b is composited (two dependent HBM/L2 round
-  // trips per batch otherwise dominate: ~3000 entries per tile at 256x256)
-  auto load_rec = [&](uint32_t e, float4& q, float4& r, float& bb) {
+  float4 cq[EPL], cr[EPL];
+  float cb[EPL];
+  uint32_t nid[EPL];
+#pragma unroll
+  for (int u = 0; u < EPL; ++u) {
+    const uint32_t e = start + u * 64 + lane;
+    cq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    cr[u] = cq[u];
+    cb[u] = 0.f;
     if (e < end) {
-      const uint32_t id = (uint32_t)keys[e];
-      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
-      q = rec[0];
-      r = rec[1];
-      bb = rec[2].x;
+      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)(uint32_t)keys[e] * GS);
+      cq[u] = rec[0];
+      cr[u] = rec[1];
+      cb[u] = rec[2].x;
     }
-  };
-  float4 cq = make_float4(0.f, 0.f, 0.f, 0.f), cr = cq;
-  float cb = 0.f;
-  load_rec(start + tid, cq, cr, cb);
-  for (uint32_t base = start; base < end; base += NT) {
-    if (__syncthreads_count(done) == NT) break;
-    const uint32_t i = base + tid;
-    float4 nq = make_float4(0.f, 0.f, 0.f, 0.f), nr = nq;
-    float nb = 0.f;
-    load_rec(i + NT, nq, nr, nb);  // next batch, consumed next iteration
-    const uint32_t m = i < end ? subtile_mask(cq, cr, tx0, ty0) : 0u;
-    s_q[tid] = cq;
-    s_r[tid] = cr;
-    s_bl[tid] = cb;
-    s_mask[tid] = m;
-    cq = nq;
-    cr = nr;
-    cb = nb;
-    __syncthreads();
+    const uint32_t e1 = e + CH;
+    nid[u] = e1 < end ? (uint32_t)keys[e1] : 0xffffffffu;
+  }
+  for (uint32_t base = start; base < end && !__all(Tr < 0.0f); base += CH) {
+    float4 nq[EPL], nr[EPL];
+    float nb[EPL];
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) {
+      nq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      nr[u] = nq[u];
+      nb[u] = 0.f;
+      if (nid[u] != 0xffffffffu) {
+        const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)nid[u] * GS);
+        nq[u] = rec[0];
+        nr[u] = rec[1];
+        nb[u] = rec[2].x;
+      }
+      const uint32_t e2 = base + 2 * CH + u * 64 + lane;
+      nid[u] = e2 < end ? (uint32_t)keys[e2] : 0xffffffffu;
+    }
     int cnt = 0;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int e = c * 64 + lane;
-      const bool mine = (s_mask[e] >> w) & 1u;
+    for (int u = 0; u < EPL; ++u) {
+      const uint32_t e = base + u * 64 + lane;
+      const bool mine = e < end && subtile_hit(cq[u], cr[u], fx0, fy0);
       const uint64_t bal = __ballot(mine);
       if (mine) {
-        const int slot = cnt + __popcll(bal & lt);
-        const float4 rr = s_r[e];
-        w_q[w][slot] = scaled_conic_q(s_q[e]);
-        w_r[w][slot] = make_float4(-0.5f * kLog2e * rr.x, rr.y, rr.z, rr.w);
-        w_bp[w][slot] = make_float2(s_bl[e], __uint_as_float(base - start + (uint32_t)e + 1u));
+        const float4 sq = scaled_conic_q(cq[u]);  // (x, y, A, B)
+        ListRec& d = list[cnt + __popcll(bal & lt)];
+        d.q = make_float4(sq.x, sq.y, sq.z, -0.5f * kLog2e * cr[u].x);
+        d.r = make_float4(sq.w, cr[u].y, cr[u].z, cr[u].w);
+        d.bp = make_float2(cb[u], __uint_as_float(e - start + 1u));
       }
       cnt += __popcll(bal);
     }
+    if (lane < 4) {  // pad: opacity 0 -> alpha 0 -> never blends
+      ListRec& d = list[cnt + lane];
+      d.q = make_float4(0.f, 0.f, 0.f, 0.f);
+      d.r = d.q;
+      d.bp = make_float2(0.f, 0.f);
+    }
     __builtin_amdgcn_wave_barrier();
-    if (cnt > 0 && !__all(done)) {
-      // two entries per step: both records are read before either is composited
-      for (int k = 0; k < cnt; k += 2) {
-        const float4 qa = w_q[w][k], ra = w_r[w][k];
-        const float2 ba = w_bp[w][k];
-        const int k1 = min(k + 1, NT - 1);
-        const float4 qb = w_q[w][k1], rb = w_r[w][k1];
-        const float2 bb = w_bp[w][k1];
-        const bool has_b = k + 1 < cnt;
+    const ListRec* p = list;
+    ListRec e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
+    for (int k = 0; k < cnt; k += 4) {
+      p += 4;
+      const ListRec f0 = p[0], f1 = p[1], f2 = p[2], f3 = p[3];  // in bounds: k + 7 <= CH + 3
+      composite_step(e0, pfx, pfy, Tr, C0, C1, C2, last);
+      composite_step(e1, pfx, pfy, Tr, C0, C1, C2, last);
+      composite_step(e2, pfx, pfy, Tr, C0, C1, C2, last);
+      composite_step(e3, pfx, pfy, Tr, C0, C1, C2, last);
+      if (__all(Tr < 0.0f)) break;
+      e0 = f0;
+      e1 = f1;
+      e2 = f2;
+      e3 = f3;
+    }
+    __builtin_amdgcn_wave_barrier();  // list reads of this chunk before the next chunk's writes
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const float4 q = u ? qb : qa;
-          const float4 r = u ? rb : ra;
-          const float2 bp = u ? bb : ba;
-          const float dx = q.x - pfx, dy = q.y - pfy;
-          const float p2 = falloff_p2(q.z, q.w, r.x, dx, dy);
-          const float alpha = fminf(0.99f, r.y * __builtin_amdgcn_exp2f(p2));
-          const bool ok = (u == 0 || has_b) && !done && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
-          const float testT = Tr * (1 - alpha);
-          const bool stop = ok && testT < 0.0001f;
-          const bool blend = ok && !stop;
-          done = done || stop;
-          // select the result, not the weight: a lane reading past the list end (u = 1,
-          // k + 1 == cnt) sees stale LDS that may hold NaN, and NaN * 0 is NaN
-          const float wgt = alpha * Tr;
-          C0 = blend ? fmaf(r.z, wgt, C0) : C0;
-          C1 = blend ? fmaf(r.w, wgt, C1) : C1;
-          C2 = blend ? fmaf(bp.x, wgt, C2) : C2;
-          Tr = blend ? testT : Tr;
-          last = blend ? __float_as_uint(bp.y) : last;
-        }
-        if (__all(done)) break;
-      }
+    for (int u = 0; u < EPL; ++u) {
+      cq[u] = nq[u];
+      cr[u] = nr[u];
+      cb[u] = nb[u];
     }
   }
   if (inside) {
     const size_t HW = (size_t)H * W;
     const size_t pix = (size_t)py * W + px;
     const float* bg = cams[v].bg;
-    finalT[v * HW + pix] = Tr;
+    const float Tf = fabsf(Tr);
+    finalT[v * HW + pix] = Tf;
     ncontrib[v * HW + pix] = last;
-    out[(size_t)v * 3 * HW + pix] = C0 + Tr * bg[0];
-    out[(size_t)v * 3 * HW + HW + pix] = C1 + Tr * bg[1];
-    out[(size_t)v * 3 * HW + 2 * HW + pix] = C2 + Tr * bg[2];
+    out[(size_t)v * 3 * HW + pix] = C0 + Tf * bg[0];
+    out[(size_t)v * 3 * HW + HW + pix] = C1 + Tf * bg[1];
+    out[(size_t)v * 3 * HW + 2 * HW + pix] = C2 + Tf * bg[2];
   }
 }
 
