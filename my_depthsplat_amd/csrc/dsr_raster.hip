@@ -61,6 +61,44 @@ __device__ __forceinline__ void tile_rect(float px, float py, int r, int gx, int
   y1 = min(gy, max(0, (int)((py + r + BY - 1) / BY)));
 }
 
+// Per-wave balanced expansion of tile rectangles: the wave's (Gaussian, tile) pairs are
+// numbered by an exclusive scan of the rect areas and handed out 64 at a time, so one lane
+// with a huge rect no longer serialises its whole wave (radii are heavy-tailed: a few
+// Gaussians touch hundreds of tiles, the median touches one or two). f(tile, owner lane)
+// runs once per pair; ws_* are this wave's 64-entry LDS slots.
+struct WaveRects {
+  uint32_t ex[64];    // exclusive scan of areas
+  uint32_t org[64];   // x0 | y0 << 16
+  uint32_t wid[64];   // rect width in tiles
+};
+template <typename F>
+__device__ __forceinline__ void for_each_rect_tile(WaveRects& wr, int lane, int x0, int y0, int x1, int y1,
+                                                   bool has, int gx, F f) {
+  const uint32_t area = has ? (uint32_t)((x1 - x0) * (y1 - y0)) : 0u;
+  const uint32_t incl = dsplat::wave_incl_scan(area, lane);
+  const uint32_t total = __shfl(incl, 63, 64);
+  wr.ex[lane] = incl - area;
+  wr.org[lane] = (uint32_t)x0 | ((uint32_t)y0 << 16);
+  wr.wid[lane] = (uint32_t)max(x1 - x0, 1);
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t j = lane; j < total; j += 64) {
+    // owner = last lane with ex <= j (a zero-area lane never is: its successor has the same ex)
+    int o = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1)
+      if (wr.ex[o + step] <= j) o += step;
+    const uint32_t local = j - wr.ex[o];
+    const uint32_t wd = wr.wid[o];
+    uint32_t dy = (uint32_t)(((float)local + 0.5f) * (1.0f / (float)wd));
+    if (dy * wd > local) --dy;
+    if ((dy + 1) * wd <= local) ++dy;
+    const uint32_t dx = local - dy * wd;
+    const uint32_t og = wr.org[o];
+    f((int)(((og >> 16) + dy) * (uint32_t)gx + (og & 0xFFFFu) + dx), o);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 struct Cov2D {
   float T[2][3];
   float a, b, c;
@@ -149,6 +187,10 @@ __device__ __forceinline__ float load_cov(const float* cov, size_t sg, int k, in
 template <int NC>
 __device__ __forceinline__ void load_sh(const float* shs, size_t sg, int M, int layout, float* out) {
   const float* p = shs + sg * (size_t)M * 3;
+#ifdef PP_NOSH
+  for (int k = 0; k < NC * 3; ++k) out[k] = 0.01f * k + (float)(sg & 7);
+  return;
+#endif
   if (layout & kLayoutShChannelMajor) {
 #pragma unroll
     for (int k = 0; k < NC; ++k)
@@ -256,15 +298,14 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
     radii[(size_t)v * G + g] = r;
   }
   uint32_t* gcount = seg_count + (size_t)v * T;
-  if (r > 0) {
-    for (int y = y0; y < y1; ++y)
-      for (int x = x0; x < x1; ++x) {
-        if (lds_hist)
-          atomicAdd(&s_hist[y * gx + x], 1u);
-        else
-          atomicAdd(&gcount[y * gx + x], 1u);
-      }
-  }
+  __shared__ WaveRects s_wr[NT / 64];
+  const int lane = tid & 63;
+  if (lds_hist)
+    for_each_rect_tile(s_wr[tid >> 6], lane, x0, y0, x1, y1, r > 0, gx,
+                       [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
+  else
+    for_each_rect_tile(s_wr[tid >> 6], lane, x0, y0, x1, y1, r > 0, gx,
+                       [&](int t, int) { atomicAdd(&gcount[t], 1u); });
   if (lds_hist) {
     __syncthreads();
     for (int t = tid; t < T; t += NT) {
@@ -342,22 +383,25 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int gx, int gy, const flo
     }
   }
   uint32_t* gcur = cursor + (size_t)v * T;
+  __shared__ WaveRects s_wr[NT / 64];
+  __shared__ uint64_t s_key[NT];
+  const int lane = tid & 63, w = tid >> 6;
+  s_key[tid] = key;
+  WaveRects& wr = s_wr[w];
+  const uint64_t* wkey = s_key + w * 64;
   if (lds_hist) {
-    if (r > 0)
-      for (int y = y0; y < y1; ++y)
-        for (int x = x0; x < x1; ++x) atomicAdd(&s_hist[y * gx + x], 1u);
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
     __syncthreads();
     for (int t = tid; t < T; t += NT) {
       const uint32_t c = s_hist[t];
       if (c) s_hist[t] = atomicAdd(&gcur[t], c);
     }
     __syncthreads();
-    if (r > 0)
-      for (int y = y0; y < y1; ++y)
-        for (int x = x0; x < x1; ++x) keys[atomicAdd(&s_hist[y * gx + x], 1u)] = key;
-  } else if (r > 0) {
-    for (int y = y0; y < y1; ++y)
-      for (int x = x0; x < x1; ++x) keys[atomicAdd(&gcur[y * gx + x], 1u)] = key;
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
+                       [&](int t, int o) { keys[atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
+  } else {
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
+                       [&](int t, int o) { keys[atomicAdd(&gcur[t], 1u)] = wkey[o]; });
   }
 }
 
@@ -917,10 +961,62 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
 }
 
 // ------------------------------------------------------------------------------------
-// K7: back-to-front gradient of the compositing (same 4 x 8x8 sub-tile culling). Per
-// entry, the 64 pixel contributions of a wave are summed with shuffles, the 4 waves
-// combine through LDS float atomics, and each staged batch is flushed with one global
-// atomic per (Gaussian, component) per tile instead of one per pixel.
+// Wave64 sum with DPP (no LDS round trips): after the 4 row shifts lane 15 of each row holds
+// its row's sum; row_bcast:15 / row_bcast:31 fold the rows so lane 63 ends with the total.
+__device__ __forceinline__ float dpp_add(float v, float t) { return v + t; }
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_step(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, true));
+}
+__device__ __forceinline__ float wave_sum_to_lane63(float v) {
+  v = dpp_step<0x111, 0xf>(v);  // row_shr:1
+  v = dpp_step<0x112, 0xf>(v);  // row_shr:2
+  v = dpp_step<0x114, 0xf>(v);  // row_shr:4
+  v = dpp_step<0x118, 0xf>(v);  // row_shr:8
+  v = dpp_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v = dpp_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+
+// The same reduction for 9 values at once with fused v_add_f32_dpp: each step is issued for
+// all 9 values before the next, so no DPP read follows the write of its operand closer than
+// the 2 wait states the hardware needs (one s_nop covers the compiler-scheduled producers).
+#define DSR_DPP9(ctrl)                                                                              \
+  asm volatile("v_add_f32_dpp %0, %0, %0 " ctrl "\n v_add_f32_dpp %1, %1, %1 " ctrl                \
+               "\n v_add_f32_dpp %2, %2, %2 " ctrl "\n v_add_f32_dpp %3, %3, %3 " ctrl               \
+               "\n v_add_f32_dpp %4, %4, %4 " ctrl "\n v_add_f32_dpp %5, %5, %5 " ctrl               \
+               "\n v_add_f32_dpp %6, %6, %6 " ctrl "\n v_add_f32_dpp %7, %7, %7 " ctrl               \
+               "\n v_add_f32_dpp %8, %8, %8 " ctrl                                                    \
+               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), "+v"(a8))
+__device__ __forceinline__ void wave_sum9_to_lane63(float& a0, float& a1, float& a2, float& a3, float& a4,
+                                                    float& a5, float& a6, float& a7, float& a8) {
+  asm volatile("s_nop 1" ::: "memory");
+  DSR_DPP9("row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1");
+  DSR_DPP9("row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1");
+  DSR_DPP9("row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1");
+  DSR_DPP9("row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1");
+  DSR_DPP9("row_bcast:15 row_mask:0xa bank_mask:0xf");
+  DSR_DPP9("row_bcast:31 row_mask:0xc bank_mask:0xf");
+  asm volatile("s_nop 1" ::: "memory");
+}
+#undef DSR_DPP9_UNUSED
+
+// one compacted backward list entry
+struct __align__(16) BwdRec {
+  float4 q;   // x, y, A, C (scaled conic, as in the forward)
+  float4 r;   // B, opacity, red, green
+  float4 s;   // blue, conic a, b, c
+  uint32_t id, pos, pad0, pad1;
+};
+
+// K7: back-to-front gradient of the compositing (upstream renderCUDA backward semantics).
+// Same wave layout as K6: wave w owns sub-tile (w & 1, w >> 1), waves are independent. Each
+// wave walks the tile list backwards from the largest n_contrib of its pixels, CH entries at a
+// time: entries that can reach its sub-tile (same exact test as the forward) go to a
+// wave-private LDS list; per entry the 64 pixel gradients (9 values) are summed with DPP and
+// lane 63 parks the sums in LDS; at the end of the chunk the wave adds them to dgeom with
+// one global atomic per non-zero (entry, component).
+constexpr int BCH = 64;
 __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, int T,
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
@@ -930,29 +1026,26 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
                                                    const uint32_t* __restrict__ ncontrib,
                                                    const float* __restrict__ dpix,
                                                    float* __restrict__ dgeom) {
-  __shared__ float4 s_q[NT];
-  __shared__ float4 s_r[NT];
-  __shared__ float s_bl[NT];
-  __shared__ uint32_t s_id[NT];
-  __shared__ uint32_t s_mask[NT];
-  __shared__ uint16_t s_list[4][NT];
-  __shared__ float s_acc[NT * 9];
-  __shared__ uint32_t s_max;
+  __shared__ BwdRec l_rec[4][BCH + 1];
+  __shared__ float l_acc[4][BCH * 9];
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int tx0 = blockIdx.x * BX, ty0 = blockIdx.y * BY;
-  const int px = tx0 + (w & 1) * SUB + (lane & (SUB - 1));
-  const int py = ty0 + (w >> 1) * SUB + (lane >> 3);
+  const int sx0 = blockIdx.x * BX + (w & 1) * SUB, sy0 = blockIdx.y * BY + (w >> 1) * SUB;
+  const int px = sx0 + (lane & (SUB - 1));
+  const int py = sy0 + (lane >> 3);
   const bool inside = px < W && py < H;
   const int seg = v * T + blockIdx.y * gx + blockIdx.x;
   const uint32_t start = seg_start[seg], end = seg_start[seg + 1];
   const size_t HW = (size_t)H * W;
   const size_t pix = (size_t)py * W + px;
   const float pfx = (float)px, pfy = (float)py;
+  const float fx0 = (float)sx0, fy0 = (float)sy0;
   const float* gv = geom + (size_t)v * G * GS;
   float* dgv = dgeom + (size_t)v * G * GS;
   const float* bg = cams[v].bg;
   const uint64_t lt = dsplat::lanemask_lt(lane);
+  BwdRec* list = l_rec[w];
+  float* acc = l_acc[w];
   const float Tfin = inside ? finalT[v * HW + pix] : 0.f;
   const uint32_t lastc = inside ? ncontrib[v * HW + pix] : 0u;
   float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
@@ -962,104 +1055,102 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
     dp2 = dpix[(size_t)v * 3 * HW + 2 * HW + pix];
   }
   const float bg_dot = bg[0] * dp0 + bg[1] * dp1 + bg[2] * dp2;
-  if (tid == 0) s_max = 0;
-  __syncthreads();
-  atomicMax(&s_max, lastc);
-  __syncthreads();
-  const uint32_t nproc = min(end - start, s_max);
+  uint32_t wmax = lastc;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, off, 64));
+  const uint32_t nproc = min(end - start, wmax);
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   float Tr = Tfin;
   float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
   float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f, last_alpha = 0.f;
-  for (int hi = (int)nproc; hi > 0; hi -= NT) {
-    const int lo = max(0, hi - NT);
-    const int cnt = hi - lo;
-    uint32_t m = 0;
-    if (tid < cnt) {
-      const uint32_t id = (uint32_t)keys[start + lo + tid];
+  for (int hi = (int)nproc; hi > 0; hi -= BCH) {
+    const int lo = max(0, hi - BCH);
+    const uint32_t e = start + (uint32_t)(lo + lane);
+    bool mine = false;
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f), r = q;
+    float bl = 0.f;
+    uint32_t id = 0;
+    if (lo + lane < hi) {
+      id = (uint32_t)keys[e];
       const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
-      const float4 q = rec[0], r = rec[1];
-      s_q[tid] = q;
-      s_r[tid] = r;
-      s_bl[tid] = rec[2].x;
-      s_id[tid] = id;
-      m = subtile_mask(q, r, tx0, ty0);
+      q = rec[0];
+      r = rec[1];
+      bl = rec[2].x;
+      mine = subtile_hit(q, r, fx0, fy0);
     }
-    s_mask[tid] = m;
-    for (int k = tid; k < cnt * 9; k += NT) s_acc[k] = 0.f;
-    __syncthreads();
-    int n = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const bool mine = (s_mask[c * 64 + lane] >> w) & 1u;
-      const uint64_t bal = __ballot(mine);
-      if (mine) s_list[w][n + __popcll(bal & lt)] = (uint16_t)(c * 64 + lane);
-      n += __popcll(bal);
+    const uint64_t bal = __ballot(mine);
+    if (mine) {
+      BwdRec& d = list[__popcll(bal & lt)];
+      const float4 sq = scaled_conic_q(q);
+      d.q = make_float4(sq.x, sq.y, sq.z, -0.5f * kLog2e * r.x);
+      d.r = make_float4(sq.w, r.y, r.z, r.w);
+      d.s = make_float4(bl, q.z, q.w, r.x);
+      d.id = id;
+      d.pos = (uint32_t)(lo + lane);
     }
+    const int cnt = __popcll(bal);
     __builtin_amdgcn_wave_barrier();
-    for (int k = n - 1; k >= 0; --k) {
-      const int j = s_list[w][k];
-      const uint32_t pos = (uint32_t)(lo + j);
-      float g[9];
-#pragma unroll
-      for (int c = 0; c < 9; ++c) g[c] = 0.f;
-      bool act = false;
-      if (pos < lastc) {
-        const float4 q = s_q[j];
-        const float4 r = s_r[j];
-        const float dx = q.x - pfx, dy = q.y - pfy;
-        // same falloff sequence as k_render_fwd (decisions must agree with the forward)
-        const float p2 = falloff_p2(-0.5f * kLog2e * q.z, -kLog2e * q.w, -0.5f * kLog2e * r.x, dx, dy);
-        if (p2 <= 0.0f) {
-          const float Gs = __builtin_amdgcn_exp2f(p2);
-          const float alpha = fminf(0.99f, r.y * Gs);
-          if (alpha >= 1.0f / 255.0f) {
-            act = true;
-            Tr = Tr / (1.f - alpha);
-            const float dchannel_dcolor = alpha * Tr;
-            const float c0 = r.z, c1 = r.w, c2 = s_bl[j];
-            acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-            acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-            acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-            lc0 = c0;
-            lc1 = c1;
-            lc2 = c2;
-            float dL_dalpha = (c0 - acc0) * dp0;
-            dL_dalpha += (c1 - acc1) * dp1;
-            dL_dalpha += (c2 - acc2) * dp2;
-            g[6] = dchannel_dcolor * dp0;
-            g[7] = dchannel_dcolor * dp1;
-            g[8] = dchannel_dcolor * dp2;
-            dL_dalpha *= Tr;
-            last_alpha = alpha;
-            dL_dalpha += (-Tfin / (1.f - alpha)) * bg_dot;
-            const float dL_dG = r.y * dL_dalpha;
-            const float gdx = Gs * dx, gdy = Gs * dy;
-            const float dG_ddelx = -gdx * q.z - gdy * q.w;
-            const float dG_ddely = -gdy * r.x - gdx * q.w;
-            g[0] = dL_dG * dG_ddelx * ddelx_dx;
-            g[1] = dL_dG * dG_ddely * ddely_dy;
-            g[2] = -0.5f * gdx * dx * dL_dG;
-            g[3] = -0.5f * gdx * dy * dL_dG;
-            g[4] = -0.5f * gdy * dy * dL_dG;
-            g[5] = Gs * dL_dalpha;
-          }
-        }
+    BwdRec cur = list[max(cnt - 1, 0)];
+    for (int k = cnt - 1; k >= 0; --k) {
+      const BwdRec nxt = list[max(k - 1, 0)];  // read ahead
+      float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
+      const float dx = cur.q.x - pfx, dy = cur.q.y - pfy;
+      // same falloff sequence as k_render_fwd (decisions must agree with the forward)
+      const float p2 = falloff_p2(cur.q.z, cur.r.x, cur.q.w, dx, dy);
+      const float Gs = __builtin_amdgcn_exp2f(p2);
+      const float alpha = fminf(0.99f, cur.r.y * Gs);
+      const bool act = cur.pos < lastc && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+      if (act) {
+        Tr = Tr / (1.f - alpha);
+        const float dchannel_dcolor = alpha * Tr;
+        const float c0 = cur.r.z, c1 = cur.r.w, c2 = cur.s.x;
+        acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
+        acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
+        acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+        lc0 = c0;
+        lc1 = c1;
+        lc2 = c2;
+        float dL_dalpha = (c0 - acc0) * dp0;
+        dL_dalpha += (c1 - acc1) * dp1;
+        dL_dalpha += (c2 - acc2) * dp2;
+        g6 = dchannel_dcolor * dp0;
+        g7 = dchannel_dcolor * dp1;
+        g8 = dchannel_dcolor * dp2;
+        dL_dalpha *= Tr;
+        last_alpha = alpha;
+        dL_dalpha += (-Tfin / (1.f - alpha)) * bg_dot;
+        const float dL_dG = cur.r.y * dL_dalpha;
+        const float gdx = Gs * dx, gdy = Gs * dy;
+        const float dG_ddelx = -gdx * cur.s.y - gdy * cur.s.z;
+        const float dG_ddely = -gdy * cur.s.w - gdx * cur.s.z;
+        g0 = dL_dG * dG_ddelx * ddelx_dx;
+        g1 = dL_dG * dG_ddely * ddely_dy;
+        g2 = -0.5f * gdx * dx * dL_dG;
+        g3 = -0.5f * gdx * dy * dL_dG;
+        g4 = -0.5f * gdy * dy * dL_dG;
+        g5 = Gs * dL_dalpha;
       }
       if (__ballot(act) != 0ull) {
-#pragma unroll
-        for (int c = 0; c < 9; ++c) {
-          const float sum = dsplat::wave_sum(g[c]);
-          if (lane == 0) atomicAdd(&s_acc[j * 9 + c], sum);
+        wave_sum9_to_lane63(g0, g1, g2, g3, g4, g5, g6, g7, g8);
+        if (lane == 63) {
+          float* a9 = acc + k * 9;
+          a9[0] = g0; a9[1] = g1; a9[2] = g2; a9[3] = g3; a9[4] = g4;
+          a9[5] = g5; a9[6] = g6; a9[7] = g7; a9[8] = g8;
         }
+      } else if (lane == 63) {
+        float* a9 = acc + k * 9;
+#pragma unroll
+        for (int c = 0; c < 9; ++c) a9[c] = 0.f;
       }
+      cur = nxt;
     }
-    __syncthreads();
-    for (int k = tid; k < cnt * 9; k += NT) {
-      const float a = s_acc[k];
-      if (a != 0.f) atomicAdd(&dgv[(size_t)s_id[k / 9] * GS + (k % 9)], a);
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < cnt * 9; i += 64) {
+      const float a = acc[i];
+      const int k = i / 9;
+      if (a != 0.f) atomicAdd(&dgv[(size_t)list[k].id * GS + (i - k * 9)], a);
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
   }
 }
 

@@ -58,6 +58,42 @@ def main():
                 return lib.dsr_render_fwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(),
                                           state.seg_start.data_ptr(), state.keys.data_ptr(), out[0].data_ptr(),
                                           out[1].data_ptr(), out[2].data_ptr(), st)
+        elif a.kernel == "preprocess":
+            out = [torch.empty_like(state.geom), torch.empty_like(state.radii),
+                   torch.empty(V * state.seg_start.numel(), dtype=torch.int32, device=dev)]
+
+            def launch():
+                return lib.dsr_preprocess_fwd(1, G, V, H, W, 2, g.harmonics.shape[-1], g.means.data_ptr(),
+                                              g.harmonics.data_ptr(), None, g.opacities.data_ptr(),
+                                              g.covariances.data_ptr(), cams.data_ptr(), out[0].data_ptr(),
+                                              out[1].data_ptr(), out[2].data_ptr(), layout, st)
+        elif a.kernel == "scatter":  # scan + scatter (the scan resets the cursors)
+            cur = torch.empty_like(state.seg_start)
+            tot = torch.empty(4, dtype=torch.int32, device=dev)
+            out = [torch.empty_like(state.keys)]
+            seg_count = (state.seg_start[1:] - state.seg_start[:-1]).contiguous()
+            ss = torch.empty_like(state.seg_start)
+
+            def launch():
+                rc = lib.dsr_bin_scan(V, H, W, seg_count.data_ptr(), ss.data_ptr(), cur.data_ptr(), tot.data_ptr(),
+                                      st)
+                return rc or lib.dsr_bin_scatter(G, V, H, W, state.geom.data_ptr(), cur.data_ptr(),
+                                                 out[0].data_ptr(), st)
+        elif a.kernel == "sort":  # copy of the unsorted keys + sort
+            cur = torch.empty_like(state.seg_start)
+            tot = torch.empty(4, dtype=torch.int32, device=dev)
+            seg_count = (state.seg_start[1:] - state.seg_start[:-1]).contiguous()
+            ss = torch.empty_like(state.seg_start)
+            unsorted = torch.empty_like(state.keys)
+            lib.dsr_bin_scan(V, H, W, seg_count.data_ptr(), ss.data_ptr(), cur.data_ptr(), tot.data_ptr(), st)
+            lib.dsr_bin_scatter(G, V, H, W, state.geom.data_ptr(), cur.data_ptr(), unsorted.data_ptr(), st)
+            out = [torch.empty_like(state.keys)]
+            nk = int(state.totals[0])
+            maxc = int(state.totals[1])
+
+            def launch():
+                out[0][:nk].copy_(unsorted[:nk])
+                return lib.dsr_bin_sort(G, V, H, W, state.seg_start.data_ptr(), out[0].data_ptr(), None, maxc, st)
         else:
             out = [torch.zeros_like(state.geom)]
 
