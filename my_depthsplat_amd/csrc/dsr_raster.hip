@@ -548,32 +548,44 @@ __device__ void sort_segment(uint64_t* A, uint64_t* B, uint32_t n, int id_bits, 
 template <int KMAX>
 __device__ __forceinline__ uint32_t padi(uint32_t i) { return i + i / KMAX; }
 
+// digit of a key: ((32-bit word at word_shift) - dbase) >> shift & 15
 template <int KMAX>
-__device__ bool reg_pass(uint64_t* buf, uint32_t n, int shift, uint16_t* cnt, uint32_t* wsum) {
+__device__ __forceinline__ uint32_t key_digit(uint64_t k, int word_shift, uint32_t dbase, int shift) {
+  return (((uint32_t)(k >> word_shift) - dbase) >> shift) & 15u;
+}
+
+template <int KMAX>
+__device__ bool reg_pass(uint64_t* buf, uint32_t n, int word_shift, uint32_t dbase, int shift, uint16_t* cnt,
+                         uint32_t* wsum) {
   // in place: every key of the pass is in registers before the first barrier, so the
   // scatter can overwrite the same LDS buffer (one buffer -> more workgroups per CU)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t base = (uint32_t)tid * KMAX;
+  // registers: the keys, their within-thread ranks packed 4 per word (digits are recomputed
+  // at the scatter), and the 16 per-thread digit counters packed 8 per 64-bit word
   uint64_t k[KMAX];
-  uint32_t dg[KMAX], loc[KMAX];
+  uint32_t locp[(KMAX + 3) / 4];
+#pragma unroll
+  for (int i = 0; i < (KMAX + 3) / 4; ++i) locp[i] = 0u;
   uint64_t c_lo = 0, c_hi = 0;
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
     const uint32_t idx = base + i;
     const bool valid = idx < n;
     k[i] = valid ? buf[padi<KMAX>(idx)] : 0ull;
-    const uint32_t d = valid ? (uint32_t)(k[i] >> shift) & 15u : 16u;
-    dg[i] = d;
+    const uint32_t d = valid ? key_digit<KMAX>(k[i], word_shift, dbase, shift) : 16u;
     const uint32_t sh8 = 8u * (d & 7u);
+    uint32_t loc;
     if (d < 8u) {
-      loc[i] = (uint32_t)(c_lo >> sh8) & 255u;
+      loc = (uint32_t)(c_lo >> sh8) & 255u;
       c_lo += 1ull << sh8;
     } else {
-      loc[i] = (uint32_t)(c_hi >> sh8) & 255u;
+      loc = (uint32_t)(c_hi >> sh8) & 255u;
       if (d < 16u) c_hi += 1ull << sh8;
     }
+    locp[i / 4] |= loc << (8 * (i % 4));
   }
-  const uint32_t d0 = (uint32_t)(buf[0] >> shift) & 15u;  // digit of key 0 (broadcast read)
+  const uint32_t d0 = key_digit<KMAX>(buf[0], word_shift, dbase, shift);  // digit of key 0 (broadcast read)
 #pragma unroll
   for (int d = 0; d < 16; ++d) cnt[d * NT + tid] = (uint16_t)(((d < 8 ? c_lo : c_hi) >> (8 * (d & 7))) & 255u);
   __syncthreads();
@@ -616,51 +628,124 @@ __device__ bool reg_pass(uint64_t* buf, uint32_t n, int shift, uint16_t* cnt, ui
   if (s1 - s0 == n) return false;  // nothing written; the next pass re-reads buf
 #pragma unroll
   for (int i = 0; i < KMAX; ++i)
-    if (dg[i] < 16u) buf[padi<KMAX>((uint32_t)cnt[dg[i] * NT + tid] + loc[i])] = k[i];
+    if (base + i < n) {
+      const uint32_t d = key_digit<KMAX>(k[i], word_shift, dbase, shift);
+      const uint32_t loc = (locp[i / 4] >> (8 * (i % 4))) & 255u;
+      buf[padi<KMAX>((uint32_t)cnt[d * NT + tid] + loc)] = k[i];
+    }
   __syncthreads();
   return true;
 }
 
+// Sort of one segment in LDS. Keys are (depth bits << 32 | id), all distinct. The passes
+// only look at the 16 bits of (depth - min depth) below the highest bit in which the
+// segment's depths differ (4 passes instead of 8); keys that agree on those bits form runs
+// that are then put in full-key order by one thread each (insertion sort). Bits above the
+// range are common to every key and bits below the window only order keys inside a run, so
+// this is the full (depth, id) order. Runs longer than 32 (depths packed far tighter than the
+// segment's range) fall back to full-width passes: ids, then all 32 depth bits (stable).
 template <int KMAX>
 __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, uint32_t* wsum, uint32_t* flag) {
-  for (int sh = 32; sh < 64; sh += 4) reg_pass<KMAX>(A, n, sh, cnt, wsum);
-  if (threadIdx.x == 0) *flag = 0;
+  const int tid = threadIdx.x;
+  uint32_t mn = 0xffffffffu, mx = 0u;
+  for (uint32_t i = tid; i < n; i += NT) {
+    const uint32_t d = (uint32_t)(A[padi<KMAX>(i)] >> 32);
+    mn = min(mn, d);
+    mx = max(mx, d);
+  }
+  // block min / max: wave shuffles, then 4 wave results through LDS (flag[0..7])
+  const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+  }
+  if (lane == 0) {
+    flag[w] = mn;
+    flag[4 + w] = mx;
+  }
   __syncthreads();
-  uint32_t ties = 0;
-  for (uint32_t i = threadIdx.x; i + 1 < n; i += NT)
-    ties += (uint32_t)((A[padi<KMAX>(i)] >> 32) == (A[padi<KMAX>(i + 1)] >> 32));
-  if (ties) atomicAdd(flag, ties);
+  mn = min(min(flag[0], flag[1]), min(flag[2], flag[3]));
+  mx = max(max(flag[4], flag[5]), max(flag[6], flag[7]));
   __syncthreads();
-  ties = *flag;
-  __syncthreads();
-  if (ties != 0 && ties <= 32) {
-    for (uint32_t i = threadIdx.x; i + 1 < n; i += NT) {
-      const uint64_t d = A[padi<KMAX>(i)] >> 32;
-      if ((A[padi<KMAX>(i + 1)] >> 32) != d || (i > 0 && (A[padi<KMAX>(i - 1)] >> 32) == d)) continue;
-      uint32_t e = i + 1;
-      while (e < n && (A[padi<KMAX>(e)] >> 32) == d) ++e;
-      for (uint32_t k = i + 1; k < e; ++k) {
-        const uint64_t x = A[padi<KMAX>(k)];
-        uint32_t m = k;
-        while (m > i && A[padi<KMAX>(m - 1)] > x) {
-          A[padi<KMAX>(m)] = A[padi<KMAX>(m - 1)];
-          --m;
+  const uint32_t range = mx - mn;
+  const int msb = range ? 31 - __clz(range) : -1;
+  const int lo_shift = max(0, msb - 15);
+#ifdef SORT_DIAG_NOPASS
+  if (n > 100000)
+#endif
+  for (int sh = lo_shift; sh <= msb; sh += 4) reg_pass<KMAX>(A, n, 32, mn, sh, cnt, wsum);
+#ifdef SORT_DIAG_NOFIX
+  if (n < 100000) return;
+#endif
+#define pref(i) ((((uint32_t)(A[padi<KMAX>(i)] >> 32)) - mn) >> lo_shift)
+  // runs of keys equal on (depth - mn) >> lo_shift: thread t walks the runs that start in
+  // its KMAX positions and insertion-sorts each (full 64-bit keys; runs may extend past its
+  // range); the longest run decides whether the window was too coarse
+  uint32_t longest = 0;
+  {
+    // prefixes of positions i0 - 1 .. i0 + KMAX (independent LDS reads, all in flight)
+    const uint32_t i0 = (uint32_t)tid * KMAX;
+    uint32_t pf[KMAX + 2];
+#pragma unroll
+    for (int j = 0; j < KMAX + 2; ++j) {
+      const uint32_t i = i0 + (uint32_t)j - 1u;
+      pf[j] = (j > 0 || i0 > 0) && i0 + j - 1 < n ? pref(i) : 0xffffffffu - (uint32_t)j;
+    }
+    uint32_t starts = 0;  // bit j: a run (>= 2 equal prefixes) starts at i0 + j
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j)
+      if (i0 + j + 1 < n && pf[j + 1] != pf[j] && pf[j + 1] == pf[j + 2]) starts |= 1u << j;
+    while (starts) {
+      const int j = __builtin_ctz(starts);
+      starts &= starts - 1;
+      const uint32_t i = i0 + (uint32_t)j, p = pref(i);
+      uint32_t e = i + 2;
+      while (e < n && e - i <= 32 && pref(e) == p) ++e;
+      longest = max(longest, e - i);
+      if (e - i <= 32) {
+        if (e - i == 2) {
+          const uint64_t x0 = A[padi<KMAX>(i)], x1 = A[padi<KMAX>(i + 1)];
+          if (x0 > x1) {
+            A[padi<KMAX>(i)] = x1;
+            A[padi<KMAX>(i + 1)] = x0;
+          }
+        } else {
+          for (uint32_t k = i + 1; k < e; ++k) {
+            const uint64_t x = A[padi<KMAX>(k)];
+            uint32_t m = k;
+            while (m > i && A[padi<KMAX>(m - 1)] > x) {
+              A[padi<KMAX>(m)] = A[padi<KMAX>(m - 1)];
+              --m;
+            }
+            A[padi<KMAX>(m)] = x;
+          }
         }
-        A[padi<KMAX>(m)] = x;
       }
     }
-    __syncthreads();
-  } else if (ties > 32) {
-    for (int sh = 0; sh < id_bits; sh += 4) reg_pass<KMAX>(A, n, sh, cnt, wsum);
-    for (int sh = 32; sh < 64; sh += 4) reg_pass<KMAX>(A, n, sh, cnt, wsum);
   }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) longest = max(longest, (uint32_t)__shfl_xor((int)longest, off, 64));
+  if (lane == 0) flag[w] = longest;
+  __syncthreads();
+  longest = max(max(flag[0], flag[1]), max(flag[2], flag[3]));
+  __syncthreads();
+  if (longest <= 32) return;
+  {
+    for (int sh = 0; sh < id_bits; sh += 4) reg_pass<KMAX>(A, n, 0, 0u, sh, cnt, wsum);
+    for (int sh = 0; sh < 32; sh += 4) reg_pass<KMAX>(A, n, 32, 0u, sh, cnt, wsum);
+  }
+#undef pref
 }
 
 // One workgroup per (view, tile) segment. n <= 256*KMAX: sort in LDS. Larger: when
 // big_here, sort through HBM (keys <-> scratch) with the ballot-ranked passes; otherwise
 // leave it to k_sort_global.
+#ifndef SORT_WPE
+#define SORT_WPE 3
+#endif
 template <int KMAX>
-__global__ __launch_bounds__(NT) void k_sort_lds(const uint32_t* __restrict__ seg_start,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) void k_sort_lds(const uint32_t* __restrict__ seg_start,
                                                  uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
                                                  int id_bits, int big_here) {
   constexpr uint32_t cap = NT * KMAX;
@@ -694,7 +779,9 @@ __global__ __launch_bounds__(NT) void k_sort_lds(const uint32_t* __restrict__ se
     }
   }
   __syncthreads();
+#ifndef SORT_DIAG_NOSORT
   reg_sort<KMAX>(A, n, id_bits, cnt, wsum, flag);
+#endif
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
     const uint32_t idx = threadIdx.x + (uint32_t)i * NT;

@@ -243,14 +243,22 @@ def test_decoder_batched_views(gpu):
         assert torch.equal(out.color[b], want)
 
 
-@pytest.mark.parametrize("n_ties", [6, 100000])
+@pytest.mark.parametrize("n_ties", [6, 100000, -1])
 def test_equal_depth_ties_sorted_by_id(gpu, n_ties):
     """Equal view-space depths: a few tie pairs (insertion fix-up) and a fronto-parallel
     plane where every Gaussian shares one depth (full id-then-depth radix path). Order
     must match the oracle's stable sort (ties in Gaussian-id order) exactly."""
     sc = scene_inputs(h=64, w=64, seed=12)
     m = sc.gaussians.means.clone()
-    if n_ties >= m.shape[1]:
+    if n_ties < 0:
+        # a dense cluster a few ulps wide plus far outliers: the cluster falls in one bucket
+        # of the sort's 16-bit depth window (run > 32 -> full-width fallback passes)
+        G = m.shape[1]
+        idx = torch.arange(G)
+        m[0, :, 2] = 3.0 + 2e-6 * (idx % 40).float()
+        far = idx % 10 == 0
+        m[0, far, 2] = 3.0 + 37.0 * torch.rand(int(far.sum()), generator=torch.Generator().manual_seed(2))
+    elif n_ties >= m.shape[1]:
         m[..., 2] = 3.0
     else:
         g = torch.Generator().manual_seed(1)
