@@ -83,6 +83,19 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        float* geom, int32_t* radii, uint32_t* seg_count, int layout,
                        void* stream);
 
+/* Fused alternative to dsr_preprocess_fwd + dsr_bin_scan + dsr_bin_scatter (K1 + K3) for
+ * problems whose fixed-capacity key buffer fits: the same projection, plus the keys of every
+ * (gaussian, touched tile) written straight into segment (v, t) = keys[(v*T + t) * G ...]
+ * (a gaussian touches a tile at most once). Inputs load once per scene and project into
+ * every view of that scene. keys must hold V*T*G entries (only V*T segments' prefixes are
+ * written); seg_count [V*T] receives the entry counts (zeroed by this call). Consumers take
+ * seg_stride = G. Requires T <= 32768 and V*T*G < 2^32. */
+int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M,
+                    const float* means, const float* shs, const float* colors,
+                    const float* opacities, const float* cov6, const dsr_camera* cams,
+                    float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout,
+                    void* stream);
+
 /* Exclusive scan of seg_count[V*T] -> seg_start[V*T+1], seg_cursor[V*T] (= seg_start),
  * totals[0] = N (num_rendered over all views), totals[1] = max entries in one tile. */
 int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_start,
@@ -94,28 +107,38 @@ int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_s
 int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor,
                     uint64_t* keys, void* stream);
 
+/* Segment layout used by the sort and compositing calls:
+ *   seg_stride == 0: prefix layout, segment s = keys[seg_start[s] .. seg_start[s+1])
+ *                    (dsr_bin_scan / dsr_bin_scatter; seg_count may be NULL)
+ *   seg_stride  > 0: fixed capacity, segment s = keys[s*stride .. s*stride + seg_count[s])
+ *                    (dsr_project_bin with stride = G; seg_start may be NULL) */
+
 /* Sort every segment by (depth, id) ascending — identical to upstream's stable radix
  * sort of (tile << 32 | depth) with emission-order ties (K4/K5). max_count sizes the LDS
  * sort (0 = unknown): segments that fit sort in LDS, larger ones sort through HBM using
  * `scratch` (same size as keys). scratch may be NULL only when max_count is an exact
- * bound <= dsr_sort_lds_capacity(). */
-int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, uint64_t* keys,
-                 uint64_t* scratch, uint32_t max_count, void* stream);
+ * bound <= dsr_sort_lds_capacity(). (In the fixed-capacity layout N and the largest
+ * segment are sum / max of seg_count: no same-address atomics from every workgroup.) */
+int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const uint32_t* seg_count,
+                 uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count,
+                 void* stream);
 uint32_t dsr_sort_lds_capacity(void);
 
 /* Front-to-back compositing per 16x16 tile (K6). out_color [V,3,H,W], final_T [V,H,W],
  * n_contrib [V,H,W] (uint32). Background from cams[v].bg. */
 int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
-                   const uint32_t* seg_start, const uint64_t* keys, float* out_color,
-                   float* final_T, uint32_t* n_contrib, void* stream);
+                   const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride,
+                   const uint64_t* keys, float* out_color, float* final_T, uint32_t* n_contrib,
+                   void* stream);
 
 /* ---- rasterizer backward -----------------------------------------------------------
  * Back-to-front per tile (K7). dL_dpix [V,3,H,W]. Accumulates into dgeom [V,G,12]
  * (caller zeroes): [0..1] dL/dxy (ndc scale, as upstream dL_dmean2D), [2..4] dL/dconic,
  * [5] dL/dopacity, [6..8] dL/drgb. */
 int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
-                   const uint32_t* seg_start, const uint64_t* keys, const float* final_T,
-                   const uint32_t* n_contrib, const float* dL_dpix, float* dgeom, void* stream);
+                   const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride,
+                   const uint64_t* keys, const float* final_T, const uint32_t* n_contrib,
+                   const float* dL_dpix, float* dgeom, void* stream);
 
 /* Preprocess backward (K8 + K9), reduced over all views of each scene without atomics.
  * scene_view_start [S+1], scene_views [V] list the views of each scene.

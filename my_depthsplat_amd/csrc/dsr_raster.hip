@@ -202,8 +202,130 @@ __device__ __forceinline__ void load_sh(const float* shs, size_t sg, int M, int 
   }
 }
 
+// Segment (view, tile) bounds in the key buffer. stride == 0: prefix layout, segment s is
+// [start[s], start[s + 1]). stride > 0: fixed capacity, [s * stride, s * stride + count[s]).
+__device__ __forceinline__ void seg_bounds(const uint32_t* __restrict__ start, const uint32_t* __restrict__ count,
+                                           uint32_t stride, int seg, uint32_t& b, uint32_t& e) {
+  if (stride) {
+    b = (uint32_t)seg * stride;
+    e = b + count[seg];
+  } else {
+    b = start[seg];
+    e = start[seg + 1];
+  }
+}
+
 // ------------------------------------------------------------------------------------
-// K1: preprocess + per-(view, tile) entry counts.
+// K1 building blocks: one Gaussian's scene inputs (loaded once) and its projection into one
+// view (upstream preprocessCUDA, rows A7 of the survey).
+template <int DEG>
+struct GaussIn {
+  static constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
+  float m[3];
+  float c6[6];
+  float f[NC * 3];  // SH coefficients (coefficient-major) or the precomputed colour
+  float op;
+};
+
+template <int DEG>
+__device__ __forceinline__ void load_gauss(GaussIn<DEG>& in, size_t sg, int M, const float* __restrict__ means,
+                                           const float* __restrict__ shs, const float* __restrict__ colors,
+                                           const float* __restrict__ opac, const float* __restrict__ cov6,
+                                           int layout) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) in.m[k] = means[3 * sg + k];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) in.c6[k] = load_cov(cov6, sg, k, layout);
+  if constexpr (DEG >= 0) {
+    load_sh<GaussIn<DEG>::NC>(shs, sg, M, layout, in.f);
+  } else {
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) in.f[ch] = colors[3 * sg + ch];
+  }
+  in.op = opac[sg];
+}
+
+// Fills rec (GS floats, zero when culled) and the tile rect; returns the radius (0 = culled).
+template <int DEG>
+__device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_camera* __restrict__ cam, int H,
+                                             int W, int gx, int gy, float* rec, int& x0, int& y0, int& x1,
+                                             int& y1) {
+  int r = 0;
+#pragma unroll
+  for (int k = 0; k < GS; ++k) rec[k] = 0.f;
+  x0 = y0 = x1 = y1 = 0;
+  const float gsc = cam->scale;
+  const F3 p = {in.m[0] * gsc, in.m[1] * gsc, in.m[2] * gsc};
+  const float* view = cam->viewmatrix;
+  const float* proj = cam->projmatrix;
+  const F3 pv = xform43(view, p);
+  if (pv.z > 0.2f) {
+    const F3 ph = xform43(proj, p);
+    const float pw = 1.0f / (xform44w(proj, p) + 0.0000001f);
+    const float ndx = ph.x * pw, ndy = ph.y * pw;
+    float c6[6];
+    const float gsc2 = gsc * gsc;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) c6[k] = in.c6[k] * gsc2;
+    const float fx = W / (2.0f * cam->tanfovx);
+    const float fy = H / (2.0f * cam->tanfovy);
+    Cov2D w;
+    cov2d(p, fx, fy, cam->tanfovx, cam->tanfovy, c6, view, w);
+    const float det = w.a * w.c - w.b * w.b;
+    if (det != 0.0f) {
+      const float det_inv = 1.f / det;
+      const float mid = 0.5f * (w.a + w.c);
+      const float disc = sqrtf(fmaxf(0.1f, mid * mid - det));
+      const float l1 = mid + disc, l2 = mid - disc;
+      const int rr = (int)ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+      const float px = ndc2pix(ndx, W), py = ndc2pix(ndy, H);
+      tile_rect(px, py, rr, gx, gy, x0, y0, x1, y1);
+      if ((x1 - x0) * (y1 - y0) != 0) {
+        r = rr;
+        uint32_t clamp_bits = 0;
+        if constexpr (DEG >= 0) {
+          float dx = p.x - cam->campos[0], dy = p.y - cam->campos[1], dz = p.z - cam->campos[2];
+          const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+          dx = dx / len;
+          dy = dy / len;
+          dz = dz / len;
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) {
+            float c = sh_eval<DEG>(in.f, ch, dx, dy, dz) + 0.5f;
+            clamp_bits |= (c < 0.f ? 1u : 0u) << ch;
+            rec[6 + ch] = fmaxf(c, 0.0f);
+          }
+        } else {
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) rec[6 + ch] = in.f[ch];
+        }
+        rec[0] = px;
+        rec[1] = py;
+        rec[2] = w.c * det_inv;
+        rec[3] = -w.b * det_inv;
+        rec[4] = w.a * det_inv;
+        rec[5] = in.op;
+        rec[9] = pv.z;
+        rec[10] = __int_as_float(r);
+        rec[11] = __uint_as_float(clamp_bits);
+      } else {
+        x0 = y0 = x1 = y1 = 0;
+      }
+    }
+  }
+  return r;
+}
+
+__device__ __forceinline__ void store_geom(float* __restrict__ geom, int32_t* __restrict__ radii, size_t vg,
+                                           const float* rec, int r) {
+  float4* out = reinterpret_cast<float4*>(geom + vg * GS);
+  out[0] = make_float4(rec[0], rec[1], rec[2], rec[3]);
+  out[1] = make_float4(rec[4], rec[5], rec[6], rec[7]);
+  out[2] = make_float4(rec[8], rec[9], rec[10], rec[11]);
+  radii[vg] = r;
+}
+
+// K1: preprocess + per-(view, tile) entry counts (two-phase binning path).
 // grid = (ceil(G/256), V), block = 256. DEG = -1 -> colors_precomp path.
 template <int DEG>
 __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, int gy, int M,
@@ -227,75 +349,11 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
   const int g = blockIdx.x * NT + tid;
   int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
   if (g < G) {
-    const size_t sg = (size_t)cam->scene * G + g;
+    GaussIn<DEG> in;
+    load_gauss<DEG>(in, (size_t)cam->scene * G + g, M, means, shs, colors, opac, cov6, layout);
     float rec[GS];
-#pragma unroll
-    for (int k = 0; k < GS; ++k) rec[k] = 0.f;
-    const float gsc = cam->scale;
-    const F3 p = {means[3 * sg] * gsc, means[3 * sg + 1] * gsc, means[3 * sg + 2] * gsc};
-    const float* view = cam->viewmatrix;
-    const float* proj = cam->projmatrix;
-    const F3 pv = xform43(view, p);
-    if (pv.z > 0.2f) {
-      const F3 ph = xform43(proj, p);
-      const float pw = 1.0f / (xform44w(proj, p) + 0.0000001f);
-      const float ndx = ph.x * pw, ndy = ph.y * pw;
-      float c6[6];
-      const float gsc2 = gsc * gsc;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) c6[k] = load_cov(cov6, sg, k, layout) * gsc2;
-      const float fx = W / (2.0f * cam->tanfovx);
-      const float fy = H / (2.0f * cam->tanfovy);
-      Cov2D w;
-      cov2d(p, fx, fy, cam->tanfovx, cam->tanfovy, c6, view, w);
-      const float det = w.a * w.c - w.b * w.b;
-      if (det != 0.0f) {
-        const float det_inv = 1.f / det;
-        const float mid = 0.5f * (w.a + w.c);
-        const float disc = sqrtf(fmaxf(0.1f, mid * mid - det));
-        const float l1 = mid + disc, l2 = mid - disc;
-        const int rr = (int)ceilf(3.f * sqrtf(fmaxf(l1, l2)));
-        const float px = ndc2pix(ndx, W), py = ndc2pix(ndy, H);
-        tile_rect(px, py, rr, gx, gy, x0, y0, x1, y1);
-        if ((x1 - x0) * (y1 - y0) != 0) {
-          r = rr;
-          uint32_t clamp_bits = 0;
-          if constexpr (DEG >= 0) {
-            constexpr int NC = (DEG + 1) * (DEG + 1);
-            float sh[NC * 3];
-            load_sh<NC>(shs, sg, M, layout, sh);
-            float dx = p.x - cam->campos[0], dy = p.y - cam->campos[1], dz = p.z - cam->campos[2];
-            const float len = sqrtf(dx * dx + dy * dy + dz * dz);
-            dx = dx / len;
-            dy = dy / len;
-            dz = dz / len;
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-              float c = sh_eval<DEG>(sh, ch, dx, dy, dz) + 0.5f;
-              clamp_bits |= (c < 0.f ? 1u : 0u) << ch;
-              rec[6 + ch] = fmaxf(c, 0.0f);
-            }
-          } else {
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) rec[6 + ch] = colors[3 * sg + ch];
-          }
-          rec[0] = px;
-          rec[1] = py;
-          rec[2] = w.c * det_inv;
-          rec[3] = -w.b * det_inv;
-          rec[4] = w.a * det_inv;
-          rec[5] = opac[sg];
-          rec[9] = pv.z;
-          rec[10] = __int_as_float(r);
-          rec[11] = __uint_as_float(clamp_bits);
-        }
-      }
-    }
-    float4* out = reinterpret_cast<float4*>(geom + ((size_t)v * G + g) * GS);
-    out[0] = make_float4(rec[0], rec[1], rec[2], rec[3]);
-    out[1] = make_float4(rec[4], rec[5], rec[6], rec[7]);
-    out[2] = make_float4(rec[8], rec[9], rec[10], rec[11]);
-    radii[(size_t)v * G + g] = r;
+    r = project_gauss<DEG>(in, cam, H, W, gx, gy, rec, x0, y0, x1, y1);
+    store_geom(geom, radii, (size_t)v * G + g, rec, r);
   }
   uint32_t* gcount = seg_count + (size_t)v * T;
   __shared__ WaveRects s_wr[NT / 64];
@@ -312,6 +370,69 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
       const uint32_t c = s_hist[t];
       if (c) atomicAdd(&gcount[t], c);
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// K1+K3 fused (fixed-capacity binning): one workgroup per 256 Gaussians of one scene loads
+// their inputs once and, for every view of that scene, projects them, counts the (view,
+// tile) entries of the block in an LDS histogram, reserves a contiguous range per touched
+// tile with one global atomic, and writes the (depth, id) keys into segment (v, t), which
+// starts at (v*T + t) * G (a Gaussian touches a tile at most once, so G slots suffice). No
+// global scan is needed before the keys exist; the sort pass reads the counts.
+template <int DEG>
+__global__ __launch_bounds__(NT) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
+                                                     const float* __restrict__ means,
+                                                     const float* __restrict__ shs,
+                                                     const float* __restrict__ colors,
+                                                     const float* __restrict__ opac,
+                                                     const float* __restrict__ cov6,
+                                                     const dsr_camera* __restrict__ cams,
+                                                     float* __restrict__ geom, int32_t* __restrict__ radii,
+                                                     uint32_t* __restrict__ seg_count,
+                                                     uint64_t* __restrict__ keys, int layout) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+  __shared__ WaveRects s_wr[NT / 64];
+  __shared__ uint64_t s_key[NT];
+  const int s = blockIdx.y;
+  const int T = gx * gy;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = blockIdx.x * NT + tid;
+  GaussIn<DEG> in;
+  if (g < G) load_gauss<DEG>(in, (size_t)s * G + g, M, means, shs, colors, opac, cov6, layout);
+  WaveRects& wr = s_wr[w];
+  const uint64_t* wkey = s_key + w * 64;
+  for (int v = 0; v < V; ++v) {
+    const dsr_camera* cam = cams + v;
+    if (cam->scene != s) continue;  // uniform across the workgroup
+    for (int t = tid; t < T; t += NT) s_hist[t] = 0;
+    int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    uint64_t key = 0;
+    if (g < G) {
+      float rec[GS];
+      r = project_gauss<DEG>(in, cam, H, W, gx, gy, rec, x0, y0, x1, y1);
+      store_geom(geom, radii, (size_t)v * G + g, rec, r);
+      key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
+    }
+    s_key[tid] = key;
+    __syncthreads();
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
+    __syncthreads();
+    uint32_t* gcount = seg_count + (size_t)v * T;
+    for (int t = tid; t < T; t += NT) {
+      const uint32_t c = s_hist[t];
+      if (c) s_hist[t] = atomicAdd(&gcount[t], c);
+    }
+    __syncthreads();
+#ifdef PB_STRIDE_CAP
+    const size_t SG = (size_t)min(G, PB_STRIDE_CAP);
+#else
+    const size_t SG = (size_t)G;
+#endif
+    uint64_t* vkeys = keys + (size_t)v * T * SG;
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
+                       [&](int t, int o) { vkeys[(size_t)t * SG + atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
+    __syncthreads();
   }
 }
 
@@ -745,7 +866,8 @@ __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, ui
 #define SORT_WPE 3
 #endif
 template <int KMAX>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) void k_sort_lds(const uint32_t* __restrict__ seg_start,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(KMAX >= 32 ? 1 : SORT_WPE))) void k_sort_lds(const uint32_t* __restrict__ seg_start,
+                                                 const uint32_t* __restrict__ seg_count, uint32_t stride,
                                                  uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
                                                  int id_bits, int big_here) {
   constexpr uint32_t cap = NT * KMAX;
@@ -757,8 +879,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) 
   uint32_t* wsum = aux + 2048;
   uint32_t* flag = wsum + 16;
   const int seg = blockIdx.x;
-  const uint32_t b = seg_start[seg];
-  const uint32_t n = seg_start[seg + 1] - b;
+  uint32_t b, e;
+  seg_bounds(seg_start, seg_count, stride, seg, b, e);
+  const uint32_t n = e - b;
   if (n <= 1) return;
   if (n > cap) {
     if (big_here) sort_segment<NT>(keys + b, scratch + b, n, id_bits, aux, wsum, flag, keys + b);
@@ -796,6 +919,7 @@ constexpr size_t sort_lds_bytes() {
 
 // Segments larger than the LDS capacity: same passes through HBM, 16 waves.
 __global__ __launch_bounds__(1024) void k_sort_global(const uint32_t* __restrict__ seg_start,
+                                                      const uint32_t* __restrict__ seg_count, uint32_t stride,
                                                       uint64_t* __restrict__ keys,
                                                       uint64_t* __restrict__ scratch, int id_bits,
                                                       uint32_t cap) {
@@ -803,8 +927,9 @@ __global__ __launch_bounds__(1024) void k_sort_global(const uint32_t* __restrict
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t flag;
   const int seg = blockIdx.x;
-  const uint32_t b = seg_start[seg];
-  const uint32_t n = seg_start[seg + 1] - b;
+  uint32_t b, e;
+  seg_bounds(seg_start, seg_count, stride, seg, b, e);
+  const uint32_t n = e - b;
   if (n <= cap) return;
   sort_segment<1024>(keys + b, scratch + b, n, id_bits, hist, wsum, &flag, keys + b);
 }
@@ -935,6 +1060,7 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
                                                    const uint32_t* __restrict__ seg_start,
+                                                   const uint32_t* __restrict__ seg_count, uint32_t stride,
                                                    const uint64_t* __restrict__ keys,
                                                    float* __restrict__ out, float* __restrict__ finalT,
                                                    uint32_t* __restrict__ ncontrib) {
@@ -946,7 +1072,8 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   const int py = sy0 + (lane >> 3);
   const bool inside = px < W && py < H;
   const int seg = v * T + blockIdx.y * gx + blockIdx.x;
-  const uint32_t start = seg_start[seg], end = seg_start[seg + 1];
+  uint32_t start, end;
+  seg_bounds(seg_start, seg_count, stride, seg, start, end);
   const float pfx = (float)px, pfy = (float)py;
   const float fx0 = (float)sx0, fy0 = (float)sy0;
   const float* gv = geom + (size_t)v * G * GS;
@@ -1108,6 +1235,7 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
                                                    const uint32_t* __restrict__ seg_start,
+                                                   const uint32_t* __restrict__ seg_count, uint32_t stride,
                                                    const uint64_t* __restrict__ keys,
                                                    const float* __restrict__ finalT,
                                                    const uint32_t* __restrict__ ncontrib,
@@ -1122,7 +1250,8 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
   const int py = sy0 + (lane >> 3);
   const bool inside = px < W && py < H;
   const int seg = v * T + blockIdx.y * gx + blockIdx.x;
-  const uint32_t start = seg_start[seg], end = seg_start[seg + 1];
+  uint32_t start, end;
+  seg_bounds(seg_start, seg_count, stride, seg, start, end);
   const size_t HW = (size_t)H * W;
   const size_t pix = (size_t)py * W + px;
   const float pfx = (float)px, pfy = (float)py;
@@ -1504,6 +1633,35 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   return dsplat::check_launch("k_preprocess");
 }
 
+int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means, const float* shs,
+                    const float* colors, const float* opacities, const float* cov6, const dsr_camera* cams,
+                    float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout, void* stream) {
+  DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_project_bin: bad sizes S=%d G=%d V=%d H=%d W=%d", S, G, V, H, W);
+  DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "dsr_project_bin: exactly one of shs/colors must be given");
+  DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
+                 "dsr_project_bin: sh_degree=%d M=%d unsupported (degree 0..3, M >= (deg+1)^2)", sh_degree, M);
+  DSPLAT_REQUIRE(means && opacities && cov6 && cams && geom && radii && seg_count && keys, "dsr_project_bin: null pointer");
+  const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H), T = gx * gy;
+  DSPLAT_REQUIRE(T <= kHistLdsMax, "dsr_project_bin: %d tiles per view exceed the LDS histogram (%d)", T, kHistLdsMax);
+  DSPLAT_REQUIRE((uint64_t)V * T * G < (1ull << 32), "dsr_project_bin: V*tiles*G must fit 32-bit key offsets");
+  hipStream_t st = (hipStream_t)stream;
+  if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
+  dim3 grid((G + NT - 1) / NT, S);
+  const int deg = shs ? sh_degree : -1;
+#define DSR_PB(D)                                                                                             \
+  k_project_emit<D><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, \
+                                             geom, radii, seg_count, keys, layout)
+  switch (deg) {
+    case -1: DSR_PB(-1); break;
+    case 0: DSR_PB(0); break;
+    case 1: DSR_PB(1); break;
+    case 2: DSR_PB(2); break;
+    default: DSR_PB(3); break;
+  }
+#undef DSR_PB
+  return dsplat::check_launch("k_project_emit");
+}
+
 int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_start, uint32_t* seg_cursor,
                  uint32_t* totals, void* stream) {
   DSPLAT_REQUIRE(V > 0 && H > 0 && W > 0, "dsr_bin_scan: bad sizes");
@@ -1524,10 +1682,11 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
   return dsplat::check_launch("k_scatter");
 }
 
-int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, uint64_t* keys, uint64_t* scratch,
-                 uint32_t max_count, void* stream) {
+int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const uint32_t* seg_count,
+                 uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_sort: bad sizes");
-  DSPLAT_REQUIRE(seg_start != nullptr && keys != nullptr, "dsr_bin_sort: null pointer");
+  DSPLAT_REQUIRE(keys != nullptr && (seg_stride ? seg_count != nullptr : seg_start != nullptr),
+                 "dsr_bin_sort: null pointer");
   DSPLAT_REQUIRE(scratch != nullptr || (max_count > 0 && max_count <= kSortCap),
                  "dsr_bin_sort: without scratch, max_count (%u) must bound every segment and be <= %u", max_count,
                  kSortCap);
@@ -1557,46 +1716,55 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, uint64_t
   uint32_t cap;
   if (want <= 256 * 4) {
     cap = 256 * 4;
-    k_sort_lds<4><<<nseg, NT, sort_lds_bytes<4>(), st>>>(seg_start, keys, scratch, id_bits, big_here);
+    k_sort_lds<4><<<nseg, NT, sort_lds_bytes<4>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
+                                                                id_bits, big_here);
   } else if (want <= 256 * 8) {
     cap = 256 * 8;
-    k_sort_lds<8><<<nseg, NT, sort_lds_bytes<8>(), st>>>(seg_start, keys, scratch, id_bits, big_here);
+    k_sort_lds<8><<<nseg, NT, sort_lds_bytes<8>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
+                                                                id_bits, big_here);
   } else if (want <= 256 * 16) {
     cap = 256 * 16;
-    k_sort_lds<16><<<nseg, NT, sort_lds_bytes<16>(), st>>>(seg_start, keys, scratch, id_bits, big_here);
+    k_sort_lds<16><<<nseg, NT, sort_lds_bytes<16>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
+                                                                id_bits, big_here);
   } else {
     cap = 256 * 32;
-    k_sort_lds<32><<<nseg, NT, sort_lds_bytes<32>(), st>>>(seg_start, keys, scratch, id_bits, big_here);
+    k_sort_lds<32><<<nseg, NT, sort_lds_bytes<32>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
+                                                                id_bits, big_here);
   }
   if (int e = dsplat::check_launch("k_sort_lds")) return e;
   if (big_known) {
-    k_sort_global<<<nseg, 1024, 0, st>>>(seg_start, keys, scratch, id_bits, cap);
+    k_sort_global<<<nseg, 1024, 0, st>>>(seg_start, seg_count, seg_stride, keys, scratch, id_bits, cap);
     if (int e = dsplat::check_launch("k_sort_global")) return e;
   }
   return 0;
 }
 
 int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
-                   const uint32_t* seg_start, const uint64_t* keys, float* out_color, float* final_T,
-                   uint32_t* n_contrib, void* stream) {
+                   const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride, const uint64_t* keys,
+                   float* out_color, float* final_T, uint32_t* n_contrib, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_render_fwd: bad sizes");
-  DSPLAT_REQUIRE(cams && geom && seg_start && out_color && final_T && n_contrib, "dsr_render_fwd: null pointer");
+  DSPLAT_REQUIRE(cams && geom && (seg_stride ? seg_count != nullptr : seg_start != nullptr) && out_color && final_T &&
+                     n_contrib,
+                 "dsr_render_fwd: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
-  k_render_fwd<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, keys,
-                                                     out_color, final_T, n_contrib);
+  k_render_fwd<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count,
+                                                     seg_stride, keys, out_color, final_T, n_contrib);
   return dsplat::check_launch("k_render_fwd");
 }
 
 int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
-                   const uint32_t* seg_start, const uint64_t* keys, const float* final_T,
-                   const uint32_t* n_contrib, const float* dL_dpix, float* dgeom, void* stream) {
+                   const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride, const uint64_t* keys,
+                   const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, float* dgeom,
+                   void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_render_bwd: bad sizes");
-  DSPLAT_REQUIRE(cams && geom && seg_start && final_T && n_contrib && dL_dpix && dgeom, "dsr_render_bwd: null pointer");
+  DSPLAT_REQUIRE(cams && geom && (seg_stride ? seg_count != nullptr : seg_start != nullptr) && final_T && n_contrib &&
+                     dL_dpix && dgeom,
+                 "dsr_render_bwd: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
-  k_render_bwd<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, keys, final_T,
-                                                     n_contrib, dL_dpix, dgeom);
+  k_render_bwd<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count,
+                                                     seg_stride, keys, final_T, n_contrib, dL_dpix, dgeom);
   return dsplat::check_launch("k_render_bwd");
 }
 

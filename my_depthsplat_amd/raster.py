@@ -79,7 +79,7 @@ class KernelTimer:
 
 
 _timer: KernelTimer | None = None
-_last: dict = {"totals": None}
+_last: dict = {"counts": None}
 
 
 def set_timer(t: KernelTimer | None) -> None:
@@ -89,10 +89,10 @@ def set_timer(t: KernelTimer | None) -> None:
 
 def last_stats() -> dict:
     """(num_rendered, max tile count) of the last forward (reads the device: syncs)."""
-    t = _last["totals"]
-    if t is None:
+    c = _last["counts"]
+    if c is None:
         return {"num_rendered": 0, "max_count": 0}
-    n, m = (int(x) for x in t[:2].cpu())
+    n, m = int(c.sum()), int(c.max())
     _spec["max_count"] = m
     return {"num_rendered": n, "max_count": m}
 
@@ -105,9 +105,12 @@ def _timed(name, fn, *args):
     return r
 
 
-def algorithmic_bytes(kernel: str, *, G: int, V: int, N: int, HW: int, T: int | None = None) -> int:
-    """Minimum HBM bytes one launch must move. G Gaussians per scene, V views,
-    N (view, tile, Gaussian) entries, HW pixels per view."""
+def algorithmic_bytes(kernel: str, *, G: int, V: int, N: int, HW: int, T: int | None = None, S: int = 1) -> int:
+    """Compulsory HBM bytes of one launch: every input read once, every output
+    written once. G Gaussians per scene, S scenes, V views, N (view, tile, Gaussian) entries,
+    HW pixels per view. Per-entry gathers that caches can serve are not counted."""
+    if kernel == "k_project_emit":  # 148 B of parameters per scene Gaussian in; 52 B record +
+        return S * G * 148 + V * G * 52 + 8 * N  # radius per (view, Gaussian) + one key per entry out
     if kernel == "k_preprocess":   # 148 B of Gaussian params in, 48 B record + 4 B radius out
         return V * G * (148 + 52)
     if kernel == "k_scan":
@@ -116,8 +119,8 @@ def algorithmic_bytes(kernel: str, *, G: int, V: int, N: int, HW: int, T: int | 
         return V * G * 16 + 8 * N
     if kernel == "k_sort":         # keys in + out
         return 16 * N
-    if kernel == "k_render_fwd":   # key + 36-B record per entry; RGB + T + n_contrib out
-        return 44 * N + 20 * V * HW
+    if kernel == "k_render_fwd":   # keys; each 36-B compositing record once; RGB + T + n_contrib out
+        return 8 * N + 36 * V * G + 20 * V * HW
     raise KeyError(kernel)
 
 
@@ -126,19 +129,20 @@ class RasterState:
     """Everything the backward needs (all device tensors)."""
     geom: torch.Tensor        # [V, G, 12]
     radii: torch.Tensor       # [V, G] int32
-    seg_start: torch.Tensor   # [V*T + 1] int32 (uint32)
-    keys: torch.Tensor        # [N] int64 (uint64 keys, sorted per segment)
+    seg_start: torch.Tensor | None  # [V*T + 1] int32 (prefix layout) or None
+    seg_count: torch.Tensor   # [V*T] int32 entries per (view, tile)
+    seg_stride: int           # 0: prefix layout; > 0: segment s starts at s * seg_stride
+    keys: torch.Tensor        # int64 (uint64 keys, sorted per segment)
     final_T: torch.Tensor     # [V, H, W]
     n_contrib: torch.Tensor   # [V, H, W] int32
-    totals: torch.Tensor      # [4] int32 on device: (num_rendered, max entries per tile, ...)
 
     @property
     def num_rendered(self) -> int:  # host read: syncs
-        return int(self.totals[0].item())
+        return int(self.seg_count.sum())
 
     @property
     def max_count(self) -> int:
-        return int(self.totals[1].item())
+        return int(self.seg_count.max())
 
 
 # Key-buffer sizing. N (the number of (view, tile, Gaussian) entries) is only known on the
@@ -149,20 +153,22 @@ class RasterState:
 # Larger problems fall back to one 8-byte read of (N, max tile count) after the scan.
 KEY_BUDGET_BYTES = 8 << 30
 _spec = {"max_count": 0}
-_inflight: list = []  # (pinned int32[4], event) read-backs of totals, consumed without blocking
+_inflight: list = []  # (pinned int32 counts, event) read-backs, consumed without blocking
 
 
-def _note_totals(totals: torch.Tensor) -> None:
-    """Queue a non-blocking copy of (N, max count) to pinned memory; completed copies from
-    earlier calls update the LDS-sort size hint. Never waits on the device."""
+def _note_counts(counts: torch.Tensor) -> None:
+    """Queue a non-blocking copy of the per-segment counts to pinned memory; completed
+    copies from earlier calls update the LDS-sort size hint (their max). Never waits on the
+    device, never adds a kernel (a device-side max would need same-address atomics from
+    every workgroup, which serialise)."""
     if torch.cuda.is_current_stream_capturing():
         return  # inside a hipGraph capture: no host-side bookkeeping (hint stays fixed)
     while _inflight and _inflight[0][1].query():
         host, _ = _inflight.pop(0)
-        _spec["max_count"] = int(host[1])
+        _spec["max_count"] = int(host.max())
     if len(_inflight) < 4:
-        host = torch.empty(4, dtype=torch.int32, pin_memory=True)
-        host.copy_(totals, non_blocking=True)
+        host = torch.empty(counts.shape, dtype=torch.int32, pin_memory=True)
+        host.copy_(counts, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         _inflight.append((host, ev))
@@ -220,7 +226,12 @@ def input_layout(feats, cov6, use_sh, channel_major_sh):
 def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0):
     """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh; [S,G,3,M] with
     LAYOUT_SH_CHANNEL_MAJOR) or [S,G,3]; opacities [S,G]; cov6 [S,G,6] (or [S,G,3,3] with
-    LAYOUT_COV_FULL); cams [V,44]. Returns (color [V,3,H,W], RasterState)."""
+    LAYOUT_COV_FULL); cams [V,44]. Returns (color [V,3,H,W], RasterState).
+
+    Two binning layouts (include/dsplat_hip.h): when the fixed-capacity key buffer
+    (V*T*G slots) fits KEY_BUDGET_BYTES, dsr_project_bin projects and emits keys in one
+    kernel (no scan, no second pass over the geometry, no host sync); otherwise the
+    two-phase path counts, scans (one 8-byte read-back of N), scatters."""
     lib = _lib.load()
     _lib.require_gpu(means, feats, opacities, cov6, cams)
     S, G = means.shape[0], means.shape[1]
@@ -229,51 +240,61 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     gx, gy = tiles(H, W)
     T = gx * gy
     st = _lib.stream_of(dev)
+    deg = sh_degree if use_sh else -1
+    shs_p = feats.data_ptr() if use_sh else None
+    col_p = None if use_sh else feats.data_ptr()
     geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
     radii = torch.empty((V, G), dtype=torch.int32, device=dev)
     seg_count = torch.empty(V * T, dtype=torch.int32, device=dev)
-    _lib.check(_timed("k_preprocess", lib.dsr_preprocess_fwd,
-        S, G, V, H, W, sh_degree if use_sh else -1, M, means.data_ptr(),
-        feats.data_ptr() if use_sh else None, None if use_sh else feats.data_ptr(),
-        opacities.data_ptr(), cov6.data_ptr(), cams.data_ptr(), geom.data_ptr(), radii.data_ptr(),
-        seg_count.data_ptr(), layout, st), "dsr_preprocess_fwd")
-    seg_start = torch.empty(V * T + 1, dtype=torch.int32, device=dev)
-    cursor = torch.empty(V * T, dtype=torch.int32, device=dev)
-    totals = torch.empty(4, dtype=torch.int32, device=dev)
-    _lib.check(_timed("k_scan", lib.dsr_bin_scan, V, H, W, seg_count.data_ptr(), seg_start.data_ptr(),
-                      cursor.data_ptr(), totals.data_ptr(), st), "dsr_bin_scan")
-    cap = _key_capacity(V, G, T)
     lds_cap = lib.dsr_sort_lds_capacity()
-    if cap is None:  # too large for the worst-case buffer: one small read-back
+    cap = _key_capacity(V, G, T)
+    if cap is not None and T <= 32768 and V * T * G < (1 << 32):
+        keys = torch.empty(V * T * G, dtype=torch.int64, device=dev)
+        # scratch for segments above the LDS sort (their size is unknown before the sort)
+        scratch = torch.empty(V * T * G, dtype=torch.int64, device=dev)
+        _lib.check(_timed("k_project_emit", lib.dsr_project_bin,
+            S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+            cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout, st),
+            "dsr_project_bin")
+        maxc_hint = min(lds_cap, _spec["max_count"]) if _spec["max_count"] else lds_cap
+        _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, None, seg_count.data_ptr(), G, keys.data_ptr(),
+                          scratch.data_ptr(), maxc_hint, st), "dsr_bin_sort")
+        _note_counts(seg_count)
+        seg_start, stride = None, G
+    else:
+        _lib.check(_timed("k_preprocess", lib.dsr_preprocess_fwd,
+            S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+            cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), layout, st),
+            "dsr_preprocess_fwd")
+        seg_start = torch.empty(V * T + 1, dtype=torch.int32, device=dev)
+        cursor = torch.empty(V * T, dtype=torch.int32, device=dev)
+        totals = torch.empty(4, dtype=torch.int32, device=dev)
+        _lib.check(_timed("k_scan", lib.dsr_bin_scan, V, H, W, seg_count.data_ptr(), seg_start.data_ptr(),
+                          cursor.data_ptr(), totals.data_ptr(), st), "dsr_bin_scan")
         if torch.cuda.is_current_stream_capturing():
             raise _lib.DsplatError(f"V*G*tiles = {V * G * T} key slots exceed KEY_BUDGET_BYTES: this size needs a "
                                    "host read-back and cannot be captured into a graph")
-        tot = totals[:2].cpu()
+        tot = totals[:2].cpu()  # one small read-back: N sizes the key buffer
         N, maxc = int(tot[0]), int(tot[1])
-        cap = max(N, 1)
-    else:
-        N = maxc = None
-        # LDS-sort launch size from earlier calls (any value is correct: segments above it
-        # take the HBM path inside the same launch); first call assumes the full capacity
-        _note_totals(totals)
-        maxc_hint = min(lds_cap, _spec["max_count"]) if _spec["max_count"] else lds_cap
-    keys = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
-    # scratch: only for segments that may exceed the LDS sort (always possible when N is unknown)
-    need_scratch = maxc is None or maxc > lds_cap
-    scratch = torch.empty(max(cap, 1), dtype=torch.int64, device=dev) if need_scratch else None
-    _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
-                      keys.data_ptr(), st), "dsr_bin_scatter")
-    _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), keys.data_ptr(),
-                      None if scratch is None else scratch.data_ptr(), maxc_hint if maxc is None else maxc, st),
-               "dsr_bin_sort")
+        keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
+        scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev) if maxc > lds_cap else None
+        _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
+                          keys.data_ptr(), st), "dsr_bin_scatter")
+        _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), None, 0, keys.data_ptr(),
+                          None if scratch is None else scratch.data_ptr(), maxc, st), "dsr_bin_sort")
+        stride = 0
     color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
     _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
-                      seg_start.data_ptr(), keys.data_ptr(), color.data_ptr(), final_T.data_ptr(),
-                      n_contrib.data_ptr(), st), "dsr_render_fwd")
-    _last["totals"] = totals
-    return color, RasterState(geom, radii, seg_start, keys, final_T, n_contrib, totals)
+                      _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(), color.data_ptr(),
+                      final_T.data_ptr(), n_contrib.data_ptr(), st), "dsr_render_fwd")
+    _last["counts"] = seg_count
+    return color, RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib)
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
 
 
 def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, state: RasterState,
@@ -286,9 +307,10 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     st = _lib.stream_of(dev)
     dcolor = dcolor.contiguous().float()
     dgeom = torch.zeros((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
-    _lib.check(lib.dsr_render_bwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), state.seg_start.data_ptr(),
-                                  state.keys.data_ptr(), state.final_T.data_ptr(), state.n_contrib.data_ptr(),
-                                  dcolor.data_ptr(), dgeom.data_ptr(), st), "dsr_render_bwd")
+    _lib.check(lib.dsr_render_bwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), _ptr(state.seg_start),
+                                  state.seg_count.data_ptr(), state.seg_stride, state.keys.data_ptr(),
+                                  state.final_T.data_ptr(), state.n_contrib.data_ptr(), dcolor.data_ptr(),
+                                  dgeom.data_ptr(), st), "dsr_render_bwd")
     # views of each scene, in view order (fixed summation order -> deterministic reduce)
     order = sorted(range(V), key=lambda v: (view_scene[v], v))
     starts = [0] * (S + 1)

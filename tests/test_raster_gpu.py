@@ -34,13 +34,25 @@ def hip_forward(sc, st, gpu, use_sh=True, bg=(0.0, 0.0, 0.0)):
 
 
 def _segments(state, V, T):
-    start = state.seg_start.cpu().numpy().astype(np.int64)
+    """(start [V*T+1], keys) in the prefix layout, whichever layout the forward used."""
     keys = state.keys.cpu().numpy().view(np.uint64)
-    return start, keys
+    if state.seg_stride == 0:
+        return state.seg_start.cpu().numpy().astype(np.int64), keys
+    cnt = state.seg_count.cpu().numpy().astype(np.int64)
+    assert cnt.shape[0] == V * T
+    parts = [keys[s * state.seg_stride: s * state.seg_stride + cnt[s]] for s in range(V * T)]
+    start = np.concatenate([[0], np.cumsum(cnt)])
+    return start, np.concatenate(parts) if parts else keys[:0]
 
 
+@pytest.mark.parametrize("binning", ["fused", "two_phase"])
 @pytest.mark.parametrize("h,w,sh_degree", [(64, 64, 2), (48, 80, 3), (37, 53, 1), (64, 64, 0)])
-def test_preprocess_and_binning_bitexact(gpu, h, w, sh_degree):
+def test_preprocess_and_binning_bitexact(gpu, h, w, sh_degree, binning, monkeypatch):
+    """Both binning layouts: dsr_project_bin (fixed-capacity segments) and the two-phase
+    count / scan / scatter path that large problems take (forced by a zero key budget)."""
+    from my_depthsplat_amd import raster
+    if binning == "two_phase":
+        monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
     sc = scene_inputs(h=h, w=w, sh_degree=sh_degree, seed=1)
     st = settings_for(sc)
     color, state, _ = hip_forward(sc, st, gpu)

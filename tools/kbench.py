@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--views", type=int, default=3)
     ap.add_argument("--context", type=int, default=2)
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--stride", type=int, default=0, help="fused-layout stride override (experiments)")
+    ap.add_argument("--two-phase", action="store_true", help="force the two-phase binning layout")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -37,11 +39,13 @@ def main():
     cams = raster.build_cameras(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0], bg,
                                 [0] * V, True)
     layout = raster.input_layout(g.harmonics, g.covariances, True, True)
+    if a.two_phase:
+        raster.KEY_BUDGET_BYTES = 0
     color, state = raster.forward_raw(g.means, g.harmonics, True, 2, g.opacities, g.covariances, cams, V, H, W,
                                       layout)
     G = g.means.shape[1]
     torch.cuda.synchronize()
-    print(f"G={G} V={V} {H}x{W} N={int(state.totals[0])}", flush=True)
+    print(f"G={G} V={V} {H}x{W} N={state.num_rendered}", flush=True)
     st = _lib.stream_of(dev)
     dpix = torch.randn_like(color)
     ref = None
@@ -51,58 +55,50 @@ def main():
         for fn, (res, args) in _lib.SIGNATURES.items():
             f = getattr(lib, fn)
             f.restype, f.argtypes = res, args
+        sp = None if state.seg_start is None else state.seg_start.data_ptr()
+        sc_p, stride = state.seg_count.data_ptr(), state.seg_stride
         if a.kernel == "render_fwd":
             out = [torch.empty_like(color), torch.empty_like(state.final_T), torch.empty_like(state.n_contrib)]
 
             def launch():
-                return lib.dsr_render_fwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(),
-                                          state.seg_start.data_ptr(), state.keys.data_ptr(), out[0].data_ptr(),
-                                          out[1].data_ptr(), out[2].data_ptr(), st)
-        elif a.kernel == "preprocess":
-            out = [torch.empty_like(state.geom), torch.empty_like(state.radii),
-                   torch.empty(V * state.seg_start.numel(), dtype=torch.int32, device=dev)]
+                return lib.dsr_render_fwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), sp, sc_p, stride,
+                                          state.keys.data_ptr(), out[0].data_ptr(), out[1].data_ptr(),
+                                          out[2].data_ptr(), st)
+        elif a.kernel in ("project", "project_sort"):  # fused binning (+ sort)
+            assert stride > 0, "fused layout expected"
+            geom2, radii2 = torch.empty_like(state.geom), torch.empty_like(state.radii)
+            cnt2 = torch.empty_like(state.seg_count)
+            keys2 = torch.empty_like(state.keys)
+            scratch2 = torch.empty_like(state.keys)
+            tot2 = torch.empty(4, dtype=torch.int32, device=dev)
+            out = [geom2]
 
             def launch():
-                return lib.dsr_preprocess_fwd(1, G, V, H, W, 2, g.harmonics.shape[-1], g.means.data_ptr(),
-                                              g.harmonics.data_ptr(), None, g.opacities.data_ptr(),
-                                              g.covariances.data_ptr(), cams.data_ptr(), out[0].data_ptr(),
-                                              out[1].data_ptr(), out[2].data_ptr(), layout, st)
-        elif a.kernel == "scatter":  # scan + scatter (the scan resets the cursors)
-            cur = torch.empty_like(state.seg_start)
-            tot = torch.empty(4, dtype=torch.int32, device=dev)
-            out = [torch.empty_like(state.keys)]
-            seg_count = (state.seg_start[1:] - state.seg_start[:-1]).contiguous()
-            ss = torch.empty_like(state.seg_start)
+                rc = lib.dsr_project_bin(1, G, V, H, W, 2, g.harmonics.shape[-1], g.means.data_ptr(),
+                                         g.harmonics.data_ptr(), None, g.opacities.data_ptr(),
+                                         g.covariances.data_ptr(), cams.data_ptr(), geom2.data_ptr(),
+                                         radii2.data_ptr(), cnt2.data_ptr(), keys2.data_ptr(), layout, st)
+                if rc or a.kernel == "project":
+                    return rc
+                return lib.dsr_bin_sort(G, V, H, W, None, cnt2.data_ptr(), a.stride or G, keys2.data_ptr(),
+                                        scratch2.data_ptr(),
+                                        state.max_count, st)
+        elif a.kernel == "sort_sorted":  # re-sort the (already sorted) keys in place: pass cost only
+            tot3 = torch.empty(4, dtype=torch.int32, device=dev)
+            scr = torch.empty_like(state.keys)
+            out = [state.keys]
 
             def launch():
-                rc = lib.dsr_bin_scan(V, H, W, seg_count.data_ptr(), ss.data_ptr(), cur.data_ptr(), tot.data_ptr(),
-                                      st)
-                return rc or lib.dsr_bin_scatter(G, V, H, W, state.geom.data_ptr(), cur.data_ptr(),
-                                                 out[0].data_ptr(), st)
-        elif a.kernel == "sort":  # copy of the unsorted keys + sort
-            cur = torch.empty_like(state.seg_start)
-            tot = torch.empty(4, dtype=torch.int32, device=dev)
-            seg_count = (state.seg_start[1:] - state.seg_start[:-1]).contiguous()
-            ss = torch.empty_like(state.seg_start)
-            unsorted = torch.empty_like(state.keys)
-            lib.dsr_bin_scan(V, H, W, seg_count.data_ptr(), ss.data_ptr(), cur.data_ptr(), tot.data_ptr(), st)
-            lib.dsr_bin_scatter(G, V, H, W, state.geom.data_ptr(), cur.data_ptr(), unsorted.data_ptr(), st)
-            out = [torch.empty_like(state.keys)]
-            nk = int(state.totals[0])
-            maxc = int(state.totals[1])
-
-            def launch():
-                out[0][:nk].copy_(unsorted[:nk])
-                return lib.dsr_bin_sort(G, V, H, W, state.seg_start.data_ptr(), out[0].data_ptr(), None, maxc, st)
+                return lib.dsr_bin_sort(G, V, H, W, sp, sc_p, stride, state.keys.data_ptr(), scr.data_ptr(),
+                                        state.max_count, st)
         else:
             out = [torch.zeros_like(state.geom)]
 
             def launch():
                 out[0].zero_()
-                return lib.dsr_render_bwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(),
-                                          state.seg_start.data_ptr(), state.keys.data_ptr(),
-                                          state.final_T.data_ptr(), state.n_contrib.data_ptr(), dpix.data_ptr(),
-                                          out[0].data_ptr(), st)
+                return lib.dsr_render_bwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), sp, sc_p, stride,
+                                          state.keys.data_ptr(), state.final_T.data_ptr(),
+                                          state.n_contrib.data_ptr(), dpix.data_ptr(), out[0].data_ptr(), st)
         assert launch() == 0, lib.dsplat_last_error()
         torch.cuda.synchronize()
         if ref is None:
