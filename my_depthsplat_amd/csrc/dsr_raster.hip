@@ -223,33 +223,28 @@ struct GaussIn {
   static constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
   float m[3];
   float c6[6];
-  float f[NC * 3];  // SH coefficients (coefficient-major) or the precomputed colour
   float op;
+  size_t sg;  // scene-Gaussian index: SH / colours are read only once the Gaussian survives culling
 };
 
 template <int DEG>
-__device__ __forceinline__ void load_gauss(GaussIn<DEG>& in, size_t sg, int M, const float* __restrict__ means,
-                                           const float* __restrict__ shs, const float* __restrict__ colors,
+__device__ __forceinline__ void load_gauss(GaussIn<DEG>& in, size_t sg, const float* __restrict__ means,
                                            const float* __restrict__ opac, const float* __restrict__ cov6,
                                            int layout) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) in.m[k] = means[3 * sg + k];
 #pragma unroll
   for (int k = 0; k < 6; ++k) in.c6[k] = load_cov(cov6, sg, k, layout);
-  if constexpr (DEG >= 0) {
-    load_sh<GaussIn<DEG>::NC>(shs, sg, M, layout, in.f);
-  } else {
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) in.f[ch] = colors[3 * sg + ch];
-  }
   in.op = opac[sg];
+  in.sg = sg;
 }
 
 // Fills rec (GS floats, zero when culled) and the tile rect; returns the radius (0 = culled).
 template <int DEG>
 __device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_camera* __restrict__ cam, int H,
-                                             int W, int gx, int gy, float* rec, int& x0, int& y0, int& x1,
-                                             int& y1) {
+                                             int W, int gx, int gy, int M, const float* __restrict__ shs,
+                                             const float* __restrict__ colors, int layout, float* rec, int& x0,
+                                             int& y0, int& x1, int& y1) {
   int r = 0;
 #pragma unroll
   for (int k = 0; k < GS; ++k) rec[k] = 0.f;
@@ -284,6 +279,8 @@ __device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_c
         r = rr;
         uint32_t clamp_bits = 0;
         if constexpr (DEG >= 0) {
+          float sh[GaussIn<DEG>::NC * 3];
+          load_sh<GaussIn<DEG>::NC>(shs, in.sg, M, layout, sh);
           float dx = p.x - cam->campos[0], dy = p.y - cam->campos[1], dz = p.z - cam->campos[2];
           const float len = sqrtf(dx * dx + dy * dy + dz * dz);
           dx = dx / len;
@@ -291,13 +288,13 @@ __device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_c
           dz = dz / len;
 #pragma unroll
           for (int ch = 0; ch < 3; ++ch) {
-            float c = sh_eval<DEG>(in.f, ch, dx, dy, dz) + 0.5f;
+            float c = sh_eval<DEG>(sh, ch, dx, dy, dz) + 0.5f;
             clamp_bits |= (c < 0.f ? 1u : 0u) << ch;
             rec[6 + ch] = fmaxf(c, 0.0f);
           }
         } else {
 #pragma unroll
-          for (int ch = 0; ch < 3; ++ch) rec[6 + ch] = in.f[ch];
+          for (int ch = 0; ch < 3; ++ch) rec[6 + ch] = colors[3 * in.sg + ch];
         }
         rec[0] = px;
         rec[1] = py;
@@ -350,9 +347,9 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
   int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
   if (g < G) {
     GaussIn<DEG> in;
-    load_gauss<DEG>(in, (size_t)cam->scene * G + g, M, means, shs, colors, opac, cov6, layout);
+    load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
     float rec[GS];
-    r = project_gauss<DEG>(in, cam, H, W, gx, gy, rec, x0, y0, x1, y1);
+    r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
     store_geom(geom, radii, (size_t)v * G + g, rec, r);
   }
   uint32_t* gcount = seg_count + (size_t)v * T;
@@ -374,14 +371,18 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
 }
 
 // ------------------------------------------------------------------------------------
-// K1+K3 fused (fixed-capacity binning): one workgroup per 256 Gaussians of one scene loads
-// their inputs once and, for every view of that scene, projects them, counts the (view,
-// tile) entries of the block in an LDS histogram, reserves a contiguous range per touched
-// tile with one global atomic, and writes the (depth, id) keys into segment (v, t), which
-// starts at (v*T + t) * G (a Gaussian touches a tile at most once, so G slots suffice). No
-// global scan is needed before the keys exist; the sort pass reads the counts.
+// K1+K3 fused (fixed-capacity binning): one workgroup per (256 Gaussians, view) projects
+// them, counts the block's (view, tile) entries in an LDS histogram, reserves a contiguous
+// range per touched tile with one global atomic, and writes the (depth, id) keys into
+// segment (v, t), which starts at (v*T + t) * G (a Gaussian touches a tile at most once, so
+// G slots suffice). No global scan is needed before the keys exist. (One workgroup per
+// view, re-reading the scene's inputs through L2, beats one per scene looping over its
+// views: 3x the waves in flight hide the load and atomic latencies.)
+#ifndef PB_WPE
+#define PB_WPE 1
+#endif
 template <int DEG>
-__global__ __launch_bounds__(NT) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
                                                      const float* __restrict__ means,
                                                      const float* __restrict__ shs,
                                                      const float* __restrict__ colors,
@@ -394,23 +395,22 @@ __global__ __launch_bounds__(NT) void k_project_emit(int G, int V, int H, int W,
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
-  const int s = blockIdx.y;
+  const int v = blockIdx.y;
+  const dsr_camera* cam = cams + v;
   const int T = gx * gy;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = blockIdx.x * NT + tid;
-  GaussIn<DEG> in;
-  if (g < G) load_gauss<DEG>(in, (size_t)s * G + g, M, means, shs, colors, opac, cov6, layout);
   WaveRects& wr = s_wr[w];
   const uint64_t* wkey = s_key + w * 64;
-  for (int v = 0; v < V; ++v) {
-    const dsr_camera* cam = cams + v;
-    if (cam->scene != s) continue;  // uniform across the workgroup
+  {
     for (int t = tid; t < T; t += NT) s_hist[t] = 0;
     int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     uint64_t key = 0;
     if (g < G) {
+      GaussIn<DEG> in;
+      load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
       float rec[GS];
-      r = project_gauss<DEG>(in, cam, H, W, gx, gy, rec, x0, y0, x1, y1);
+      r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
       store_geom(geom, radii, (size_t)v * G + g, rec, r);
       key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
     }
@@ -421,18 +421,16 @@ __global__ __launch_bounds__(NT) void k_project_emit(int G, int V, int H, int W,
     uint32_t* gcount = seg_count + (size_t)v * T;
     for (int t = tid; t < T; t += NT) {
       const uint32_t c = s_hist[t];
+#ifdef PB_DIAG_NORES
+      s_hist[t] = 0;
+#else
       if (c) s_hist[t] = atomicAdd(&gcount[t], c);
+#endif
     }
     __syncthreads();
-#ifdef PB_STRIDE_CAP
-    const size_t SG = (size_t)min(G, PB_STRIDE_CAP);
-#else
-    const size_t SG = (size_t)G;
-#endif
-    uint64_t* vkeys = keys + (size_t)v * T * SG;
+    uint64_t* vkeys = keys + (size_t)v * T * G;
     for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
-                       [&](int t, int o) { vkeys[(size_t)t * SG + atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
-    __syncthreads();
+                       [&](int t, int o) { vkeys[(size_t)t * G + atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
   }
 }
 
@@ -1646,7 +1644,7 @@ int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M, con
   DSPLAT_REQUIRE((uint64_t)V * T * G < (1ull << 32), "dsr_project_bin: V*tiles*G must fit 32-bit key offsets");
   hipStream_t st = (hipStream_t)stream;
   if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
-  dim3 grid((G + NT - 1) / NT, S);
+  dim3 grid((G + NT - 1) / NT, V);
   const int deg = shs ? sh_degree : -1;
 #define DSR_PB(D)                                                                                             \
   k_project_emit<D><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, \
