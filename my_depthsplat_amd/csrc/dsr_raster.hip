@@ -1019,41 +1019,62 @@ __device__ __forceinline__ bool subtile_hit(float4 q, float4 r, float x0, float 
 #endif
 constexpr int EPL = RF_EPL;      // list entries per lane per chunk
 constexpr int CH = 64 * EPL;     // entries per chunk
-// one compacted list entry: q = (x, y, A, C), r = (B, opacity, red, green), bp = (blue, pos)
-struct __align__(16) ListRec {
-  float4 q;
-  float4 r;
-  float2 bp;
-  float2 pad;
+// Two consecutive list entries with their fields interleaved, so the falloff of both runs
+// as packed FP32 (v_pk_fma/mul/add) with no operand shuffling; per-element results are the
+// same IEEE operations as falloff_p2 (the backward's decisions still agree).
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct __align__(16) PairRec {
+  f2v x, y, A, C, B, o, r, g, b;
+  uint32_t pos[2];
 };
-
-// One compositing step (upstream renderCUDA semantics). A pixel that has stopped keeps a
-// negative T (its magnitude is the final T): for it testT <= 0, so nothing blends again.
-__device__ __forceinline__ void composite_step(const ListRec& e, float pfx, float pfy, float& Tr, float& C0,
-                                               float& C1, float& C2, uint32_t& last) {
-  const float dx = e.q.x - pfx, dy = e.q.y - pfy;
-  const float p2 = falloff_p2(e.q.z, e.r.x, e.q.w, dx, dy);
-  const float alpha = fminf(0.99f, e.r.y * __builtin_amdgcn_exp2f(p2));
-  const bool ok = p2 <= 0.0f && alpha >= 1.0f / 255.0f;
-  const float testT = Tr * (1 - alpha);
-  const bool stop = ok && testT < 0.0001f;
-  const bool blend = ok && !stop;
-  const float wgt = blend ? alpha * Tr : 0.0f;
-  C0 = fmaf(e.r.z, wgt, C0);
-  C1 = fmaf(e.r.w, wgt, C1);
-  C2 = fmaf(e.bp.x, wgt, C2);
-  Tr = blend ? testT : (stop ? -fabsf(Tr) : Tr);
-  last = blend ? __float_as_uint(e.bp.y) : last;
+__device__ __forceinline__ void pair_put(PairRec* l, int k, float x, float y, float A, float C, float B, float o,
+                                         float r, float g, float b, uint32_t pos) {
+  PairRec& d = l[k >> 1];
+  const int j = k & 1;
+  d.x[j] = x; d.y[j] = y; d.A[j] = A; d.C[j] = C; d.B[j] = B; d.o[j] = o;
+  d.r[j] = r; d.g[j] = g; d.b[j] = b; d.pos[j] = pos;
+}
+__device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v pfy2, float& Tr, f2v& C01,
+                                               float& C2, uint32_t& last) {
+  const f2v dx = P.x - pfx2, dy = P.y - pfy2;
+  const f2v Adx = P.A * dx, Cdy = P.C * dy, Bdx = P.B * dx;
+  const f2v Bdxdy = Bdx * dy;
+  const f2v p2 = __builtin_elementwise_fma(Adx, dx, __builtin_elementwise_fma(Cdy, dy, Bdxdy));
+  f2v G;
+  G.x = __builtin_amdgcn_exp2f(p2.x);
+  G.y = __builtin_amdgcn_exp2f(p2.y);
+  const f2v oG = P.o * G;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float alpha = fminf(0.99f, oG[j]);
+    const bool ok = p2[j] <= 0.0f && alpha >= 1.0f / 255.0f;
+    const float testT = Tr * (1 - alpha);
+    const bool stop = ok && testT < 0.0001f;
+    const bool blend = ok && !stop;
+    const float wgt = blend ? alpha * Tr : 0.0f;
+    f2v rg;
+    rg.x = P.r[j];
+    rg.y = P.g[j];
+    f2v w2;
+    w2.x = wgt;
+    w2.y = wgt;
+    C01 = __builtin_elementwise_fma(rg, w2, C01);
+    C2 = fmaf(P.b[j], wgt, C2);
+    Tr = blend ? testT : (stop ? -fabsf(Tr) : Tr);
+    last = blend ? P.pos[j] : last;
+  }
 }
 
 // K6: front-to-back compositing. grid = (gx, gy, V), block = 256 = 4 independent waves;
 // wave w owns the 8x8 sub-tile (w & 1, w >> 1) of the tile. There is no workgroup barrier:
 // each wave walks the tile's list CH entries at a time (EPL keys + records per lane, the
 // next chunk's records and the chunk after's keys already in flight), keeps the entries that
-// can reach its sub-tile in a wave-private LDS list (ballot compaction, list order kept, 4
-// zero-opacity pad records after the end), and composites that list four entries per step
-// with the next four records read ahead. A wave retires as soon as its own 64 pixels have
-// terminated; the waves of a workgroup share the tile's keys/records through L1.
+// can reach its sub-tile in a wave-private LDS list (ballot compaction, list order kept,
+// entry pairs field-interleaved for packed math, 8 zero-opacity pad entries after the end),
+// and composites that list four entries per step with the next four read ahead. A wave
+// retires as soon as its own 64 pixels have terminated (a stopped pixel keeps a negative T
+// whose magnitude is its final T); the waves of a workgroup share the tile's keys/records
+// through L1.
 __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, int T,
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
@@ -1062,7 +1083,7 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
                                                    const uint64_t* __restrict__ keys,
                                                    float* __restrict__ out, float* __restrict__ finalT,
                                                    uint32_t* __restrict__ ncontrib) {
-  __shared__ ListRec l_rec[4][CH + 4];
+  __shared__ PairRec l_pair[4][(CH + 8) / 2];
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int sx0 = blockIdx.x * BX + (w & 1) * SUB, sy0 = blockIdx.y * BY + (w >> 1) * SUB;
@@ -1076,7 +1097,9 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   const float fx0 = (float)sx0, fy0 = (float)sy0;
   const float* gv = geom + (size_t)v * G * GS;
   const uint64_t lt = dsplat::lanemask_lt(lane);
-  ListRec* list = l_rec[w];
+  PairRec* plist = l_pair[w];
+  const f2v pfx2 = {pfx, pfx}, pfy2 = {pfy, pfy};
+  f2v C01 = {0.f, 0.f};
   float Tr = inside ? 1.0f : -1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
   uint32_t last = 0;
   float4 cq[EPL], cr[EPL];
@@ -1122,34 +1145,26 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
       const uint64_t bal = __ballot(mine);
       if (mine) {
         const float4 sq = scaled_conic_q(cq[u]);  // (x, y, A, B)
-        ListRec& d = list[cnt + __popcll(bal & lt)];
-        d.q = make_float4(sq.x, sq.y, sq.z, -0.5f * kLog2e * cr[u].x);
-        d.r = make_float4(sq.w, cr[u].y, cr[u].z, cr[u].w);
-        d.bp = make_float2(cb[u], __uint_as_float(e - start + 1u));
+        pair_put(plist, cnt + __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * cr[u].x, sq.w, cr[u].y,
+                 cr[u].z, cr[u].w, cb[u], e - start + 1u);
       }
       cnt += __popcll(bal);
     }
-    if (lane < 4) {  // pad: opacity 0 -> alpha 0 -> never blends
-      ListRec& d = list[cnt + lane];
-      d.q = make_float4(0.f, 0.f, 0.f, 0.f);
-      d.r = d.q;
-      d.bp = make_float2(0.f, 0.f);
-    }
+    if (lane < 8)  // pad up to 8 entries: opacity 0 -> alpha 0 -> never blends
+      pair_put(plist, cnt + lane, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u);
     __builtin_amdgcn_wave_barrier();
-    const ListRec* p = list;
-    ListRec e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
-    for (int k = 0; k < cnt; k += 4) {
-      p += 4;
-      const ListRec f0 = p[0], f1 = p[1], f2 = p[2], f3 = p[3];  // in bounds: k + 7 <= CH + 3
-      composite_step(e0, pfx, pfy, Tr, C0, C1, C2, last);
-      composite_step(e1, pfx, pfy, Tr, C0, C1, C2, last);
-      composite_step(e2, pfx, pfy, Tr, C0, C1, C2, last);
-      composite_step(e3, pfx, pfy, Tr, C0, C1, C2, last);
-      if (__all(Tr < 0.0f)) break;
-      e0 = f0;
-      e1 = f1;
-      e2 = f2;
-      e3 = f3;
+    {
+      const PairRec* pp = plist;
+      PairRec a0 = pp[0], a1 = pp[1];
+      for (int k = 0; k < cnt; k += 4) {
+        pp += 2;
+        const PairRec b0 = pp[0], b1 = pp[1];  // in bounds: pair k/2 + 3 <= (CH + 8) / 2 - 1
+        composite_pair(a0, pfx2, pfy2, Tr, C01, C2, last);
+        composite_pair(a1, pfx2, pfy2, Tr, C01, C2, last);
+        if (__all(Tr < 0.0f)) break;
+        a0 = b0;
+        a1 = b1;
+      }
     }
     __builtin_amdgcn_wave_barrier();  // list reads of this chunk before the next chunk's writes
 #pragma unroll
@@ -1163,6 +1178,8 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
     const size_t HW = (size_t)H * W;
     const size_t pix = (size_t)py * W + px;
     const float* bg = cams[v].bg;
+    C0 = C01.x;
+    C1 = C01.y;
     const float Tf = fabsf(Tr);
     finalT[v * HW + pix] = Tf;
     ncontrib[v * HW + pix] = last;
