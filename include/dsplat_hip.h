@@ -189,6 +189,29 @@ int dcv_warp_bwd(int B, int C, int H, int W, int D, const float* dout, const flo
                  const float* pose, const float* depth, float clamp_min_depth, float* dfeature,
                  void* stream);
 
+/* ---- Gaussian adapter ----------------------------------------------------------------
+ * Fused encoder glue + GaussianAdapter + rotate_sh (encoder_depthsplat.py:224-346,
+ * gaussian_adapter.py:49-102, gaussians.py:8-44, sh_rotation.py:10-30), one thread per
+ * (scene, context view, pixel). head [B,V,H*W,C] (C >= 10 + 3*d_sh: opacity logit, 2 offset
+ * logits, 3 scales, 4 quaternion xyzw, 3*d_sh SH channel-major), depths [B,V,H*W],
+ * images [B,V,3,H,W], cams [B*V,104] per-view blocks (R c2w [9], t [3], K^-1 [9],
+ * Wigner-D of R for degrees 1..3 [9, 25, 49]), sh_mask [d_sh].
+ * out: means [B,G,3], covariances [B,G,3,3], harmonics [B,G,3,d_sh], opacities [B,G],
+ * G = V*H*W view-major (the decoder's Gaussians). d_sh in {1, 4, 9, 16}. */
+int dga_adapter_fwd(int B, int V, int H, int W, int d_sh, int C, const float* head,
+                    const float* depths, const float* images, const float* cams, float scale_min,
+                    float scale_max, const float* sh_mask, float* means, float* covariances,
+                    float* harmonics, float* opacities, void* stream);
+
+/* Backward of dga_adapter_fwd: any of the output gradients may be NULL (zero). dhead
+ * [B,V,H*W,C] overwritten (channels past 10 + 3*d_sh get 0); ddepths [B,V,H*W] overwritten
+ * when non-NULL. Images and cameras get no gradient. */
+int dga_adapter_bwd(int B, int V, int H, int W, int d_sh, int C, const float* head,
+                    const float* depths, const float* cams, float scale_min, float scale_max,
+                    const float* sh_mask, const float* dmeans, const float* dcovariances,
+                    const float* dharmonics, const float* dopacities, float* dhead, float* ddepths,
+                    void* stream);
+
 /* ---- misc ------------------------------------------------------------------------- */
 const char* dsplat_last_error(void);
 int dsplat_abi_version(void);

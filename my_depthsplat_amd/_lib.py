@@ -35,6 +35,9 @@ SIGNATURES: dict[str, tuple] = {
                                  _P, _P, _P]),
     "dcv_warp_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, _P, _P]),
     "dcv_warp_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, _P, _P]),
+    "dga_adapter_fwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, c_float, _P, _P, _P, _P, _P, _P]),
+    "dga_adapter_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
+                             _P]),
     "dsplat_last_error": (ctypes.c_char_p, []),
     "dsplat_abi_version": (_I, []),
 }

@@ -1,0 +1,385 @@
+// dga_adapter.hip — fused Gaussian adapter (head channels -> world-space Gaussians) for gfx950.
+//
+// One thread per (scene b, context view v, pixel p) replaces the encoder glue and adapter
+// (SURVEY §8a rows A13-A16), which in torch are ~30 small kernels plus batched 3x3 GEMMs:
+//   opacity = sigmoid(head[0])                                  encoder_depthsplat.py:258
+//   xy = pixel centre + (sigmoid(head[1:3]) - 0.5) / (W, H)      encoder_depthsplat.py:263-273
+//   scale = clamp(softplus(head[3:6] - 4), min, max)             gaussian_adapter.py:64-67
+//   q = head[6:10] / (|head[6:10]| + 1e-8)  (xyzw)               gaussian_adapter.py:72
+//   sh = head[10:].view(3, d_sh) * sh_mask; sh[:, 0] += (rgb - 0.5) / C0   :75-82
+//   cov = Rc (R S S^T R^T) Rc^T                                  :85-87, gaussians.py:8-44
+//   mean = t + Rc (K^-1 [x, y, 1] / z) * depth                  :90-91, projection.py:91-114
+//   harmonics = D_l(Rc) sh  (per degree block)                   :96, sh_rotation.py:10-30
+// and the backward of all of it w.r.t. head and depth. Per-view constants (Rc, t, K^-1 and
+// the Wigner-D blocks of Rc) come precomputed in a [B*V, 104] float block.
+// The operation order follows the torch modules (matmul sums in k = 0, 1, 2 order).
+
+#include "dsplat_common.h"
+
+namespace {
+
+constexpr float kC0 = 0.28209479177387814f;
+constexpr int kCamFloats = 104;  // R[9] t[3] Kinv[9] D1[9] D2[25] D3[49]
+constexpr int kOffR = 0, kOffT = 9, kOffKinv = 12, kOffD1 = 21, kOffD2 = 30, kOffD3 = 55;
+constexpr int NT = 256;
+
+__device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// torch.nn.functional.softplus (beta 1, threshold 20)
+__device__ __forceinline__ float softplusf(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float softplus_grad(float x) { return x > 20.0f ? 1.0f : 1.0f / (1.0f + expf(-x)); }
+
+struct QuatR {
+  float R[9];
+  float s2;  // 2 / (|q|^2 + eps)
+};
+
+// quaternion_to_matrix (gaussians.py:8-30), q = (i, j, k, r)
+__device__ __forceinline__ void quat_to_R(const float q[4], QuatR& o) {
+  const float i = q[0], j = q[1], k = q[2], r = q[3];
+  const float n = ((i * i + j * j) + k * k) + r * r;
+  const float s = 2.0f / (n + 1e-8f);
+  o.s2 = s;
+  o.R[0] = 1.0f - s * (j * j + k * k);
+  o.R[1] = s * (i * j - k * r);
+  o.R[2] = s * (i * k + j * r);
+  o.R[3] = s * (i * j + k * r);
+  o.R[4] = 1.0f - s * (i * i + k * k);
+  o.R[5] = s * (j * k - i * r);
+  o.R[6] = s * (i * k - j * r);
+  o.R[7] = s * (j * k + i * r);
+  o.R[8] = 1.0f - s * (i * i + j * j);
+}
+
+// C = A B (3x3 row-major), sums in k order
+__device__ __forceinline__ void mm3(const float* A, const float* B, float* C) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) C[a * 3 + c] = (A[a * 3] * B[c] + A[a * 3 + 1] * B[3 + c]) + A[a * 3 + 2] * B[6 + c];
+}
+// C = A B^T
+__device__ __forceinline__ void mm3t(const float* A, const float* B, float* C) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      C[a * 3 + c] = (A[a * 3] * B[c * 3] + A[a * 3 + 1] * B[c * 3 + 1]) + A[a * 3 + 2] * B[c * 3 + 2];
+}
+// C = A^T B
+__device__ __forceinline__ void mmt3(const float* A, const float* B, float* C) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) C[a * 3 + c] = (A[a] * B[c] + A[3 + a] * B[3 + c]) + A[6 + a] * B[6 + c];
+}
+
+struct Pix {
+  int b, v, p, i, j;
+  size_t n;   // flat (b, v, p)
+  size_t bg;  // b * G + v * HW + p (scene-major output index)
+};
+
+__device__ __forceinline__ bool pixel_of(size_t n, int B, int V, int H, int W, Pix& px) {
+  const size_t HW = (size_t)H * W;
+  if (n >= (size_t)B * V * HW) return false;
+  px.n = n;
+  const size_t bv = n / HW;
+  px.p = (int)(n - bv * HW);
+  px.b = (int)(bv / V);
+  px.v = (int)(bv - (size_t)px.b * V);
+  px.i = px.p / W;
+  px.j = px.p - px.i * W;
+  px.bg = (size_t)px.b * V * HW + (size_t)px.v * HW + px.p;
+  return true;
+}
+
+// pixel ray: x, y normalised coordinates -> u = K^-1 [x, y, 1], d = u / u.z, dw = Rc d
+__device__ __forceinline__ void ray(const float* cam, float x, float y, float u[3], float d[3], float dw[3]) {
+  const float* Ki = cam + kOffKinv;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) u[a] = (Ki[a * 3] * x + Ki[a * 3 + 1] * y) + Ki[a * 3 + 2] * 1.0f;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) d[a] = u[a] / u[2];
+  const float* Rc = cam + kOffR;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) dw[a] = (Rc[a * 3] * d[0] + Rc[a * 3 + 1] * d[1]) + Rc[a * 3 + 2] * d[2];
+}
+
+template <int NSH>
+__device__ __forceinline__ const float* dblock(const float* cam, int l) {
+  return cam + (l == 1 ? kOffD1 : l == 2 ? kOffD2 : kOffD3);
+}
+
+template <int NSH>
+__global__ __launch_bounds__(NT) void k_adapter_fwd(int B, int V, int H, int W, int C, const float* __restrict__ head,
+                                                    const float* __restrict__ depths,
+                                                    const float* __restrict__ images,
+                                                    const float* __restrict__ cams, float smin, float smax,
+                                                    const float* __restrict__ sh_mask, float* __restrict__ means,
+                                                    float* __restrict__ covs, float* __restrict__ harm,
+                                                    float* __restrict__ opac) {
+  Pix px;
+  if (!pixel_of((size_t)blockIdx.x * NT + threadIdx.x, B, V, H, W, px)) return;
+  const size_t HW = (size_t)H * W;
+  const float* h = head + px.n * C;
+  const float* cam = cams + ((size_t)px.b * V + px.v) * kCamFloats;
+  opac[px.bg] = sigmoidf(h[0]);
+  // position: xy from the pixel centre and the offset logits, then the camera ray
+  const float x = ((float)px.j + 0.5f) / (float)W + (sigmoidf(h[1]) - 0.5f) * (1.0f / (float)W);
+  const float y = ((float)px.i + 0.5f) / (float)H + (sigmoidf(h[2]) - 0.5f) * (1.0f / (float)H);
+  float u[3], d[3], dw[3];
+  ray(cam, x, y, u, d, dw);
+  const float z = depths[px.n];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) means[px.bg * 3 + a] = cam[kOffT + a] + dw[a] * z;
+  // covariance
+  float s[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k] = fminf(fmaxf(softplusf(h[3 + k] - 4.0f), smin), smax);
+  float q[4];
+  const float L = sqrtf(((h[6] * h[6] + h[7] * h[7]) + h[8] * h[8]) + h[9] * h[9]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = h[6 + k] / (L + 1e-8f);
+  QuatR qr;
+  quat_to_R(q, qr);
+  float M[9], Cl[9], T1[9], Cw[9];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) M[a * 3 + k] = (qr.R[a * 3 + k] * s[k]) * s[k];
+  mm3t(M, qr.R, Cl);             // (R S S^T) R^T
+  mm3(cam + kOffR, Cl, T1);      // Rc C
+  mm3t(T1, cam + kOffR, Cw);     // (Rc C) Rc^T
+#pragma unroll
+  for (int k = 0; k < 9; ++k) covs[px.bg * 9 + k] = Cw[k];
+  // harmonics: masked raw SH + the image colour in the DC term, rotated per degree block
+  const float* img = images + ((size_t)px.b * V + px.v) * 3 * HW + px.p;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float sh[NSH];
+#pragma unroll
+    for (int k = 0; k < NSH; ++k) sh[k] = h[10 + c * NSH + k] * sh_mask[k];
+    sh[0] = sh[0] + (img[c * HW] - 0.5f) / kC0;
+    float* o = harm + (px.bg * 3 + c) * NSH;
+    o[0] = sh[0];
+#pragma unroll
+    for (int l = 1; l * l < NSH; ++l) {
+      const int n = 2 * l + 1, b0 = l * l;
+      const float* D = dblock<NSH>(cam, l);
+#pragma unroll
+      for (int a = 0; a < n; ++a) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < n; ++k) acc = acc + D[a * n + k] * sh[b0 + k];
+        o[b0 + a] = acc;
+      }
+    }
+  }
+}
+
+template <int NSH>
+__global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, int C, const float* __restrict__ head,
+                                                    const float* __restrict__ depths,
+                                                    const float* __restrict__ cams, float smin, float smax,
+                                                    const float* __restrict__ sh_mask,
+                                                    const float* __restrict__ dmeans,
+                                                    const float* __restrict__ dcovs,
+                                                    const float* __restrict__ dharm,
+                                                    const float* __restrict__ dopac, float* __restrict__ dhead,
+                                                    float* __restrict__ ddepth) {
+  Pix px;
+  if (!pixel_of((size_t)blockIdx.x * NT + threadIdx.x, B, V, H, W, px)) return;
+  const float* h = head + px.n * C;
+  float* dh = dhead + px.n * C;
+  const float* cam = cams + ((size_t)px.b * V + px.v) * kCamFloats;
+  // opacity
+  {
+    const float sg = sigmoidf(h[0]);
+    dh[0] = dopac ? dopac[px.bg] * sg * (1.0f - sg) : 0.0f;
+  }
+  // mean -> depth, offsets
+  {
+    const float s1 = sigmoidf(h[1]), s2 = sigmoidf(h[2]);
+    const float x = ((float)px.j + 0.5f) / (float)W + (s1 - 0.5f) * (1.0f / (float)W);
+    const float y = ((float)px.i + 0.5f) / (float)H + (s2 - 0.5f) * (1.0f / (float)H);
+    float u[3], d[3], dw[3];
+    ray(cam, x, y, u, d, dw);
+    float gm[3] = {0.f, 0.f, 0.f};
+    if (dmeans)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) gm[a] = dmeans[px.bg * 3 + a];
+    const float z = depths[px.n];
+    if (ddepth) ddepth[px.n] = (gm[0] * dw[0] + gm[1] * dw[1]) + gm[2] * dw[2];
+    const float* Rc = cam + kOffR;
+    float gd[3];  // d L / d d = Rc^T (z gm)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gd[k] = (Rc[k] * gm[0] + Rc[3 + k] * gm[1]) + Rc[6 + k] * gm[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gd[k] *= z;
+    // d = u / u2
+    const float inv = 1.0f / u[2];
+    const float dot = (gd[0] * u[0] + gd[1] * u[1]) + gd[2] * u[2];
+    float gu[3];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) gu[b] = gd[b] * inv;
+    gu[2] -= dot * inv * inv;
+    const float* Ki = cam + kOffKinv;
+    const float gx = (Ki[0] * gu[0] + Ki[3] * gu[1]) + Ki[6] * gu[2];
+    const float gy = (Ki[1] * gu[0] + Ki[4] * gu[1]) + Ki[7] * gu[2];
+    dh[1] = gx * (1.0f / (float)W) * s1 * (1.0f - s1);
+    dh[2] = gy * (1.0f / (float)H) * s2 * (1.0f - s2);
+  }
+  // covariance -> scales, rotation
+  {
+    float s[3], sraw[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      sraw[k] = softplusf(h[3 + k] - 4.0f);
+      s[k] = fminf(fmaxf(sraw[k], smin), smax);
+    }
+    float r[4], q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = h[6 + k];
+    const float L = sqrtf(((r[0] * r[0] + r[1] * r[1]) + r[2] * r[2]) + r[3] * r[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = r[k] / (L + 1e-8f);
+    QuatR qr;
+    quat_to_R(q, qr);
+    float gCw[9], T[9], gC[9];
+    if (dcovs) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) gCw[k] = dcovs[px.bg * 9 + k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) gCw[k] = 0.f;
+    }
+    mmt3(cam + kOffR, gCw, T);  // Rc^T gCw
+    mm3(T, cam + kOffR, gC);    // (Rc^T gCw) Rc
+    // C = R diag(s^2) R^T: dR = (gC + gC^T) R diag(s^2); dsig_k = (R^T gC R)_kk
+    float gS[9], gR[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) gS[k] = gC[k] + gC[(k % 3) * 3 + k / 3];
+    float RS2[9];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) RS2[a * 3 + k] = qr.R[a * 3 + k] * (s[k] * s[k]);
+    mm3(gS, RS2, gR);
+    float GR[9];
+    mm3(gC, qr.R, GR);  // gC R
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float dsig = (qr.R[k] * GR[k] + qr.R[3 + k] * GR[3 + k]) + qr.R[6 + k] * GR[6 + k];
+      const float ds = 2.0f * s[k] * dsig;
+      const bool pass = sraw[k] >= smin && sraw[k] <= smax;  // torch.clamp gradient mask
+      dh[3 + k] = pass ? ds * softplus_grad(h[3 + k] - 4.0f) : 0.0f;
+    }
+    // R(q) = I + s2 P(q), s2 = 2 / (|q|^2 + eps)
+    const float i = q[0], j = q[1], kk = q[2], w = q[3], s2 = qr.s2;
+    const float P[9] = {-(j * j + kk * kk), i * j - kk * w, i * kk + j * w,
+                        i * j + kk * w,     -(i * i + kk * kk), j * kk - i * w,
+                        i * kk - j * w,     j * kk + i * w,     -(i * i + j * j)};
+    float gs2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) gs2 += gR[k] * P[k];
+    const float g = gR[0], g01 = gR[1], g02 = gR[2], g10 = gR[3], g11 = gR[4], g12 = gR[5], g20 = gR[6],
+                g21 = gR[7], g22 = gR[8];
+    float gq[4];
+    gq[0] = s2 * (g01 * j + g02 * kk + g10 * j - 2.f * g11 * i - g12 * w + g20 * kk + g21 * w - 2.f * g22 * i);
+    gq[1] = s2 * (-2.f * g * j + g01 * i + g02 * w + g10 * i + g12 * kk - g20 * w + g21 * kk - 2.f * g22 * j);
+    gq[2] = s2 * (-2.f * g * kk - g01 * w + g02 * i + g10 * w - 2.f * g11 * kk + g12 * j + g20 * i + g21 * j);
+    gq[3] = s2 * (-g01 * kk + g02 * j + g10 * kk - g12 * i - g20 * j + g21 * i);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) gq[m] -= gs2 * s2 * s2 * q[m];
+    // q = r / (|r| + eps)
+    const float Le = L + 1e-8f;
+    const float dqr = ((gq[0] * r[0] + gq[1] * r[1]) + gq[2] * r[2]) + gq[3] * r[3];
+    const float c2 = L > 0.f ? dqr / (L * Le * Le) : 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) dh[6 + m] = gq[m] / Le - c2 * r[m];
+  }
+  // harmonics -> raw SH: D^T per degree block, then the mask
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float gh[NSH];
+    if (dharm) {
+#pragma unroll
+      for (int k = 0; k < NSH; ++k) gh[k] = dharm[(px.bg * 3 + c) * NSH + k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NSH; ++k) gh[k] = 0.f;
+    }
+    float gs[NSH];
+    gs[0] = gh[0];
+#pragma unroll
+    for (int l = 1; l * l < NSH; ++l) {
+      const int n = 2 * l + 1, b0 = l * l;
+      const float* D = dblock<NSH>(cam, l);
+#pragma unroll
+      for (int k = 0; k < n; ++k) {
+        float acc = 0.f;
+#pragma unroll
+        for (int a = 0; a < n; ++a) acc += D[a * n + k] * gh[b0 + a];
+        gs[b0 + k] = acc;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NSH; ++k) dh[10 + c * NSH + k] = gs[k] * sh_mask[k];
+  }
+  for (int k = 10 + 3 * NSH; k < C; ++k) dh[k] = 0.f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dga_adapter_fwd(int B, int V, int H, int W, int d_sh, int C, const float* head, const float* depths,
+                    const float* images, const float* cams, float scale_min, float scale_max, const float* sh_mask,
+                    float* means, float* covariances, float* harmonics, float* opacities, void* stream) {
+  DSPLAT_REQUIRE(B > 0 && V > 0 && H > 0 && W > 0, "dga_adapter_fwd: bad sizes");
+  DSPLAT_REQUIRE(d_sh == 1 || d_sh == 4 || d_sh == 9 || d_sh == 16, "dga_adapter_fwd: d_sh=%d (1, 4, 9, 16)", d_sh);
+  DSPLAT_REQUIRE(C >= 10 + 3 * d_sh, "dga_adapter_fwd: %d head channels < 10 + 3*d_sh", C);
+  DSPLAT_REQUIRE(head && depths && images && cams && sh_mask && means && covariances && harmonics && opacities,
+                 "dga_adapter_fwd: null pointer");
+  const size_t n = (size_t)B * V * H * W;
+  const unsigned grid = (unsigned)((n + NT - 1) / NT);
+  hipStream_t st = (hipStream_t)stream;
+#define DGA_F(NS)                                                                                     \
+  k_adapter_fwd<NS><<<grid, NT, 0, st>>>(B, V, H, W, C, head, depths, images, cams, scale_min, scale_max, \
+                                         sh_mask, means, covariances, harmonics, opacities)
+  switch (d_sh) {
+    case 1: DGA_F(1); break;
+    case 4: DGA_F(4); break;
+    case 9: DGA_F(9); break;
+    default: DGA_F(16); break;
+  }
+#undef DGA_F
+  return dsplat::check_launch("k_adapter_fwd");
+}
+
+int dga_adapter_bwd(int B, int V, int H, int W, int d_sh, int C, const float* head, const float* depths,
+                    const float* cams, float scale_min, float scale_max, const float* sh_mask, const float* dmeans,
+                    const float* dcovariances, const float* dharmonics, const float* dopacities, float* dhead,
+                    float* ddepths, void* stream) {
+  DSPLAT_REQUIRE(B > 0 && V > 0 && H > 0 && W > 0, "dga_adapter_bwd: bad sizes");
+  DSPLAT_REQUIRE(d_sh == 1 || d_sh == 4 || d_sh == 9 || d_sh == 16, "dga_adapter_bwd: d_sh=%d (1, 4, 9, 16)", d_sh);
+  DSPLAT_REQUIRE(C >= 10 + 3 * d_sh, "dga_adapter_bwd: %d head channels < 10 + 3*d_sh", C);
+  DSPLAT_REQUIRE(head && depths && cams && sh_mask && dhead, "dga_adapter_bwd: null pointer");
+  const size_t n = (size_t)B * V * H * W;
+  const unsigned grid = (unsigned)((n + NT - 1) / NT);
+  hipStream_t st = (hipStream_t)stream;
+#define DGA_B(NS)                                                                                       \
+  k_adapter_bwd<NS><<<grid, NT, 0, st>>>(B, V, H, W, C, head, depths, cams, scale_min, scale_max, sh_mask, \
+                                         dmeans, dcovariances, dharmonics, dopacities, dhead, ddepths)
+  switch (d_sh) {
+    case 1: DGA_B(1); break;
+    case 4: DGA_B(4); break;
+    case 9: DGA_B(9); break;
+    default: DGA_B(16); break;
+  }
+#undef DGA_B
+  return dsplat::check_launch("k_adapter_bwd");
+}
+
+}  // extern "C"

@@ -113,7 +113,21 @@ def gaussians_from_head(head: torch.Tensor, depths: torch.Tensor, images: torch.
     offset logits, adapter input), depths [B, V, H*W, 1, 1], images [B, V, 3, H, W],
     extrinsics [B, V, 4, 4] (c2w), intrinsics [B, V, 3, 3] (normalised).
     Returns the decoder's Gaussians (means [B, G, 3], covariances [B, G, 3, 3],
-    harmonics [B, G, 3, d_sh], opacities [B, G]) with G = V*H*W, view-major."""
+    harmonics [B, G, 3, d_sh], opacities [B, G]) with G = V*H*W, view-major.
+
+    Device tensors go through the fused HIP adapter (dga_adapter_fwd/bwd: one pass, grads
+    for head and depths; the images get none). Host tensors (synthetic-data generation for
+    the CPU oracle) use the torch composition of the reference modules below."""
+    if head.is_cuda:
+        from .adapter_hip import fused_gaussians_from_head
+        return fused_gaussians_from_head(head, depths, images, extrinsics, intrinsics, adapter)
+    return gaussians_from_head_torch(head, depths, images, extrinsics, intrinsics, adapter)
+
+
+def gaussians_from_head_torch(head: torch.Tensor, depths: torch.Tensor, images: torch.Tensor,
+                              extrinsics: torch.Tensor, intrinsics: torch.Tensor, adapter: GaussianAdapter):
+    """gaussians_from_head as the reference's torch modules compute it (the fp32 reference of
+    the fused kernel, and the host-tensor path)."""
     from .decoder import Gaussians
 
     B, V = extrinsics.shape[:2]
