@@ -117,11 +117,16 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
  * sort of (tile << 32 | depth) with emission-order ties (K4/K5). max_count sizes the LDS
  * sort (0 = unknown): segments that fit sort in LDS, larger ones sort through HBM using
  * `scratch` (same size as keys). scratch may be NULL only when max_count is an exact
- * bound <= dsr_sort_lds_capacity(). (In the fixed-capacity layout N and the largest
- * segment are sum / max of seg_count: no same-address atomics from every workgroup.) */
+ * bound <= dsr_sort_lds_capacity(). When max_count exceeds the LDS capacity, segments
+ * above 4096 entries are split by depth into LDS-sized groups (one MSD pass through
+ * scratch), which needs `workspace` of dsr_bin_sort_workspace_size(V, H, W, max_count)
+ * bytes (NULL allowed when that is 0). (In the fixed-capacity layout N and the largest
+ * segment are sum / max of seg_count: no same-address atomics from every workgroup.)
+ * Offsets must stay below 2^31. */
 int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const uint32_t* seg_count,
                  uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count,
-                 void* stream);
+                 void* workspace, void* stream);
+size_t dsr_bin_sort_workspace_size(int V, int H, int W, uint32_t max_count);
 uint32_t dsr_sort_lds_capacity(void);
 
 /* Front-to-back compositing per 16x16 tile (K6). out_color [V,3,H,W], final_T [V,H,W],

@@ -859,7 +859,7 @@ __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, ui
 
 // One workgroup per (view, tile) segment. n <= 256*KMAX: sort in LDS. Larger: when
 // big_here, sort through HBM (keys <-> scratch) with the ballot-ranked passes; otherwise
-// leave it to k_sort_global.
+// leave it to the MSD split (k_msd_split + k_sort_groups).
 #ifndef SORT_WPE
 #define SORT_WPE 3
 #endif
@@ -915,22 +915,161 @@ constexpr size_t sort_lds_bytes() {
   return (size_t)(NT * KMAX + NT) * 8 + 8192 + 64 * 4;
 }
 
-// Segments larger than the LDS capacity: same passes through HBM, 16 waves.
-__global__ __launch_bounds__(1024) void k_sort_global(const uint32_t* __restrict__ seg_start,
-                                                      const uint32_t* __restrict__ seg_count, uint32_t stride,
-                                                      uint64_t* __restrict__ keys,
-                                                      uint64_t* __restrict__ scratch, int id_bits,
-                                                      uint32_t cap) {
-  __shared__ uint32_t hist[16 * 256];
-  __shared__ uint32_t wsum[4];
-  __shared__ uint32_t flag;
-  const int seg = blockIdx.x;
+// ---- segments larger than the LDS sort (6-view 448x768 and up: ~30-40K entries per tile) --
+// One MSD pass splits each such segment by the top 12 bits of (depth - segment min) into
+// 4096 buckets, written bucket-contiguous to `scratch` at the segment's own offsets; runs of
+// consecutive buckets then form groups of at most ~kGroupCap keys (a group ends at the first
+// bucket boundary past each multiple of kGroupCap/2), and every group is sorted by the full
+// key in LDS (k_sort_groups) straight into `keys`. Buckets are ordered ranges of depth, so
+// sorted groups concatenate into the sorted segment. Two HBM round trips per key instead of
+// eight radix passes. A group still above the LDS capacity (one bucket holding > ~2K keys
+// of near-equal depth) takes the HBM radix path inside k_sort_groups.
+constexpr int kSplitNB = 4096;
+constexpr uint32_t kGroupCap = NT * 16;  // k_sort_groups<16>
+constexpr uint32_t kGroupHalf = kGroupCap / 2;
+constexpr uint32_t kFromKeys = 0x80000000u;  // group flag: data still in keys (not split)
+
+__host__ __device__ inline int split_groups(uint32_t max_count) { return (int)((max_count + kGroupHalf - 1) / kGroupHalf) + 1; }
+
+__global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__ seg_start,
+                                                    const uint32_t* __restrict__ seg_count, uint32_t stride,
+                                                    const uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
+                                                    uint32_t small_cap, uint32_t* __restrict__ groups, int gmax) {
+  __shared__ uint32_t hist[kSplitNB];
+  __shared__ uint32_t red[32];
+  const int seg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t* gout = groups + (size_t)seg * gmax * 2;
   uint32_t b, e;
   seg_bounds(seg_start, seg_count, stride, seg, b, e);
   const uint32_t n = e - b;
-  if (n <= cap) return;
-  sort_segment<1024>(keys + b, scratch + b, n, id_bits, hist, wsum, &flag, keys + b);
+  if (n <= small_cap) {  // sorted by k_sort_lds already
+    for (int g = tid; g < gmax; g += 1024) gout[2 * g] = gout[2 * g + 1] = 0u;
+    return;
+  }
+  if ((int)((n + kGroupHalf - 1) / kGroupHalf) + 1 > gmax) {  // larger than the launch was sized for
+    for (int g = tid; g < gmax; g += 1024) {
+      gout[2 * g] = g == 0 ? b : 0u;
+      gout[2 * g + 1] = g == 0 ? (e | kFromKeys) : 0u;
+    }
+    return;
+  }
+  // segment min / max of the depth word
+  uint32_t mn = 0xffffffffu, mx = 0u;
+  for (uint32_t i = tid; i < n; i += 1024) {
+    const uint32_t d = (uint32_t)(keys[b + i] >> 32);
+    mn = min(mn, d);
+    mx = max(mx, d);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+  }
+  if (lane == 0) {
+    red[w] = mn;
+    red[16 + w] = mx;
+  }
+  for (int k = tid; k < kSplitNB; k += 1024) hist[k] = 0u;
+  __syncthreads();
+  mn = red[0];
+  mx = red[16];
+  for (int k = 1; k < 16; ++k) {
+    mn = min(mn, red[k]);
+    mx = max(mx, red[16 + k]);
+  }
+  const uint32_t range = mx - mn;
+  const int msb = range ? 31 - __clz(range) : 0;
+  const int sh = max(0, msb - 11);
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += 1024) atomicAdd(&hist[((uint32_t)(keys[b + i] >> 32) - mn) >> sh], 1u);
+  __syncthreads();
+  // exclusive scan: thread t owns buckets [4t, 4t + 4)
+  uint32_t c[4], tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    c[k] = hist[4 * tid + k];
+    tot += c[k];
+  }
+  const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
+  if (lane == 63) red[w] = incl;
+  __syncthreads();
+  uint32_t off = incl - tot;
+  for (int k = 0; k < w; ++k) off += red[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hist[4 * tid + k] = off;
+    off += c[k];
+  }
+  __syncthreads();
+  // group g = [B_g, B_{g+1}) with B_g = first bucket offset >= g * kGroupHalf (n if none)
+  if (tid < gmax) {
+    auto bound = [&](uint32_t target) -> uint32_t {
+      if (target == 0) return 0u;
+      if (target >= n) return n;
+      int lo = 0, hi = kSplitNB;  // first k with hist[k] >= target
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (hist[mid] >= target) hi = mid;
+        else lo = mid + 1;
+      }
+      return lo < kSplitNB ? hist[lo] : n;
+    };
+    const uint32_t g0 = bound((uint32_t)tid * kGroupHalf), g1 = bound((uint32_t)(tid + 1) * kGroupHalf);
+    gout[2 * tid] = b + g0;
+    gout[2 * tid + 1] = b + g1;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += 1024) {
+    const uint64_t k = keys[b + i];
+    const uint32_t pos = atomicAdd(&hist[((uint32_t)(k >> 32) - mn) >> sh], 1u);
+    scratch[b + pos] = k;
+  }
 }
+
+// Sort every group produced by k_msd_split into `keys` (from scratch, or from keys when the
+// segment was not split). grid = nseg * gmax.
+template <int KMAX>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) void k_sort_groups(
+    const uint32_t* __restrict__ groups, uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits) {
+  constexpr uint32_t cap = NT * KMAX;
+  constexpr uint32_t padded = cap + cap / KMAX;
+  extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
+  uint64_t* A = s_keys;
+  uint32_t* aux = reinterpret_cast<uint32_t*>(A + padded);
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(aux);
+  uint32_t* wsum = aux + 2048;
+  uint32_t* flag = wsum + 16;
+  const uint32_t b = groups[2 * blockIdx.x], ew = groups[2 * blockIdx.x + 1];
+  const uint32_t e = ew & ~kFromKeys;
+  if (e <= b) return;
+  const uint32_t n = e - b;
+  uint64_t* src = (ew & kFromKeys) ? keys : scratch;
+  if (n > cap) {
+    sort_segment<NT>(src + b, (src == keys ? scratch : keys) + b, n, id_bits, aux, wsum, flag, keys + b);
+    return;
+  }
+  {
+    uint64_t tmp[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      const uint32_t idx = threadIdx.x + (uint32_t)i * NT;
+      tmp[i] = idx < n ? src[b + idx] : 0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      const uint32_t idx = threadIdx.x + (uint32_t)i * NT;
+      if (idx < n) A[padi<KMAX>(idx)] = tmp[i];
+    }
+  }
+  __syncthreads();
+  if (n > 1) reg_sort<KMAX>(A, n, id_bits, cnt, wsum, flag);
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const uint32_t idx = threadIdx.x + (uint32_t)i * NT;
+    if (idx < n) keys[b + idx] = A[padi<KMAX>(idx)];
+  }
+}
+
 
 // ------------------------------------------------------------------------------------
 // K6/K7 shared structure. A 16x16 tile = 4 waves; wave w owns the 8x8 sub-tile
@@ -1697,8 +1836,15 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
   return dsplat::check_launch("k_scatter");
 }
 
+size_t dsr_bin_sort_workspace_size(int V, int H, int W, uint32_t max_count) {
+  if (max_count <= kSortCap) return 0;
+  const size_t nseg = (size_t)V * dsplat::tiles_x(W) * dsplat::tiles_y(H);
+  return nseg * (size_t)split_groups(max_count) * 2 * sizeof(uint32_t);
+}
+
 int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const uint32_t* seg_count,
-                 uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count, void* stream) {
+                 uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count, void* workspace,
+                 void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_sort: bad sizes");
   DSPLAT_REQUIRE(keys != nullptr && (seg_stride ? seg_count != nullptr : seg_start != nullptr),
                  "dsr_bin_sort: null pointer");
@@ -1711,9 +1857,11 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
   while (id_bits < 32 && ((uint64_t)1 << id_bits) < (uint64_t)G) ++id_bits;
   const uint32_t want = max_count ? max_count : kSortCap;
   // segments above the LDS capacity: sorted in this launch through HBM unless they are
-  // known to be large (max_count > kSortCap): then the 16-wave k_sort_global takes them
+  // known to be large (max_count > kSortCap): then the MSD split + grouped LDS sort take them
   const bool big_known = scratch != nullptr && max_count > kSortCap;
   const int big_here = scratch != nullptr && !big_known;
+  DSPLAT_REQUIRE(!big_known || workspace != nullptr,
+                 "dsr_bin_sort: max_count %u > %u needs workspace (dsr_bin_sort_workspace_size)", max_count, kSortCap);
   static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted into once
   if (!attr_set) {
     if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds<32>,
@@ -1729,7 +1877,11 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
     attr_set = true;
   }
   uint32_t cap;
-  if (want <= 256 * 4) {
+  if (big_known) {  // small segments in LDS now, the rest split below
+    cap = 256 * 16;
+    k_sort_lds<16><<<nseg, NT, sort_lds_bytes<16>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
+                                                                id_bits, 0);
+  } else if (want <= 256 * 4) {
     cap = 256 * 4;
     k_sort_lds<4><<<nseg, NT, sort_lds_bytes<4>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
                                                                 id_bits, big_here);
@@ -1748,8 +1900,12 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
   }
   if (int e = dsplat::check_launch("k_sort_lds")) return e;
   if (big_known) {
-    k_sort_global<<<nseg, 1024, 0, st>>>(seg_start, seg_count, seg_stride, keys, scratch, id_bits, cap);
-    if (int e = dsplat::check_launch("k_sort_global")) return e;
+    const int gmax = split_groups(max_count);
+    uint32_t* groups = static_cast<uint32_t*>(workspace);
+    k_msd_split<<<nseg, 1024, 0, st>>>(seg_start, seg_count, seg_stride, keys, scratch, cap, groups, gmax);
+    if (int e = dsplat::check_launch("k_msd_split")) return e;
+    k_sort_groups<16><<<(unsigned)(nseg * gmax), NT, sort_lds_bytes<16>(), st>>>(groups, keys, scratch, id_bits);
+    if (int e = dsplat::check_launch("k_sort_groups")) return e;
   }
   return 0;
 }

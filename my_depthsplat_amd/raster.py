@@ -256,9 +256,10 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
             cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout, st),
             "dsr_project_bin")
-        maxc_hint = min(lds_cap, _spec["max_count"]) if _spec["max_count"] else lds_cap
+        maxc_hint = _spec["max_count"] or lds_cap
+        ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
         _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, None, seg_count.data_ptr(), G, keys.data_ptr(),
-                          scratch.data_ptr(), maxc_hint, st), "dsr_bin_sort")
+                          scratch.data_ptr(), maxc_hint, _ptr(ws), st), "dsr_bin_sort")
         _note_counts(seg_count)
         seg_start, stride = None, G
     else:
@@ -280,8 +281,9 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev) if maxc > lds_cap else None
         _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
                           keys.data_ptr(), st), "dsr_bin_scatter")
+        ws = _sort_workspace(lib, V, H, W, maxc, dev)
         _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), None, 0, keys.data_ptr(),
-                          None if scratch is None else scratch.data_ptr(), maxc, st), "dsr_bin_sort")
+                          None if scratch is None else scratch.data_ptr(), maxc, _ptr(ws), st), "dsr_bin_sort")
         stride = 0
     color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
@@ -295,6 +297,11 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
 
 def _ptr(t):
     return None if t is None else t.data_ptr()
+
+
+def _sort_workspace(lib, V, H, W, max_count, dev):
+    n = lib.dsr_bin_sort_workspace_size(V, H, W, max_count)
+    return torch.empty(n, dtype=torch.uint8, device=dev) if n else None
 
 
 def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, state: RasterState,

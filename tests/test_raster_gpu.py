@@ -156,10 +156,19 @@ def test_render_backward_matches_oracle(gpu):
     close(dopac[0].cpu().numpy(), acc["dopacity"], "opacity")
 
 
-def test_large_tiles_global_sort_path(gpu):
-    """Big Gaussians -> tiles with > LDS-capacity entries (k_sort_global)."""
-    from my_depthsplat_amd import _lib
+@pytest.mark.parametrize("binning,hint", [("fused", "low"), ("fused", "exact"), ("fused", "between"),
+                                          ("two_phase", "exact")])
+def test_large_tiles_sort_paths(gpu, binning, hint, monkeypatch):
+    """Big Gaussians -> tiles with > LDS-capacity entries. hint = the max-count hint the
+    forward sizes the sort with: low -> in-kernel HBM radix path; exact -> MSD split into
+    LDS-sized groups; between (above the LDS capacity, below the real maximum) -> split
+    launch whose too-large segments fall back to one HBM-sorted group."""
+    from my_depthsplat_amd import _lib, raster
     cap = _lib.load().dsr_sort_lds_capacity()
+    if binning == "two_phase":
+        monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+    monkeypatch.setitem(raster._spec, "max_count", {"low": 1, "exact": 12288 + 8, "between": cap + 1}[hint])
+    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)  # keep the hint fixed
     sc = scene_inputs(h=32, w=32, seed=5, n_ctx=2)
     g = sc.gaussians
     # blow covariances up so every Gaussian covers many tiles; 2 x 32 x 32 = 2048 Gaussians

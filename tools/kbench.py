@@ -56,6 +56,8 @@ def main():
             f = getattr(lib, fn)
             f.restype, f.argtypes = res, args
         sp = None if state.seg_start is None else state.seg_start.data_ptr()
+        ws = raster._sort_workspace(lib, V, H, W, state.max_count, dev)
+        ws_p = None if ws is None else ws.data_ptr()
         sc_p, stride = state.seg_count.data_ptr(), state.seg_stride
         if a.kernel == "render_fwd":
             out = [torch.empty_like(color), torch.empty_like(state.final_T), torch.empty_like(state.n_contrib)]
@@ -81,8 +83,7 @@ def main():
                 if rc or a.kernel == "project":
                     return rc
                 return lib.dsr_bin_sort(G, V, H, W, None, cnt2.data_ptr(), a.stride or G, keys2.data_ptr(),
-                                        scratch2.data_ptr(),
-                                        state.max_count, st)
+                                        scratch2.data_ptr(), state.max_count, ws_p, st)
         elif a.kernel == "sort_sorted":  # re-sort the (already sorted) keys in place: pass cost only
             tot3 = torch.empty(4, dtype=torch.int32, device=dev)
             scr = torch.empty_like(state.keys)
@@ -90,7 +91,7 @@ def main():
 
             def launch():
                 return lib.dsr_bin_sort(G, V, H, W, sp, sc_p, stride, state.keys.data_ptr(), scr.data_ptr(),
-                                        state.max_count, st)
+                                        state.max_count, ws_p, st)
         else:
             out = [torch.zeros_like(state.geom)]
 
