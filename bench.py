@@ -42,6 +42,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--eager", action="store_true", help="time eager launches instead of hipGraph replays")
+    p.add_argument("--extra", default="train,dl3dv",
+                   help="secondary measurements: train (config C step), dl3dv (6-view 448x768 render); '' = none")
+    p.add_argument("--extra-steps", type=int, default=10)
     return p.parse_args()
 
 
@@ -68,7 +71,7 @@ def main():
     H = W = args.size
     sc = make_scene(batch=args.batch, n_context=args.context, n_targets=args.views, height=H, width=W,
                     seed=1000 + rank, device=dev)
-    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]})
+    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
     dec = dec.to(dev)
 
     def step():
@@ -133,14 +136,23 @@ def main():
         launches, avg_ms = ktimes[name]
         alg = raster.algorithmic_bytes(name, G=G, V=V, N=n_rendered, HW=HW)
         achieved = alg / (avg_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(name, f"{args.context}v{H}x{W}x{args.views}b{args.batch}")
         roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_ms": round(avg_ms, 5), "algorithmic_bytes_per_launch": alg,
                 "launches_timed": launches,
                 "per_kernel_avg_ms_probe": {k: round(v[1], 5) for k, v in sorted(all_kernels.items())}}
         psnr, l1, cpu = None, None, None
         if not args.no_cpu_baseline:
             psnr, l1, cpu = cpu_leg(sc, out, args, H, W)
+    extra = {}
+    wanted = [e for e in args.extra.split(",") if e]
+    if "train" in wanted:
+        extra["train_config_c"] = train_leg(args, dev, rank, world, timed)
+    if "dl3dv" in wanted:
+        extra["render_config_d"] = dl3dv_leg(args, dev, rank, world, timed)
+    if rank == 0:
         line = {
             "metric": "rendered views/sec + PSNR, 2-view 256x256 RE10K, 1/2/4/8 MI355X",
             "value": round(value, 2), "unit": "views/s", "n_gpus": world, "steps": args.steps,
@@ -154,10 +166,106 @@ def main():
                        "num_rendered_per_step": n_rendered, "parallelism": f"dp{world} (per-scene, no collective)"},
             "psnr_vs_oracle_db": psnr, "l1_vs_oracle": l1,
             "roofline": roof, "cpu_baseline": cpu,
+            **extra,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same
+    workload (profiles/pmc_traffic.json, written by tools/pmc_summary.py --json: FETCH_SIZE
+    x2 per the gfx950 correction + WRITE_SIZE, separate --pmc passes). None if absent."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None, None
+    d = json.loads(f.read_text())
+    rec = d.get("kernels", {}).get(kernel)
+    if d.get("workload") != workload or rec is None:
+        return None, None
+    return int(rec["hbm_bytes"]), f"profiles/pmc_traffic.json ({d.get('source', '')})"
+
+
+def train_leg(args, dev, rank, world, timed):
+    """Config C (BASELINE.json configs[2]): 2-view 256x256, 16 scenes x 4 target views per
+    step, Gaussians from the adapter (head outputs are the trainable leaf), rasterizer forward
+    + backward of an L1 + MSE colour loss, SGD update of the head. Per GPU; weak scaling."""
+    import torch
+
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg, gaussians_from_head
+    from my_depthsplat_amd.synthetic import context_cameras, target_cameras
+
+    B, V, v, H, W = 16, 2, 4, 256, 256
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    adapter = GaussianAdapter(GaussianAdapterCfg(1e-10, 3.0, 2)).to(dev)
+    head = torch.randn(B, V, H * W, 3 + adapter.d_in, generator=g, device=dev).requires_grad_(True)
+    depths = torch.rand(B, V, H * W, 1, 1, generator=g, device=dev) * 9 + 1
+    images = torch.rand(B, V, 3, H, W, generator=g, device=dev)
+    gt = torch.rand(B, v, 3, H, W, generator=g, device=dev)
+    ctx = context_cameras(V)[None].repeat(B, 1, 1, 1).to(dev)
+    K = torch.tensor([[1.0, 0, 0.5], [0, 1.0, 0.5], [0, 0, 1]], device=dev)
+    ctx_k = K.expand(B, V, 3, 3).contiguous()
+    tgt = target_cameras(context_cameras(V), v)[None].repeat(B, 1, 1, 1).to(dev)
+    tgt_k = K.expand(B, v, 3, 3).contiguous()
+    near = torch.full((B, v), 0.5, device=dev)
+    far = torch.full((B, v), 100.0, device=dev)
+    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
+
+    def step():
+        gs = gaussians_from_head(head, depths, images, ctx, ctx_k, adapter)
+        color = dec(gs, tgt, tgt_k, near, far, (H, W)).color
+        loss = (color - gt).abs().mean() + ((color - gt) ** 2).mean()
+        loss.backward()
+        with torch.no_grad():
+            head.sub_(1e-3 * head.grad)
+            head.grad = None
+        return loss
+
+    for _ in range(2):
+        step()
+    el = timed(step, args.extra_steps)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    ms = 1e3 * el / args.extra_steps
+    return {"workload": "config C: 2-view 256x256, 16 scenes x 4 target views, adapter + raster fwd+bwd, "
+                        "L1+MSE loss, SGD on head outputs (no encoder network: out of scope)",
+            "ms_per_step": round(ms, 3), "views_per_s": round(B * v * world / (ms * 1e-3), 1), "steps": args.extra_steps,
+            "n_gpus": world}
+
+
+def dl3dv_leg(args, dev, rank, world, timed):
+    """6-view 448x768 (north_star's second input), 1 Gaussian per pixel (G = 2,064,384),
+    8 target views per scene, forward render through the decoder. Per GPU; weak scaling."""
+    import torch
+
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.synthetic import make_scene
+
+    H, W, v = 448, 768, 8
+    sc = make_scene(batch=1, n_context=6, n_targets=v, height=H, width=W, seed=2000 + rank, device=dev)
+    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
+
+    def step():
+        with torch.no_grad():
+            return dec(sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near, sc.far, (H, W))
+
+    for _ in range(2):
+        step()
+    el = timed(step, args.extra_steps)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    ms = 1e3 * el / args.extra_steps
+    return {"workload": f"6-view {H}x{W} render, G={sc.gaussians.means.shape[1]}, {v} target views/scene, fp32",
+            "ms_per_step": round(ms, 3), "views_per_s": round(v * world / (ms * 1e-3), 1), "steps": args.extra_steps,
+            "n_gpus": world}
 
 
 def cpu_leg(sc, out, args, H, W):

@@ -195,6 +195,29 @@ def device_index(values, device) -> torch.Tensor:
     return t
 
 
+_bg_cache: dict = {}
+
+
+def _dense_bg(bg: torch.Tensor) -> torch.Tensor:
+    """Contiguous [V, 3] background. The decoder passes its background buffer expanded over
+    the views (stride 0); materialising it each call costs a copy kernel per step, so the
+    dense copy is cached per (storage, view count, version)."""
+    if bg.is_contiguous() and bg.dtype == torch.float32:
+        return bg.detach()
+    base = bg._base if bg._base is not None else bg
+    key = (id(base), bg.storage_offset(), tuple(bg.shape), tuple(bg.stride()))
+    hit = _bg_cache.get(key)
+    # the entry holds the base tensor itself (so its id / memory cannot be reused while
+    # cached) and its version counter (so in-place edits of the background invalidate it)
+    if hit is not None and hit[0] is base and hit[1] == base._version:
+        return hit[2]
+    if len(_bg_cache) > 64:
+        _bg_cache.clear()
+    t = bg.detach().contiguous().float()
+    _bg_cache[key] = (base, base._version, t)
+    return t
+
+
 def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True) -> torch.Tensor:
     """Device-side camera set-up (dsr_build_cameras) -> [V, 44] float32 dsr_camera array."""
     lib = _lib.load()
@@ -205,7 +228,8 @@ def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invar
     vs = view_scene.to(device=dev, dtype=torch.int32) if isinstance(view_scene, torch.Tensor) \
         else device_index(view_scene, dev)
     f = lambda t: t.detach().contiguous().float()  # noqa: E731
-    ext, K, n, fa, b = f(extrinsics), f(intrinsics), f(near), f(far), f(bg)
+    ext, K, n, fa = f(extrinsics), f(intrinsics), f(near), f(far)
+    b = _dense_bg(bg)
     _lib.check(lib.dsr_build_cameras(V, ext.data_ptr(), K.data_ptr(), n.data_ptr(), fa.data_ptr(), b.data_ptr(),
                                      vs.data_ptr(), int(bool(scale_invariant)), cams.data_ptr(),
                                      _lib.stream_of(dev)), "dsr_build_cameras")
