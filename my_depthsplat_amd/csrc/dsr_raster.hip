@@ -1329,45 +1329,40 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
 }
 
 // ------------------------------------------------------------------------------------
-// Wave64 sum with DPP (no LDS round trips): after the 4 row shifts lane 15 of each row holds
-// its row's sum; row_bcast:15 / row_bcast:31 fold the rows so lane 63 ends with the total.
-__device__ __forceinline__ float dpp_add(float v, float t) { return v + t; }
-template <int CTRL, int ROWS>
-__device__ __forceinline__ float dpp_step(float v) {
-  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, true));
+// Sums of 4 entries x 9 gradient values over the wave (36 values, 90 instructions instead
+// of 4 x 54): v_permlane32_swap pairs entries (0,1) and (2,3) across the wave halves,
+// v_permlane16_swap pairs the results across rows, and a 4-step DPP row sum finishes:
+// lane 15 of row 0 / 1 / 2 / 3 ends with the totals of entry 0 / 2 / 1 / 3.
+__device__ __forceinline__ float swap32_add(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
-__device__ __forceinline__ float wave_sum_to_lane63(float v) {
-  v = dpp_step<0x111, 0xf>(v);  // row_shr:1
-  v = dpp_step<0x112, 0xf>(v);  // row_shr:2
-  v = dpp_step<0x114, 0xf>(v);  // row_shr:4
-  v = dpp_step<0x118, 0xf>(v);  // row_shr:8
-  v = dpp_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
-  v = dpp_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
-  return v;
+__device__ __forceinline__ float swap16_add(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
-
-// The same reduction for 9 values at once with fused v_add_f32_dpp: each step is issued for
-// all 9 values before the next, so no DPP read follows the write of its operand closer than
-// the 2 wait states the hardware needs (one s_nop covers the compiler-scheduled producers).
-#define DSR_DPP9(ctrl)                                                                              \
+#define DSR_ROW9(ctrl)                                                                              \
   asm volatile("v_add_f32_dpp %0, %0, %0 " ctrl "\n v_add_f32_dpp %1, %1, %1 " ctrl                \
                "\n v_add_f32_dpp %2, %2, %2 " ctrl "\n v_add_f32_dpp %3, %3, %3 " ctrl               \
                "\n v_add_f32_dpp %4, %4, %4 " ctrl "\n v_add_f32_dpp %5, %5, %5 " ctrl               \
                "\n v_add_f32_dpp %6, %6, %6 " ctrl "\n v_add_f32_dpp %7, %7, %7 " ctrl               \
                "\n v_add_f32_dpp %8, %8, %8 " ctrl                                                    \
-               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), "+v"(a8))
-__device__ __forceinline__ void wave_sum9_to_lane63(float& a0, float& a1, float& a2, float& a3, float& a4,
-                                                    float& a5, float& a6, float& a7, float& a8) {
+               : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), \
+                 "+v"(R[7]), "+v"(R[8]))
+__device__ __forceinline__ void reduce36(const float (&g)[4][9], float (&R)[9]) {
+#pragma unroll
+  for (int c = 0; c < 9; ++c) {
+    const float P = swap32_add(g[0][c], g[1][c]);
+    const float Q = swap32_add(g[2][c], g[3][c]);
+    R[c] = swap16_add(P, Q);
+  }
   asm volatile("s_nop 1" ::: "memory");
-  DSR_DPP9("row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1");
-  DSR_DPP9("row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1");
-  DSR_DPP9("row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1");
-  DSR_DPP9("row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1");
-  DSR_DPP9("row_bcast:15 row_mask:0xa bank_mask:0xf");
-  DSR_DPP9("row_bcast:31 row_mask:0xc bank_mask:0xf");
+  DSR_ROW9("row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1");
+  DSR_ROW9("row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1");
+  DSR_ROW9("row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1");
+  DSR_ROW9("row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1");
   asm volatile("s_nop 1" ::: "memory");
 }
-#undef DSR_DPP9_UNUSED
 
 // one compacted backward list entry
 struct __align__(16) BwdRec {
@@ -1460,59 +1455,78 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
     }
     const int cnt = __popcll(bal);
     __builtin_amdgcn_wave_barrier();
-    BwdRec cur = list[max(cnt - 1, 0)];
-    for (int k = cnt - 1; k >= 0; --k) {
-      const BwdRec nxt = list[max(k - 1, 0)];  // read ahead
-      float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
-      const float dx = cur.q.x - pfx, dy = cur.q.y - pfy;
-      // same falloff sequence as k_render_fwd (decisions must agree with the forward)
-      const float p2 = falloff_p2(cur.q.z, cur.r.x, cur.q.w, dx, dy);
-      const float Gs = __builtin_amdgcn_exp2f(p2);
-      const float alpha = fminf(0.99f, cur.r.y * Gs);
-      const bool act = cur.pos < lastc && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
-      if (act) {
-        Tr = Tr / (1.f - alpha);
-        const float dchannel_dcolor = alpha * Tr;
-        const float c0 = cur.r.z, c1 = cur.r.w, c2 = cur.s.x;
-        acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-        acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-        acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-        lc0 = c0;
-        lc1 = c1;
-        lc2 = c2;
-        float dL_dalpha = (c0 - acc0) * dp0;
-        dL_dalpha += (c1 - acc1) * dp1;
-        dL_dalpha += (c2 - acc2) * dp2;
-        g6 = dchannel_dcolor * dp0;
-        g7 = dchannel_dcolor * dp1;
-        g8 = dchannel_dcolor * dp2;
-        dL_dalpha *= Tr;
-        last_alpha = alpha;
-        dL_dalpha += (-Tfin / (1.f - alpha)) * bg_dot;
-        const float dL_dG = cur.r.y * dL_dalpha;
-        const float gdx = Gs * dx, gdy = Gs * dy;
-        const float dG_ddelx = -gdx * cur.s.y - gdy * cur.s.z;
-        const float dG_ddely = -gdy * cur.s.w - gdx * cur.s.z;
-        g0 = dL_dG * dG_ddelx * ddelx_dx;
-        g1 = dL_dG * dG_ddely * ddely_dy;
-        g2 = -0.5f * gdx * dx * dL_dG;
-        g3 = -0.5f * gdx * dy * dL_dG;
-        g4 = -0.5f * gdy * dy * dL_dG;
-        g5 = Gs * dL_dalpha;
-      }
-      if (__ballot(act) != 0ull) {
-        wave_sum9_to_lane63(g0, g1, g2, g3, g4, g5, g6, g7, g8);
-        if (lane == 63) {
-          float* a9 = acc + k * 9;
-          a9[0] = g0; a9[1] = g1; a9[2] = g2; a9[3] = g3; a9[4] = g4;
-          a9[5] = g5; a9[6] = g6; a9[7] = g7; a9[8] = g8;
-        }
-      } else if (lane == 63) {
-        float* a9 = acc + k * 9;
+    // four entries per step (back to front): the T chain runs entry by entry, then the 36
+    // gradient values are summed over the wave together (reduce36)
+    for (int k = cnt - 1; k >= 0; k -= 4) {
+      float g[4][9];
+      bool any = false;
 #pragma unroll
-        for (int c = 0; c < 9; ++c) a9[c] = 0.f;
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k - j;
+        const BwdRec cur = list[max(kk, 0)];
+#pragma unroll
+        for (int c = 0; c < 9; ++c) g[j][c] = 0.f;
+        const float dx = cur.q.x - pfx, dy = cur.q.y - pfy;
+        // same falloff sequence as k_render_fwd (decisions must agree with the forward)
+        const float p2 = falloff_p2(cur.q.z, cur.r.x, cur.q.w, dx, dy);
+        const float Gs = __builtin_amdgcn_exp2f(p2);
+        const float alpha = fminf(0.99f, cur.r.y * Gs);
+        const bool act = kk >= 0 && cur.pos < lastc && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+        any = any || act;
+        if (act) {
+          const float inv1ma = __builtin_amdgcn_rcpf(1.f - alpha);  // 1 ulp; the grads' tolerance is 2e-3
+          Tr = Tr * inv1ma;
+          const float dchannel_dcolor = alpha * Tr;
+          const float c0 = cur.r.z, c1 = cur.r.w, c2 = cur.s.x;
+          acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
+          acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
+          acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+          lc0 = c0;
+          lc1 = c1;
+          lc2 = c2;
+          float dL_dalpha = (c0 - acc0) * dp0;
+          dL_dalpha += (c1 - acc1) * dp1;
+          dL_dalpha += (c2 - acc2) * dp2;
+          g[j][6] = dchannel_dcolor * dp0;
+          g[j][7] = dchannel_dcolor * dp1;
+          g[j][8] = dchannel_dcolor * dp2;
+          dL_dalpha *= Tr;
+          last_alpha = alpha;
+          dL_dalpha += (-Tfin * inv1ma) * bg_dot;
+          const float dL_dG = cur.r.y * dL_dalpha;
+          const float gdx = Gs * dx, gdy = Gs * dy;
+          const float dG_ddelx = -gdx * cur.s.y - gdy * cur.s.z;
+          const float dG_ddely = -gdy * cur.s.w - gdx * cur.s.z;
+          g[j][0] = dL_dG * dG_ddelx * ddelx_dx;
+          g[j][1] = dL_dG * dG_ddely * ddely_dy;
+          g[j][2] = -0.5f * gdx * dx * dL_dG;
+          g[j][3] = -0.5f * gdx * dy * dL_dG;
+          g[j][4] = -0.5f * gdy * dy * dL_dG;
+          g[j][5] = Gs * dL_dalpha;
+        }
       }
-      cur = nxt;
+      if (__ballot(any) != 0ull) {
+        float R[9];
+        reduce36(g, R);
+        // lane 15 of row r holds the sums of entry k - {0, 2, 1, 3}[r]
+        if ((lane & 15) == 15) {
+          const int row = lane >> 4;
+          const int kk = k - ((row & 1) * 2 + (row >> 1));
+          if (kk >= 0) {
+            float* a9 = acc + kk * 9;
+#pragma unroll
+            for (int c = 0; c < 9; ++c) a9[c] = R[c];
+          }
+        }
+      } else if ((lane & 15) == 15) {
+        const int row = lane >> 4;
+        const int kk = k - ((row & 1) * 2 + (row >> 1));
+        if (kk >= 0) {
+          float* a9 = acc + kk * 9;
+#pragma unroll
+          for (int c = 0; c < 9; ++c) a9[c] = 0.f;
+        }
+      }
     }
     __builtin_amdgcn_wave_barrier();
     for (int i = lane; i < cnt * 9; i += 64) {
