@@ -106,10 +106,50 @@ __device__ __forceinline__ void ray(const float* cam, float x, float y, float u[
   for (int a = 0; a < 3; ++a) dw[a] = (Rc[a * 3] * d[0] + Rc[a * 3 + 1] * d[1]) + Rc[a * 3 + 2] * d[2];
 }
 
+// Row-block staging through LDS: a block's rows of a [*, row] array are one contiguous
+// span, so it moves as 16-byte vectors (coalesced) and every thread then reads / writes its
+// own row in LDS (odd row lengths are bank-conflict free). Per-thread rows of 37 / 27 / 9
+// floats read directly would make every load touch 64 different cache lines.
+__device__ __forceinline__ void stage_in(const float* __restrict__ src, size_t nfloat, float* lds) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(src);
+  if ((addr & 15) == 0) {
+    const size_t n4 = nfloat / 4;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    for (size_t i = threadIdx.x; i < n4; i += NT) {
+      const float4 v = s4[i];
+      lds[4 * i] = v.x;
+      lds[4 * i + 1] = v.y;
+      lds[4 * i + 2] = v.z;
+      lds[4 * i + 3] = v.w;
+    }
+    for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NT) lds[i] = src[i];
+  } else {
+    for (size_t i = threadIdx.x; i < nfloat; i += NT) lds[i] = src[i];
+  }
+}
+__device__ __forceinline__ void stage_out(float* __restrict__ dst, size_t nfloat, const float* lds) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(dst);
+  if ((addr & 15) == 0) {
+    const size_t n4 = nfloat / 4;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (size_t i = threadIdx.x; i < n4; i += NT)
+      d4[i] = make_float4(lds[4 * i], lds[4 * i + 1], lds[4 * i + 2], lds[4 * i + 3]);
+    for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NT) dst[i] = lds[i];
+  } else {
+    for (size_t i = threadIdx.x; i < nfloat; i += NT) dst[i] = lds[i];
+  }
+}
+
 template <int NSH>
 __device__ __forceinline__ const float* dblock(const float* cam, int l) {
   return cam + (l == 1 ? kOffD1 : l == 2 ? kOffD2 : kOffD3);
 }
+
+// Per-thread copies of one pixel's row (staged through LDS; kHead = channels used).
+template <int NSH>
+struct Rows {
+  static constexpr int kHead = 10 + 3 * NSH;
+};
 
 template <int NSH>
 __global__ __launch_bounds__(NT) void k_adapter_fwd(int B, int V, int H, int W, int C, const float* __restrict__ head,
@@ -119,63 +159,93 @@ __global__ __launch_bounds__(NT) void k_adapter_fwd(int B, int V, int H, int W, 
                                                     const float* __restrict__ sh_mask, float* __restrict__ means,
                                                     float* __restrict__ covs, float* __restrict__ harm,
                                                     float* __restrict__ opac) {
+  constexpr int KH = Rows<NSH>::kHead;
+  extern __shared__ float lds[];  // NT * max(C, 3 * NSH) floats
+  const size_t total = (size_t)B * V * H * W;
+  const size_t n0 = (size_t)blockIdx.x * NT;
+  const int nrows = (int)min((size_t)NT, total - n0);
+  const int tid = threadIdx.x;
   Pix px;
-  if (!pixel_of((size_t)blockIdx.x * NT + threadIdx.x, B, V, H, W, px)) return;
+  const bool valid = pixel_of(n0 + tid, B, V, H, W, px);  // px.bg == px.n: outputs share the row order
+  stage_in(head + n0 * C, (size_t)nrows * C, lds);
+  __syncthreads();
+  float h[KH];
+#pragma unroll
+  for (int k = 0; k < KH; ++k) h[k] = valid ? lds[tid * C + k] : 0.f;
+  __syncthreads();
   const size_t HW = (size_t)H * W;
-  const float* h = head + px.n * C;
-  const float* cam = cams + ((size_t)px.b * V + px.v) * kCamFloats;
-  opac[px.bg] = sigmoidf(h[0]);
-  // position: xy from the pixel centre and the offset logits, then the camera ray
-  const float x = ((float)px.j + 0.5f) / (float)W + (sigmoidf(h[1]) - 0.5f) * (1.0f / (float)W);
-  const float y = ((float)px.i + 0.5f) / (float)H + (sigmoidf(h[2]) - 0.5f) * (1.0f / (float)H);
-  float u[3], d[3], dw[3];
-  ray(cam, x, y, u, d, dw);
-  const float z = depths[px.n];
+  float mo[3], Cw[9], ho[3 * NSH];
+  if (valid) {
+    const float* cam = cams + ((size_t)px.b * V + px.v) * kCamFloats;
+    opac[px.n] = sigmoidf(h[0]);
+    // position: xy from the pixel centre and the offset logits, then the camera ray
+    const float x = ((float)px.j + 0.5f) / (float)W + (sigmoidf(h[1]) - 0.5f) * (1.0f / (float)W);
+    const float y = ((float)px.i + 0.5f) / (float)H + (sigmoidf(h[2]) - 0.5f) * (1.0f / (float)H);
+    float u[3], d[3], dw[3];
+    ray(cam, x, y, u, d, dw);
+    const float z = depths[px.n];
 #pragma unroll
-  for (int a = 0; a < 3; ++a) means[px.bg * 3 + a] = cam[kOffT + a] + dw[a] * z;
-  // covariance
-  float s[3];
+    for (int a = 0; a < 3; ++a) mo[a] = cam[kOffT + a] + dw[a] * z;
+    // covariance
+    float sc[3];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) s[k] = fminf(fmaxf(softplusf(h[3 + k] - 4.0f), smin), smax);
-  float q[4];
-  const float L = sqrtf(((h[6] * h[6] + h[7] * h[7]) + h[8] * h[8]) + h[9] * h[9]);
+    for (int k = 0; k < 3; ++k) sc[k] = fminf(fmaxf(softplusf(h[3 + k] - 4.0f), smin), smax);
+    float q[4];
+    const float L = sqrtf(((h[6] * h[6] + h[7] * h[7]) + h[8] * h[8]) + h[9] * h[9]);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) q[k] = h[6 + k] / (L + 1e-8f);
-  QuatR qr;
-  quat_to_R(q, qr);
-  float M[9], Cl[9], T1[9], Cw[9];
+    for (int k = 0; k < 4; ++k) q[k] = h[6 + k] / (L + 1e-8f);
+    QuatR qr;
+    quat_to_R(q, qr);
+    float M[9], Cl[9], T1[9];
 #pragma unroll
-  for (int a = 0; a < 3; ++a)
+    for (int a = 0; a < 3; ++a)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) M[a * 3 + k] = (qr.R[a * 3 + k] * s[k]) * s[k];
-  mm3t(M, qr.R, Cl);             // (R S S^T) R^T
-  mm3(cam + kOffR, Cl, T1);      // Rc C
-  mm3t(T1, cam + kOffR, Cw);     // (Rc C) Rc^T
+      for (int k = 0; k < 3; ++k) M[a * 3 + k] = (qr.R[a * 3 + k] * sc[k]) * sc[k];
+    mm3t(M, qr.R, Cl);          // (R S S^T) R^T
+    mm3(cam + kOffR, Cl, T1);   // Rc C
+    mm3t(T1, cam + kOffR, Cw);  // (Rc C) Rc^T
+    // harmonics: masked raw SH + the image colour in the DC term, rotated per degree block
+    const float* img = images + ((size_t)px.b * V + px.v) * 3 * HW + px.p;
 #pragma unroll
-  for (int k = 0; k < 9; ++k) covs[px.bg * 9 + k] = Cw[k];
-  // harmonics: masked raw SH + the image colour in the DC term, rotated per degree block
-  const float* img = images + ((size_t)px.b * V + px.v) * 3 * HW + px.p;
+    for (int c = 0; c < 3; ++c) {
+      float sh[NSH];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    float sh[NSH];
+      for (int k = 0; k < NSH; ++k) sh[k] = h[10 + c * NSH + k] * sh_mask[k];
+      sh[0] = sh[0] + (img[c * HW] - 0.5f) / kC0;
+      float* o = ho + c * NSH;
+      o[0] = sh[0];
 #pragma unroll
-    for (int k = 0; k < NSH; ++k) sh[k] = h[10 + c * NSH + k] * sh_mask[k];
-    sh[0] = sh[0] + (img[c * HW] - 0.5f) / kC0;
-    float* o = harm + (px.bg * 3 + c) * NSH;
-    o[0] = sh[0];
+      for (int l = 1; l * l < NSH; ++l) {
+        const int n = 2 * l + 1, b0 = l * l;
+        const float* D = dblock<NSH>(cam, l);
 #pragma unroll
-    for (int l = 1; l * l < NSH; ++l) {
-      const int n = 2 * l + 1, b0 = l * l;
-      const float* D = dblock<NSH>(cam, l);
+        for (int a2 = 0; a2 < n; ++a2) {
+          float acc = 0.0f;
 #pragma unroll
-      for (int a = 0; a < n; ++a) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int k = 0; k < n; ++k) acc = acc + D[a * n + k] * sh[b0 + k];
-        o[b0 + a] = acc;
+          for (int k = 0; k < n; ++k) acc = acc + D[a2 * n + k] * sh[b0 + k];
+          o[b0 + a2] = acc;
+        }
       }
     }
   }
+  // coalesced row writes through LDS
+  if (valid)
+#pragma unroll
+    for (int k = 0; k < 3 * NSH; ++k) lds[tid * 3 * NSH + k] = ho[k];
+  __syncthreads();
+  stage_out(harm + n0 * 3 * NSH, (size_t)nrows * 3 * NSH, lds);
+  __syncthreads();
+  if (valid)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) lds[tid * 9 + k] = Cw[k];
+  __syncthreads();
+  stage_out(covs + n0 * 9, (size_t)nrows * 9, lds);
+  __syncthreads();
+  if (valid)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) lds[tid * 3 + k] = mo[k];
+  __syncthreads();
+  stage_out(means + n0 * 3, (size_t)nrows * 3, lds);
 }
 
 template <int NSH>
@@ -188,146 +258,181 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
                                                     const float* __restrict__ dharm,
                                                     const float* __restrict__ dopac, float* __restrict__ dhead,
                                                     float* __restrict__ ddepth) {
+  constexpr int KH = Rows<NSH>::kHead;
+  extern __shared__ float lds[];  // NT * max(C, 3 * NSH) floats
+  const size_t total = (size_t)B * V * H * W;
+  const size_t n0 = (size_t)blockIdx.x * NT;
+  const int nrows = (int)min((size_t)NT, total - n0);
+  const int tid = threadIdx.x;
   Pix px;
-  if (!pixel_of((size_t)blockIdx.x * NT + threadIdx.x, B, V, H, W, px)) return;
-  const float* h = head + px.n * C;
-  float* dh = dhead + px.n * C;
-  const float* cam = cams + ((size_t)px.b * V + px.v) * kCamFloats;
-  // opacity
-  {
-    const float sg = sigmoidf(h[0]);
-    dh[0] = dopac ? dopac[px.bg] * sg * (1.0f - sg) : 0.0f;
+  const bool valid = pixel_of(n0 + tid, B, V, H, W, px);
+  // rows in: head, then the output gradients (each staged through the same LDS buffer)
+  float h[KH], gh[3 * NSH], gCw[9], gm[3];
+  stage_in(head + n0 * C, (size_t)nrows * C, lds);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < KH; ++k) h[k] = valid ? lds[tid * C + k] : 0.f;
+  __syncthreads();
+  if (dharm) {
+    stage_in(dharm + n0 * 3 * NSH, (size_t)nrows * 3 * NSH, lds);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 3 * NSH; ++k) gh[k] = valid ? lds[tid * 3 * NSH + k] : 0.f;
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3 * NSH; ++k) gh[k] = 0.f;
   }
-  // mean -> depth, offsets
-  {
-    const float s1 = sigmoidf(h[1]), s2 = sigmoidf(h[2]);
-    const float x = ((float)px.j + 0.5f) / (float)W + (s1 - 0.5f) * (1.0f / (float)W);
-    const float y = ((float)px.i + 0.5f) / (float)H + (s2 - 0.5f) * (1.0f / (float)H);
-    float u[3], d[3], dw[3];
-    ray(cam, x, y, u, d, dw);
-    float gm[3] = {0.f, 0.f, 0.f};
-    if (dmeans)
+  if (dcovs) {
+    stage_in(dcovs + n0 * 9, (size_t)nrows * 9, lds);
+    __syncthreads();
 #pragma unroll
-      for (int a = 0; a < 3; ++a) gm[a] = dmeans[px.bg * 3 + a];
-    const float z = depths[px.n];
-    if (ddepth) ddepth[px.n] = (gm[0] * dw[0] + gm[1] * dw[1]) + gm[2] * dw[2];
-    const float* Rc = cam + kOffR;
-    float gd[3];  // d L / d d = Rc^T (z gm)
+    for (int k = 0; k < 9; ++k) gCw[k] = valid ? lds[tid * 9 + k] : 0.f;
+    __syncthreads();
+  } else {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) gd[k] = (Rc[k] * gm[0] + Rc[3 + k] * gm[1]) + Rc[6 + k] * gm[2];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) gd[k] *= z;
-    // d = u / u2
-    const float inv = 1.0f / u[2];
-    const float dot = (gd[0] * u[0] + gd[1] * u[1]) + gd[2] * u[2];
-    float gu[3];
-#pragma unroll
-    for (int b = 0; b < 3; ++b) gu[b] = gd[b] * inv;
-    gu[2] -= dot * inv * inv;
-    const float* Ki = cam + kOffKinv;
-    const float gx = (Ki[0] * gu[0] + Ki[3] * gu[1]) + Ki[6] * gu[2];
-    const float gy = (Ki[1] * gu[0] + Ki[4] * gu[1]) + Ki[7] * gu[2];
-    dh[1] = gx * (1.0f / (float)W) * s1 * (1.0f - s1);
-    dh[2] = gy * (1.0f / (float)H) * s2 * (1.0f - s2);
+    for (int k = 0; k < 9; ++k) gCw[k] = 0.f;
   }
-  // covariance -> scales, rotation
-  {
-    float s[3], sraw[3];
+  if (dmeans) {
+    stage_in(dmeans + n0 * 3, (size_t)nrows * 3, lds);
+    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      sraw[k] = softplusf(h[3 + k] - 4.0f);
-      s[k] = fminf(fmaxf(sraw[k], smin), smax);
-    }
-    float r[4], q[4];
+    for (int k = 0; k < 3; ++k) gm[k] = valid ? lds[tid * 3 + k] : 0.f;
+    __syncthreads();
+  } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = h[6 + k];
-    const float L = sqrtf(((r[0] * r[0] + r[1] * r[1]) + r[2] * r[2]) + r[3] * r[3]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = r[k] / (L + 1e-8f);
-    QuatR qr;
-    quat_to_R(q, qr);
-    float gCw[9], T[9], gC[9];
-    if (dcovs) {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) gCw[k] = dcovs[px.bg * 9 + k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) gCw[k] = 0.f;
-    }
-    mmt3(cam + kOffR, gCw, T);  // Rc^T gCw
-    mm3(T, cam + kOffR, gC);    // (Rc^T gCw) Rc
-    // C = R diag(s^2) R^T: dR = (gC + gC^T) R diag(s^2); dsig_k = (R^T gC R)_kk
-    float gS[9], gR[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) gS[k] = gC[k] + gC[(k % 3) * 3 + k / 3];
-    float RS2[9];
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) RS2[a * 3 + k] = qr.R[a * 3 + k] * (s[k] * s[k]);
-    mm3(gS, RS2, gR);
-    float GR[9];
-    mm3(gC, qr.R, GR);  // gC R
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const float dsig = (qr.R[k] * GR[k] + qr.R[3 + k] * GR[3 + k]) + qr.R[6 + k] * GR[6 + k];
-      const float ds = 2.0f * s[k] * dsig;
-      const bool pass = sraw[k] >= smin && sraw[k] <= smax;  // torch.clamp gradient mask
-      dh[3 + k] = pass ? ds * softplus_grad(h[3 + k] - 4.0f) : 0.0f;
-    }
-    // R(q) = I + s2 P(q), s2 = 2 / (|q|^2 + eps)
-    const float i = q[0], j = q[1], kk = q[2], w = q[3], s2 = qr.s2;
-    const float P[9] = {-(j * j + kk * kk), i * j - kk * w, i * kk + j * w,
-                        i * j + kk * w,     -(i * i + kk * kk), j * kk - i * w,
-                        i * kk - j * w,     j * kk + i * w,     -(i * i + j * j)};
-    float gs2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) gs2 += gR[k] * P[k];
-    const float g = gR[0], g01 = gR[1], g02 = gR[2], g10 = gR[3], g11 = gR[4], g12 = gR[5], g20 = gR[6],
-                g21 = gR[7], g22 = gR[8];
-    float gq[4];
-    gq[0] = s2 * (g01 * j + g02 * kk + g10 * j - 2.f * g11 * i - g12 * w + g20 * kk + g21 * w - 2.f * g22 * i);
-    gq[1] = s2 * (-2.f * g * j + g01 * i + g02 * w + g10 * i + g12 * kk - g20 * w + g21 * kk - 2.f * g22 * j);
-    gq[2] = s2 * (-2.f * g * kk - g01 * w + g02 * i + g10 * w - 2.f * g11 * kk + g12 * j + g20 * i + g21 * j);
-    gq[3] = s2 * (-g01 * kk + g02 * j + g10 * kk - g12 * i - g20 * j + g21 * i);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) gq[m] -= gs2 * s2 * s2 * q[m];
-    // q = r / (|r| + eps)
-    const float Le = L + 1e-8f;
-    const float dqr = ((gq[0] * r[0] + gq[1] * r[1]) + gq[2] * r[2]) + gq[3] * r[3];
-    const float c2 = L > 0.f ? dqr / (L * Le * Le) : 0.f;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) dh[6 + m] = gq[m] / Le - c2 * r[m];
+    for (int k = 0; k < 3; ++k) gm[k] = 0.f;
   }
-  // harmonics -> raw SH: D^T per degree block, then the mask
+  float dh[KH];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    float gh[NSH];
-    if (dharm) {
-#pragma unroll
-      for (int k = 0; k < NSH; ++k) gh[k] = dharm[(px.bg * 3 + c) * NSH + k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < NSH; ++k) gh[k] = 0.f;
+  for (int k = 0; k < KH; ++k) dh[k] = 0.f;
+  if (valid) {
+    const float* cam = cams + ((size_t)px.b * V + px.v) * kCamFloats;
+    // opacity
+    {
+      const float sg = sigmoidf(h[0]);
+      dh[0] = dopac ? dopac[px.n] * sg * (1.0f - sg) : 0.0f;
     }
-    float gs[NSH];
-    gs[0] = gh[0];
+    // mean -> depth, offsets
+    {
+      const float s1 = sigmoidf(h[1]), s2 = sigmoidf(h[2]);
+      const float x = ((float)px.j + 0.5f) / (float)W + (s1 - 0.5f) * (1.0f / (float)W);
+      const float y = ((float)px.i + 0.5f) / (float)H + (s2 - 0.5f) * (1.0f / (float)H);
+      float u[3], d[3], dw[3];
+      ray(cam, x, y, u, d, dw);
+      const float z = depths[px.n];
+      if (ddepth) ddepth[px.n] = (gm[0] * dw[0] + gm[1] * dw[1]) + gm[2] * dw[2];
+      const float* Rc = cam + kOffR;
+      float gd[3];  // d L / d d = Rc^T (z gm)
 #pragma unroll
-    for (int l = 1; l * l < NSH; ++l) {
-      const int n = 2 * l + 1, b0 = l * l;
-      const float* D = dblock<NSH>(cam, l);
+      for (int k = 0; k < 3; ++k) gd[k] = (Rc[k] * gm[0] + Rc[3 + k] * gm[1]) + Rc[6 + k] * gm[2];
 #pragma unroll
-      for (int k = 0; k < n; ++k) {
-        float acc = 0.f;
+      for (int k = 0; k < 3; ++k) gd[k] *= z;
+      // d = u / u2
+      const float inv = 1.0f / u[2];
+      const float dot = (gd[0] * u[0] + gd[1] * u[1]) + gd[2] * u[2];
+      float gu[3];
 #pragma unroll
-        for (int a = 0; a < n; ++a) acc += D[a * n + k] * gh[b0 + a];
-        gs[b0 + k] = acc;
+      for (int b = 0; b < 3; ++b) gu[b] = gd[b] * inv;
+      gu[2] -= dot * inv * inv;
+      const float* Ki = cam + kOffKinv;
+      const float gx = (Ki[0] * gu[0] + Ki[3] * gu[1]) + Ki[6] * gu[2];
+      const float gy = (Ki[1] * gu[0] + Ki[4] * gu[1]) + Ki[7] * gu[2];
+      dh[1] = gx * (1.0f / (float)W) * s1 * (1.0f - s1);
+      dh[2] = gy * (1.0f / (float)H) * s2 * (1.0f - s2);
+    }
+    // covariance -> scales, rotation
+    {
+      float sc[3], sraw[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        sraw[k] = softplusf(h[3 + k] - 4.0f);
+        sc[k] = fminf(fmaxf(sraw[k], smin), smax);
       }
-    }
+      float r[4], q[4];
 #pragma unroll
-    for (int k = 0; k < NSH; ++k) dh[10 + c * NSH + k] = gs[k] * sh_mask[k];
+      for (int k = 0; k < 4; ++k) r[k] = h[6 + k];
+      const float L = sqrtf(((r[0] * r[0] + r[1] * r[1]) + r[2] * r[2]) + r[3] * r[3]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = r[k] / (L + 1e-8f);
+      QuatR qr;
+      quat_to_R(q, qr);
+      float T[9], gC[9];
+      mmt3(cam + kOffR, gCw, T);  // Rc^T gCw
+      mm3(T, cam + kOffR, gC);    // (Rc^T gCw) Rc
+      // C = R diag(s^2) R^T: dR = (gC + gC^T) R diag(s^2); dsig_k = (R^T gC R)_kk
+      float gS[9], gR[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) gS[k] = gC[k] + gC[(k % 3) * 3 + k / 3];
+      float RS2[9];
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) RS2[a * 3 + k] = qr.R[a * 3 + k] * (sc[k] * sc[k]);
+      mm3(gS, RS2, gR);
+      float GR[9];
+      mm3(gC, qr.R, GR);  // gC R
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float dsig = (qr.R[k] * GR[k] + qr.R[3 + k] * GR[3 + k]) + qr.R[6 + k] * GR[6 + k];
+        const float ds = 2.0f * sc[k] * dsig;
+        const bool pass = sraw[k] >= smin && sraw[k] <= smax;  // torch.clamp gradient mask
+        dh[3 + k] = pass ? ds * softplus_grad(h[3 + k] - 4.0f) : 0.0f;
+      }
+      // R(q) = I + s2 P(q), s2 = 2 / (|q|^2 + eps)
+      const float i = q[0], j = q[1], kk = q[2], w = q[3], s2 = qr.s2;
+      const float P[9] = {-(j * j + kk * kk), i * j - kk * w, i * kk + j * w,
+                          i * j + kk * w,     -(i * i + kk * kk), j * kk - i * w,
+                          i * kk - j * w,     j * kk + i * w,     -(i * i + j * j)};
+      float gs2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) gs2 += gR[k] * P[k];
+      const float g = gR[0], g01 = gR[1], g02 = gR[2], g10 = gR[3], g11 = gR[4], g12 = gR[5], g20 = gR[6],
+                  g21 = gR[7], g22 = gR[8];
+      float gq[4];
+      gq[0] = s2 * (g01 * j + g02 * kk + g10 * j - 2.f * g11 * i - g12 * w + g20 * kk + g21 * w - 2.f * g22 * i);
+      gq[1] = s2 * (-2.f * g * j + g01 * i + g02 * w + g10 * i + g12 * kk - g20 * w + g21 * kk - 2.f * g22 * j);
+      gq[2] = s2 * (-2.f * g * kk - g01 * w + g02 * i + g10 * w - 2.f * g11 * kk + g12 * j + g20 * i + g21 * j);
+      gq[3] = s2 * (-g01 * kk + g02 * j + g10 * kk - g12 * i - g20 * j + g21 * i);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) gq[m] -= gs2 * s2 * s2 * q[m];
+      // q = r / (|r| + eps)
+      const float Le = L + 1e-8f;
+      const float dqr = ((gq[0] * r[0] + gq[1] * r[1]) + gq[2] * r[2]) + gq[3] * r[3];
+      const float c2 = L > 0.f ? dqr / (L * Le * Le) : 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) dh[6 + m] = gq[m] / Le - c2 * r[m];
+    }
+    // harmonics -> raw SH: D^T per degree block, then the mask
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float* g2 = gh + c * NSH;
+      float gs[NSH];
+      gs[0] = g2[0];
+#pragma unroll
+      for (int l = 1; l * l < NSH; ++l) {
+        const int n = 2 * l + 1, b0 = l * l;
+        const float* D = dblock<NSH>(cam, l);
+#pragma unroll
+        for (int k = 0; k < n; ++k) {
+          float acc = 0.f;
+#pragma unroll
+          for (int a = 0; a < n; ++a) acc += D[a * n + k] * g2[b0 + a];
+          gs[b0 + k] = acc;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NSH; ++k) dh[10 + c * NSH + k] = gs[k] * sh_mask[k];
+    }
   }
-  for (int k = 10 + 3 * NSH; k < C; ++k) dh[k] = 0.f;
+  // dhead rows out through LDS (channels past 10 + 3 d_sh are 0)
+  if (valid) {
+#pragma unroll
+    for (int k = 0; k < KH; ++k) lds[tid * C + k] = dh[k];
+    for (int k = KH; k < C; ++k) lds[tid * C + k] = 0.f;
+  }
+  __syncthreads();
+  stage_out(dhead + n0 * C, (size_t)nrows * C, lds);
 }
 
 }  // namespace
@@ -344,9 +449,14 @@ int dga_adapter_fwd(int B, int V, int H, int W, int d_sh, int C, const float* he
                  "dga_adapter_fwd: null pointer");
   const size_t n = (size_t)B * V * H * W;
   const unsigned grid = (unsigned)((n + NT - 1) / NT);
+  const size_t lds = (size_t)NT * (size_t)max(C, 3 * d_sh) * sizeof(float);
+  DSPLAT_REQUIRE(lds <= 160 * 1024, "dga_adapter_fwd: %d head channels exceed the LDS row staging", C);
   hipStream_t st = (hipStream_t)stream;
 #define DGA_F(NS)                                                                                     \
-  k_adapter_fwd<NS><<<grid, NT, 0, st>>>(B, V, H, W, C, head, depths, images, cams, scale_min, scale_max, \
+  if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_adapter_fwd<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                             (int)lds) != hipSuccess)                                            \
+    return dsplat::check_launch("hipFuncSetAttribute(k_adapter_fwd)");                                                  \
+  k_adapter_fwd<NS><<<grid, NT, lds, st>>>(B, V, H, W, C, head, depths, images, cams, scale_min, scale_max, \
                                          sh_mask, means, covariances, harmonics, opacities)
   switch (d_sh) {
     case 1: DGA_F(1); break;
@@ -368,9 +478,14 @@ int dga_adapter_bwd(int B, int V, int H, int W, int d_sh, int C, const float* he
   DSPLAT_REQUIRE(head && depths && cams && sh_mask && dhead, "dga_adapter_bwd: null pointer");
   const size_t n = (size_t)B * V * H * W;
   const unsigned grid = (unsigned)((n + NT - 1) / NT);
+  const size_t lds = (size_t)NT * (size_t)max(C, 3 * d_sh) * sizeof(float);
+  DSPLAT_REQUIRE(lds <= 160 * 1024, "dga_adapter_bwd: %d head channels exceed the LDS row staging", C);
   hipStream_t st = (hipStream_t)stream;
-#define DGA_B(NS)                                                                                       \
-  k_adapter_bwd<NS><<<grid, NT, 0, st>>>(B, V, H, W, C, head, depths, cams, scale_min, scale_max, sh_mask, \
+#define DGA_B(NS)                                                                                     \
+  if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_adapter_bwd<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                             (int)lds) != hipSuccess)                                            \
+    return dsplat::check_launch("hipFuncSetAttribute(k_adapter_bwd)");                                                  \
+  k_adapter_bwd<NS><<<grid, NT, lds, st>>>(B, V, H, W, C, head, depths, cams, scale_min, scale_max, sh_mask, \
                                          dmeans, dcovariances, dharmonics, dopacities, dhead, ddepths)
   switch (d_sh) {
     case 1: DGA_B(1); break;

@@ -1532,7 +1532,12 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
     for (int i = lane; i < cnt * 9; i += 64) {
       const float a = acc[i];
       const int k = i / 9;
-      if (a != 0.f) atomicAdd(&dgv[(size_t)list[k].id * GS + (i - k * 9)], a);
+#ifdef BWD_DIAG_NOFLUSH
+      if (a == 12345.f)
+#else
+      if (a != 0.f)
+#endif
+        atomicAdd(&dgv[(size_t)list[k].id * GS + (i - k * 9)], a);
     }
     __builtin_amdgcn_wave_barrier();
   }
