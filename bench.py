@@ -195,6 +195,7 @@ def train_leg(args, dev, rank, world, timed):
 
     from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
     from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg, gaussians_from_head
+    from my_depthsplat_amd.loss import l1_mse_loss
     from my_depthsplat_amd.synthetic import context_cameras, target_cameras
 
     B, V, v, H, W = 16, 2, 4, 256, 256
@@ -216,7 +217,7 @@ def train_leg(args, dev, rank, world, timed):
     def step():
         gs = gaussians_from_head(head, depths, images, ctx, ctx_k, adapter)
         color = dec(gs, tgt, tgt_k, near, far, (H, W)).color
-        loss = (color - gt).abs().mean() + ((color - gt) ** 2).mean()
+        loss = l1_mse_loss(color, gt, 1.0, 1.0)  # fused loss + gradient (dls_l1_mse_psnr)
         loss.backward()
         with torch.no_grad():
             head.sub_(1e-3 * head.grad)

@@ -217,6 +217,16 @@ int dga_adapter_bwd(int B, int V, int H, int W, int d_sh, int C, const float* he
                     const float* dharmonics, const float* dopacities, float* dhead, float* ddepths,
                     void* stream);
 
+/* ---- loss / metric (the step after the rasterizer) ------------------------------------
+ * One pass over n_images images of n_per_image floats: loss[0] = w_l1 mean|p - t| +
+ * w_mse mean (p - t)^2 (loss_mse.py:33-44), grad (optional) = dloss/dp, psnr (optional)
+ * [n_images] = -10 log10 mean (clip01(p) - clip01(t))^2 (metrics.py:12-19). Deterministic
+ * (fixed-order fold of per-block partials in `workspace`, dls_loss_workspace_size bytes). */
+size_t dls_loss_workspace_size(int n_images, int64_t n_per_image);
+int dls_l1_mse_psnr(int n_images, int64_t n_per_image, const float* pred, const float* target,
+                    float w_l1, float w_mse, float* loss, float* grad, float* psnr, void* workspace,
+                    void* stream);
+
 /* ---- misc ------------------------------------------------------------------------- */
 const char* dsplat_last_error(void);
 int dsplat_abi_version(void);

@@ -39,6 +39,8 @@ SIGNATURES: dict[str, tuple] = {
     "dga_adapter_fwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, c_float, _P, _P, _P, _P, _P, _P]),
     "dga_adapter_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
                              _P]),
+    "dls_loss_workspace_size": (ctypes.c_size_t, [_I, ctypes.c_int64]),
+    "dls_l1_mse_psnr": (_I, [_I, ctypes.c_int64, _P, _P, c_float, c_float, _P, _P, _P, _P, _P]),
     "dsplat_last_error": (ctypes.c_char_p, []),
     "dsplat_abi_version": (_I, []),
 }

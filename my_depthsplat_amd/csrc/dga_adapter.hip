@@ -106,40 +106,6 @@ __device__ __forceinline__ void ray(const float* cam, float x, float y, float u[
   for (int a = 0; a < 3; ++a) dw[a] = (Rc[a * 3] * d[0] + Rc[a * 3 + 1] * d[1]) + Rc[a * 3 + 2] * d[2];
 }
 
-// Row-block staging through LDS: a block's rows of a [*, row] array are one contiguous
-// span, so it moves as 16-byte vectors (coalesced) and every thread then reads / writes its
-// own row in LDS (odd row lengths are bank-conflict free). Per-thread rows of 37 / 27 / 9
-// floats read directly would make every load touch 64 different cache lines.
-__device__ __forceinline__ void stage_in(const float* __restrict__ src, size_t nfloat, float* lds) {
-  const uintptr_t addr = reinterpret_cast<uintptr_t>(src);
-  if ((addr & 15) == 0) {
-    const size_t n4 = nfloat / 4;
-    const float4* s4 = reinterpret_cast<const float4*>(src);
-    for (size_t i = threadIdx.x; i < n4; i += NT) {
-      const float4 v = s4[i];
-      lds[4 * i] = v.x;
-      lds[4 * i + 1] = v.y;
-      lds[4 * i + 2] = v.z;
-      lds[4 * i + 3] = v.w;
-    }
-    for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NT) lds[i] = src[i];
-  } else {
-    for (size_t i = threadIdx.x; i < nfloat; i += NT) lds[i] = src[i];
-  }
-}
-__device__ __forceinline__ void stage_out(float* __restrict__ dst, size_t nfloat, const float* lds) {
-  const uintptr_t addr = reinterpret_cast<uintptr_t>(dst);
-  if ((addr & 15) == 0) {
-    const size_t n4 = nfloat / 4;
-    float4* d4 = reinterpret_cast<float4*>(dst);
-    for (size_t i = threadIdx.x; i < n4; i += NT)
-      d4[i] = make_float4(lds[4 * i], lds[4 * i + 1], lds[4 * i + 2], lds[4 * i + 3]);
-    for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NT) dst[i] = lds[i];
-  } else {
-    for (size_t i = threadIdx.x; i < nfloat; i += NT) dst[i] = lds[i];
-  }
-}
-
 template <int NSH>
 __device__ __forceinline__ const float* dblock(const float* cam, int l) {
   return cam + (l == 1 ? kOffD1 : l == 2 ? kOffD2 : kOffD3);
@@ -167,7 +133,7 @@ __global__ __launch_bounds__(NT) void k_adapter_fwd(int B, int V, int H, int W, 
   const int tid = threadIdx.x;
   Pix px;
   const bool valid = pixel_of(n0 + tid, B, V, H, W, px);  // px.bg == px.n: outputs share the row order
-  stage_in(head + n0 * C, (size_t)nrows * C, lds);
+  dsplat::stage_in<NT>(head + n0 * C, (size_t)nrows * C, lds);
   __syncthreads();
   float h[KH];
 #pragma unroll
@@ -233,19 +199,19 @@ __global__ __launch_bounds__(NT) void k_adapter_fwd(int B, int V, int H, int W, 
 #pragma unroll
     for (int k = 0; k < 3 * NSH; ++k) lds[tid * 3 * NSH + k] = ho[k];
   __syncthreads();
-  stage_out(harm + n0 * 3 * NSH, (size_t)nrows * 3 * NSH, lds);
+  dsplat::stage_out<NT>(harm + n0 * 3 * NSH, (size_t)nrows * 3 * NSH, lds);
   __syncthreads();
   if (valid)
 #pragma unroll
     for (int k = 0; k < 9; ++k) lds[tid * 9 + k] = Cw[k];
   __syncthreads();
-  stage_out(covs + n0 * 9, (size_t)nrows * 9, lds);
+  dsplat::stage_out<NT>(covs + n0 * 9, (size_t)nrows * 9, lds);
   __syncthreads();
   if (valid)
 #pragma unroll
     for (int k = 0; k < 3; ++k) lds[tid * 3 + k] = mo[k];
   __syncthreads();
-  stage_out(means + n0 * 3, (size_t)nrows * 3, lds);
+  dsplat::stage_out<NT>(means + n0 * 3, (size_t)nrows * 3, lds);
 }
 
 template <int NSH>
@@ -268,13 +234,13 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
   const bool valid = pixel_of(n0 + tid, B, V, H, W, px);
   // rows in: head, then the output gradients (each staged through the same LDS buffer)
   float h[KH], gh[3 * NSH], gCw[9], gm[3];
-  stage_in(head + n0 * C, (size_t)nrows * C, lds);
+  dsplat::stage_in<NT>(head + n0 * C, (size_t)nrows * C, lds);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < KH; ++k) h[k] = valid ? lds[tid * C + k] : 0.f;
   __syncthreads();
   if (dharm) {
-    stage_in(dharm + n0 * 3 * NSH, (size_t)nrows * 3 * NSH, lds);
+    dsplat::stage_in<NT>(dharm + n0 * 3 * NSH, (size_t)nrows * 3 * NSH, lds);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 3 * NSH; ++k) gh[k] = valid ? lds[tid * 3 * NSH + k] : 0.f;
@@ -284,7 +250,7 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
     for (int k = 0; k < 3 * NSH; ++k) gh[k] = 0.f;
   }
   if (dcovs) {
-    stage_in(dcovs + n0 * 9, (size_t)nrows * 9, lds);
+    dsplat::stage_in<NT>(dcovs + n0 * 9, (size_t)nrows * 9, lds);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 9; ++k) gCw[k] = valid ? lds[tid * 9 + k] : 0.f;
@@ -294,7 +260,7 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
     for (int k = 0; k < 9; ++k) gCw[k] = 0.f;
   }
   if (dmeans) {
-    stage_in(dmeans + n0 * 3, (size_t)nrows * 3, lds);
+    dsplat::stage_in<NT>(dmeans + n0 * 3, (size_t)nrows * 3, lds);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 3; ++k) gm[k] = valid ? lds[tid * 3 + k] : 0.f;
@@ -432,7 +398,7 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
     for (int k = KH; k < C; ++k) lds[tid * C + k] = 0.f;
   }
   __syncthreads();
-  stage_out(dhead + n0 * C, (size_t)nrows * C, lds);
+  dsplat::stage_out<NT>(dhead + n0 * C, (size_t)nrows * C, lds);
 }
 
 }  // namespace

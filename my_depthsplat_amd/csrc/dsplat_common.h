@@ -56,6 +56,42 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 __global__ void k_zero_u32(uint32_t* __restrict__ p, size_t n);
 int zero_async(void* p, size_t bytes, hipStream_t st, const char* what);
 
+// Row-block staging through LDS: the rows of a [*, row] array owned by one block are one
+// contiguous span, so it moves as 16-byte vectors (coalesced) and each thread then reads /
+// writes its own row in LDS (odd row lengths are bank-conflict free). Per-thread rows of
+// 9 / 27 / 37 floats accessed directly make every load instruction touch ~64 cache lines.
+template <int NTH>
+__device__ __forceinline__ void stage_in(const float* __restrict__ src, size_t nfloat, float* lds) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(src);
+  if ((addr & 15) == 0) {
+    const size_t n4 = nfloat / 4;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    for (size_t i = threadIdx.x; i < n4; i += NTH) {
+      const float4 v = s4[i];
+      lds[4 * i] = v.x;
+      lds[4 * i + 1] = v.y;
+      lds[4 * i + 2] = v.z;
+      lds[4 * i + 3] = v.w;
+    }
+    for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NTH) lds[i] = src[i];
+  } else {
+    for (size_t i = threadIdx.x; i < nfloat; i += NTH) lds[i] = src[i];
+  }
+}
+template <int NTH>
+__device__ __forceinline__ void stage_out(float* __restrict__ dst, size_t nfloat, const float* lds) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(dst);
+  if ((addr & 15) == 0) {
+    const size_t n4 = nfloat / 4;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (size_t i = threadIdx.x; i < n4; i += NTH)
+      d4[i] = make_float4(lds[4 * i], lds[4 * i + 1], lds[4 * i + 2], lds[4 * i + 3]);
+    for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NTH) dst[i] = lds[i];
+  } else {
+    for (size_t i = threadIdx.x; i < nfloat; i += NTH) dst[i] = lds[i];
+  }
+}
+
 inline int tiles_x(int W) { return (W + DSR_TILE - 1) / DSR_TILE; }
 inline int tiles_y(int H) { return (H + DSR_TILE - 1) / DSR_TILE; }
 

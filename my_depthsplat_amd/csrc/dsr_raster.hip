@@ -1554,14 +1554,19 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
     float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D, int layout) {
   constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
+  extern __shared__ float lds[];  // NT * max(3 M, 9) floats: row staging
   const int s = blockIdx.y;
-  const int g = blockIdx.x * NT + threadIdx.x;
-  if (g >= G) return;
-  const size_t sg = (size_t)s * G + g;
-  const F3 m0 = {means[3 * sg], means[3 * sg + 1], means[3 * sg + 2]};
+  const int tid = threadIdx.x;
+  const int g0 = blockIdx.x * NT;
+  const int nrows = min(NT, G - g0);
+  const int g = g0 + tid;
+  const bool valid = tid < nrows;
+  const size_t sg0 = (size_t)s * G + g0;
+  const size_t sg = sg0 + tid;
+  const int cw = (layout & kLayoutCovFull) ? 9 : 6;
+  // scene inputs of the block's Gaussians: coalesced through LDS
+  F3 m0 = {0.f, 0.f, 0.f};
   float c60[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) c60[k] = load_cov(cov6, sg, k, layout);
   float sh[NC * 3];
   float dsh[NC * 3];
 #pragma unroll
@@ -1569,15 +1574,44 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     sh[k] = 0.f;
     dsh[k] = 0.f;
   }
-  if constexpr (DEG >= 0) load_sh<NC>(shs, sg, M, layout, sh);
+  dsplat::stage_in<NT>(means + 3 * sg0, (size_t)3 * nrows, lds);
+  __syncthreads();
+  if (valid) m0 = {lds[3 * tid], lds[3 * tid + 1], lds[3 * tid + 2]};
+  __syncthreads();
+  dsplat::stage_in<NT>(cov6 + cw * sg0, (size_t)cw * nrows, lds);
+  __syncthreads();
+  {
+    constexpr int full_idx[6] = {0, 1, 2, 4, 5, 8};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) c60[k] = valid ? lds[tid * cw + (cw == 9 ? full_idx[k] : k)] : 0.f;
+  }
+  __syncthreads();
+  if constexpr (DEG >= 0) {
+    const int rw = 3 * M;
+    dsplat::stage_in<NT>(shs + (size_t)rw * sg0, (size_t)rw * nrows, lds);
+    __syncthreads();
+    if (valid) {
+      const float* p = lds + tid * rw;
+      if (layout & kLayoutShChannelMajor) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) sh[k * 3 + ch] = p[ch * M + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < NC * 3; ++k) sh[k] = p[k];
+      }
+    }
+    __syncthreads();
+  }
   float dm0 = 0.f, dm1 = 0.f, dm2 = 0.f, dop = 0.f, dcol0 = 0.f, dcol1 = 0.f, dcol2 = 0.f;
   float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int vb = scene_view_start[s], ve = scene_view_start[s + 1];
+  const int vb = valid ? scene_view_start[s] : 0, ve = valid ? scene_view_start[s + 1] : 0;
   for (int k = vb; k < ve; ++k) {
     const int v = scene_views[k];
     const size_t vg = (size_t)v * G + g;
-    const float* rec = geom + vg * GS;
-    const int radius = __float_as_int(rec[10]);
+    const float4 rec2 = reinterpret_cast<const float4*>(geom + vg * GS)[2];  // depth, radius, clamp bits
+    const int radius = __float_as_int(rec2.z);
     if (radius <= 0) {
       if (dmean2D) {
         dmean2D[3 * vg] = 0.f;
@@ -1586,7 +1620,9 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
       }
       continue;
     }
-    const float* dg = dgeom + vg * GS;
+    const float4* dg4 = reinterpret_cast<const float4*>(dgeom + vg * GS);
+    const float4 dgA = dg4[0], dgB = dg4[1], dgC = dg4[2];
+    const float dg[9] = {dgA.x, dgA.y, dgA.z, dgA.w, dgB.x, dgB.y, dgB.z, dgB.w, dgC.x};
     const dsr_camera* cam = cams + v;
     // scale-invariant rescale of this view: forward used m*s and cov*s^2
     const float gsc = cam->scale, gsc2 = gsc * gsc;
@@ -1669,7 +1705,7 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
       dcol1 += drgb1;
       dcol2 += drgb2;
     } else {
-      const uint32_t cb = __float_as_uint(rec[11]);
+      const uint32_t cb = __float_as_uint(rec2.w);
       const float dR[3] = {(cb & 1u) ? 0.f : drgb0, (cb & 2u) ? 0.f : drgb1, (cb & 4u) ? 0.f : drgb2};
       const float dx0 = m.x - cam->campos[0], dy0 = m.y - cam->campos[1], dz0 = m.z - cam->campos[2];
       const float len = sqrtf(dx0 * dx0 + dy0 * dy0 + dz0 * dz0);
@@ -1732,37 +1768,55 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     dm1 += e1 * gsc;
     dm2 += e2 * gsc;
   }
-  dmeans[3 * sg] = dm0;
-  dmeans[3 * sg + 1] = dm1;
-  dmeans[3 * sg + 2] = dm2;
-  if (layout & kLayoutCovFull) {  // gradient lands on the upper triangle only (triu gather)
-    float* o = dcov6 + 9 * sg;
-    o[0] = dc[0]; o[1] = dc[1]; o[2] = dc[2];
-    o[3] = 0.f;   o[4] = dc[3]; o[5] = dc[4];
-    o[6] = 0.f;   o[7] = 0.f;   o[8] = dc[5];
-  } else {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) dcov6[6 * sg + k] = dc[k];
+  // outputs: coalesced through LDS
+  if (valid) {
+    lds[3 * tid] = dm0;
+    lds[3 * tid + 1] = dm1;
+    lds[3 * tid + 2] = dm2;
   }
-  dopac[sg] = dop;
-  if constexpr (DEG < 0) {
-    dcolors[3 * sg] = dcol0;
-    dcolors[3 * sg + 1] = dcol1;
-    dcolors[3 * sg + 2] = dcol2;
-  } else {
-    float* o = dshs + sg * (size_t)M * 3;
-    if (layout & kLayoutShChannelMajor) {
-#pragma unroll
-      for (int k = 0; k < NC; ++k)
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) o[ch * M + k] = dsh[k * 3 + ch];
-      for (int k = NC; k < M; ++k)
-        for (int ch = 0; ch < 3; ++ch) o[ch * M + k] = 0.f;
+  __syncthreads();
+  dsplat::stage_out<NT>(dmeans + 3 * sg0, (size_t)3 * nrows, lds);
+  __syncthreads();
+  if (valid) {
+    float* o = lds + tid * cw;
+    if (cw == 9) {  // gradient lands on the upper triangle only (triu gather)
+      o[0] = dc[0]; o[1] = dc[1]; o[2] = dc[2];
+      o[3] = 0.f;   o[4] = dc[3]; o[5] = dc[4];
+      o[6] = 0.f;   o[7] = 0.f;   o[8] = dc[5];
     } else {
 #pragma unroll
-      for (int k = 0; k < NC * 3; ++k) o[k] = dsh[k];
-      for (int k = NC * 3; k < M * 3; ++k) o[k] = 0.f;
+      for (int k = 0; k < 6; ++k) o[k] = dc[k];
     }
+  }
+  __syncthreads();
+  dsplat::stage_out<NT>(dcov6 + cw * sg0, (size_t)cw * nrows, lds);
+  if (valid) dopac[sg] = dop;
+  if constexpr (DEG < 0) {
+    if (valid) {
+      dcolors[3 * sg] = dcol0;
+      dcolors[3 * sg + 1] = dcol1;
+      dcolors[3 * sg + 2] = dcol2;
+    }
+  } else {
+    const int rw = 3 * M;
+    __syncthreads();
+    if (valid) {
+      float* o = lds + tid * rw;
+      if (layout & kLayoutShChannelMajor) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) o[ch * M + k] = dsh[k * 3 + ch];
+        for (int k = NC; k < M; ++k)
+          for (int ch = 0; ch < 3; ++ch) o[ch * M + k] = 0.f;
+      } else {
+#pragma unroll
+        for (int k = 0; k < NC * 3; ++k) o[k] = dsh[k];
+        for (int k = NC * 3; k < rw; ++k) o[k] = 0.f;
+      }
+    }
+    __syncthreads();
+    dsplat::stage_out<NT>(dshs + (size_t)rw * sg0, (size_t)rw * nrows, lds);
   }
 }
 
@@ -1973,8 +2027,10 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((G + NT - 1) / NT, S);
   const int deg = shs ? sh_degree : -1;
+  const size_t lds = (size_t)NT * (size_t)max(shs ? 3 * M : 0, 9) * sizeof(float);
+  DSPLAT_REQUIRE(lds <= 64 * 1024, "dsr_preprocess_bwd: M=%d SH coefficients exceed the LDS row staging", M);
 #define DSR_PREB(D)                                                                                              \
-  k_preprocess_bwd<D><<<grid, NT, 0, st>>>(G, H, W, M, means, shs, cov6, cams, geom, dgeom, scene_view_start, \
+  k_preprocess_bwd<D><<<grid, NT, lds, st>>>(G, H, W, M, means, shs, cov6, cams, geom, dgeom, scene_view_start, \
                                            scene_views, dmeans, dshs, dcolors, dopac, dcov6, dmean2D, layout)
   switch (deg) {
     case -1: DSR_PREB(-1); break;
