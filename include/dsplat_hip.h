@@ -203,6 +203,13 @@ int dcv_warp_bwd(int B, int C, int H, int W, int D, const float* dout, const flo
  * Wigner-D of R for degrees 1..3 [9, 25, 49]), sh_mask [d_sh].
  * out: means [B,G,3], covariances [B,G,3,3], harmonics [B,G,3,d_sh], opacities [B,G],
  * G = V*H*W view-major (the decoder's Gaussians). d_sh in {1, 4, 9, 16}. */
+/* Per-view blocks for dga_adapter_fwd/bwd from c2w extrinsics [BV,4,4] and normalised
+ * intrinsics [BV,3,3]: R, t, K^-1 and the Wigner-D blocks of R up to sh_degree (zeros
+ * above). `probes`: for l = 1..3, the probe directions [4(2l+1)+8, 3] then pinv of their
+ * real SH [2l+1, 4(2l+1)+8], float64, concatenated (sh_rotation.py builds them). */
+int dga_adapter_cameras(int BV, const float* extrinsics, const float* intrinsics, int sh_degree,
+                        const double* probes, float* cams, void* stream);
+
 int dga_adapter_fwd(int B, int V, int H, int W, int d_sh, int C, const float* head,
                     const float* depths, const float* images, const float* cams, float scale_min,
                     float scale_max, const float* sh_mask, float* means, float* covariances,

@@ -11,13 +11,45 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .sh_rotation import wigner_d
+from .sh_rotation import _probe, wigner_d
 
 CAM_FLOATS = 104  # R[9] t[3] Kinv[9] D1[9] D2[25] D3[49] (include/dsplat_hip.h)
 
 
+_probe_cache: dict = {}
+
+
+def _probes(device) -> torch.Tensor:
+    """sh_rotation's probe directions and pseudo-inverses for l = 1..3 (float64, on device)."""
+    key = str(device)
+    t = _probe_cache.get(key)
+    if t is None:
+        parts = []
+        for l in (1, 2, 3):
+            pts, pinv = _probe(l)
+            parts += [pts.reshape(-1), pinv.reshape(-1)]
+        t = torch.cat(parts).to(torch.float64).to(device)
+        _probe_cache[key] = t
+    return t
+
+
 def adapter_cameras(extrinsics: torch.Tensor, intrinsics: torch.Tensor, sh_degree: int) -> torch.Tensor:
-    """[B, V, 4, 4] c2w + [B, V, 3, 3] normalised K -> [B*V, 104] float32 view blocks."""
+    """[B, V, 4, 4] c2w + [B, V, 3, 3] normalised K -> [B*V, 104] float32 view blocks, built
+    on the device in one kernel (dga_adapter_cameras)."""
+    lib = _lib.load()
+    B, V = extrinsics.shape[:2]
+    ext = extrinsics.detach().reshape(B * V, 4, 4).contiguous().float()
+    K = intrinsics.detach().reshape(B * V, 3, 3).contiguous().float()
+    _lib.require_gpu(ext, K)
+    cams = torch.empty((B * V, CAM_FLOATS), dtype=torch.float32, device=ext.device)
+    _lib.check(lib.dga_adapter_cameras(B * V, ext.data_ptr(), K.data_ptr(), int(sh_degree),
+                                       _probes(ext.device).data_ptr(), cams.data_ptr(), _lib.stream_of(ext.device)),
+               "dga_adapter_cameras")
+    return cams
+
+
+def adapter_cameras_torch(extrinsics: torch.Tensor, intrinsics: torch.Tensor, sh_degree: int) -> torch.Tensor:
+    """The same blocks from the torch functions the reference path uses (test reference)."""
     B, V = extrinsics.shape[:2]
     ext = extrinsics.detach().reshape(B * V, 4, 4).float()
     K = intrinsics.detach().reshape(B * V, 3, 3).float()

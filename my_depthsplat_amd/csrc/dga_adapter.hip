@@ -401,9 +401,98 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
   dsplat::stage_out<NT>(dhead + n0 * C, (size_t)nrows * C, lds);
 }
 
+// Per-view constant blocks (dga_adapter_cameras): R, t of c2w, K^-1 (double, adjugate) and
+// the Wigner-D matrices of R for degrees 1..3, solved exactly as sh_rotation.wigner_d does:
+// D_l = Y_l(R x_n)^T pinv(Y_l(x_n))^T over fixed probe directions x_n (same probes and
+// pseudo-inverses, passed in double), so the fused and torch adapters rotate identically.
+__device__ void e3nn_sh(int l, double x, double y, double z, double* out) {
+  const double s3 = 1.7320508075688772;
+  if (l == 1) {
+    out[0] = x;
+    out[1] = y;
+    out[2] = z;
+    return;
+  }
+  const double y2 = y * y, x2z2 = x * x + z * z, s20 = s3 * x * z, s24 = s3 / 2.0 * (z * z - x * x);
+  if (l == 2) {
+    out[0] = s20;
+    out[1] = s3 * x * y;
+    out[2] = y2 - 0.5 * x2z2;
+    out[3] = s3 * y * z;
+    out[4] = s24;
+    return;
+  }
+  out[0] = sqrt(5.0 / 6.0) * (s20 * z + s24 * x);
+  out[1] = sqrt(5.0) * s20 * y;
+  out[2] = sqrt(3.0 / 8.0) * (4 * y2 - x2z2) * x;
+  out[3] = 0.5 * y * (2 * y2 - 3 * x2z2);
+  out[4] = sqrt(3.0 / 8.0) * z * (4 * y2 - x2z2);
+  out[5] = sqrt(5.0) * s24 * y;
+  out[6] = sqrt(5.0 / 6.0) * (s24 * z - s20 * x);
+}
+
+__global__ void k_adapter_cams(int BV, const float* __restrict__ ext, const float* __restrict__ intr, int sh_degree,
+                               const double* __restrict__ probes, float* __restrict__ cams) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= BV) return;
+  const float* E = ext + (size_t)v * 16;
+  const float* K = intr + (size_t)v * 9;
+  float* o = cams + (size_t)v * kCamFloats;
+  double R[9];
+  for (int a = 0; a < 3; ++a) {
+    for (int c = 0; c < 3; ++c) {
+      R[a * 3 + c] = E[a * 4 + c];
+      o[kOffR + a * 3 + c] = E[a * 4 + c];
+    }
+    o[kOffT + a] = E[a * 4 + 3];
+  }
+  {
+    const double a = K[0], b = K[1], c = K[2], d = K[3], e = K[4], f = K[5], g = K[6], h = K[7], i = K[8];
+    const double A = e * i - f * h, Bc = -(d * i - f * g), Cc = d * h - e * g;
+    const double id = 1.0 / (a * A + b * Bc + c * Cc);
+    const double inv[9] = {A * id, -(b * i - c * h) * id, (b * f - c * e) * id,
+                           Bc * id, (a * i - c * g) * id, -(a * f - c * d) * id,
+                           Cc * id, -(a * h - b * g) * id, (a * e - b * d) * id};
+    for (int k = 0; k < 9; ++k) o[kOffKinv + k] = (float)inv[k];
+  }
+  const double* pr = probes;
+  for (int l = 1; l <= 3; ++l) {
+    const int n = 2 * l + 1, np = 4 * n + 8;
+    const double* pts = pr;             // [np, 3]
+    const double* pinv = pr + 3 * np;   // [n, np]
+    pr += 3 * np + n * np;
+    float* D = o + (l == 1 ? kOffD1 : l == 2 ? kOffD2 : kOffD3);
+    if (l > sh_degree) {
+      for (int k = 0; k < n * n; ++k) D[k] = 0.f;
+      continue;
+    }
+    double acc[49];
+    for (int k = 0; k < n * n; ++k) acc[k] = 0.0;
+    for (int p = 0; p < np; ++p) {
+      const double x = pts[3 * p], y = pts[3 * p + 1], z = pts[3 * p + 2];
+      const double rx = R[0] * x + R[1] * y + R[2] * z;
+      const double ry = R[3] * x + R[4] * y + R[5] * z;
+      const double rz = R[6] * x + R[7] * y + R[8] * z;
+      double Y[7];
+      e3nn_sh(l, rx, ry, rz, Y);
+      for (int k = 0; k < n; ++k)
+        for (int m = 0; m < n; ++m) acc[k * n + m] += Y[k] * pinv[m * np + p];
+    }
+    for (int k = 0; k < n * n; ++k) D[k] = (float)acc[k];
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int dga_adapter_cameras(int BV, const float* extrinsics, const float* intrinsics, int sh_degree, const double* probes,
+                        float* cams, void* stream) {
+  DSPLAT_REQUIRE(BV > 0 && sh_degree >= 0 && sh_degree <= 3, "dga_adapter_cameras: BV=%d sh_degree=%d", BV, sh_degree);
+  DSPLAT_REQUIRE(extrinsics && intrinsics && probes && cams, "dga_adapter_cameras: null pointer");
+  k_adapter_cams<<<(BV + 63) / 64, 64, 0, (hipStream_t)stream>>>(BV, extrinsics, intrinsics, sh_degree, probes, cams);
+  return dsplat::check_launch("k_adapter_cams");
+}
 
 int dga_adapter_fwd(int B, int V, int H, int W, int d_sh, int C, const float* head, const float* depths,
                     const float* images, const float* cams, float scale_min, float scale_max, const float* sh_mask,

@@ -93,3 +93,13 @@ def test_fused_adapter_drives_the_decoder(gpu):
     b = dec(gaussians_from_head_torch(head, depths, images, ext, K, adapter), tgt, Kt, near, far, (32, 32)).color
     assert float((a - b).abs().mean()) < 1e-5
     assert math.isfinite(float(a.sum()))
+
+
+def test_device_camera_blocks_match_torch(gpu):
+    """dga_adapter_cameras (K^-1 and Wigner-D on the device) vs the torch construction."""
+    from my_depthsplat_amd.adapter_hip import adapter_cameras, adapter_cameras_torch
+    _, _, _, ext, K, _ = _inputs(3, B=3, V=2, seed=21)
+    for deg in (0, 1, 2, 3):
+        a = adapter_cameras(ext, K, deg)
+        b = adapter_cameras_torch(ext, K, deg)
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=2e-6)
