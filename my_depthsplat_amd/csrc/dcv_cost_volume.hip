@@ -207,6 +207,444 @@ __global__ __launch_bounds__(256) void k_cost_fwd(int J, int C, int H, int W, in
   }
 }
 
+// ---- MFMA formulation ------------------------------------------------------------------
+// The bilinear warp is linear, so cost(p, d) = sum_j sum_taps w * (ref[p] . tgt_j[q_tap]) / (sqrt C J):
+// every (pixel, depth) only needs the correlation of its pixel with the <= 4 target pixels it
+// taps. A workgroup takes TP = 16 consecutive reference pixels of a row; for each source view
+// it finds the distinct target pixels all its (pixel, depth) samples tap (an LDS bitmap over
+// the target image + a prefix of popcounts = a rank for every tapped pixel), computes the
+// correlations [16 pixels x U tapped pixels] as an exact-f32 GEMM on the matrix cores
+// (v_mfma_f32_16x16x4_f32, K = C channels, channel-last target rows as B), and finishes with
+// the 4-tap bilinear gather from LDS. Small-baseline epipolar segments of neighbouring pixels
+// overlap, so U is a few tens to a few hundred, far below 16 x D x 4 taps. Tiles whose U
+// exceeds kUMax fall back to a direct dot product per tap.
+constexpr int TP = 16;      // reference pixels per workgroup
+constexpr int DCH = 128;    // depth hypotheses per pass
+constexpr int kUMax = 512;  // tapped target pixels held in LDS per (tile, view)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct CvLds {
+  float* aref;   // [TP][C]
+  float2* samp;  // [DCH][TP] sample position (ix, iy); ix = NaN: outside
+  uint32_t* bm;  // [NW] tapped-pixel bitmap
+  uint32_t* bmp; // [NW] exclusive popcount prefix
+  int* list;     // [kUMax] tapped pixel ids in rank order
+  float* corr;   // [TP][kUMax]
+  float* acc;    // [DCH][TP] cost accumulated over views
+  uint32_t* misc;
+};
+
+__device__ __forceinline__ int tap_rank(const CvLds& L, int q) {
+  const uint32_t w = L.bm[q >> 5];
+  return (int)(L.bmp[q >> 5] + __popc(w & ((1u << (q & 31)) - 1u)));
+}
+
+__global__ __launch_bounds__(256) void k_cost_mfma(int J, int C, int H, int W, int D, int depth_per_pixel,
+                                                   const float* __restrict__ ref,
+                                                   const float* __restrict__ tgt_hwc,
+                                                   const float* __restrict__ intr, const float* __restrict__ pose,
+                                                   const float* __restrict__ depth, float clampz,
+                                                   float* __restrict__ cost) {
+  extern __shared__ __attribute__((aligned(16))) float cv_lds[];
+  const int HW = H * W, NW = (HW + 31) / 32;
+  CvLds L;
+  {
+    float* p = cv_lds;
+    L.aref = p;
+    p += TP * C;
+    L.samp = reinterpret_cast<float2*>(p);
+    p += 2 * DCH * TP;
+    L.acc = p;
+    p += DCH * TP;
+    L.corr = p;
+    p += TP * kUMax;
+    L.list = reinterpret_cast<int*>(p);
+    p += kUMax;
+    L.bm = reinterpret_cast<uint32_t*>(p);
+    p += NW;
+    L.bmp = reinterpret_cast<uint32_t*>(p);
+    p += NW;
+    L.misc = reinterpret_cast<uint32_t*>(p);
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tpr = (W + TP - 1) / TP;
+  const int y = blockIdx.x / tpr, x0 = (blockIdx.x % tpr) * TP;
+  const int b = blockIdx.y;
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  // reference tile as the A operand: aref[i][c]
+  for (int k = tid; k < TP * C; k += 256) {
+    const int i = k & (TP - 1), c = k >> 4;
+    L.aref[i * C + c] = (x0 + i < W) ? ref[((size_t)b * C + c) * HW + (size_t)y * W + x0 + i] : 0.f;
+  }
+  for (int d0 = 0; d0 < D; d0 += DCH) {
+    for (int k = tid; k < DCH * TP; k += 256) L.acc[k] = 0.f;
+    for (int j = 0; j < J; ++j) {
+      Cam cam;
+      load_cam(intr + ((size_t)b * J + j) * 9, pose + ((size_t)b * J + j) * 16, cam);
+      for (int w = tid; w < NW; w += 256) L.bm[w] = 0u;
+      __syncthreads();
+      // sample positions of every (pixel, depth) of the tile, taps marked in the bitmap
+      for (int k = tid; k < DCH * TP; k += 256) {
+        const int i = k & (TP - 1), dd = k >> 4, d = d0 + dd;
+        float2 sp = make_float2(__int_as_float(0x7fc00000), 0.f);
+        if (d < D && x0 + i < W) {
+          const float px = (float)(x0 + i), py = (float)y;
+          const float qx = cam.Kinv[0] * px + cam.Kinv[1] * py + cam.Kinv[2];
+          const float qy = cam.Kinv[3] * px + cam.Kinv[4] * py + cam.Kinv[5];
+          const float qz = cam.Kinv[6] * px + cam.Kinv[7] * py + cam.Kinv[8];
+          const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
+          const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
+          const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
+          const float dep = depth_per_pixel ? depth[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i]
+                                            : depth[(size_t)b * D + d];
+          const float X = prx * dep + cam.t[0];
+          const float Y = pry * dep + cam.t[1];
+          const float Z = prz * dep + cam.t[2];
+          const float xx = cam.K[0] * X + cam.K[1] * Y + cam.K[2] * Z;
+          const float yy = cam.K[3] * X + cam.K[4] * Y + cam.K[5] * Z;
+          const float zz = fmaxf(cam.K[6] * X + cam.K[7] * Y + cam.K[8] * Z, clampz);
+          const float u = xx / zz, v = yy / zz;
+          const float gxn = 2 * u / (W - 1) - 1;
+          const float gyn = 2 * v / (H - 1) - 1;
+          const float ix = ((gxn + 1) / 2) * (W - 1);
+          const float iy = ((gyn + 1) / 2) * (H - 1);
+          if (ix > -2.f && ix < (float)W + 1.f && iy > -2.f && iy < (float)H + 1.f) {
+            sp = make_float2(ix, iy);
+            const int tx0 = (int)floorf(ix), ty0 = (int)floorf(iy);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+              if (tx >= 0 && tx < W && ty >= 0 && ty < H) {
+                const int q = ty * W + tx;
+                atomicOr(&L.bm[q >> 5], 1u << (q & 31));
+              }
+            }
+          }
+        }
+        L.samp[k] = sp;
+      }
+      __syncthreads();
+      // exclusive prefix of the bitmap popcounts (thread t owns a contiguous run of words)
+      {
+        const int per = (NW + 255) / 256;
+        const int w0 = tid * per, w1 = min(NW, w0 + per);
+        uint32_t tot = 0;
+        for (int w = w0; w < w1; ++w) tot += __popc(L.bm[w]);
+        const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
+        if (lane == 63) L.misc[wv] = incl;
+        __syncthreads();
+        uint32_t off = incl - tot;
+        for (int k = 0; k < wv; ++k) off += L.misc[k];
+        for (int w = w0; w < w1; ++w) {
+          L.bmp[w] = off;
+          off += __popc(L.bm[w]);
+        }
+        if (tid == 255) L.misc[4] = off;
+      }
+      __syncthreads();
+      const int U = (int)L.misc[4];
+      if (U <= kUMax) {
+        for (int w = tid; w < NW; w += 256) {
+          uint32_t bits = L.bm[w];
+          int r = (int)L.bmp[w];
+          while (bits) {
+            const int bpos = __builtin_ctz(bits);
+            bits &= bits - 1u;
+            L.list[r++] = w * 32 + bpos;
+          }
+        }
+        __syncthreads();
+        // corr[16 x U] = aref[16 x C] . tgt[U x C]^T on the matrix cores; per 16-channel step
+        // lane l feeds channels cb + 4 (l >> 4) + s in MFMA s (A and B permuted alike)
+        const float* tg = tgt_hwc + ((size_t)b * J + j) * (size_t)HW * C;
+        const int nblk = (U + 15) / 16;
+        for (int blk = wv; blk < nblk; blk += 4) {
+          const int u = blk * 16 + (lane & 15);
+          const int q = u < U ? L.list[u] : -1;
+          f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
+          const float* brow = tg + (size_t)(q < 0 ? 0 : q) * C + 4 * (lane >> 4);
+          const float* arow = L.aref + (lane & 15) * C + 4 * (lane >> 4);
+          for (int cb = 0; cb < C; cb += 16) {
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q >= 0) bv = *reinterpret_cast<const float4*>(brow + cb);
+            const float4 av = *reinterpret_cast<const float4*>(arow + cb);
+            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc4, 0, 0, 0);
+            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc4, 0, 0, 0);
+            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc4, 0, 0, 0);
+            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc4, 0, 0, 0);
+          }
+          // D[row][col]: col = lane & 15 (tapped pixel), row = 4 (lane >> 4) + r (ref pixel)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) L.corr[(4 * (lane >> 4) + r) * kUMax + u] = acc4[r];
+        }
+        __syncthreads();
+        for (int k = tid; k < DCH * TP; k += 256) {
+          const float2 sp = L.samp[k];
+          if (!(sp.x == sp.x)) continue;
+          const int i = k & (TP - 1);
+          const float fx0 = floorf(sp.x), fy0 = floorf(sp.y);
+          const int tx0 = (int)fx0, ty0 = (int)fy0;
+          const float wx0 = (float)(tx0 + 1) - sp.x, wx1 = sp.x - fx0, wy0 = (float)(ty0 + 1) - sp.y,
+                      wy1 = sp.y - fy0;
+          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
+          float s = 0.f;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+            if (tx >= 0 && tx < W && ty >= 0 && ty < H) s += wt[t] * L.corr[i * kUMax + tap_rank(L, ty * W + tx)];
+          }
+          L.acc[k] += s;
+        }
+      } else {
+        // too many distinct taps for LDS: direct dot products (rare: very wide epipolar bands)
+        const float* tg = tgt_hwc + ((size_t)b * J + j) * (size_t)HW * C;
+        for (int k = tid; k < DCH * TP; k += 256) {
+          const float2 sp = L.samp[k];
+          if (!(sp.x == sp.x)) continue;
+          const int i = k & (TP - 1);
+          const float fx0 = floorf(sp.x), fy0 = floorf(sp.y);
+          const int tx0 = (int)fx0, ty0 = (int)fy0;
+          const float wx0 = (float)(tx0 + 1) - sp.x, wx1 = sp.x - fx0, wy0 = (float)(ty0 + 1) - sp.y,
+                      wy1 = sp.y - fy0;
+          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
+          float s = 0.f;
+          for (int t = 0; t < 4; ++t) {
+            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+            if (!(tx >= 0 && tx < W && ty >= 0 && ty < H)) continue;
+            const float* row = tg + (size_t)(ty * W + tx) * C;
+            float dot = 0.f;
+            for (int c = 0; c < C; ++c) dot += L.aref[i * C + c] * row[c];
+            s += wt[t] * dot;
+          }
+          L.acc[k] += s;
+        }
+      }
+      __syncthreads();
+    }
+    for (int k = tid; k < DCH * TP; k += 256) {
+      const int i = k & (TP - 1), d = d0 + (k >> 4);
+      if (d < D && x0 + i < W) cost[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i] = L.acc[k] * scale;
+    }
+    __syncthreads();
+  }
+}
+
+// Backward with the same tiling. Per (tile, view): G[i][u] = sum over the tile's (pixel i,
+// depth d) samples tapping target pixel list[u] of dcost(i, d) * w_tap / (sqrt C J) (LDS
+// float atomics), then on the matrix cores
+//   dref[i][c] += sum_u G[i][u] tgt[list[u]][c]      ([16 x U] x [U x C], K = U)
+//   dtgt[list[u]][c] += sum_i G[i][u] ref[i][c]       ([U x 16] x [16 x C], K = 16; global atomics)
+__global__ __launch_bounds__(256) void k_cost_mfma_bwd(int J, int C, int H, int W, int D, int depth_per_pixel,
+                                                       const float* __restrict__ ref,
+                                                       const float* __restrict__ tgt_hwc,
+                                                       const float* __restrict__ intr,
+                                                       const float* __restrict__ pose,
+                                                       const float* __restrict__ depth, float clampz,
+                                                       const float* __restrict__ dcost, float* __restrict__ dref,
+                                                       float* __restrict__ dtgt_hwc) {
+  extern __shared__ __attribute__((aligned(16))) float cv_lds[];
+  const int HW = H * W, NW = (HW + 31) / 32;
+  CvLds L;
+  float* dacc;  // [TP][C] dref accumulated over views and depth chunks
+  {
+    float* p = cv_lds;
+    L.aref = p;
+    p += TP * C;
+    L.samp = reinterpret_cast<float2*>(p);
+    p += 2 * DCH * TP;
+    L.acc = p;  // G: [TP][kUMax]
+    p += TP * kUMax;
+    dacc = p;
+    p += TP * C;
+    L.list = reinterpret_cast<int*>(p);
+    p += kUMax;
+    L.bm = reinterpret_cast<uint32_t*>(p);
+    p += NW;
+    L.bmp = reinterpret_cast<uint32_t*>(p);
+    p += NW;
+    L.misc = reinterpret_cast<uint32_t*>(p);
+  }
+  float* Gm = L.acc;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tpr = (W + TP - 1) / TP;
+  const int y = blockIdx.x / tpr, x0 = (blockIdx.x % tpr) * TP;
+  const int b = blockIdx.y;
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  for (int k = tid; k < TP * C; k += 256) {
+    const int i = k & (TP - 1), c = k >> 4;
+    L.aref[i * C + c] = (x0 + i < W) ? ref[((size_t)b * C + c) * HW + (size_t)y * W + x0 + i] : 0.f;
+    dacc[i * C + c] = 0.f;
+  }
+  for (int d0 = 0; d0 < D; d0 += DCH) {
+    for (int j = 0; j < J; ++j) {
+      Cam cam;
+      load_cam(intr + ((size_t)b * J + j) * 9, pose + ((size_t)b * J + j) * 16, cam);
+      for (int w = tid; w < NW; w += 256) L.bm[w] = 0u;
+      __syncthreads();
+      for (int k = tid; k < DCH * TP; k += 256) {
+        const int i = k & (TP - 1), dd = k >> 4, d = d0 + dd;
+        float2 sp = make_float2(__int_as_float(0x7fc00000), 0.f);
+        if (d < D && x0 + i < W) {
+          const float px = (float)(x0 + i), py = (float)y;
+          const float qx = cam.Kinv[0] * px + cam.Kinv[1] * py + cam.Kinv[2];
+          const float qy = cam.Kinv[3] * px + cam.Kinv[4] * py + cam.Kinv[5];
+          const float qz = cam.Kinv[6] * px + cam.Kinv[7] * py + cam.Kinv[8];
+          const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
+          const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
+          const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
+          const float dep = depth_per_pixel ? depth[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i]
+                                            : depth[(size_t)b * D + d];
+          const float X = prx * dep + cam.t[0];
+          const float Y = pry * dep + cam.t[1];
+          const float Z = prz * dep + cam.t[2];
+          const float xx = cam.K[0] * X + cam.K[1] * Y + cam.K[2] * Z;
+          const float yy = cam.K[3] * X + cam.K[4] * Y + cam.K[5] * Z;
+          const float zz = fmaxf(cam.K[6] * X + cam.K[7] * Y + cam.K[8] * Z, clampz);
+          const float u = xx / zz, v = yy / zz;
+          const float gxn = 2 * u / (W - 1) - 1;
+          const float gyn = 2 * v / (H - 1) - 1;
+          const float ix = ((gxn + 1) / 2) * (W - 1);
+          const float iy = ((gyn + 1) / 2) * (H - 1);
+          if (ix > -2.f && ix < (float)W + 1.f && iy > -2.f && iy < (float)H + 1.f) {
+            sp = make_float2(ix, iy);
+            const int tx0 = (int)floorf(ix), ty0 = (int)floorf(iy);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+              if (tx >= 0 && tx < W && ty >= 0 && ty < H) {
+                const int q = ty * W + tx;
+                atomicOr(&L.bm[q >> 5], 1u << (q & 31));
+              }
+            }
+          }
+        }
+        L.samp[k] = sp;
+      }
+      __syncthreads();
+      {
+        const int per = (NW + 255) / 256;
+        const int w0 = tid * per, w1 = min(NW, w0 + per);
+        uint32_t tot = 0;
+        for (int w = w0; w < w1; ++w) tot += __popc(L.bm[w]);
+        const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
+        if (lane == 63) L.misc[wv] = incl;
+        __syncthreads();
+        uint32_t off = incl - tot;
+        for (int k = 0; k < wv; ++k) off += L.misc[k];
+        for (int w = w0; w < w1; ++w) {
+          L.bmp[w] = off;
+          off += __popc(L.bm[w]);
+        }
+        if (tid == 255) L.misc[4] = off;
+      }
+      __syncthreads();
+      const int U = (int)L.misc[4];
+      float* dtg = dtgt_hwc + ((size_t)b * J + j) * (size_t)HW * C;
+      const float* tg = tgt_hwc + ((size_t)b * J + j) * (size_t)HW * C;
+      if (U <= kUMax) {
+        const int Up = (U + 15) & ~15;
+        for (int w = tid; w < NW; w += 256) {
+          uint32_t bits = L.bm[w];
+          int r = (int)L.bmp[w];
+          while (bits) {
+            const int bpos = __builtin_ctz(bits);
+            bits &= bits - 1u;
+            L.list[r++] = w * 32 + bpos;
+          }
+        }
+        for (int k = tid; k < TP * Up; k += 256) Gm[(k / Up) * kUMax + (k % Up)] = 0.f;
+        __syncthreads();
+        for (int k = tid; k < DCH * TP; k += 256) {
+          const float2 sp = L.samp[k];
+          if (!(sp.x == sp.x)) continue;
+          const int i = k & (TP - 1), d = d0 + (k >> 4);
+          const float g = dcost[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i] * scale;
+          const float fx0 = floorf(sp.x), fy0 = floorf(sp.y);
+          const int tx0 = (int)fx0, ty0 = (int)fy0;
+          const float wx0 = (float)(tx0 + 1) - sp.x, wx1 = sp.x - fx0, wy0 = (float)(ty0 + 1) - sp.y,
+                      wy1 = sp.y - fy0;
+          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+            if (tx >= 0 && tx < W && ty >= 0 && ty < H) atomicAdd(&Gm[i * kUMax + tap_rank(L, ty * W + tx)], g * wt[t]);
+          }
+        }
+        __syncthreads();
+        // dref[16 x C] += G[16 x U] . T[U x C]: blocks of 16 channels, K = taps (4 per MFMA)
+        for (int cb = wv * 16; cb < C; cb += 64) {
+          f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
+          for (int u0 = 0; u0 < Up; u0 += 4) {
+            const int u = u0 + (lane >> 4);
+            const float a = Gm[(lane & 15) * kUMax + u];
+            const float bv = u < U ? tg[(size_t)L.list[u] * C + cb + (lane & 15)] : 0.f;
+            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc4, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dacc[(4 * (lane >> 4) + r) * C + cb + (lane & 15)] += acc4[r];
+        }
+        // dtgt[U x C] += G^T[U x 16] . aref[16 x C]: blocks of 16 taps x 16 channels, K = pixels
+        const int nub = Up / 16, ncb = C / 16;
+        for (int blk = wv; blk < nub * ncb; blk += 4) {
+          const int ub = (blk / ncb) * 16, cb = (blk % ncb) * 16;
+          f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) {
+            const int i = 4 * s2 + (lane >> 4);
+            const float a = Gm[i * kUMax + ub + (lane & 15)];
+            const float bv = L.aref[i * C + cb + (lane & 15)];
+            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc4, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int u = ub + 4 * (lane >> 4) + r;
+            if (u < U && acc4[r] != 0.f) atomicAdd(&dtg[(size_t)L.list[u] * C + cb + (lane & 15)], acc4[r]);
+          }
+        }
+      } else {
+        // direct scatter (very wide tap sets): per sample and tap, all channels
+        for (int k = tid; k < DCH * TP; k += 256) {
+          const float2 sp = L.samp[k];
+          if (!(sp.x == sp.x)) continue;
+          const int i = k & (TP - 1), d = d0 + (k >> 4);
+          const float g = dcost[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i] * scale;
+          const float fx0 = floorf(sp.x), fy0 = floorf(sp.y);
+          const int tx0 = (int)fx0, ty0 = (int)fy0;
+          const float wx0 = (float)(tx0 + 1) - sp.x, wx1 = sp.x - fx0, wy0 = (float)(ty0 + 1) - sp.y,
+                      wy1 = sp.y - fy0;
+          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
+          for (int t = 0; t < 4; ++t) {
+            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+            if (!(tx >= 0 && tx < W && ty >= 0 && ty < H)) continue;
+            const float gw = g * wt[t];
+            const size_t row = (size_t)(ty * W + tx) * C;
+            for (int c = 0; c < C; ++c) {
+              atomicAdd(&dacc[i * C + c], gw * tg[row + c]);
+              atomicAdd(&dtg[row + c], gw * L.aref[i * C + c]);
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int k = tid; k < TP * C; k += 256) {
+    const int i = k & (TP - 1), c = k >> 4;
+    if (x0 + i < W) dref[((size_t)b * C + c) * HW + (size_t)y * W + x0 + i] = dacc[i * C + c];
+  }
+}
+
+size_t cost_mfma_bwd_lds_bytes(int C, int HW) {
+  const int NW = (HW + 31) / 32;
+  return sizeof(float) * ((size_t)2 * TP * C + 2 * DCH * TP + TP * kUMax + kUMax + 2 * NW + 8);
+}
+
+size_t cost_mfma_lds_bytes(int C, int HW) {
+  const int NW = (HW + 31) / 32;
+  return sizeof(float) * ((size_t)TP * C + 2 * DCH * TP + DCH * TP + TP * kUMax + kUMax + 2 * NW + 8);
+}
+
 // Backward: one wave per (b, pixel); lanes over channels.
 //   dref[c,p]   += sum_{j,d} g(d) * warp_j[c,d,p]
 //   dtgt[q,c]   += g(d) * w_k * ref[c,p] for each tap (atomics into channel-last scratch)
@@ -345,6 +783,20 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
   const int HW = H * W;
   k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, tgt, tgt_hwc);
   if (int e = dsplat::check_launch("k_to_hwc")) return e;
+  const size_t lds = cost_mfma_lds_bytes(C, HW);
+  if (C % 16 == 0 && lds <= 160 * 1024) {  // matrix-core path
+    static size_t attr = 0;
+    if (lds > 64 * 1024 && lds > attr) {
+      if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_cost_mfma,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                                    "hipFuncSetAttribute(k_cost_mfma)"))
+        return e;
+      attr = lds;
+    }
+    k_cost_mfma<<<dim3((unsigned)(((W + TP - 1) / TP) * H), B), 256, lds, st>>>(
+        J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose, depth, clamp_min_depth, cost);
+    return dsplat::check_launch("k_cost_mfma");
+  }
   k_cost_fwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
                                                    depth, clamp_min_depth, cost);
   return dsplat::check_launch("k_cost_fwd");
@@ -360,9 +812,24 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
   hipStream_t st = (hipStream_t)stream;
   const int HW = H * W;
   if (int e = dsplat::zero_async(dtgt_hwc, (size_t)B * J * HW * C * 4, st, "zero dtgt_hwc")) return e;
-  k_cost_bwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
-                                                   depth, clamp_min_depth, dcost, dref, dtgt_hwc);
-  if (int e = dsplat::check_launch("k_cost_bwd")) return e;
+  const size_t lds = cost_mfma_bwd_lds_bytes(C, HW);
+  if (C % 16 == 0 && lds <= 160 * 1024) {  // matrix-core path
+    static size_t attr = 0;
+    if (lds > 64 * 1024 && lds > attr) {
+      if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_cost_mfma_bwd,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                                    "hipFuncSetAttribute(k_cost_mfma_bwd)"))
+        return e;
+      attr = lds;
+    }
+    k_cost_mfma_bwd<<<dim3((unsigned)(((W + TP - 1) / TP) * H), B), 256, lds, st>>>(
+        J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose, depth, clamp_min_depth, dcost, dref, dtgt_hwc);
+    if (int e = dsplat::check_launch("k_cost_mfma_bwd")) return e;
+  } else {
+    k_cost_bwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
+                                                     depth, clamp_min_depth, dcost, dref, dtgt_hwc);
+    if (int e = dsplat::check_launch("k_cost_bwd")) return e;
+  }
   k_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, dtgt_hwc, dtgt);
   return dsplat::check_launch("k_to_chw");
 }

@@ -104,3 +104,38 @@ def test_hip_cost_volume_large_vs_oracle(gpu):
     cost = plane_sweep_cost_volume(ref.to(gpu), tgt.to(gpu), K.to(gpu), pose.to(gpu), depth.to(gpu))
     want = ocv.cost_volume(ref, tgt, K, pose, depth)
     rel_close(cost.cpu(), want, 1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spread", ["narrow", "wide"])
+def test_hip_cost_volume_rotated_views_vs_oracle(gpu, spread):
+    """Two source views with rotations and translations. narrow: per-image candidates
+    (matrix-core path, a few hundred tapped pixels per tile); wide: random per-pixel depths
+    scatter the taps over the image (more than the LDS tap budget -> direct fallback)."""
+    g = torch.Generator().manual_seed(5)
+    B, J, C, H, W, D = 1, 2, 32, 40, 56, 64
+    ref = torch.randn(B, C, H, W, generator=g)
+    tgt = torch.randn(B, J, C, H, W, generator=g)
+    K = torch.tensor([[W * 0.9, 0, W / 2], [0, H * 1.1, H / 2], [0, 0, 1]]).expand(B, J, 3, 3).contiguous()
+    pose = torch.eye(4).repeat(B, J, 1, 1)
+    for j, (a, t) in enumerate([(0.05, (0.1, 0.02, 0.0)), (-0.08, (-0.05, 0.1, 0.03))]):
+        c, s = float(np.cos(a)), float(np.sin(a))
+        pose[:, j, 0, 0], pose[:, j, 0, 2], pose[:, j, 2, 0], pose[:, j, 2, 2] = c, s, -s, c
+        pose[:, j, :3, 3] = torch.tensor(t)
+    if spread == "narrow":
+        depth = 1.0 / torch.linspace(1 / 0.8, 1 / 30.0, D).expand(B, D).contiguous()
+        want = ocv.cost_volume(ref, tgt, K, pose, depth)
+    else:
+        depth = 0.3 + 20 * torch.rand(B, D, H, W, generator=g)
+        want = ocv.cost_volume(ref, tgt, K, pose, depth)
+    from my_depthsplat_amd.matching import plane_sweep_cost_volume
+    rg, tg_ = ref.to(gpu).requires_grad_(True), tgt.to(gpu).requires_grad_(True)
+    cost = plane_sweep_cost_volume(rg, tg_, K.to(gpu), pose.to(gpu), depth.to(gpu))
+    rel_close(cost.detach().cpu(), want, 1e-4)
+    # gradients (matrix-core backward, or its direct fallback) vs autograd of the oracle
+    dcost = torch.randn(want.shape, generator=g)
+    (cost * dcost.to(gpu)).sum().backward()
+    r2, t2 = ref.clone().requires_grad_(True), tgt.clone().requires_grad_(True)
+    (ocv.cost_volume(r2, t2, K, pose, depth) * dcost).sum().backward()
+    rel_close(rg.grad.cpu(), r2.grad, 1e-4)
+    rel_close(tg_.grad.cpu(), t2.grad, 1e-4)
