@@ -122,18 +122,36 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
  * scratch), which needs `workspace` of dsr_bin_sort_workspace_size(V, H, W, max_count)
  * bytes (NULL allowed when that is 0). (In the fixed-capacity layout N and the largest
  * segment are sum / max of seg_count: no same-address atomics from every workgroup.)
- * Offsets must stay below 2^31. */
+ * Offsets must stay below 2^31.
+ *
+ * Prefix mode (prefix > 0, needs seg_sorted [nseg]): in that split path, a segment longer
+ * than `prefix` only has its nearest entries sorted — keys[0, P) hold the P >= prefix
+ * smallest keys in order, keys[P, n) the rest, unordered — and seg_sorted[s] = P
+ * (= n for fully sorted segments; always written when seg_sorted is given). The
+ * compositor needs little more than a few hundred entries per tile, so the rest of a
+ * 30-40K entry list is never put in order; dsr_render_fwd checks the tail and flags the
+ * rare tile that does need it. seg_filter (non-NULL, needs scratch): sort in full only
+ * the segments with seg_filter[s] != 0 (the flagged tiles), leaving the others as they are.
+ * The reference sorts every key (cuda_rasterizer/rasterizer_impl.cu, SortPairs). */
 int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const uint32_t* seg_count,
                  uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count,
-                 void* workspace, void* stream);
+                 void* workspace, uint32_t prefix, uint32_t* seg_sorted, const uint32_t* seg_filter,
+                 void* stream);
 size_t dsr_bin_sort_workspace_size(int V, int H, int W, uint32_t max_count);
 uint32_t dsr_sort_lds_capacity(void);
 
 /* Front-to-back compositing per 16x16 tile (K6). out_color [V,3,H,W], final_T [V,H,W],
- * n_contrib [V,H,W] (uint32). Background from cams[v].bg. */
+ * n_contrib [V,H,W] (uint32). Background from cams[v].bg.
+ * seg_sorted (NULL = every segment fully sorted): entries past seg_sorted[s] are an
+ * unordered tail (dsr_bin_sort prefix mode); they are only checked, and if one of them
+ * passes the alpha test at a pixel that is still live, seg_overflow[s] is set to 1 (caller
+ * zeroes it) and that tile's outputs are void: sort the flagged segments in full
+ * (dsr_bin_sort with seg_filter = seg_overflow) and call again with seg_filter =
+ * seg_overflow and seg_sorted = NULL, which renders only those tiles. */
 int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride,
-                   const uint64_t* keys, float* out_color, float* final_T, uint32_t* n_contrib,
+                   const uint64_t* keys, const uint32_t* seg_sorted, uint32_t* seg_overflow,
+                   const uint32_t* seg_filter, float* out_color, float* final_T, uint32_t* n_contrib,
                    void* stream);
 
 /* ---- rasterizer backward -----------------------------------------------------------

@@ -867,7 +867,8 @@ template <int KMAX>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(KMAX >= 32 ? 1 : SORT_WPE))) void k_sort_lds(const uint32_t* __restrict__ seg_start,
                                                  const uint32_t* __restrict__ seg_count, uint32_t stride,
                                                  uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
-                                                 int id_bits, int big_here) {
+                                                 int id_bits, int big_here, const uint32_t* __restrict__ filter,
+                                                 uint32_t* __restrict__ seg_sorted) {
   constexpr uint32_t cap = NT * KMAX;
   constexpr uint32_t padded = cap + cap / KMAX;
   extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
@@ -877,9 +878,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(KMAX >= 32 ?
   uint32_t* wsum = aux + 2048;
   uint32_t* flag = wsum + 16;
   const int seg = blockIdx.x;
+  if (filter && !filter[seg]) return;
   uint32_t b, e;
   seg_bounds(seg_start, seg_count, stride, seg, b, e);
   const uint32_t n = e - b;
+  if (seg_sorted && threadIdx.x == 0 && (n <= cap || big_here)) seg_sorted[seg] = n;
   if (n <= 1) return;
   if (n > cap) {
     if (big_here) sort_segment<NT>(keys + b, scratch + b, n, id_bits, aux, wsum, flag, keys + b);
@@ -931,12 +934,36 @@ constexpr uint32_t kFromKeys = 0x80000000u;  // group flag: data still in keys (
 
 __host__ __device__ inline int split_groups(uint32_t max_count) { return (int)((max_count + kGroupHalf - 1) / kGroupHalf) + 1; }
 
+__device__ __forceinline__ uint32_t split_bound(const uint32_t* hist, uint32_t target, uint32_t n) {
+  // first bucket offset >= target (n if none); hist holds exclusive bucket offsets
+  if (target == 0) return 0u;
+  if (target >= n) return n;
+  int lo = 0, hi = kSplitNB;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (hist[mid] >= target) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo < kSplitNB ? hist[lo] : n;
+}
+
+// Prefix mode (prefix > 0, for the segments longer than `prefix`): only the nearest part of
+// the segment is sorted. The split's bucket offsets give P = the first bucket boundary at or
+// past `prefix`; keys of the buckets below it go to scratch (bucket-contiguous) and are
+// sorted into keys[0, P) by k_sort_groups, while the keys of the remaining buckets (all
+// deeper than every prefix key) are left, unordered, in keys[P, n): those already there
+// stay, and those that sat in [0, P) move into the holes left by prefix keys found in
+// [P, n) (the two counts are equal). seg_sorted[seg] = P. The compositor only has to
+// confirm that no tail key reaches a pixel that is still live (k_render_fwd).
+constexpr uint32_t kHoleCap = 8192;
 __global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ seg_count, uint32_t stride,
-                                                    const uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
-                                                    uint32_t small_cap, uint32_t* __restrict__ groups, int gmax) {
+                                                    uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
+                                                    uint32_t small_cap, uint32_t* __restrict__ groups, int gmax,
+                                                    uint32_t prefix, uint32_t* __restrict__ seg_sorted) {
   __shared__ uint32_t hist[kSplitNB];
-  __shared__ uint32_t red[32];
+  __shared__ uint32_t holes[kHoleCap];
+  __shared__ uint32_t red[34];
   const int seg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t* gout = groups + (size_t)seg * gmax * 2;
   uint32_t b, e;
@@ -944,13 +971,16 @@ __global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__
   const uint32_t n = e - b;
   if (n <= small_cap) {  // sorted by k_sort_lds already
     for (int g = tid; g < gmax; g += 1024) gout[2 * g] = gout[2 * g + 1] = 0u;
+    if (seg_sorted && tid == 0) seg_sorted[seg] = n;
     return;
   }
-  if ((int)((n + kGroupHalf - 1) / kGroupHalf) + 1 > gmax) {  // larger than the launch was sized for
+  const bool pfx = prefix != 0 && n > prefix;
+  if (!pfx && (int)((n + kGroupHalf - 1) / kGroupHalf) + 1 > gmax) {  // larger than the launch was sized for
     for (int g = tid; g < gmax; g += 1024) {
       gout[2 * g] = g == 0 ? b : 0u;
       gout[2 * g + 1] = g == 0 ? (e | kFromKeys) : 0u;
     }
+    if (seg_sorted && tid == 0) seg_sorted[seg] = n;
     return;
   }
   // segment min / max of the depth word
@@ -970,6 +1000,7 @@ __global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__
     red[16 + w] = mx;
   }
   for (int k = tid; k < kSplitNB; k += 1024) hist[k] = 0u;
+  if (tid == 0) red[32] = red[33] = 0u;
   __syncthreads();
   mn = red[0];
   mx = red[16];
@@ -1001,28 +1032,57 @@ __global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__
     off += c[k];
   }
   __syncthreads();
-  // group g = [B_g, B_{g+1}) with B_g = first bucket offset >= g * kGroupHalf (n if none)
-  if (tid < gmax) {
-    auto bound = [&](uint32_t target) -> uint32_t {
-      if (target == 0) return 0u;
-      if (target >= n) return n;
-      int lo = 0, hi = kSplitNB;  // first k with hist[k] >= target
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (hist[mid] >= target) hi = mid;
-        else lo = mid + 1;
+  // prefix cut: buckets >= kc (offsets >= P) stay unsorted in keys[P, n)
+  uint32_t P = n;
+  int kc = kSplitNB;
+  if (pfx) {
+    int lo = 0, hi = kSplitNB;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (hist[mid] >= prefix) hi = mid;
+      else lo = mid + 1;
+    }
+    kc = lo;
+    P = lo < kSplitNB ? hist[lo] : n;
+    if (min(P, n - P) > kHoleCap) {  // pathological depth clustering: sort all of it
+      P = n;
+      kc = kSplitNB;
+    }
+    // groups [B_g, B_g+1) for g < prefix / kGroupHalf cover [0, P) whatever P - prefix is;
+    // only a full sort of a segment this long can need more than the launch has
+    if (P == n && (int)((n + kGroupHalf - 1) / kGroupHalf) + 1 > gmax) {  // uniform across the workgroup
+      for (int g = tid; g < gmax; g += 1024) {
+        gout[2 * g] = g == 0 ? b : 0u;
+        gout[2 * g + 1] = g == 0 ? (e | kFromKeys) : 0u;
       }
-      return lo < kSplitNB ? hist[lo] : n;
-    };
-    const uint32_t g0 = bound((uint32_t)tid * kGroupHalf), g1 = bound((uint32_t)(tid + 1) * kGroupHalf);
+      if (seg_sorted && tid == 0) seg_sorted[seg] = n;
+      return;
+    }
+  }
+  if (seg_sorted && tid == 0) seg_sorted[seg] = P;
+  // group g = [B_g, B_{g+1}) clipped to [0, P), B_g = first bucket offset >= g * kGroupHalf
+  if (tid < gmax) {
+    const uint32_t g0 = min(split_bound(hist, (uint32_t)tid * kGroupHalf, n), P);
+    const uint32_t g1 = min(split_bound(hist, (uint32_t)(tid + 1) * kGroupHalf, n), P);
     gout[2 * tid] = b + g0;
     gout[2 * tid + 1] = b + g1;
   }
   __syncthreads();
   for (uint32_t i = tid; i < n; i += 1024) {
     const uint64_t k = keys[b + i];
-    const uint32_t pos = atomicAdd(&hist[((uint32_t)(k >> 32) - mn) >> sh], 1u);
-    scratch[b + pos] = k;
+    const int bk = (int)(((uint32_t)(k >> 32) - mn) >> sh);
+    if (bk < kc) {
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      scratch[b + pos] = k;
+      if (i >= P) holes[atomicAdd(&red[32], 1u)] = i;
+    }
+  }
+  if (P < n) {
+    __syncthreads();
+    for (uint32_t i = tid; i < P; i += 1024) {
+      const uint64_t k = keys[b + i];
+      if ((int)(((uint32_t)(k >> 32) - mn) >> sh) >= kc) keys[b + holes[atomicAdd(&red[33], 1u)]] = k;
+    }
   }
 }
 
@@ -1204,6 +1264,50 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v p
   }
 }
 
+// Tail check for prefix-sorted segments: the keys in [b, e) are all deeper than the sorted
+// prefix but unordered. Compositing them in depth order changes a pixel only if one of them
+// passes the per-pixel test (power <= 0, alpha >= 1/255) while the pixel is still live, so
+// when none does the prefix alone gives the exact result. Returns (wave-uniform) whether
+// one does.
+__device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* __restrict__ keys, uint32_t b,
+                                  uint32_t e, float fx0, float fy0, f2v pfx2, f2v pfy2, float Tr, PairRec* plist,
+                                  uint64_t lt, int lane) {
+  uint32_t nid = b + lane < e ? (uint32_t)keys[b + lane] : 0xffffffffu;
+  for (uint32_t base = b; base < e && !__all(Tr < 0.0f); base += 64) {
+    const uint32_t id = nid;
+    nid = base + 64 + lane < e ? (uint32_t)keys[base + 64 + lane] : 0xffffffffu;
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f), r = q;
+    if (id != 0xffffffffu) {
+      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
+      q = rec[0];
+      r = rec[1];
+    }
+    const bool mine = id != 0xffffffffu && subtile_hit(q, r, fx0, fy0);
+    const uint64_t bal = __ballot(mine);
+    if (mine) {
+      const float4 sq = scaled_conic_q(q);
+      pair_put(plist, __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * r.x, sq.w, r.y, 0.f, 0.f, 0.f, 0u);
+    }
+    const int cnt = __popcll(bal);
+    if (lane < 2) pair_put(plist, cnt + lane, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u);
+    __builtin_amdgcn_wave_barrier();
+    bool hit = false;
+    for (int k = 0; k < cnt; k += 2) {
+      const PairRec& P = plist[k >> 1];
+      const f2v dx = P.x - pfx2, dy = P.y - pfy2;
+      const f2v p2 = __builtin_elementwise_fma(P.A * dx, dx, __builtin_elementwise_fma(P.C * dy, dy, P.B * dx * dy));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float alpha = fminf(0.99f, P.o[j] * __builtin_amdgcn_exp2f(p2[j]));
+        hit |= p2[j] <= 0.0f && alpha >= 1.0f / 255.0f;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (__any(hit && Tr > 0.0f)) return true;
+  }
+  return false;
+}
+
 // K6: front-to-back compositing. grid = (gx, gy, V), block = 256 = 4 independent waves;
 // wave w owns the 8x8 sub-tile (w & 1, w >> 1) of the tile. There is no workgroup barrier:
 // each wave walks the tile's list CH entries at a time (EPL keys + records per lane, the
@@ -1220,6 +1324,9 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
                                                    const uint32_t* __restrict__ seg_start,
                                                    const uint32_t* __restrict__ seg_count, uint32_t stride,
                                                    const uint64_t* __restrict__ keys,
+                                                   const uint32_t* __restrict__ seg_sorted,
+                                                   uint32_t* __restrict__ seg_overflow,
+                                                   const uint32_t* __restrict__ seg_filter,
                                                    float* __restrict__ out, float* __restrict__ finalT,
                                                    uint32_t* __restrict__ ncontrib) {
   __shared__ PairRec l_pair[4][(CH + 8) / 2];
@@ -1230,8 +1337,11 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   const int py = sy0 + (lane >> 3);
   const bool inside = px < W && py < H;
   const int seg = v * T + blockIdx.y * gx + blockIdx.x;
+  if (seg_filter && !seg_filter[seg]) return;
   uint32_t start, end;
   seg_bounds(seg_start, seg_count, stride, seg, start, end);
+  const uint32_t tail_end = end;  // [end, tail_end): unsorted tail (prefix-sorted segments)
+  if (seg_sorted) end = start + min(seg_sorted[seg], end - start);
   const float pfx = (float)px, pfy = (float)py;
   const float fx0 = (float)sx0, fy0 = (float)sy0;
   const float* gv = geom + (size_t)v * G * GS;
@@ -1313,6 +1423,9 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
       cb[u] = nb[u];
     }
   }
+  if (end < tail_end && tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pfx2, pfy2, Tr, plist, lt, lane) &&
+      lane == 0)
+    seg_overflow[seg] = 1u;  // the tile's output is void: re-sorted in full and re-rendered by the caller
   if (inside) {
     const size_t HW = (size_t)H * W;
     const size_t pix = (size_t)py * W + px;
@@ -1917,13 +2030,15 @@ size_t dsr_bin_sort_workspace_size(int V, int H, int W, uint32_t max_count) {
 
 int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const uint32_t* seg_count,
                  uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count, void* workspace,
-                 void* stream) {
+                 uint32_t prefix, uint32_t* seg_sorted, const uint32_t* seg_filter, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_sort: bad sizes");
   DSPLAT_REQUIRE(keys != nullptr && (seg_stride ? seg_count != nullptr : seg_start != nullptr),
                  "dsr_bin_sort: null pointer");
   DSPLAT_REQUIRE(scratch != nullptr || (max_count > 0 && max_count <= kSortCap),
                  "dsr_bin_sort: without scratch, max_count (%u) must bound every segment and be <= %u", max_count,
                  kSortCap);
+  DSPLAT_REQUIRE(prefix == 0 || seg_sorted != nullptr, "dsr_bin_sort: prefix mode needs seg_sorted");
+  DSPLAT_REQUIRE(seg_filter == nullptr || scratch != nullptr, "dsr_bin_sort: seg_filter needs scratch");
   hipStream_t st = (hipStream_t)stream;
   const int nseg = V * dsplat::tiles_x(W) * dsplat::tiles_y(H);
   int id_bits = 0;
@@ -1931,7 +2046,7 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
   const uint32_t want = max_count ? max_count : kSortCap;
   // segments above the LDS capacity: sorted in this launch through HBM unless they are
   // known to be large (max_count > kSortCap): then the MSD split + grouped LDS sort take them
-  const bool big_known = scratch != nullptr && max_count > kSortCap;
+  const bool big_known = scratch != nullptr && max_count > kSortCap && seg_filter == nullptr;
   const int big_here = scratch != nullptr && !big_known;
   DSPLAT_REQUIRE(!big_known || workspace != nullptr,
                  "dsr_bin_sort: max_count %u > %u needs workspace (dsr_bin_sort_workspace_size)", max_count, kSortCap);
@@ -1950,32 +2065,39 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
     attr_set = true;
   }
   uint32_t cap;
-  if (big_known) {  // small segments in LDS now, the rest split below
+  if (big_known || seg_filter) {  // small segments in LDS now, the rest split below (or through HBM)
     cap = 256 * 16;
     k_sort_lds<16><<<nseg, NT, sort_lds_bytes<16>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, 0);
+                                                                id_bits, big_here, seg_filter, seg_sorted);
   } else if (want <= 256 * 4) {
     cap = 256 * 4;
     k_sort_lds<4><<<nseg, NT, sort_lds_bytes<4>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, big_here);
+                                                                id_bits, big_here, nullptr, seg_sorted);
   } else if (want <= 256 * 8) {
     cap = 256 * 8;
     k_sort_lds<8><<<nseg, NT, sort_lds_bytes<8>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, big_here);
+                                                                id_bits, big_here, nullptr, seg_sorted);
   } else if (want <= 256 * 16) {
     cap = 256 * 16;
     k_sort_lds<16><<<nseg, NT, sort_lds_bytes<16>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, big_here);
+                                                                id_bits, big_here, nullptr, seg_sorted);
   } else {
     cap = 256 * 32;
     k_sort_lds<32><<<nseg, NT, sort_lds_bytes<32>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, big_here);
+                                                                id_bits, big_here, nullptr, seg_sorted);
   }
   if (int e = dsplat::check_launch("k_sort_lds")) return e;
   if (big_known) {
-    const int gmax = split_groups(max_count);
+    uint32_t pfx = 0;
+    int gmax = split_groups(max_count);
+    if (prefix) {  // a multiple of the group half-size, at least the LDS capacity
+      pfx = max(cap, (prefix + kGroupHalf - 1) / kGroupHalf * kGroupHalf);
+      if (pfx < max_count) gmax = min(gmax, (int)(pfx / kGroupHalf) + 1);
+      else pfx = 0;
+    }
     uint32_t* groups = static_cast<uint32_t*>(workspace);
-    k_msd_split<<<nseg, 1024, 0, st>>>(seg_start, seg_count, seg_stride, keys, scratch, cap, groups, gmax);
+    k_msd_split<<<nseg, 1024, 0, st>>>(seg_start, seg_count, seg_stride, keys, scratch, cap, groups, gmax, pfx,
+                                       seg_sorted);
     if (int e = dsplat::check_launch("k_msd_split")) return e;
     k_sort_groups<16><<<(unsigned)(nseg * gmax), NT, sort_lds_bytes<16>(), st>>>(groups, keys, scratch, id_bits);
     if (int e = dsplat::check_launch("k_sort_groups")) return e;
@@ -1985,7 +2107,9 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
 
 int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride, const uint64_t* keys,
-                   float* out_color, float* final_T, uint32_t* n_contrib, void* stream) {
+                   const uint32_t* seg_sorted, uint32_t* seg_overflow, const uint32_t* seg_filter, float* out_color,
+                   float* final_T, uint32_t* n_contrib, void* stream) {
+  DSPLAT_REQUIRE(seg_sorted == nullptr || seg_overflow != nullptr, "dsr_render_fwd: seg_sorted needs seg_overflow");
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_render_fwd: bad sizes");
   DSPLAT_REQUIRE(cams && geom && (seg_stride ? seg_count != nullptr : seg_start != nullptr) && out_color && final_T &&
                      n_contrib,
@@ -1993,7 +2117,8 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
   k_render_fwd<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count,
-                                                     seg_stride, keys, out_color, final_T, n_contrib);
+                                                     seg_stride, keys, seg_sorted, seg_overflow, seg_filter,
+                                                     out_color, final_T, n_contrib);
   return dsplat::check_launch("k_render_fwd");
 }
 

@@ -11,6 +11,7 @@ needed to size the key buffer.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -135,6 +136,8 @@ class RasterState:
     keys: torch.Tensor        # int64 (uint64 keys, sorted per segment)
     final_T: torch.Tensor     # [V, H, W]
     n_contrib: torch.Tensor   # [V, H, W] int32
+    seg_sorted: torch.Tensor | None = None    # [V*T] sorted entries per segment (prefix-sort mode)
+    seg_overflow: torch.Tensor | None = None  # [V*T] tiles re-sorted in full and re-rendered
 
     @property
     def num_rendered(self) -> int:  # host read: syncs
@@ -152,6 +155,10 @@ class RasterState:
 # untouched pages cost no bandwidth); the whole forward then runs with NO host sync.
 # Larger problems fall back to one 8-byte read of (N, max tile count) after the scan.
 KEY_BUDGET_BYTES = 8 << 30
+# Segments larger than this many entries (only when some exceed the LDS sort) get only their
+# nearest SORT_PREFIX entries put in order (dsr_bin_sort prefix mode): at 6x448x768 the
+# compositor uses at most ~1.2K of 30-40K entries per tile. 0 sorts everything.
+SORT_PREFIX = int(os.environ.get("DSPLAT_SORT_PREFIX", "4096"))
 _spec = {"max_count": 0}
 _inflight: list = []  # (pinned int32 counts, event) read-backs, consumed without blocking
 
@@ -281,11 +288,11 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout, st),
             "dsr_project_bin")
         maxc_hint = _spec["max_count"] or lds_cap
-        ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
-        _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, None, seg_count.data_ptr(), G, keys.data_ptr(),
-                          scratch.data_ptr(), maxc_hint, _ptr(ws), st), "dsr_bin_sort")
-        _note_counts(seg_count)
         seg_start, stride = None, G
+        ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
+        seg_sorted = _prefix_sort(lib, G, V, H, W, None, seg_count, stride, keys, scratch, maxc_hint, ws, st,
+                                  lds_cap)
+        _note_counts(seg_count)
     else:
         _lib.check(_timed("k_preprocess", lib.dsr_preprocess_fwd,
             S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
@@ -306,17 +313,41 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
                           keys.data_ptr(), st), "dsr_bin_scatter")
         ws = _sort_workspace(lib, V, H, W, maxc, dev)
-        _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), None, 0, keys.data_ptr(),
-                          None if scratch is None else scratch.data_ptr(), maxc, _ptr(ws), st), "dsr_bin_sort")
         stride = 0
+        seg_sorted = _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, maxc, ws, st,
+                                  lds_cap)
     color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
+    outs = (color.data_ptr(), final_T.data_ptr(), n_contrib.data_ptr(), st)
+    overflow = None
+    if seg_sorted is not None:
+        overflow = torch.zeros(V * T, dtype=torch.int32, device=dev)
     _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
-                      _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(), color.data_ptr(),
-                      final_T.data_ptr(), n_contrib.data_ptr(), st), "dsr_render_fwd")
+                      _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(), _ptr(seg_sorted),
+                      _ptr(overflow), None, *outs), "dsr_render_fwd")
+    if overflow is not None:
+        # tiles whose unsorted tail would have blended: sort those in full, render them again
+        # (both launches return at once for unflagged tiles; no host sync)
+        _lib.check(lib.dsr_bin_sort(G, V, H, W, _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(),
+                                    scratch.data_ptr(), 0, None, 0, seg_sorted.data_ptr(), overflow.data_ptr(), st),
+                   "dsr_bin_sort(overflow)")
+        _lib.check(lib.dsr_render_fwd(G, V, H, W, cams.data_ptr(), geom.data_ptr(), _ptr(seg_start),
+                                      seg_count.data_ptr(), stride, keys.data_ptr(), None, None, overflow.data_ptr(),
+                                      *outs), "dsr_render_fwd(overflow)")
     _last["counts"] = seg_count
-    return color, RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib)
+    return color, RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, seg_sorted,
+                              overflow)
+
+
+def _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, max_count, ws, st, lds_cap):
+    """dsr_bin_sort; prefix mode (returns seg_sorted) when segments exceed the LDS sort."""
+    prefix = SORT_PREFIX if (scratch is not None and max_count > lds_cap and SORT_PREFIX > 0) else 0
+    seg_sorted = torch.empty(seg_count.numel(), dtype=torch.int32, device=keys.device) if prefix else None
+    _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, _ptr(seg_start), seg_count.data_ptr(), stride,
+                      keys.data_ptr(), _ptr(scratch), max_count, _ptr(ws), prefix, _ptr(seg_sorted), None, st),
+               "dsr_bin_sort")
+    return seg_sorted
 
 
 def _ptr(t):

@@ -52,10 +52,10 @@ def test_load_without_gpu_and_error_channel():
     if not _lib.LIB_PATH.exists():
         pytest.skip("extension not built")
     lib = _lib.load()
-    assert lib.dsplat_abi_version() == 2
+    assert lib.dsplat_abi_version() == 3
     assert lib.dsr_sort_lds_capacity() >= 256
     # argument validation happens before any HIP call -> works on a GPU-less host
-    rc = lib.dsr_render_fwd(0, 1, 8, 8, None, None, None, None, 0, None, None, None, None, None)
+    rc = lib.dsr_render_fwd(0, 1, 8, 8, None, None, None, None, 0, None, None, None, None, None, None, None, None)
     assert rc == 1 and b"bad sizes" in lib.dsplat_last_error()
     with pytest.raises(_lib.DsplatError):
         _lib.check(rc, "dsr_render_fwd")

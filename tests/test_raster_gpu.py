@@ -156,19 +156,7 @@ def test_render_backward_matches_oracle(gpu):
     close(dopac[0].cpu().numpy(), acc["dopacity"], "opacity")
 
 
-@pytest.mark.parametrize("binning,hint", [("fused", "low"), ("fused", "exact"), ("fused", "between"),
-                                          ("two_phase", "exact")])
-def test_large_tiles_sort_paths(gpu, binning, hint, monkeypatch):
-    """Big Gaussians -> tiles with > LDS-capacity entries. hint = the max-count hint the
-    forward sizes the sort with: low -> in-kernel HBM radix path; exact -> MSD split into
-    LDS-sized groups; between (above the LDS capacity, below the real maximum) -> split
-    launch whose too-large segments fall back to one HBM-sorted group."""
-    from my_depthsplat_amd import _lib, raster
-    cap = _lib.load().dsr_sort_lds_capacity()
-    if binning == "two_phase":
-        monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
-    monkeypatch.setitem(raster._spec, "max_count", {"low": 1, "exact": 12288 + 8, "between": cap + 1}[hint])
-    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)  # keep the hint fixed
+def _large_tile_scene(opacity_scale=0.05, constant_opacity=None):
     sc = scene_inputs(h=32, w=32, seed=5, n_ctx=2)
     g = sc.gaussians
     # blow covariances up so every Gaussian covers many tiles; 2 x 32 x 32 = 2048 Gaussians
@@ -177,21 +165,132 @@ def test_large_tiles_sort_paths(gpu, binning, hint, monkeypatch):
     g.means = g.means.repeat(1, rep, 1) + 0.001 * torch.arange(rep).repeat_interleave(2048)[None, :, None]
     g.covariances = g.covariances.repeat(1, rep, 1, 1) * 400.0
     g.harmonics = g.harmonics.repeat(1, rep, 1, 1)
-    g.opacities = g.opacities.repeat(1, rep) * 0.05
+    g.opacities = g.opacities.repeat(1, rep) * opacity_scale
+    if constant_opacity is not None:
+        g.opacities = torch.full_like(g.opacities, constant_opacity)
+    return sc
+
+
+def _check_segments_vs_oracle(state, orcs, V, T):
+    """Segment ids vs the oracle's sorted ids: all of them, or with prefix-sorted segments
+    the sorted prefix exactly and the unordered tail as a set."""
+    start, keys = _segments(state, V, T)
+    srt = None if state.seg_sorted is None else state.seg_sorted.cpu().numpy()
+    for v, o in enumerate(orcs):
+        okeys, ovals, ranges = o.binning()
+        for t in range(T):
+            s = v * T + t
+            hk = (keys[start[s]:start[s + 1]] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+            ob, oe = ranges[t]
+            if srt is None:
+                np.testing.assert_array_equal(hk, ovals[ob:oe])
+                continue
+            P = int(srt[s])
+            assert min(oe - ob, 4096) <= P <= oe - ob
+            np.testing.assert_array_equal(hk[:P], ovals[ob:ob + P])
+            np.testing.assert_array_equal(np.sort(hk[P:]), np.sort(ovals[ob + P:oe]))
+
+
+@pytest.mark.parametrize("binning,hint,prefix", [("fused", "low", 4096), ("fused", "exact", 4096),
+                                                 ("fused", "exact", 0), ("fused", "between", 0),
+                                                 ("fused", "between", 4096), ("two_phase", "exact", 4096),
+                                                 ("two_phase", "exact", 0)])
+def test_large_tiles_sort_paths(gpu, binning, hint, prefix, monkeypatch):
+    """Big Gaussians -> tiles with > LDS-capacity entries. hint = the max-count hint the
+    forward sizes the sort with: low -> in-kernel HBM radix path; exact -> MSD split into
+    LDS-sized groups; between (above the LDS capacity, below the real maximum) -> split
+    launch whose too-large segments fall back to one HBM-sorted group (prefix 0) or are
+    prefix-sorted. prefix: raster.SORT_PREFIX (0 = sort every entry)."""
+    from my_depthsplat_amd import _lib, raster
+    cap = _lib.load().dsr_sort_lds_capacity()
+    if binning == "two_phase":
+        monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+    monkeypatch.setattr(raster, "SORT_PREFIX", prefix)
+    monkeypatch.setitem(raster._spec, "max_count", {"low": 1, "exact": 12288 + 8, "between": cap + 1}[hint])
+    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)  # keep the hint fixed
+    sc = _large_tile_scene()
     st = settings_for(sc)
     color, state, _ = hip_forward(sc, st, gpu)
     assert state.max_count > cap
+    assert (state.seg_sorted is not None) == (prefix > 0 and hint != "low")
     orcs = oracle_views(sc, st)
-    start, keys = _segments(state, 2, 4)
+    _check_segments_vs_oracle(state, orcs, 2, 4)
+    ncon = state.n_contrib.cpu().numpy()
     for v, o in enumerate(orcs):
-        okeys, ovals, ranges = o.binning()
-        for t in range(4):
-            hk = keys[start[v * 4 + t]:start[v * 4 + t + 1]]
-            ob, oe = ranges[t]
-            np.testing.assert_array_equal((hk & np.uint64(0xFFFFFFFF)).astype(np.uint32), ovals[ob:oe])
-        oc, _, _ = o.image()
+        oc, _, on = o.image()
         assert float(np.abs(color[v].cpu().numpy() - oc).mean()) < 1e-4
+        assert (ncon[v] == on).mean() > 0.999
         o.close()
+
+
+@pytest.mark.parametrize("binning", ["fused", "two_phase"])
+def test_prefix_sort_overflow_fixup(gpu, binning, monkeypatch):
+    """Faint Gaussians (alpha just above 1/255): no pixel saturates, so the unsorted tail of
+    every long segment would still blend -> each such tile is flagged, sorted in full and
+    rendered again. Outputs and gradients must equal those of a full sort, bit for bit."""
+    from my_depthsplat_amd import raster
+    if binning == "two_phase":
+        monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+    monkeypatch.setitem(raster._spec, "max_count", 12288 + 8)
+    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
+    sc = _large_tile_scene(constant_opacity=0.0045)
+    st = settings_for(sc)
+    runs = {}
+    for prefix in (4096, 0):
+        monkeypatch.setattr(raster, "SORT_PREFIX", prefix)
+        color, state, cams = hip_forward(sc, st, gpu)
+        runs[prefix] = (color.cpu(), state.final_T.cpu(), state.n_contrib.cpu(), state)
+    st4 = runs[4096][3]
+    assert st4.seg_overflow is not None
+    big = st4.seg_count.cpu() > 4096
+    flagged = st4.seg_overflow.cpu() != 0
+    assert bool(flagged.any()) and not bool(flagged[~big].any())
+    assert torch.equal(st4.seg_sorted.cpu()[flagged], st4.seg_count.cpu()[flagged])  # re-sorted in full
+    for a, b in zip(runs[4096][:3], runs[0][:3]):
+        assert torch.equal(a, b)
+    orcs = oracle_views(sc, st)
+    _check_segments_vs_oracle(runs[0][3], orcs, 2, 4)
+    for v, o in enumerate(orcs):
+        oc, _, on = o.image()
+        assert float(np.abs(runs[4096][0][v].numpy() - oc).mean()) < 1e-4
+        assert (runs[4096][2][v].numpy() == on).mean() > 0.999
+        o.close()
+
+
+def test_prefix_sort_matches_full_sort(gpu, monkeypatch):
+    """Default opacities: the sorted prefix suffices (no tile flagged) and forward outputs
+    and backward gradients are bit-identical to sorting every entry."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setitem(raster._spec, "max_count", 12288 + 8)
+    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
+    sc = _large_tile_scene(opacity_scale=1.0)
+    st = settings_for(sc)
+    means, shs, opac, cov6 = flat_inputs(sc)
+    B, v = sc.target_extrinsics.shape[:2]
+    view_scene = [i // v for i in range(B * v)]
+    h, w = sc.image_shape
+    deg = math.isqrt(shs.shape[2]) - 1
+    out = {}
+    for prefix in (4096, 0):
+        monkeypatch.setattr(raster, "SORT_PREFIX", prefix)
+        cams = packed_cams(st, view_scene, (0.0, 0.0, 0.0)).to(gpu)
+        args = [t.to(gpu) for t in (means, shs, opac, cov6)]
+        color, state = raster.forward_raw(args[0], args[1], True, deg, args[2], args[3], cams, B * v, h, w)
+        dcolor = torch.linspace(-1, 1, color.numel(), device=gpu).view_as(color)
+        grads = raster.backward_raw(args[0], args[1], True, deg, args[2], args[3], cams, view_scene, state, dcolor,
+                                    want_mean2d=True)
+        torch.cuda.synchronize()
+        out[prefix] = (state, [color.cpu(), state.final_T.cpu(), state.n_contrib.cpu()] +
+                       [g.cpu() for g in grads if g is not None])
+    st4 = out[4096][0]
+    assert st4.seg_sorted is not None
+    unsorted_tail = st4.seg_sorted.cpu() < st4.seg_count.cpu()
+    assert bool(unsorted_tail.any())  # the prefix sufficed for some long segment
+    fa, fb = out[4096][1], out[0][1]
+    for a, b in zip(fa[:3], fb[:3]):  # forward: bit-identical
+        assert torch.equal(a, b)
+    for a, b in zip(fa[3:], fb[3:]):  # gradients: same terms, float atomics add them in any order
+        assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max())
 
 
 def test_empty_and_culled(gpu):

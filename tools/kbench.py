@@ -64,7 +64,7 @@ def main():
 
             def launch():
                 return lib.dsr_render_fwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), sp, sc_p, stride,
-                                          state.keys.data_ptr(), out[0].data_ptr(), out[1].data_ptr(),
+                                          state.keys.data_ptr(), None, None, None, out[0].data_ptr(), out[1].data_ptr(),
                                           out[2].data_ptr(), st)
         elif a.kernel in ("project", "project_sort"):  # fused binning (+ sort)
             assert stride > 0, "fused layout expected"
@@ -83,7 +83,7 @@ def main():
                 if rc or a.kernel == "project":
                     return rc
                 return lib.dsr_bin_sort(G, V, H, W, None, cnt2.data_ptr(), a.stride or G, keys2.data_ptr(),
-                                        scratch2.data_ptr(), state.max_count, ws_p, st)
+                                        scratch2.data_ptr(), state.max_count, ws_p, 0, None, None, st)
         elif a.kernel == "sort_sorted":  # re-sort the (already sorted) keys in place: pass cost only
             tot3 = torch.empty(4, dtype=torch.int32, device=dev)
             scr = torch.empty_like(state.keys)
@@ -91,7 +91,7 @@ def main():
 
             def launch():
                 return lib.dsr_bin_sort(G, V, H, W, sp, sc_p, stride, state.keys.data_ptr(), scr.data_ptr(),
-                                        state.max_count, ws_p, st)
+                                        state.max_count, ws_p, 0, None, None, st)
         else:
             out = [torch.zeros_like(state.geom)]
 
