@@ -66,6 +66,25 @@ __device__ __forceinline__ void tile_rect(float px, float py, int r, int gx, int
 // with a huge rect no longer serialises its whole wave (radii are heavy-tailed: a few
 // Gaussians touch hundreds of tiles, the median touches one or two). f(tile, owner lane)
 // runs once per pair; ws_* are this wave's 64-entry LDS slots.
+// Workgroup -> (view, block) placement by XCD. Workgroups are dispatched round-robin over
+// the 8 XCDs (id % 8), each with its own L2. The (view, block) items are cut into 8
+// contiguous ranges, one per XCD, so a view's segments are written (keys) and counted
+// (atomics) through one or two L2s instead of all eight: 8-byte key stores to a segment's
+// frontier lines then merge in that L2 before write-back, and count atomics stay local.
+// grid.x = 8 * ceil(items / 8); returns false for the padding workgroups.
+__device__ __forceinline__ bool xcd_item(int blocks_per_view, int V, int& v, int& blk) {
+  const int items = blocks_per_view * V;
+  const int per = (items + 7) >> 3;
+  const int item = (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
+  if ((int)(blockIdx.x >> 3) >= per || item >= items) return false;
+  v = item / blocks_per_view;
+  blk = item - v * blocks_per_view;
+  return true;
+}
+__host__ __device__ constexpr unsigned xcd_grid(int blocks_per_view, int V) {
+  return 8u * (unsigned)((blocks_per_view * V + 7) / 8);
+}
+
 struct WaveRects {
   uint32_t ex[64];    // exclusive scan of areas
   uint32_t org[64];   // x0 | y0 << 16
@@ -325,7 +344,7 @@ __device__ __forceinline__ void store_geom(float* __restrict__ geom, int32_t* __
 // K1: preprocess + per-(view, tile) entry counts (two-phase binning path).
 // grid = (ceil(G/256), V), block = 256. DEG = -1 -> colors_precomp path.
 template <int DEG>
-__global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, int gy, int M,
+__global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, int gx, int gy, int M,
                                                    const float* __restrict__ means,
                                                    const float* __restrict__ shs,
                                                    const float* __restrict__ colors,
@@ -335,7 +354,8 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
                                                    float* __restrict__ geom, int32_t* __restrict__ radii,
                                                    uint32_t* __restrict__ seg_count, int lds_hist, int layout) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
-  const int v = blockIdx.y;
+  int v, blk;
+  if (!xcd_item((G + NT - 1) / NT, V, v, blk)) return;
   const int T = gx * gy;
   const int tid = threadIdx.x;
   const dsr_camera* cam = cams + v;
@@ -343,7 +363,7 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int H, int W, int gx, 
     for (int t = tid; t < T; t += NT) s_hist[t] = 0;
     __syncthreads();
   }
-  const int g = blockIdx.x * NT + tid;
+  const int g = blk * NT + tid;
   int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
   if (g < G) {
     GaussIn<DEG> in;
@@ -395,11 +415,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
-  const int v = blockIdx.y;
+  int v, blk;
+  if (!xcd_item((G + NT - 1) / NT, V, v, blk)) return;
   const dsr_camera* cam = cams + v;
   const int T = gx * gy;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = blockIdx.x * NT + tid;
+  const int g = blk * NT + tid;
   WaveRects& wr = s_wr[w];
   const uint64_t* wkey = s_key + w * 64;
   {
@@ -479,18 +500,19 @@ __global__ __launch_bounds__(1024) void k_scan(int n, const uint32_t* __restrict
 
 // ------------------------------------------------------------------------------------
 // K3: emit (depth, id) keys into their (view, tile) bucket.
-__global__ __launch_bounds__(NT) void k_scatter(int G, int gx, int gy, const float* __restrict__ geom,
+__global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, const float* __restrict__ geom,
                                                 uint32_t* __restrict__ cursor,
                                                 uint64_t* __restrict__ keys, int lds_hist) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
-  const int v = blockIdx.y;
+  int v, blk;
+  if (!xcd_item((G + NT - 1) / NT, V, v, blk)) return;
   const int T = gx * gy;
   const int tid = threadIdx.x;
   if (lds_hist) {
     for (int t = tid; t < T; t += NT) s_hist[t] = 0;
     __syncthreads();
   }
-  const int g = blockIdx.x * NT + tid;
+  const int g = blk * NT + tid;
   int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
   uint64_t key = 0;
   if (g < G) {
@@ -955,41 +977,83 @@ __device__ __forceinline__ uint32_t split_bound(const uint32_t* hist, uint32_t t
 // stay, and those that sat in [0, P) move into the holes left by prefix keys found in
 // [P, n) (the two counts are equal). seg_sorted[seg] = P. The compositor only has to
 // confirm that no tail key reaches a pixel that is still live (k_render_fwd).
-constexpr uint32_t kHoleCap = 8192;
-__global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__ seg_start,
-                                                    const uint32_t* __restrict__ seg_count, uint32_t stride,
-                                                    uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
-                                                    uint32_t small_cap, uint32_t* __restrict__ groups, int gmax,
-                                                    uint32_t prefix, uint32_t* __restrict__ seg_sorted) {
-  __shared__ uint32_t hist[kSplitNB];
-  __shared__ uint32_t holes[kHoleCap];
-  __shared__ uint32_t red[34];
+constexpr int kSplitNT = 512;
+constexpr int kSplitKPT = 82;         // depth words per thread kept in registers: segments up to 41984
+constexpr uint32_t kStageCap = 5120;  // prefix keys assembled in LDS, then written out contiguously
+constexpr uint32_t kHoleCap = 5120;
+constexpr uint32_t kMinPrefix = 1024;
+constexpr size_t split_lds_bytes() { return (size_t)kStageCap * 8 + (size_t)(kSplitNB + kHoleCap) * 4; }
+
+// One workgroup per long segment (two per CU). The depth words of a segment of up to
+// NTH*KPT keys are read once and held in registers for the min/max, histogram and
+// classification passes; only the keys that move (the sorted prefix, and tail keys sitting
+// inside [0, P)) are read again in full. Longer segments re-read per pass. The prefix is
+// assembled in LDS and written to scratch with contiguous stores. In prefix mode P is the
+// first bucket boundary at or past `prefix`, or, when that exceeds kStageCap, the last one
+// below it (if at least kMinPrefix): a shorter prefix is still exact (the compositor's tail
+// check catches what it misses) and keeps the work bounded.
+template <int NTH, int KPT>
+__global__ __launch_bounds__(NTH) void k_msd_split(const uint32_t* __restrict__ seg_start,
+                                                   const uint32_t* __restrict__ seg_count, uint32_t stride,
+                                                   uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
+                                                   uint32_t small_cap, uint32_t* __restrict__ groups, int gmax,
+                                                   uint32_t prefix, uint32_t* __restrict__ seg_sorted) {
+  constexpr int NW = NTH / 64;
+  constexpr int BPT = kSplitNB / NTH;  // buckets per thread in the scan
+  extern __shared__ __attribute__((aligned(16))) uint64_t s_stage[];  // kStageCap
+  uint32_t* hist = reinterpret_cast<uint32_t*>(s_stage + kStageCap);
+  uint32_t* holes = hist + kSplitNB;
+  __shared__ uint32_t red[2 * NW + 2];
   const int seg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t* gout = groups + (size_t)seg * gmax * 2;
   uint32_t b, e;
   seg_bounds(seg_start, seg_count, stride, seg, b, e);
   const uint32_t n = e - b;
   if (n <= small_cap) {  // sorted by k_sort_lds already
-    for (int g = tid; g < gmax; g += 1024) gout[2 * g] = gout[2 * g + 1] = 0u;
+    for (int g = tid; g < gmax; g += NTH) gout[2 * g] = gout[2 * g + 1] = 0u;
     if (seg_sorted && tid == 0) seg_sorted[seg] = n;
     return;
   }
   const bool pfx = prefix != 0 && n > prefix;
   if (!pfx && (int)((n + kGroupHalf - 1) / kGroupHalf) + 1 > gmax) {  // larger than the launch was sized for
-    for (int g = tid; g < gmax; g += 1024) {
+    for (int g = tid; g < gmax; g += NTH) {
       gout[2 * g] = g == 0 ? b : 0u;
       gout[2 * g + 1] = g == 0 ? (e | kFromKeys) : 0u;
     }
     if (seg_sorted && tid == 0) seg_sorted[seg] = n;
     return;
   }
+  const bool inreg = n <= (uint32_t)(NTH * KPT);  // uniform
+  uint32_t rd[KPT];
+  if (inreg) {
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      const uint32_t i = tid + (uint32_t)q * NTH;
+      rd[q] = i < n ? (uint32_t)(keys[b + i] >> 32) : 0u;
+    }
+  }
+  // BODY sees the depth word d of key index i (valid lanes only)
+#define SPLIT_VISIT(BODY)                                  \
+  if (inreg) {                                             \
+    _Pragma("unroll") for (int q = 0; q < KPT; ++q) {      \
+      const uint32_t i = tid + (uint32_t)q * NTH;          \
+      if (i < n) {                                         \
+        const uint32_t d = rd[q];                          \
+        BODY                                               \
+      }                                                    \
+    }                                                      \
+  } else {                                                 \
+    for (uint32_t i = tid; i < n; i += NTH) {              \
+      const uint32_t d = (uint32_t)(keys[b + i] >> 32);    \
+      BODY                                                 \
+    }                                                      \
+  }
   // segment min / max of the depth word
   uint32_t mn = 0xffffffffu, mx = 0u;
-  for (uint32_t i = tid; i < n; i += 1024) {
-    const uint32_t d = (uint32_t)(keys[b + i] >> 32);
+  SPLIT_VISIT({
     mn = min(mn, d);
     mx = max(mx, d);
-  }
+  })
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
@@ -997,28 +1061,28 @@ __global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__
   }
   if (lane == 0) {
     red[w] = mn;
-    red[16 + w] = mx;
+    red[NW + w] = mx;
   }
-  for (int k = tid; k < kSplitNB; k += 1024) hist[k] = 0u;
-  if (tid == 0) red[32] = red[33] = 0u;
+  for (int k = tid; k < kSplitNB; k += NTH) hist[k] = 0u;
+  if (tid == 0) red[2 * NW] = red[2 * NW + 1] = 0u;
   __syncthreads();
   mn = red[0];
-  mx = red[16];
-  for (int k = 1; k < 16; ++k) {
+  mx = red[NW];
+  for (int k = 1; k < NW; ++k) {
     mn = min(mn, red[k]);
-    mx = max(mx, red[16 + k]);
+    mx = max(mx, red[NW + k]);
   }
   const uint32_t range = mx - mn;
   const int msb = range ? 31 - __clz(range) : 0;
   const int sh = max(0, msb - 11);
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += 1024) atomicAdd(&hist[((uint32_t)(keys[b + i] >> 32) - mn) >> sh], 1u);
+  SPLIT_VISIT({ atomicAdd(&hist[(d - mn) >> sh], 1u); })
   __syncthreads();
-  // exclusive scan: thread t owns buckets [4t, 4t + 4)
-  uint32_t c[4], tot = 0;
+  // exclusive scan: thread t owns buckets [BPT t, BPT t + BPT)
+  uint32_t c[BPT], tot = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    c[k] = hist[4 * tid + k];
+  for (int k = 0; k < BPT; ++k) {
+    c[k] = hist[BPT * tid + k];
     tot += c[k];
   }
   const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
@@ -1027,8 +1091,8 @@ __global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__
   uint32_t off = incl - tot;
   for (int k = 0; k < w; ++k) off += red[k];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    hist[4 * tid + k] = off;
+  for (int k = 0; k < BPT; ++k) {
+    hist[BPT * tid + k] = off;
     off += c[k];
   }
   __syncthreads();
@@ -1044,14 +1108,18 @@ __global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__
     }
     kc = lo;
     P = lo < kSplitNB ? hist[lo] : n;
+    if (P > kStageCap && kc > 0 && hist[kc - 1] >= kMinPrefix) {  // shorter prefix, one bucket less
+      --kc;
+      P = hist[kc];
+    }
     if (min(P, n - P) > kHoleCap) {  // pathological depth clustering: sort all of it
       P = n;
       kc = kSplitNB;
     }
-    // groups [B_g, B_g+1) for g < prefix / kGroupHalf cover [0, P) whatever P - prefix is;
+    // groups [B_g, B_g+1) for g < prefix / kGroupHalf cover [0, P) whenever P <= bound(prefix);
     // only a full sort of a segment this long can need more than the launch has
     if (P == n && (int)((n + kGroupHalf - 1) / kGroupHalf) + 1 > gmax) {  // uniform across the workgroup
-      for (int g = tid; g < gmax; g += 1024) {
+      for (int g = tid; g < gmax; g += NTH) {
         gout[2 * g] = g == 0 ? b : 0u;
         gout[2 * g + 1] = g == 0 ? (e | kFromKeys) : 0u;
       }
@@ -1061,29 +1129,33 @@ __global__ __launch_bounds__(1024) void k_msd_split(const uint32_t* __restrict__
   }
   if (seg_sorted && tid == 0) seg_sorted[seg] = P;
   // group g = [B_g, B_{g+1}) clipped to [0, P), B_g = first bucket offset >= g * kGroupHalf
-  if (tid < gmax) {
-    const uint32_t g0 = min(split_bound(hist, (uint32_t)tid * kGroupHalf, n), P);
-    const uint32_t g1 = min(split_bound(hist, (uint32_t)(tid + 1) * kGroupHalf, n), P);
-    gout[2 * tid] = b + g0;
-    gout[2 * tid + 1] = b + g1;
+  for (int g = tid; g < gmax; g += NTH) {
+    const uint32_t g0 = min(split_bound(hist, (uint32_t)g * kGroupHalf, n), P);
+    const uint32_t g1 = min(split_bound(hist, (uint32_t)(g + 1) * kGroupHalf, n), P);
+    gout[2 * g] = b + g0;
+    gout[2 * g + 1] = b + g1;
   }
+  const bool stage = P <= kStageCap;
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += 1024) {
-    const uint64_t k = keys[b + i];
-    const int bk = (int)(((uint32_t)(k >> 32) - mn) >> sh);
+  SPLIT_VISIT({
+    const int bk = (int)((d - mn) >> sh);
     if (bk < kc) {
-      const uint32_t pos = atomicAdd(&hist[bk], 1u);
-      scratch[b + pos] = k;
-      if (i >= P) holes[atomicAdd(&red[32], 1u)] = i;
-    }
-  }
-  if (P < n) {
-    __syncthreads();
-    for (uint32_t i = tid; i < P; i += 1024) {
       const uint64_t k = keys[b + i];
-      if ((int)(((uint32_t)(k >> 32) - mn) >> sh) >= kc) keys[b + holes[atomicAdd(&red[33], 1u)]] = k;
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      if (stage) s_stage[pos] = k;
+      else scratch[b + pos] = k;
+      if (i >= P) holes[atomicAdd(&red[2 * NW], 1u)] = i;
     }
+  })
+  __syncthreads();
+  if (stage)
+    for (uint32_t i = tid; i < P; i += NTH) scratch[b + i] = s_stage[i];
+  if (P < n) {
+    SPLIT_VISIT({
+      if (i < P && (int)((d - mn) >> sh) >= kc) keys[b + holes[atomicAdd(&red[2 * NW + 1], 1u)]] = keys[b + i];
+    })
   }
+#undef SPLIT_VISIT
 }
 
 // Sort every group produced by k_msd_split into `keys` (from scratch, or from keys when the
@@ -1957,10 +2029,10 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H), T = gx * gy;
   if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
   const int lds = lds_hist_bytes(T);
-  dim3 grid((G + NT - 1) / NT, V);
+  const unsigned grid = xcd_grid((G + NT - 1) / NT, V);
   const int deg = shs ? sh_degree : -1;
-#define DSR_PRE(D)                                                                                     \
-  k_preprocess<D><<<grid, NT, lds, st>>>(G, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, \
+#define DSR_PRE(D)                                                                                        \
+  k_preprocess<D><<<grid, NT, lds, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, \
                                          geom, radii, seg_count, lds > 0, layout)
   switch (deg) {
     case -1: DSR_PRE(-1); break;
@@ -1986,7 +2058,7 @@ int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M, con
   DSPLAT_REQUIRE((uint64_t)V * T * G < (1ull << 32), "dsr_project_bin: V*tiles*G must fit 32-bit key offsets");
   hipStream_t st = (hipStream_t)stream;
   if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
-  dim3 grid((G + NT - 1) / NT, V);
+  const unsigned grid = xcd_grid((G + NT - 1) / NT, V);
   const int deg = shs ? sh_degree : -1;
 #define DSR_PB(D)                                                                                             \
   k_project_emit<D><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, \
@@ -2017,8 +2089,8 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
   DSPLAT_REQUIRE(geom && seg_cursor, "dsr_bin_scatter: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   const int lds = lds_hist_bytes(gx * gy);
-  dim3 grid((G + NT - 1) / NT, V);
-  k_scatter<<<grid, NT, lds, (hipStream_t)stream>>>(G, gx, gy, geom, seg_cursor, keys, lds > 0);
+  k_scatter<<<xcd_grid((G + NT - 1) / NT, V), NT, lds, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor, keys,
+                                                                              lds > 0);
   return dsplat::check_launch("k_scatter");
 }
 
@@ -2062,6 +2134,11 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
                                                       (int)sort_lds_bytes<16>()),
                                   "hipFuncSetAttribute(k_sort_lds)"))
       return e;
+    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_msd_split<kSplitNT, kSplitKPT>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      (int)split_lds_bytes()),
+                                  "hipFuncSetAttribute(k_msd_split)"))
+      return e;
     attr_set = true;
   }
   uint32_t cap;
@@ -2096,8 +2173,8 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
       else pfx = 0;
     }
     uint32_t* groups = static_cast<uint32_t*>(workspace);
-    k_msd_split<<<nseg, 1024, 0, st>>>(seg_start, seg_count, seg_stride, keys, scratch, cap, groups, gmax, pfx,
-                                       seg_sorted);
+    k_msd_split<kSplitNT, kSplitKPT><<<nseg, kSplitNT, split_lds_bytes(), st>>>(
+        seg_start, seg_count, seg_stride, keys, scratch, cap, groups, gmax, pfx, seg_sorted);
     if (int e = dsplat::check_launch("k_msd_split")) return e;
     k_sort_groups<16><<<(unsigned)(nseg * gmax), NT, sort_lds_bytes<16>(), st>>>(groups, keys, scratch, id_bits);
     if (int e = dsplat::check_launch("k_sort_groups")) return e;

@@ -186,7 +186,7 @@ def _check_segments_vs_oracle(state, orcs, V, T):
                 np.testing.assert_array_equal(hk, ovals[ob:oe])
                 continue
             P = int(srt[s])
-            assert min(oe - ob, 4096) <= P <= oe - ob
+            assert min(oe - ob, 1024) <= P <= oe - ob
             np.testing.assert_array_equal(hk[:P], ovals[ob:ob + P])
             np.testing.assert_array_equal(np.sort(hk[P:]), np.sort(ovals[ob + P:oe]))
 

@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="render_fwd")
     ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--views", type=int, default=3)
     ap.add_argument("--context", type=int, default=2)
     ap.add_argument("--iters", type=int, default=200)
@@ -31,7 +33,7 @@ def main():
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    H = W = a.size
+    H, W = a.height or a.size, a.width or a.size
     sc = make_scene(batch=1, n_context=a.context, n_targets=a.views, height=H, width=W, seed=1000, device=dev)
     g = sc.gaussians
     V = a.views
@@ -84,6 +86,15 @@ def main():
                     return rc
                 return lib.dsr_bin_sort(G, V, H, W, None, cnt2.data_ptr(), a.stride or G, keys2.data_ptr(),
                                         scratch2.data_ptr(), state.max_count, ws_p, 0, None, None, st)
+        elif a.kernel == "scatter":  # two-phase key scatter from the scan's segment starts
+            assert stride == 0, "two-phase layout expected (--two-phase)"
+            cur = torch.empty_like(state.seg_start)
+            keys3 = torch.empty_like(state.keys)
+            out = [state.seg_count]
+
+            def launch():
+                cur.copy_(state.seg_start)
+                return lib.dsr_bin_scatter(G, V, H, W, state.geom.data_ptr(), cur.data_ptr(), keys3.data_ptr(), st)
         elif a.kernel == "sort_sorted":  # re-sort the (already sorted) keys in place: pass cost only
             tot3 = torch.empty(4, dtype=torch.int32, device=dev)
             scr = torch.empty_like(state.keys)
