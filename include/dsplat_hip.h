@@ -65,7 +65,11 @@ typedef struct dsr_camera {
  * Computed in double per view (torch does it in float32: agreement ~1e-7 relative). */
 int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, const float* near,
                       const float* far, const float* bg, const int32_t* view_scene,
-                      int scale_invariant, dsr_camera* cams, void* stream);
+                      int scale_invariant, dsr_camera* cams, uint32_t* zero_counts,
+                      uint32_t n_zero, void* stream);
+/* zero_counts / n_zero (optional): also zero n_zero words there — the seg_count array of the
+ * dsr_project_bin / dsr_preprocess_fwd call that follows, which then gets
+ * DSR_LAYOUT_COUNTS_ZEROED and skips its own zeroing launch. */
 
 /* ---- rasterizer forward ------------------------------------------------------------
  * Replaces preprocessCUDA + tiles_touched (upstream K1). Per view v and gaussian g of
@@ -77,6 +81,7 @@ int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, c
  *   out: geom [V,G,12], radii [V,G] int32, seg_count [V*T] (zeroed by this call).  */
 #define DSR_LAYOUT_SH_CHANNEL_MAJOR 1  /* shs given as [S,G,3,M] (Gaussians.harmonics)      */
 #define DSR_LAYOUT_COV_FULL 2          /* covariance given as [S,G,3,3]; grads: upper triangle */
+#define DSR_LAYOUT_COUNTS_ZEROED 4     /* seg_count already zeroed (dsr_build_cameras)       */
 int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,

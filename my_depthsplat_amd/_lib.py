@@ -19,7 +19,7 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / "libdsplat_hip.so"
 _P = c_void_p
 _I = c_int
 SIGNATURES: dict[str, tuple] = {
-    "dsr_build_cameras": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),
+    "dsr_build_cameras": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _P, _P, c_uint32, _P]),
     "dsr_preprocess_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dsr_bin_scan": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
     "dsr_bin_scatter": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),

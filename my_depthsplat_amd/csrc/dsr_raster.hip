@@ -24,6 +24,10 @@ constexpr int BX = DSR_TILE, BY = DSR_TILE;
 constexpr int NT = BX * BY;  // 256 threads = 4 waves per tile
 constexpr int GS = DSR_GEOM_STRIDE;
 constexpr uint32_t kSortCap = 8192;           // max keys sorted in LDS (2 x 64 KiB)
+#ifndef SORT_NTH
+#define SORT_NTH 256
+#endif
+constexpr int kSortNT = SORT_NTH;  // threads per segment in the LDS sort
 constexpr int kHistLdsMax = 32768;            // tiles per view histogrammed in LDS
 
 constexpr float SH_C0 = 0.28209479177387814f;
@@ -195,7 +199,7 @@ __device__ __forceinline__ float sh_eval(const float* sh, int ch, float x, float
 // decoder's Gaussians.harmonics) instead of the rasterizer's coefficient-major [S,G,M,3];
 // bit 1: full covariance [S,G,3,3] instead of cov6 — the upper triangle is read, exactly
 // what cuda_splatting.py:114,122's triu gather hands the rasterizer.
-constexpr int kLayoutShChannelMajor = 1, kLayoutCovFull = 2;
+constexpr int kLayoutShChannelMajor = 1, kLayoutCovFull = 2, kLayoutCountsZeroed = 4;
 __device__ __forceinline__ float load_cov(const float* cov, size_t sg, int k, int layout) {
   if (layout & kLayoutCovFull) {
     constexpr int idx[6] = {0, 1, 2, 4, 5, 8};
@@ -449,9 +453,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
 #endif
     }
     __syncthreads();
+#ifdef PB_STRIDE  // layout experiment: segment stride PB_STRIDE instead of G (no overflow check)
+    uint64_t* vkeys = keys + (size_t)v * T * PB_STRIDE;
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
+                       [&](int t, int o) { vkeys[(size_t)t * PB_STRIDE + atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
+#else
     uint64_t* vkeys = keys + (size_t)v * T * G;
     for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
                        [&](int t, int o) { vkeys[(size_t)t * G + atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
+#endif
   }
 }
 
@@ -695,7 +705,7 @@ __device__ __forceinline__ uint32_t key_digit(uint64_t k, int word_shift, uint32
   return (((uint32_t)(k >> word_shift) - dbase) >> shift) & 15u;
 }
 
-template <int KMAX>
+template <int KMAX, int NTH = NT>
 __device__ bool reg_pass(uint64_t* buf, uint32_t n, int word_shift, uint32_t dbase, int shift, uint16_t* cnt,
                          uint32_t* wsum) {
   // in place: every key of the pass is in registers before the first barrier, so the
@@ -728,7 +738,7 @@ __device__ bool reg_pass(uint64_t* buf, uint32_t n, int word_shift, uint32_t dba
   }
   const uint32_t d0 = key_digit<KMAX>(buf[0], word_shift, dbase, shift);  // digit of key 0 (broadcast read)
 #pragma unroll
-  for (int d = 0; d < 16; ++d) cnt[d * NT + tid] = (uint16_t)(((d < 8 ? c_lo : c_hi) >> (8 * (d & 7))) & 255u);
+  for (int d = 0; d < 16; ++d) cnt[d * NTH + tid] = (uint16_t)(((d < 8 ? c_lo : c_hi) >> (8 * (d & 7))) & 255u);
   __syncthreads();
   // exclusive scan of the 4096 counters in (digit, thread) order; thread t owns [16t, 16t+16)
   uint32_t v[16];
@@ -764,15 +774,15 @@ __device__ bool reg_pass(uint64_t* buf, uint32_t n, int word_shift, uint32_t dba
   }
   __syncthreads();
   // a digit holding every key makes the pass the identity (same decision in every thread)
-  const uint32_t s0 = cnt[d0 * NT];
-  const uint32_t s1 = d0 < 15 ? (uint32_t)cnt[(d0 + 1) * NT] : n;
+  const uint32_t s0 = cnt[d0 * NTH];
+  const uint32_t s1 = d0 < 15 ? (uint32_t)cnt[(d0 + 1) * NTH] : n;
   if (s1 - s0 == n) return false;  // nothing written; the next pass re-reads buf
 #pragma unroll
   for (int i = 0; i < KMAX; ++i)
     if (base + i < n) {
       const uint32_t d = key_digit<KMAX>(k[i], word_shift, dbase, shift);
       const uint32_t loc = (locp[i / 4] >> (8 * (i % 4))) & 255u;
-      buf[padi<KMAX>((uint32_t)cnt[d * NT + tid] + loc)] = k[i];
+      buf[padi<KMAX>((uint32_t)cnt[d * NTH + tid] + loc)] = k[i];
     }
   __syncthreads();
   return true;
@@ -785,11 +795,11 @@ __device__ bool reg_pass(uint64_t* buf, uint32_t n, int word_shift, uint32_t dba
 // range are common to every key and bits below the window only order keys inside a run, so
 // this is the full (depth, id) order. Runs longer than 32 (depths packed far tighter than the
 // segment's range) fall back to full-width passes: ids, then all 32 depth bits (stable).
-template <int KMAX>
+template <int KMAX, int NTH = NT>
 __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, uint32_t* wsum, uint32_t* flag) {
   const int tid = threadIdx.x;
   uint32_t mn = 0xffffffffu, mx = 0u;
-  for (uint32_t i = tid; i < n; i += NT) {
+  for (uint32_t i = tid; i < n; i += NTH) {
     const uint32_t d = (uint32_t)(A[padi<KMAX>(i)] >> 32);
     mn = min(mn, d);
     mx = max(mx, d);
@@ -801,13 +811,19 @@ __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, ui
     mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
   }
+  constexpr int NW = NTH / 64;
   if (lane == 0) {
     flag[w] = mn;
-    flag[4 + w] = mx;
+    flag[NW + w] = mx;
   }
   __syncthreads();
-  mn = min(min(flag[0], flag[1]), min(flag[2], flag[3]));
-  mx = max(max(flag[4], flag[5]), max(flag[6], flag[7]));
+  mn = flag[0];
+  mx = flag[NW];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) {
+    mn = min(mn, flag[k]);
+    mx = max(mx, flag[NW + k]);
+  }
   __syncthreads();
   const uint32_t range = mx - mn;
   const int msb = range ? 31 - __clz(range) : -1;
@@ -815,7 +831,7 @@ __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, ui
 #ifdef SORT_DIAG_NOPASS
   if (n > 100000)
 #endif
-  for (int sh = lo_shift; sh <= msb; sh += 4) reg_pass<KMAX>(A, n, 32, mn, sh, cnt, wsum);
+  for (int sh = lo_shift; sh <= msb; sh += 4) reg_pass<KMAX, NTH>(A, n, 32, mn, sh, cnt, wsum);
 #ifdef SORT_DIAG_NOFIX
   if (n < 100000) return;
 #endif
@@ -869,12 +885,14 @@ __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, ui
   for (int off = 32; off > 0; off >>= 1) longest = max(longest, (uint32_t)__shfl_xor((int)longest, off, 64));
   if (lane == 0) flag[w] = longest;
   __syncthreads();
-  longest = max(max(flag[0], flag[1]), max(flag[2], flag[3]));
+  longest = flag[0];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) longest = max(longest, flag[k]);
   __syncthreads();
   if (longest <= 32) return;
   {
-    for (int sh = 0; sh < id_bits; sh += 4) reg_pass<KMAX>(A, n, 0, 0u, sh, cnt, wsum);
-    for (int sh = 0; sh < 32; sh += 4) reg_pass<KMAX>(A, n, 32, 0u, sh, cnt, wsum);
+    for (int sh = 0; sh < id_bits; sh += 4) reg_pass<KMAX, NTH>(A, n, 0, 0u, sh, cnt, wsum);
+    for (int sh = 0; sh < 32; sh += 4) reg_pass<KMAX, NTH>(A, n, 32, 0u, sh, cnt, wsum);
   }
 #undef pref
 }
@@ -885,19 +903,19 @@ __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, ui
 #ifndef SORT_WPE
 #define SORT_WPE 3
 #endif
-template <int KMAX>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(KMAX >= 32 ? 1 : SORT_WPE))) void k_sort_lds(const uint32_t* __restrict__ seg_start,
+template <int KMAX, int NTH = NT>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(KMAX * NTH >= 8192 ? 1 : SORT_WPE))) void k_sort_lds(const uint32_t* __restrict__ seg_start,
                                                  const uint32_t* __restrict__ seg_count, uint32_t stride,
                                                  uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
                                                  int id_bits, int big_here, const uint32_t* __restrict__ filter,
                                                  uint32_t* __restrict__ seg_sorted) {
-  constexpr uint32_t cap = NT * KMAX;
+  constexpr uint32_t cap = NTH * KMAX;
   constexpr uint32_t padded = cap + cap / KMAX;
   extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
   uint64_t* A = s_keys;
   uint32_t* aux = reinterpret_cast<uint32_t*>(A + padded);  // 8 KiB counters (u16) / HBM-path histogram
   uint16_t* cnt = reinterpret_cast<uint16_t*>(aux);
-  uint32_t* wsum = aux + 2048;
+  uint32_t* wsum = aux + NTH * 8;
   uint32_t* flag = wsum + 16;
   const int seg = blockIdx.x;
   if (filter && !filter[seg]) return;
@@ -907,7 +925,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(KMAX >= 32 ?
   if (seg_sorted && threadIdx.x == 0 && (n <= cap || big_here)) seg_sorted[seg] = n;
   if (n <= 1) return;
   if (n > cap) {
-    if (big_here) sort_segment<NT>(keys + b, scratch + b, n, id_bits, aux, wsum, flag, keys + b);
+    if (big_here) sort_segment<NTH>(keys + b, scratch + b, n, id_bits, aux, wsum, flag, keys + b);
     return;
   }
   // all KMAX global loads of a thread in flight at once (coalesced across the workgroup)
@@ -915,29 +933,29 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(KMAX >= 32 ?
     uint64_t tmp[KMAX];
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
-      const uint32_t idx = threadIdx.x + (uint32_t)i * NT;
+      const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
       tmp[i] = idx < n ? keys[b + idx] : 0ull;
     }
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
-      const uint32_t idx = threadIdx.x + (uint32_t)i * NT;
+      const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
       if (idx < n) A[padi<KMAX>(idx)] = tmp[i];
     }
   }
   __syncthreads();
 #ifndef SORT_DIAG_NOSORT
-  reg_sort<KMAX>(A, n, id_bits, cnt, wsum, flag);
+  reg_sort<KMAX, NTH>(A, n, id_bits, cnt, wsum, flag);
 #endif
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
-    const uint32_t idx = threadIdx.x + (uint32_t)i * NT;
+    const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
     if (idx < n) keys[b + idx] = A[padi<KMAX>(idx)];
   }
 }
 
-template <int KMAX>
+template <int KMAX, int NTH = NT>
 constexpr size_t sort_lds_bytes() {
-  return (size_t)(NT * KMAX + NT) * 8 + 8192 + 64 * 4;
+  return (size_t)(NTH * KMAX + NTH) * 8 + (size_t)NTH * 32 + 64 * 4;
 }
 
 // ---- segments larger than the LDS sort (6-view 448x768 and up: ~30-40K entries per tile) --
@@ -1441,7 +1459,32 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
     const uint32_t e1 = e + CH;
     nid[u] = e1 < end ? (uint32_t)keys[e1] : 0xffffffffu;
   }
+#ifdef RF_PD2  // records two chunks ahead (c1), keys three ahead
+  float4 c1q[EPL], c1r[EPL];
+  float c1b[EPL];
+#pragma unroll
+  for (int u = 0; u < EPL; ++u) {
+    c1q[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    c1r[u] = c1q[u];
+    c1b[u] = 0.f;
+    if (nid[u] != 0xffffffffu) {
+      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)nid[u] * GS);
+      c1q[u] = rec[0];
+      c1r[u] = rec[1];
+      c1b[u] = rec[2].x;
+    }
+    const uint32_t e2 = start + 2 * CH + u * 64 + lane;
+    nid[u] = e2 < end ? (uint32_t)keys[e2] : 0xffffffffu;
+  }
+#endif
+#ifdef RF_DIAG_WAVESTATS
+  const uint64_t t_begin = wall_clock64();
+  uint32_t d_chunks = 0, d_comp = 0;
+#endif
   for (uint32_t base = start; base < end && !__all(Tr < 0.0f); base += CH) {
+#ifdef RF_DIAG_WAVESTATS
+    ++d_chunks;
+#endif
     float4 nq[EPL], nr[EPL];
     float nb[EPL];
 #pragma unroll
@@ -1455,7 +1498,11 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
         nr[u] = rec[1];
         nb[u] = rec[2].x;
       }
+#ifdef RF_PD2
+      const uint32_t e2 = base + 3 * CH + u * 64 + lane;
+#else
       const uint32_t e2 = base + 2 * CH + u * 64 + lane;
+#endif
       nid[u] = e2 < end ? (uint32_t)keys[e2] : 0xffffffffu;
     }
     int cnt = 0;
@@ -1473,6 +1520,9 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
     }
     if (lane < 8)  // pad up to 8 entries: opacity 0 -> alpha 0 -> never blends
       pair_put(plist, cnt + lane, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u);
+#ifdef RF_DIAG_WAVESTATS
+    d_comp += cnt;
+#endif
     __builtin_amdgcn_wave_barrier();
     {
       const PairRec* pp = plist;
@@ -1490,9 +1540,18 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
     __builtin_amdgcn_wave_barrier();  // list reads of this chunk before the next chunk's writes
 #pragma unroll
     for (int u = 0; u < EPL; ++u) {
+#ifdef RF_PD2
+      cq[u] = c1q[u];
+      cr[u] = c1r[u];
+      cb[u] = c1b[u];
+      c1q[u] = nq[u];
+      c1r[u] = nr[u];
+      c1b[u] = nb[u];
+#else
       cq[u] = nq[u];
       cr[u] = nr[u];
       cb[u] = nb[u];
+#endif
     }
   }
   if (end < tail_end && tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pfx2, pfy2, Tr, plist, lt, lane) &&
@@ -1507,6 +1566,11 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
     const float Tf = fabsf(Tr);
     finalT[v * HW + pix] = Tf;
     ncontrib[v * HW + pix] = last;
+#ifdef RF_DIAG_WAVESTATS  // timing experiment: lanes 0-2 report (ticks, chunks, composited entries)
+    if (lane == 0) ncontrib[v * HW + pix] = (uint32_t)(wall_clock64() - t_begin);
+    if (lane == 1) ncontrib[v * HW + pix] = d_chunks;
+    if (lane == 2) ncontrib[v * HW + pix] = d_comp;
+#endif
     out[(size_t)v * 3 * HW + pix] = C0 + Tf * bg[0];
     out[(size_t)v * 3 * HW + HW + pix] = C1 + Tf * bg[1];
     out[(size_t)v * 3 * HW + 2 * HW + pix] = C2 + Tf * bg[2];
@@ -2027,7 +2091,8 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   DSPLAT_REQUIRE(means && opacities && cov6 && cams && geom && radii && seg_count, "dsr_preprocess_fwd: null pointer");
   hipStream_t st = (hipStream_t)stream;
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H), T = gx * gy;
-  if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
+  if (!(layout & kLayoutCountsZeroed))
+    if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
   const int lds = lds_hist_bytes(T);
   const unsigned grid = xcd_grid((G + NT - 1) / NT, V);
   const int deg = shs ? sh_degree : -1;
@@ -2057,7 +2122,8 @@ int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M, con
   DSPLAT_REQUIRE(T <= kHistLdsMax, "dsr_project_bin: %d tiles per view exceed the LDS histogram (%d)", T, kHistLdsMax);
   DSPLAT_REQUIRE((uint64_t)V * T * G < (1ull << 32), "dsr_project_bin: V*tiles*G must fit 32-bit key offsets");
   hipStream_t st = (hipStream_t)stream;
-  if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
+  if (!(layout & kLayoutCountsZeroed))
+    if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
   const unsigned grid = xcd_grid((G + NT - 1) / NT, V);
   const int deg = shs ? sh_degree : -1;
 #define DSR_PB(D)                                                                                             \
@@ -2100,6 +2166,24 @@ size_t dsr_bin_sort_workspace_size(int V, int H, int W, uint32_t max_count) {
   return nseg * (size_t)split_groups(max_count) * 2 * sizeof(uint32_t);
 }
 
+}  // extern "C"
+namespace {
+// dynamic LDS above 64 KiB must be opted into, once per kernel instantiation
+template <int KM, int NTH_>
+int sort_lds_attr() {
+  static bool done = false;
+  if (done || sort_lds_bytes<KM, NTH_>() <= 65536) return 0;
+  if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds<KM, NTH_>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    (int)sort_lds_bytes<KM, NTH_>()),
+                                "hipFuncSetAttribute(k_sort_lds)"))
+    return e;
+  done = true;
+  return 0;
+}
+}  // namespace
+extern "C" {
+
 int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const uint32_t* seg_count,
                  uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count, void* workspace,
                  uint32_t prefix, uint32_t* seg_sorted, const uint32_t* seg_filter, void* stream) {
@@ -2134,6 +2218,11 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
                                                       (int)sort_lds_bytes<16>()),
                                   "hipFuncSetAttribute(k_sort_lds)"))
       return e;
+    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds<kSortCap / kSortNT, kSortNT>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      (int)sort_lds_bytes<kSortCap / kSortNT, kSortNT>()),
+                                  "hipFuncSetAttribute(k_sort_lds)"))
+      return e;
     if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_msd_split<kSplitNT, kSplitKPT>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                                       (int)split_lds_bytes()),
@@ -2142,27 +2231,26 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
     attr_set = true;
   }
   uint32_t cap;
+#define DSR_SORT_LDS(KM, NTH_, FILT)                                                                        \
+  do {                                                                                                      \
+    if (int e = sort_lds_attr<KM, NTH_>()) return e;                                                        \
+    cap = (uint32_t)(KM) * (NTH_);                                                                          \
+    k_sort_lds<KM, NTH_><<<nseg, NTH_, sort_lds_bytes<KM, NTH_>(), st>>>(seg_start, seg_count, seg_stride,   \
+                                                                          keys, scratch, id_bits, big_here, \
+                                                                          FILT, seg_sorted);                \
+  } while (0)
   if (big_known || seg_filter) {  // small segments in LDS now, the rest split below (or through HBM)
-    cap = 256 * 16;
-    k_sort_lds<16><<<nseg, NT, sort_lds_bytes<16>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, big_here, seg_filter, seg_sorted);
-  } else if (want <= 256 * 4) {
-    cap = 256 * 4;
-    k_sort_lds<4><<<nseg, NT, sort_lds_bytes<4>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, big_here, nullptr, seg_sorted);
-  } else if (want <= 256 * 8) {
-    cap = 256 * 8;
-    k_sort_lds<8><<<nseg, NT, sort_lds_bytes<8>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, big_here, nullptr, seg_sorted);
-  } else if (want <= 256 * 16) {
-    cap = 256 * 16;
-    k_sort_lds<16><<<nseg, NT, sort_lds_bytes<16>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, big_here, nullptr, seg_sorted);
+    DSR_SORT_LDS(16, NT, seg_filter);
+  } else if (want <= kSortNT * 4) {
+    DSR_SORT_LDS(4, kSortNT, nullptr);
+  } else if (want <= kSortNT * 8) {
+    DSR_SORT_LDS(8, kSortNT, nullptr);
+  } else if (want <= kSortNT * 16 && kSortNT * 16 < kSortCap) {
+    DSR_SORT_LDS(16, kSortNT, nullptr);
   } else {
-    cap = 256 * 32;
-    k_sort_lds<32><<<nseg, NT, sort_lds_bytes<32>(), st>>>(seg_start, seg_count, seg_stride, keys, scratch,
-                                                                id_bits, big_here, nullptr, seg_sorted);
+    DSR_SORT_LDS(kSortCap / kSortNT, kSortNT, nullptr);
   }
+#undef DSR_SORT_LDS
   if (int e = dsplat::check_launch("k_sort_lds")) return e;
   if (big_known) {
     uint32_t pfx = 0;
@@ -2301,8 +2389,11 @@ __device__ double edge_angle(const double* ki, double x0, double y0, double x1, 
 __global__ void k_cameras(int V, const float* __restrict__ ext, const float* __restrict__ intr,
                           const float* __restrict__ near, const float* __restrict__ far,
                           const float* __restrict__ bg, const int32_t* __restrict__ view_scene,
-                          int scale_invariant, dsr_camera* __restrict__ cams) {
+                          int scale_invariant, dsr_camera* __restrict__ cams, uint32_t* __restrict__ zero,
+                          uint32_t n_zero) {
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  // the next kernels' per-(view, tile) counters, zeroed here to save them a launch
+  for (uint32_t i = (uint32_t)v; i < n_zero; i += gridDim.x * blockDim.x) zero[i] = 0u;
   if (v >= V) return;
   double E[16], K[9], Ki[9], Wc[16];
   for (int i = 0; i < 16; ++i) E[i] = ext[16 * v + i];
@@ -2357,10 +2448,13 @@ __global__ void k_cameras(int V, const float* __restrict__ ext, const float* __r
 
 extern "C" int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, const float* near,
                                  const float* far, const float* bg, const int32_t* view_scene,
-                                 int scale_invariant, dsr_camera* cams, void* stream) {
+                                 int scale_invariant, dsr_camera* cams, uint32_t* zero_counts,
+                                 uint32_t n_zero, void* stream) {
   DSPLAT_REQUIRE(V > 0, "dsr_build_cameras: V=%d", V);
   DSPLAT_REQUIRE(extrinsics && intrinsics && near && far && bg && view_scene && cams, "dsr_build_cameras: null pointer");
-  k_cameras<<<(V + 63) / 64, 64, 0, (hipStream_t)stream>>>(V, extrinsics, intrinsics, near, far, bg, view_scene,
-                                                         scale_invariant, cams);
+  DSPLAT_REQUIRE(n_zero == 0 || zero_counts != nullptr, "dsr_build_cameras: n_zero without zero_counts");
+  const unsigned blocks = (unsigned)max((V + 255) / 256, min((int)((n_zero + 255) / 256), 64));
+  k_cameras<<<blocks, 256, 0, (hipStream_t)stream>>>(V, extrinsics, intrinsics, near, far, bg, view_scene,
+                                                     scale_invariant, cams, zero_counts, n_zero);
   return dsplat::check_launch("k_cameras");
 }

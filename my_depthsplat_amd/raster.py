@@ -225,8 +225,10 @@ def _dense_bg(bg: torch.Tensor) -> torch.Tensor:
     return t
 
 
-def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True) -> torch.Tensor:
-    """Device-side camera set-up (dsr_build_cameras) -> [V, 44] float32 dsr_camera array."""
+def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True,
+                  zero_counts: torch.Tensor | None = None) -> torch.Tensor:
+    """Device-side camera set-up (dsr_build_cameras) -> [V, 44] float32 dsr_camera array.
+    zero_counts (int32, optional) is zeroed by the same launch (see rasterize_views)."""
     lib = _lib.load()
     V = extrinsics.shape[0]
     dev = extrinsics.device
@@ -239,12 +241,14 @@ def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invar
     b = _dense_bg(bg)
     _lib.check(lib.dsr_build_cameras(V, ext.data_ptr(), K.data_ptr(), n.data_ptr(), fa.data_ptr(), b.data_ptr(),
                                      vs.data_ptr(), int(bool(scale_invariant)), cams.data_ptr(),
+                                     _ptr(zero_counts), 0 if zero_counts is None else zero_counts.numel(),
                                      _lib.stream_of(dev)), "dsr_build_cameras")
     return cams
 
 
 LAYOUT_SH_CHANNEL_MAJOR = 1  # feats [S,G,3,M] (Gaussians.harmonics) instead of [S,G,M,3]
 LAYOUT_COV_FULL = 2          # covariance [S,G,3,3] instead of cov6 [S,G,6]
+LAYOUT_COUNTS_ZEROED = 4     # seg_count handed in already zeroed
 
 
 def input_layout(feats, cov6, use_sh, channel_major_sh):
@@ -254,7 +258,7 @@ def input_layout(feats, cov6, use_sh, channel_major_sh):
     return lay
 
 
-def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0):
+def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0, zeroed_counts=None):
     """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh; [S,G,3,M] with
     LAYOUT_SH_CHANNEL_MAJOR) or [S,G,3]; opacities [S,G]; cov6 [S,G,6] (or [S,G,3,3] with
     LAYOUT_COV_FULL); cams [V,44]. Returns (color [V,3,H,W], RasterState).
@@ -276,7 +280,12 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     col_p = None if use_sh else feats.data_ptr()
     geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
     radii = torch.empty((V, G), dtype=torch.int32, device=dev)
-    seg_count = torch.empty(V * T, dtype=torch.int32, device=dev)
+    if zeroed_counts is not None:  # zeroed by dsr_build_cameras (one launch fewer)
+        assert zeroed_counts.numel() == V * T and zeroed_counts.dtype == torch.int32
+        seg_count = zeroed_counts
+        layout |= LAYOUT_COUNTS_ZEROED
+    else:
+        seg_count = torch.empty(V * T, dtype=torch.int32, device=dev)
     lds_cap = lib.dsr_sort_lds_capacity()
     cap = _key_capacity(V, G, T)
     if cap is not None and T <= 32768 and V * T * G < (1 << 32):
@@ -397,9 +406,11 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
 
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, means, feats, opacities, cov6, means2d, cams, view_scene, use_sh, sh_degree, H, W, layout):
+    def forward(ctx, means, feats, opacities, cov6, means2d, cams, view_scene, use_sh, sh_degree, H, W, layout,
+                zeroed_counts):
         V = len(view_scene)
-        color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout)
+        color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout,
+                                   zeroed_counts)
         ctx.save_for_backward(means, feats, opacities, cov6, cams)
         ctx.state = state
         ctx.meta = (view_scene, use_sh, sh_degree, None if means2d is None else means2d.shape, layout)
@@ -416,18 +427,19 @@ class _RasterizeViews(torch.autograd.Function):
             want_mean2d=want_m2d, layout=layout)
         if dmean2d is not None:
             dmean2d = dmean2d.view(m2d_shape)
-        return dmeans, dfeat, dopac, dcov6, dmean2d, None, None, None, None, None, None, None
+        return dmeans, dfeat, dopac, dcov6, dmean2d, None, None, None, None, None, None, None, None
 
 
 def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.Tensor, cov6: torch.Tensor,
                     cams: torch.Tensor, view_scene: list[int], *, use_sh: bool, sh_degree: int,
                     image_height: int, image_width: int, means2d: torch.Tensor | None = None,
-                    channel_major_sh: bool = False):
+                    channel_major_sh: bool = False, zeroed_counts: torch.Tensor | None = None):
     """Differentiable render of V views. means [S,G,3]; feats [S,G,M,3] (SH, coefficient-major
     like the rasterizer's `shs`; [S,G,3,M] = Gaussians.harmonics with channel_major_sh) or
     [S,G,3] (colors_precomp); opacities [S,G]; cov6 [S,G,6] or the full [S,G,3,3] matrices
     (read through the reference's triu gather); cams [V,44] (pack_cameras / build_cameras);
-    view_scene[v] = scene index of view v. Returns color [V,3,H,W] and radii [V,G] (int32)."""
+    view_scene[v] = scene index of view v. zeroed_counts: optional [V*tiles] int32 buffer already
+    zeroed (build_cameras(zero_counts=...)). Returns color [V,3,H,W] and radii [V,G] (int32)."""
     S = means.shape[0]
     if len(view_scene) != cams.shape[0]:
         raise ValueError(f"view_scene has {len(view_scene)} entries for {cams.shape[0]} cameras")
@@ -442,7 +454,7 @@ def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.T
     layout = input_layout(feats, cov6, use_sh, channel_major_sh)
     return _RasterizeViews.apply(f(means), f(feats), f(opacities), f(cov6), means2d, cams.contiguous(),
                                  list(view_scene), use_sh, int(sh_degree), int(image_height), int(image_width),
-                                 layout)
+                                 layout, zeroed_counts)
 
 
 def sh_degree_of(n_coeffs: int) -> int:
