@@ -1275,13 +1275,13 @@ __device__ __forceinline__ uint32_t subtile_mask(float4 q, float4 r, int tx0, in
 // where it is a clamped 1-D quadratic. The margin absorbs the rounding of the compositing
 // arithmetic, so the entries dropped here are exactly ones the per-pixel test would skip.
 // Degenerate / NaN conics are kept.
-__device__ __forceinline__ bool subtile_hit(float4 q, float4 r, float x0, float y0) {
+__device__ __forceinline__ bool rect_hit(float4 q, float4 r, float x0, float y0, float x1, float y1) {
   const float op = r.y;
   if (!(op >= 1.0f / 255.0f)) return false;
   const float a = q.z, b = q.w, c = r.x;
   const float t2 = 2.0f * __logf(255.0f * op) * 1.002f + 0.02f;
-  const float lx = x0 - q.x, hx = x0 + (SUB - 1) - q.x;  // box relative to the centre
-  const float ly = y0 - q.y, hy = y0 + (SUB - 1) - q.y;
+  const float lx = x0 - q.x, hx = x1 - q.x;  // box relative to the centre
+  const float ly = y0 - q.y, hy = y1 - q.y;
   if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;
   if (lx <= 0.f && hx >= 0.f && ly <= 0.f && hy >= 0.f) return true;
   const float ia = 1.0f / a, ic = 1.0f / c;
@@ -1302,6 +1302,24 @@ __device__ __forceinline__ bool subtile_hit(float4 q, float4 r, float x0, float 
   }
   return !(m > t2);
 }
+__device__ __forceinline__ bool subtile_hit(float4 q, float4 r, float x0, float y0) {
+  return rect_hit(q, r, x0, y0, x0 + (SUB - 1), y0 + (SUB - 1));
+}
+
+// Bounding box (pixel centres) of the wave's still-live pixels (lane = 8 * row + col of the
+// 8x8 sub-tile at (fx0, fy0)); live != 0. Entries that cannot reach it would only meet
+// pixels that have stopped (or lie outside the image) and change nothing there.
+__device__ __forceinline__ void live_rect(uint64_t live, float fx0, float fy0, float& x0, float& y0, float& x1,
+                                          float& y1) {
+  uint64_t cols = live | (live >> 32);
+  cols |= cols >> 16;
+  cols |= cols >> 8;
+  const uint32_t cb = (uint32_t)cols & 0xFFu;
+  y0 = fy0 + (float)(__builtin_ctzll(live) >> 3);
+  y1 = fy0 + (float)((63 - __builtin_clzll(live)) >> 3);
+  x0 = fx0 + (float)__builtin_ctz(cb);
+  x1 = fx0 + (float)(31 - __builtin_clz(cb));
+}
 
 #ifndef RF_EPL
 #define RF_EPL 1
@@ -1313,7 +1331,9 @@ constexpr int CH = 64 * EPL;     // entries per chunk
 // same IEEE operations as falloff_p2 (the backward's decisions still agree).
 typedef float f2v __attribute__((ext_vector_type(2)));
 struct __align__(16) PairRec {
-  f2v x, y, A, C, B, o, r, g, b;
+  f2v x, y, A, C, B, o;  // falloff fields of entries 0 and 1, interleaved (packed math)
+  f2v rg[2];             // (r, g) of entry j: one packed FMA into the pixel's (R, G)
+  f2v b;
   uint32_t pos[2];
 };
 __device__ __forceinline__ void pair_put(PairRec* l, int k, float x, float y, float A, float C, float B, float o,
@@ -1321,10 +1341,12 @@ __device__ __forceinline__ void pair_put(PairRec* l, int k, float x, float y, fl
   PairRec& d = l[k >> 1];
   const int j = k & 1;
   d.x[j] = x; d.y[j] = y; d.A[j] = A; d.C[j] = C; d.B[j] = B; d.o[j] = o;
-  d.r[j] = r; d.g[j] = g; d.b[j] = b; d.pos[j] = pos;
+  d.rg[j] = f2v{r, g}; d.b[j] = b; d.pos[j] = pos;
 }
-__device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v pfy2, float& Tr, f2v& C01,
-                                               float& C2, uint32_t& last) {
+// alive: the pixel has not stopped (and lies in the image); a lane mask, so the stop logic
+// is scalar mask arithmetic and T keeps its value for the final_T output.
+__device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v pfy2, float& Tr, bool& alive,
+                                               f2v& C01, float& C2, uint32_t& last) {
   const f2v dx = P.x - pfx2, dy = P.y - pfy2;
   const f2v Adx = P.A * dx, Cdy = P.C * dy, Bdx = P.B * dx;
   const f2v Bdxdy = Bdx * dy;
@@ -1336,20 +1358,19 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v p
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const float alpha = fminf(0.99f, oG[j]);
-    const bool ok = p2[j] <= 0.0f && alpha >= 1.0f / 255.0f;
+    const bool ok = alive && p2[j] <= 0.0f && alpha >= 1.0f / 255.0f;
     const float testT = Tr * (1 - alpha);
     const bool stop = ok && testT < 0.0001f;
     const bool blend = ok && !stop;
+    alive = alive && !stop;
     const float wgt = blend ? alpha * Tr : 0.0f;
-    f2v rg;
-    rg.x = P.r[j];
-    rg.y = P.g[j];
+    const f2v rg = P.rg[j];
     f2v w2;
     w2.x = wgt;
     w2.y = wgt;
     C01 = __builtin_elementwise_fma(rg, w2, C01);
     C2 = fmaf(P.b[j], wgt, C2);
-    Tr = blend ? testT : (stop ? -fabsf(Tr) : Tr);
+    Tr = blend ? testT : Tr;
     last = blend ? P.pos[j] : last;
   }
 }
@@ -1360,10 +1381,14 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v p
 // when none does the prefix alone gives the exact result. Returns (wave-uniform) whether
 // one does.
 __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* __restrict__ keys, uint32_t b,
-                                  uint32_t e, float fx0, float fy0, f2v pfx2, f2v pfy2, float Tr, PairRec* plist,
+                                  uint32_t e, float fx0, float fy0, f2v pfx2, f2v pfy2, bool alive, PairRec* plist,
                                   uint64_t lt, int lane) {
   uint32_t nid = b + lane < e ? (uint32_t)keys[b + lane] : 0xffffffffu;
-  for (uint32_t base = b; base < e && !__all(Tr < 0.0f); base += 64) {
+  for (uint32_t base = b; base < e; base += 64) {
+    const uint64_t live = __ballot(alive);
+    if (!live) break;
+    float lx0, ly0, lx1, ly1;
+    live_rect(live, fx0, fy0, lx0, ly0, lx1, ly1);
     const uint32_t id = nid;
     nid = base + 64 + lane < e ? (uint32_t)keys[base + 64 + lane] : 0xffffffffu;
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f), r = q;
@@ -1372,7 +1397,7 @@ __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* 
       q = rec[0];
       r = rec[1];
     }
-    const bool mine = id != 0xffffffffu && subtile_hit(q, r, fx0, fy0);
+    const bool mine = id != 0xffffffffu && rect_hit(q, r, lx0, ly0, lx1, ly1);
     const uint64_t bal = __ballot(mine);
     if (mine) {
       const float4 sq = scaled_conic_q(q);
@@ -1393,7 +1418,7 @@ __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* 
       }
     }
     __builtin_amdgcn_wave_barrier();
-    if (__any(hit && Tr > 0.0f)) return true;
+    if (__any(hit && alive)) return true;
   }
   return false;
 }
@@ -1439,7 +1464,8 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   PairRec* plist = l_pair[w];
   const f2v pfx2 = {pfx, pfx}, pfy2 = {pfy, pfy};
   f2v C01 = {0.f, 0.f};
-  float Tr = inside ? 1.0f : -1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
+  float Tr = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
+  bool alive = inside;
   uint32_t last = 0;
   float4 cq[EPL], cr[EPL];
   float cb[EPL];
@@ -1481,7 +1507,11 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   const uint64_t t_begin = wall_clock64();
   uint32_t d_chunks = 0, d_comp = 0;
 #endif
-  for (uint32_t base = start; base < end && !__all(Tr < 0.0f); base += CH) {
+  for (uint32_t base = start; base < end; base += CH) {
+    const uint64_t live = __ballot(alive);
+    if (!live) break;
+    float lx0, ly0, lx1, ly1;
+    live_rect(live, fx0, fy0, lx0, ly0, lx1, ly1);
 #ifdef RF_DIAG_WAVESTATS
     ++d_chunks;
 #endif
@@ -1509,7 +1539,11 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
 #pragma unroll
     for (int u = 0; u < EPL; ++u) {
       const uint32_t e = base + u * 64 + lane;
+#ifdef RF_FULL_SUBTILE
       const bool mine = e < end && subtile_hit(cq[u], cr[u], fx0, fy0);
+#else
+      const bool mine = e < end && rect_hit(cq[u], cr[u], lx0, ly0, lx1, ly1);
+#endif
       const uint64_t bal = __ballot(mine);
       if (mine) {
         const float4 sq = scaled_conic_q(cq[u]);  // (x, y, A, B)
@@ -1530,9 +1564,9 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
       for (int k = 0; k < cnt; k += 4) {
         pp += 2;
         const PairRec b0 = pp[0], b1 = pp[1];  // in bounds: pair k/2 + 3 <= (CH + 8) / 2 - 1
-        composite_pair(a0, pfx2, pfy2, Tr, C01, C2, last);
-        composite_pair(a1, pfx2, pfy2, Tr, C01, C2, last);
-        if (__all(Tr < 0.0f)) break;
+        composite_pair(a0, pfx2, pfy2, Tr, alive, C01, C2, last);
+        composite_pair(a1, pfx2, pfy2, Tr, alive, C01, C2, last);
+        if (!__any(alive)) break;
         a0 = b0;
         a1 = b1;
       }
@@ -1554,7 +1588,7 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
 #endif
     }
   }
-  if (end < tail_end && tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pfx2, pfy2, Tr, plist, lt, lane) &&
+  if (end < tail_end && tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pfx2, pfy2, alive, plist, lt, lane) &&
       lane == 0)
     seg_overflow[seg] = 1u;  // the tile's output is void: re-sorted in full and re-rendered by the caller
   if (inside) {
@@ -1563,7 +1597,7 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
     const float* bg = cams[v].bg;
     C0 = C01.x;
     C1 = C01.y;
-    const float Tf = fabsf(Tr);
+    const float Tf = Tr;
     finalT[v * HW + pix] = Tf;
     ncontrib[v * HW + pix] = last;
 #ifdef RF_DIAG_WAVESTATS  // timing experiment: lanes 0-2 report (ticks, chunks, composited entries)
