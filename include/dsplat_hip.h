@@ -116,7 +116,49 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
  *   seg_stride == 0: prefix layout, segment s = keys[seg_start[s] .. seg_start[s+1])
  *                    (dsr_bin_scan / dsr_bin_scatter; seg_count may be NULL)
  *   seg_stride  > 0: fixed capacity, segment s = keys[s*stride .. s*stride + seg_count[s])
- *                    (dsr_project_bin with stride = G; seg_start may be NULL) */
+ *                    (dsr_project_bin with stride = G; seg_start may be NULL)
+ *   seg_stride == DSR_SEG_ENDS: segment s = keys[seg_start[s] .. seg_count[s]), seg_count
+ *                    holding absolute END offsets (the cursors after dsr_bin_scatter_cut:
+ *                    only the near part of each prefix-layout segment is written) */
+#define DSR_SEG_ENDS 0xFFFFFFFFu
+
+/* ---- depth-cut binning (large problems: 6-view 448x768 and up) -----------------------
+ * At 6x448x768 a tile's list holds ~31K entries while the compositor consumes at most ~1.1K
+ * (every pixel saturates): writing, sorting and reading the other 30K is the dominant cost.
+ * These calls write only each tile's nearest entries, chosen with a depth histogram:
+ *   1. dsr_preprocess_cut = dsr_preprocess_fwd + a per-(view, super-block) histogram of
+ *      depth buckets (DSR_CUT_BUCKETS log-spaced buckets, 16 per octave of view depth from
+ *      0.25 near-units, each Gaussian counted once per touched tile);
+ *   2. dsr_bin_cutoff picks per (view, super-block) the nearest bucket whose cumulative count
+ *      reaches `prefix` entries per tile;
+ *   3. dsr_bin_scatter_cut (tail = 0) emits only the entries at or before that bucket into the
+ *      prefix layout of dsr_bin_scan (full counts): seg_cursor ends at each segment's written
+ *      end -> DSR_SEG_ENDS layout for dsr_bin_sort / dsr_render_fwd / dsr_render_bwd.
+ * Every emitted entry is nearer than every omitted one (buckets are depth ranges), so the
+ * sorted written part IS the head of the full sorted list. dsr_render_fwd flags a tile whose
+ * pixels are not all saturated at the end of its written part (seg_overflow[s] = 1 and
+ * seg_overflow[V*T] = 1); dsr_bin_scatter_cut with tail = 1 then appends the omitted entries
+ * of flagged tiles only (returns at once when seg_overflow[V*T] == 0), after which those
+ * tiles are sorted in full and rendered again (seg_filter = seg_overflow). */
+#define DSR_CUT_BUCKETS 128
+/* Super-block edge in tiles for a W x H image (0: the image is too large for this path). */
+int dsr_cut_superblock(int H, int W);
+/* depth_hist [V, nsb, DSR_CUT_BUCKETS] uint32 (zeroed by this call), nsb = ceil(tiles_x/sb)
+ * * ceil(tiles_y/sb); other arguments and outputs as dsr_preprocess_fwd. */
+int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M,
+                       const float* means, const float* shs, const float* colors,
+                       const float* opacities, const float* cov6, const dsr_camera* cams,
+                       float* geom, int32_t* radii, uint32_t* seg_count, uint32_t* depth_hist,
+                       int layout, void* stream);
+/* cut [V, nsb] uint32: last bucket emitted per super-block (DSR_CUT_BUCKETS - 1 = all). */
+int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t prefix, uint32_t* cut,
+                   void* stream);
+/* As dsr_bin_scatter, restricted by cut: tail = 0 -> entries with bucket <= cut; tail = 1 ->
+ * entries with bucket > cut of the segments with seg_overflow[s] != 0 (seg_overflow has
+ * V*T + 1 words; the last is the any-flag). seg_cursor advances past what is written. */
+int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor,
+                        uint64_t* keys, const uint32_t* cut, int tail, const uint32_t* seg_overflow,
+                        void* stream);
 
 /* Sort every segment by (depth, id) ascending — identical to upstream's stable radix
  * sort of (tile << 32 | depth) with emission-order ties (K4/K5). max_count sizes the LDS
@@ -152,7 +194,10 @@ uint32_t dsr_sort_lds_capacity(void);
  * passes the alpha test at a pixel that is still live, seg_overflow[s] is set to 1 (caller
  * zeroes it) and that tile's outputs are void: sort the flagged segments in full
  * (dsr_bin_sort with seg_filter = seg_overflow) and call again with seg_filter =
- * seg_overflow and seg_sorted = NULL, which renders only those tiles. */
+ * seg_overflow and seg_sorted = NULL, which renders only those tiles. In the DSR_SEG_ENDS
+ * layout (depth-cut binning) with seg_overflow given, a segment whose written end is below
+ * seg_start[s+1] is flagged when any of its pixels is still live at that end. seg_overflow
+ * has V*T + 1 words: the last one is set to 1 whenever any tile is flagged. */
 int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride,
                    const uint64_t* keys, const uint32_t* seg_sorted, uint32_t* seg_overflow,

@@ -50,6 +50,26 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
   return v;
 }
 
+// Inclusive wave64 scans on the DPP network: row_shr 1/2/4/8 scan each 16-lane row, then
+// row_bcast:15 / row_bcast:31 carry row totals into the rows above (GFX9-family DPP).
+// Lanes a DPP step cannot source read 0, the identity of both + and unsigned max.
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_incl_dpp(uint32_t v, Op op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_add_dpp(uint32_t v) {
+  return wave_incl_dpp(v, [](uint32_t a, uint32_t b) { return a + b; });
+}
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t v) {
+  return wave_incl_dpp(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+}
+
 // Zero a buffer with a plain kernel rather than hipMemsetAsync: the fill must be an
 // ordinary kernel node when callers capture the stream into a hipGraph (a captured
 // small hipMemsetAsync was observed not to re-run on replays 2+, leaving stale counts).

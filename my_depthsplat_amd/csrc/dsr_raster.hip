@@ -15,6 +15,8 @@
 // All floating-point expressions feeding the bit-exact outputs (depth, radius, xy, tile
 // rect, sort keys) keep the evaluation order of oracle/dsr_oracle.cpp (-ffp-contract=off).
 
+#include <type_traits>
+
 #include "dsplat_common.h"
 
 namespace {
@@ -93,33 +95,49 @@ struct WaveRects {
   uint32_t ex[64];    // exclusive scan of areas
   uint32_t org[64];   // x0 | y0 << 16
   uint32_t wid[64];   // rect width in tiles
+  uint32_t mark[64];  // owner + 1 of each window slot where a rect's run of pairs begins
 };
+// Pairs are handed out 64 per step: the owner of pair j is the lane whose run [ex, ex + area)
+// holds j, found per window by marking each run's first slot and a wave max-scan of the
+// marks (DPP, no dependent LDS search); the tile comes from (j - ex) / width with a hardware
+// reciprocal and exact integer fix-ups. f(tile, owner lane[, tile x, tile y]).
 template <typename F>
 __device__ __forceinline__ void for_each_rect_tile(WaveRects& wr, int lane, int x0, int y0, int x1, int y1,
                                                    bool has, int gx, F f) {
   const uint32_t area = has ? (uint32_t)((x1 - x0) * (y1 - y0)) : 0u;
-  const uint32_t incl = dsplat::wave_incl_scan(area, lane);
-  const uint32_t total = __shfl(incl, 63, 64);
-  wr.ex[lane] = incl - area;
+  const uint32_t incl = dsplat::wave_incl_add_dpp(area);
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  const uint32_t ex = incl - area;
+  wr.ex[lane] = ex;
   wr.org[lane] = (uint32_t)x0 | ((uint32_t)y0 << 16);
   wr.wid[lane] = (uint32_t)max(x1 - x0, 1);
-  __builtin_amdgcn_wave_barrier();
-  for (uint32_t j = lane; j < total; j += 64) {
-    // owner = last lane with ex <= j (a zero-area lane never is: its successor has the same ex)
-    int o = 0;
-#pragma unroll
-    for (int step = 32; step > 0; step >>= 1)
-      if (wr.ex[o + step] <= j) o += step;
-    const uint32_t local = j - wr.ex[o];
-    const uint32_t wd = wr.wid[o];
-    uint32_t dy = (uint32_t)(((float)local + 0.5f) * (1.0f / (float)wd));
-    if (dy * wd > local) --dy;
-    if ((dy + 1) * wd <= local) ++dy;
-    const uint32_t dx = local - dy * wd;
-    const uint32_t og = wr.org[o];
-    f((int)(((og >> 16) + dy) * (uint32_t)gx + (og & 0xFFFFu) + dx), o);
+  uint32_t carry = 0u;  // owner + 1 of the window's first slot when no run starts there
+  for (uint32_t base = 0; base < total; base += 64) {
+    wr.mark[lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (area != 0u && ex - base < 64u) wr.mark[ex - base] = (uint32_t)lane + 1u;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t m = wr.mark[lane];
+    if (lane == 0) m = max(m, carry);
+    const uint32_t own = dsplat::wave_incl_max_dpp(m);
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
+    const uint32_t j = base + (uint32_t)lane;
+    if (j < total) {
+      const int o = (int)own - 1;
+      const uint32_t local = j - wr.ex[o];
+      const uint32_t wd = wr.wid[o];
+      uint32_t dy = (uint32_t)(((float)local + 0.5f) * __builtin_amdgcn_rcpf((float)wd));
+      if (dy * wd > local) --dy;
+      if ((dy + 1) * wd <= local) ++dy;
+      const uint32_t og = wr.org[o];
+      const int tx = (int)((og & 0xFFFFu) + local - dy * wd), ty = (int)((og >> 16) + dy);
+      if constexpr (std::is_invocable_v<F, int, int, int, int>)
+        f(ty * gx + tx, o, tx, ty);
+      else
+        f(ty * gx + tx, o);
+    }
+    __builtin_amdgcn_wave_barrier();
   }
-  __builtin_amdgcn_wave_barrier();
 }
 
 struct Cov2D {
@@ -227,9 +245,15 @@ __device__ __forceinline__ void load_sh(const float* shs, size_t sg, int M, int 
 
 // Segment (view, tile) bounds in the key buffer. stride == 0: prefix layout, segment s is
 // [start[s], start[s + 1]). stride > 0: fixed capacity, [s * stride, s * stride + count[s]).
+// stride == DSR_SEG_ENDS: [start[s], count[s]) — count holds absolute end offsets (the
+// depth-cut binning writes only the near part of each prefix-layout segment).
+constexpr uint32_t kSegEnds = DSR_SEG_ENDS;
 __device__ __forceinline__ void seg_bounds(const uint32_t* __restrict__ start, const uint32_t* __restrict__ count,
                                            uint32_t stride, int seg, uint32_t& b, uint32_t& e) {
-  if (stride) {
+  if (stride == kSegEnds) {
+    b = start[seg];
+    e = count[seg];
+  } else if (stride) {
     b = (uint32_t)seg * stride;
     e = b + count[seg];
   } else {
@@ -509,19 +533,62 @@ __global__ __launch_bounds__(1024) void k_scan(int n, const uint32_t* __restrict
 }
 
 // ------------------------------------------------------------------------------------
-// K3: emit (depth, id) keys into their (view, tile) bucket.
+// ---- depth-cut binning (include/dsplat_hip.h: dsr_preprocess_cut / dsr_bin_cutoff /
+// dsr_bin_scatter_cut). Depth bucket = 16 per octave of the view-space depth (in near units)
+// from 0.25, read off the float bits; monotone in the depth, so a bucket range is a depth range.
+constexpr int kCutBuckets = DSR_CUT_BUCKETS;
+constexpr int kCutLdsWords = 24576;  // count histogram + super-block depth histograms (96 KiB)
+constexpr int kCutMaxSB = kCutLdsWords / kCutBuckets;
+__device__ __forceinline__ int depth_bucket(uint32_t zbits) {
+  return min(kCutBuckets - 1, max(0, (int)(zbits >> 19) - (125 << 4)));
+}
+__host__ __device__ inline int cut_superblock(int gx, int gy) {
+  for (int sb = 4; sb <= 64; sb *= 2) {
+    const int nsb = ((gx + sb - 1) / sb) * ((gy + sb - 1) / sb);
+    if (gx * gy + nsb * kCutBuckets <= kCutLdsWords) return sb;
+  }
+  return 0;
+}
+
+// K3: emit (depth, id) keys into their (view, tile) bucket. CUT: only the entries the
+// depth cut keeps (tail == 0: bucket <= cut of the tile's super-block; tail == 1: the others,
+// of flagged segments only).
+template <bool CUT>
 __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, const float* __restrict__ geom,
                                                 uint32_t* __restrict__ cursor,
-                                                uint64_t* __restrict__ keys, int lds_hist) {
+                                                uint64_t* __restrict__ keys, int lds_hist,
+                                                const uint32_t* __restrict__ cut, int tail,
+                                                const uint32_t* __restrict__ seg_overflow) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+  __shared__ uint32_t s_cut[CUT ? kCutMaxSB : 1];
   int v, blk;
   if (!xcd_item((G + NT - 1) / NT, V, v, blk)) return;
   const int T = gx * gy;
+  if (CUT && tail && seg_overflow[(size_t)V * T] == 0u) return;  // no tile flagged (uniform)
   const int tid = threadIdx.x;
+  int sb = 1, sbl = 0, nsx = 1;
+  if constexpr (CUT) {
+    sb = cut_superblock(gx, gy);
+    sbl = __builtin_ctz((unsigned)sb);
+    nsx = (gx + sb - 1) / sb;
+    const int nsb = nsx * ((gy + sb - 1) / sb);
+    for (int s = tid; s < nsb; s += NT) s_cut[s] = cut[(size_t)v * nsb + s];
+    if (!lds_hist) __syncthreads();
+  }
   if (lds_hist) {
     for (int t = tid; t < T; t += NT) s_hist[t] = 0;
     __syncthreads();
   }
+  const uint32_t* vov = CUT && tail ? seg_overflow + (size_t)v * T : nullptr;
+  // the cut: does the entry (tile t, key) belong to this pass?
+  auto keep = [&](int t, int tx, int ty, uint64_t key) -> bool {
+    if constexpr (!CUT) {
+      return true;
+    } else {
+      const bool nearer = depth_bucket((uint32_t)(key >> 32)) <= (int)s_cut[(ty >> sbl) * nsx + (tx >> sbl)];
+      return tail ? (!nearer && vov[t] != 0u) : nearer;
+    }
+  };
   const int g = blk * NT + tid;
   int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
   uint64_t key = 0;
@@ -531,6 +598,22 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
     if (r > 0) {
       tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
       key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
+      if constexpr (CUT) {
+        // whole-Gaussian pre-test over the super-blocks its rect touches (the cut keeps ~10%
+        // of the entries at 6x448x768, and most of the rest belong to Gaussians deeper than
+        // every cut they meet): skip the per-tile expansion when no tile can take it
+        const int sx0 = x0 >> sbl, sx1 = ((x1 - 1) >> sbl) + 1, sy0 = y0 >> sbl, sy1 = ((y1 - 1) >> sbl) + 1;
+        if ((sx1 - sx0) * (sy1 - sy0) <= 16) {
+          const int bk = depth_bucket((uint32_t)(key >> 32));
+          bool any = false;
+          for (int sy = sy0; sy < sy1; ++sy)
+            for (int sx = sx0; sx < sx1; ++sx) {
+              const bool nearer = bk <= (int)s_cut[sy * nsx + sx];
+              any |= tail ? !nearer : nearer;
+            }
+          if (!any) r = 0;
+        }
+      }
     }
   }
   uint32_t* gcur = cursor + (size_t)v * T;
@@ -541,19 +624,126 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
   WaveRects& wr = s_wr[w];
   const uint64_t* wkey = s_key + w * 64;
   if (lds_hist) {
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
+      if (keep(t, tx, ty, wkey[o])) atomicAdd(&s_hist[t], 1u);
+    });
     __syncthreads();
     for (int t = tid; t < T; t += NT) {
       const uint32_t c = s_hist[t];
       if (c) s_hist[t] = atomicAdd(&gcur[t], c);
     }
     __syncthreads();
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
-                       [&](int t, int o) { keys[atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
+      const uint64_t k = wkey[o];
+      if (keep(t, tx, ty, k)) keys[atomicAdd(&s_hist[t], 1u)] = k;
+    });
   } else {
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
-                       [&](int t, int o) { keys[atomicAdd(&gcur[t], 1u)] = wkey[o]; });
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
+      const uint64_t k = wkey[o];
+      if (keep(t, tx, ty, k)) keys[atomicAdd(&gcur[t], 1u)] = k;
+    });
   }
+}
+
+// K1 + depth histogram (dsr_preprocess_cut). NTH threads per workgroup; each workgroup owns
+// one view and a contiguous run of NTH-Gaussian blocks (a persistent grid sized to the
+// resident capacity), so its LDS count and depth histograms are flushed to HBM once for many
+// blocks instead of once per block. Depth histogram: per super-block of sb x sb tiles, each
+// (Gaussian, touched super-block) adds the number of its tiles inside that super-block to
+// the bucket of its depth (super-blocks, not tiles: at 6x448x768 a 16-tile super-block
+// keeps the whole view's histogram in 43 KiB of LDS).
+template <int DEG, int NTH>
+__global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int W, int gx, int gy, int M,
+                                                        const float* __restrict__ means,
+                                                        const float* __restrict__ shs,
+                                                        const float* __restrict__ colors,
+                                                        const float* __restrict__ opac,
+                                                        const float* __restrict__ cov6,
+                                                        const dsr_camera* __restrict__ cams,
+                                                        float* __restrict__ geom, int32_t* __restrict__ radii,
+                                                        uint32_t* __restrict__ seg_count,
+                                                        uint32_t* __restrict__ depth_hist, int per_view,
+                                                        int layout) {
+  constexpr int NW = NTH / 64;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_mem[];
+  __shared__ WaveRects s_wr[NW];
+  __shared__ uint32_t s_rx[NW][64], s_ry[NW][64], s_bk[NW][64];
+  const int T = gx * gy;
+  const int sb = cut_superblock(gx, gy), sbl = __builtin_ctz((unsigned)sb);
+  const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((gy + sb - 1) / sb);
+  uint32_t* s_cnt = s_mem;
+  uint32_t* s_dh = s_mem + T;
+  const int v = blockIdx.x / per_view, p = blockIdx.x - v * per_view;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int k = tid; k < T + nsb * kCutBuckets; k += NTH) s_mem[k] = 0u;
+  __syncthreads();
+  const dsr_camera* cam = cams + v;
+  const int nblk = (G + NTH - 1) / NTH;
+  const int b0 = (int)((int64_t)nblk * p / per_view), b1 = (int)((int64_t)nblk * (p + 1) / per_view);
+  WaveRects& wr = s_wr[w];
+  for (int blk = b0; blk < b1; ++blk) {
+    const int g = blk * NTH + tid;
+    int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    uint32_t zb = 0u;
+    if (g < G) {
+      GaussIn<DEG> in;
+      load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
+      float rec[GS];
+      r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
+      store_geom(geom, radii, (size_t)v * G + g, rec, r);
+      zb = __float_as_uint(rec[9]);
+    }
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_cnt[t], 1u); });
+    s_rx[w][lane] = (uint32_t)x0 | ((uint32_t)x1 << 16);
+    s_ry[w][lane] = (uint32_t)y0 | ((uint32_t)y1 << 16);
+    s_bk[w][lane] = (uint32_t)depth_bucket(zb);
+    const int sx0 = x0 >> sbl, sy0 = y0 >> sbl;
+    const int sx1 = r > 0 ? ((x1 - 1) >> sbl) + 1 : sx0, sy1 = r > 0 ? ((y1 - 1) >> sbl) + 1 : sy0;
+    for_each_rect_tile(wr, lane, sx0, sy0, sx1, sy1, r > 0, nsx, [&](int s, int o, int sx, int sy) {
+      const uint32_t rx = s_rx[w][o], ry = s_ry[w][o];
+      const int ox = min((int)(rx >> 16), sx * sb + sb) - max((int)(rx & 0xFFFFu), sx * sb);
+      const int oy = min((int)(ry >> 16), sy * sb + sb) - max((int)(ry & 0xFFFFu), sy * sb);
+      atomicAdd(&s_dh[s * kCutBuckets + (int)s_bk[w][o]], (uint32_t)(ox * oy));
+    });
+  }
+  __syncthreads();
+  uint32_t* gc = seg_count + (size_t)v * T;
+  for (int t = tid; t < T; t += NTH) {
+    const uint32_t c = s_cnt[t];
+    if (c) atomicAdd(&gc[t], c);
+  }
+  uint32_t* gh = depth_hist + (size_t)v * nsb * kCutBuckets;
+  for (int k = tid; k < nsb * kCutBuckets; k += NTH) {
+    const uint32_t c = s_dh[k];
+    if (c) atomicAdd(&gh[k], c);
+  }
+}
+
+// One wave per (view, super-block): the nearest bucket at which the super-block's cumulative
+// entry count reaches `prefix` per tile (kCutBuckets - 1, i.e. everything, if it never does).
+__global__ __launch_bounds__(256) void k_bin_cutoff(int V, int gx, int gy, const uint32_t* __restrict__ hist,
+                                                    uint32_t prefix, uint32_t* __restrict__ cut) {
+  const int sb = cut_superblock(gx, gy);
+  const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((gy + sb - 1) / sb);
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (item >= V * nsb) return;
+  const int s = item % nsb, sy = s / nsx, sx = s - sy * nsx;
+  const uint32_t ntiles = (uint32_t)((min(gx, sx * sb + sb) - sx * sb) * (min(gy, sy * sb + sb) - sy * sb));
+  const uint64_t target = (uint64_t)prefix * ntiles;
+  static_assert(kCutBuckets == 128, "two buckets per lane");
+  const uint32_t* h = hist + (size_t)item * kCutBuckets;
+  const uint32_t a = h[2 * lane], b = h[2 * lane + 1];
+  const uint32_t incl = dsplat::wave_incl_scan(a + b, lane);
+  const uint32_t before = incl - (a + b);
+  const uint64_t reach = __ballot((uint64_t)incl >= target);
+  uint32_t c = kCutBuckets - 1;
+  if (reach) {
+    const int L = __ffsll((unsigned long long)reach) - 1;
+    const uint32_t bL = (uint32_t)__shfl((int)before, L, 64);
+    const uint32_t aL = (uint32_t)__shfl((int)a, L, 64);
+    c = 2u * L + ((uint64_t)bL + aL >= target ? 0u : 1u);
+  }
+  if (lane == 0) cut[item] = c;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1457,6 +1647,8 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   seg_bounds(seg_start, seg_count, stride, seg, start, end);
   const uint32_t tail_end = end;  // [end, tail_end): unsorted tail (prefix-sorted segments)
   if (seg_sorted) end = start + min(seg_sorted[seg], end - start);
+  // depth-cut binning: entries past `end` were never written (all deeper than the written ones)
+  const bool absent_tail = stride == kSegEnds && seg_overflow != nullptr && end < seg_start[seg + 1];
   const float pfx = (float)px, pfy = (float)py;
   const float fx0 = (float)sx0, fy0 = (float)sy0;
   const float* gv = geom + (size_t)v * G * GS;
@@ -1588,9 +1780,15 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
 #endif
     }
   }
-  if (end < tail_end && tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pfx2, pfy2, alive, plist, lt, lane) &&
-      lane == 0)
-    seg_overflow[seg] = 1u;  // the tile's output is void: re-sorted in full and re-rendered by the caller
+  bool void_tile = false;  // wave-uniform
+  if (absent_tail)
+    void_tile = __any(alive);  // a pixel still live at the end of the written part: the rest may blend
+  else if (end < tail_end)
+    void_tile = tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pfx2, pfy2, alive, plist, lt, lane);
+  if (void_tile && lane == 0) {  // the tile's output is void: completed, sorted and re-rendered by the caller
+    seg_overflow[seg] = 1u;
+    seg_overflow[(size_t)gridDim.z * T] = 1u;  // any-flag
+  }
   if (inside) {
     const size_t HW = (size_t)H * W;
     const size_t pix = (size_t)py * W + px;
@@ -2103,6 +2301,10 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
   }
 }
 
+// pointers a segment layout needs (seg_bounds): ENDS both, fixed capacity the counts, prefix the starts
+inline bool seg_ptrs_ok(const uint32_t* start, const uint32_t* count, uint32_t stride) {
+  return stride == kSegEnds ? (start != nullptr && count != nullptr) : stride ? count != nullptr : start != nullptr;
+}
 int lds_hist_bytes(int T) { return T <= kHistLdsMax ? T * 4 : 0; }
 
 }  // namespace
@@ -2189,9 +2391,88 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
   DSPLAT_REQUIRE(geom && seg_cursor, "dsr_bin_scatter: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   const int lds = lds_hist_bytes(gx * gy);
-  k_scatter<<<xcd_grid((G + NT - 1) / NT, V), NT, lds, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor, keys,
-                                                                              lds > 0);
+  k_scatter<false><<<xcd_grid((G + NT - 1) / NT, V), NT, lds, (hipStream_t)stream>>>(
+      G, V, gx, gy, geom, seg_cursor, keys, lds > 0, nullptr, 0, nullptr);
   return dsplat::check_launch("k_scatter");
+}
+
+int dsr_cut_superblock(int H, int W) {
+  if (H <= 0 || W <= 0) return 0;
+  return cut_superblock(dsplat::tiles_x(W), dsplat::tiles_y(H));
+}
+
+int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
+                       const float* shs, const float* colors, const float* opacities, const float* cov6,
+                       const dsr_camera* cams, float* geom, int32_t* radii, uint32_t* seg_count,
+                       uint32_t* depth_hist, int layout, void* stream) {
+  DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_preprocess_cut: bad sizes S=%d G=%d V=%d H=%d W=%d", S, G, V, H, W);
+  DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "dsr_preprocess_cut: exactly one of shs/colors must be given");
+  DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
+                 "dsr_preprocess_cut: sh_degree=%d M=%d unsupported (degree 0..3, M >= (deg+1)^2)", sh_degree, M);
+  DSPLAT_REQUIRE(means && opacities && cov6 && cams && geom && radii && seg_count && depth_hist,
+                 "dsr_preprocess_cut: null pointer");
+  const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H), T = gx * gy;
+  const int sb = cut_superblock(gx, gy);
+  DSPLAT_REQUIRE(sb > 0, "dsr_preprocess_cut: %dx%d tiles exceed the LDS histograms", gx, gy);
+  const int nsb = ((gx + sb - 1) / sb) * ((gy + sb - 1) / sb);
+  hipStream_t st = (hipStream_t)stream;
+  if (!(layout & kLayoutCountsZeroed))
+    if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
+  if (int e = dsplat::zero_async(depth_hist, (size_t)V * nsb * kCutBuckets * 4, st, "zero depth_hist")) return e;
+  constexpr int kNTH = 512;
+  const size_t lds = (size_t)(T + nsb * kCutBuckets) * 4;
+  // persistent grid: about the resident workgroup count (LDS-limited), split evenly over views
+  const int per_cu = max(1, min(4, (int)((160 * 1024) / (lds + 8 * 1024))));
+  const int nblk = (G + kNTH - 1) / kNTH;
+  const int per_view = max(1, min(nblk, (256 * per_cu) / V));
+  const int deg = shs ? sh_degree : -1;
+#define DSR_PC(D)                                                                                            \
+  do {                                                                                                       \
+    static bool attr = false;                                                                                \
+    if (!attr) {                                                                                             \
+      if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_preprocess_cut<D, kNTH>,              \
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,          \
+                                                        kCutLdsWords * 4),                                   \
+                                    "hipFuncSetAttribute(k_preprocess_cut)"))                                \
+        return e;                                                                                            \
+      attr = true;                                                                                           \
+    }                                                                                                        \
+    k_preprocess_cut<D, kNTH><<<(unsigned)(V * per_view), kNTH, lds, st>>>(                                  \
+        G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, geom, radii, seg_count, depth_hist, \
+        per_view, layout);                                                                                   \
+  } while (0)
+  switch (deg) {
+    case -1: DSR_PC(-1); break;
+    case 0: DSR_PC(0); break;
+    case 1: DSR_PC(1); break;
+    case 2: DSR_PC(2); break;
+    default: DSR_PC(3); break;
+  }
+#undef DSR_PC
+  return dsplat::check_launch("k_preprocess_cut");
+}
+
+int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t prefix, uint32_t* cut, void* stream) {
+  DSPLAT_REQUIRE(V > 0 && H > 0 && W > 0, "dsr_bin_cutoff: bad sizes");
+  DSPLAT_REQUIRE(depth_hist && cut, "dsr_bin_cutoff: null pointer");
+  const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
+  const int sb = cut_superblock(gx, gy);
+  DSPLAT_REQUIRE(sb > 0, "dsr_bin_cutoff: %dx%d tiles exceed the LDS histograms", gx, gy);
+  const int items = V * ((gx + sb - 1) / sb) * ((gy + sb - 1) / sb);
+  k_bin_cutoff<<<(unsigned)((items + 3) / 4), 256, 0, (hipStream_t)stream>>>(V, gx, gy, depth_hist, prefix, cut);
+  return dsplat::check_launch("k_bin_cutoff");
+}
+
+int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor, uint64_t* keys,
+                        const uint32_t* cut, int tail, const uint32_t* seg_overflow, void* stream) {
+  DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_scatter_cut: bad sizes");
+  DSPLAT_REQUIRE(geom && seg_cursor && keys && cut && (!tail || seg_overflow), "dsr_bin_scatter_cut: null pointer");
+  const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
+  DSPLAT_REQUIRE(cut_superblock(gx, gy) > 0, "dsr_bin_scatter_cut: %dx%d tiles exceed the LDS histograms", gx, gy);
+  const int lds = lds_hist_bytes(gx * gy);
+  k_scatter<true><<<xcd_grid((G + NT - 1) / NT, V), NT, lds, (hipStream_t)stream>>>(
+      G, V, gx, gy, geom, seg_cursor, keys, lds > 0, cut, tail, seg_overflow);
+  return dsplat::check_launch("k_scatter_cut");
 }
 
 size_t dsr_bin_sort_workspace_size(int V, int H, int W, uint32_t max_count) {
@@ -2222,7 +2503,7 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
                  uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count, void* workspace,
                  uint32_t prefix, uint32_t* seg_sorted, const uint32_t* seg_filter, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_sort: bad sizes");
-  DSPLAT_REQUIRE(keys != nullptr && (seg_stride ? seg_count != nullptr : seg_start != nullptr),
+  DSPLAT_REQUIRE(keys != nullptr && seg_ptrs_ok(seg_start, seg_count, seg_stride),
                  "dsr_bin_sort: null pointer");
   DSPLAT_REQUIRE(scratch != nullptr || (max_count > 0 && max_count <= kSortCap),
                  "dsr_bin_sort: without scratch, max_count (%u) must bound every segment and be <= %u", max_count,
@@ -2310,7 +2591,7 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
                    float* final_T, uint32_t* n_contrib, void* stream) {
   DSPLAT_REQUIRE(seg_sorted == nullptr || seg_overflow != nullptr, "dsr_render_fwd: seg_sorted needs seg_overflow");
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_render_fwd: bad sizes");
-  DSPLAT_REQUIRE(cams && geom && (seg_stride ? seg_count != nullptr : seg_start != nullptr) && out_color && final_T &&
+  DSPLAT_REQUIRE(cams && geom && seg_ptrs_ok(seg_start, seg_count, seg_stride) && out_color && final_T &&
                      n_contrib,
                  "dsr_render_fwd: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
@@ -2326,7 +2607,7 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
                    const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, float* dgeom,
                    void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_render_bwd: bad sizes");
-  DSPLAT_REQUIRE(cams && geom && (seg_stride ? seg_count != nullptr : seg_start != nullptr) && final_T && n_contrib &&
+  DSPLAT_REQUIRE(cams && geom && seg_ptrs_ok(seg_start, seg_count, seg_stride) && final_T && n_contrib &&
                      dL_dpix && dgeom,
                  "dsr_render_bwd: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);

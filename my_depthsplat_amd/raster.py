@@ -137,15 +137,27 @@ class RasterState:
     final_T: torch.Tensor     # [V, H, W]
     n_contrib: torch.Tensor   # [V, H, W] int32
     seg_sorted: torch.Tensor | None = None    # [V*T] sorted entries per segment (prefix-sort mode)
-    seg_overflow: torch.Tensor | None = None  # [V*T] tiles re-sorted in full and re-rendered
+    seg_overflow: torch.Tensor | None = None  # [V*T(+1)] tiles re-sorted in full and re-rendered
+    tile_count: torch.Tensor | None = None    # [V*T] all entries per tile (depth-cut mode: seg_count = ends)
+
+    @property
+    def counts(self) -> torch.Tensor:
+        """Entries per (view, tile), whether or not all of them were written."""
+        return self.seg_count if self.tile_count is None else self.tile_count
 
     @property
     def num_rendered(self) -> int:  # host read: syncs
-        return int(self.seg_count.sum())
+        return int(self.counts.sum())
 
     @property
     def max_count(self) -> int:
-        return int(self.seg_count.max())
+        return int(self.counts.max())
+
+    def written(self) -> torch.Tensor:
+        """Entries per segment present (sorted) in `keys`."""
+        if self.seg_stride == SEG_ENDS:
+            return self.seg_count.long() - self.seg_start[:-1].long()
+        return self.seg_count
 
 
 # Key-buffer sizing. N (the number of (view, tile, Gaussian) entries) is only known on the
@@ -159,6 +171,12 @@ KEY_BUDGET_BYTES = 8 << 30
 # nearest SORT_PREFIX entries put in order (dsr_bin_sort prefix mode): at 6x448x768 the
 # compositor uses at most ~1.2K of 30-40K entries per tile. 0 sorts everything.
 SORT_PREFIX = int(os.environ.get("DSPLAT_SORT_PREFIX", "4096"))
+# Depth-cut binning for the two-phase path (include/dsplat_hip.h): only about CUT_PREFIX
+# entries per tile, the nearest depth buckets, are written and sorted; tiles whose pixels do
+# not all saturate within them get the rest appended, sorted and rendered again. 0 = off.
+CUT_PREFIX = int(os.environ.get("DSPLAT_CUT_PREFIX", "2048"))
+CUT_SORT_HINT = 4096  # LDS sort size for the written parts (larger ones sort through HBM)
+SEG_ENDS = 0xFFFFFFFF  # DSR_SEG_ENDS
 _spec = {"max_count": 0}
 _inflight: list = []  # (pinned int32 counts, event) read-backs, consumed without blocking
 
@@ -303,10 +321,19 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                   lds_cap)
         _note_counts(seg_count)
     else:
-        _lib.check(_timed("k_preprocess", lib.dsr_preprocess_fwd,
-            S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-            cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), layout, st),
-            "dsr_preprocess_fwd")
+        sb = lib.dsr_cut_superblock(H, W) if CUT_PREFIX > 0 else 0
+        if sb > 0:
+            nsb = -(-gx // sb) * -(-gy // sb)
+            hist = torch.empty(V * nsb * 128, dtype=torch.int32, device=dev)
+            _lib.check(_timed("k_preprocess_cut", lib.dsr_preprocess_cut,
+                S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), hist.data_ptr(), layout,
+                st), "dsr_preprocess_cut")
+        else:
+            _lib.check(_timed("k_preprocess", lib.dsr_preprocess_fwd,
+                S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), layout, st),
+                "dsr_preprocess_fwd")
         seg_start = torch.empty(V * T + 1, dtype=torch.int32, device=dev)
         cursor = torch.empty(V * T, dtype=torch.int32, device=dev)
         totals = torch.empty(4, dtype=torch.int32, device=dev)
@@ -318,35 +345,53 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         tot = totals[:2].cpu()  # one small read-back: N sizes the key buffer
         N, maxc = int(tot[0]), int(tot[1])
         keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
-        scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev) if maxc > lds_cap else None
-        _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
-                          keys.data_ptr(), st), "dsr_bin_scatter")
-        ws = _sort_workspace(lib, V, H, W, maxc, dev)
-        stride = 0
-        seg_sorted = _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, maxc, ws, st,
-                                  lds_cap)
+        if sb > 0:
+            # depth cut: write only each tile's nearest entries (cursor ends at their end)
+            scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev)  # only big segments touch it
+            cut = torch.empty(V * nsb, dtype=torch.int32, device=dev)
+            _lib.check(_timed("k_bin_cutoff", lib.dsr_bin_cutoff, V, H, W, hist.data_ptr(), CUT_PREFIX,
+                              cut.data_ptr(), st), "dsr_bin_cutoff")
+            _lib.check(_timed("k_scatter", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
+                              keys.data_ptr(), cut.data_ptr(), 0, None, st), "dsr_bin_scatter_cut")
+            tile_count, seg_count, stride = seg_count, cursor, SEG_ENDS
+            _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), seg_count.data_ptr(),
+                              stride, keys.data_ptr(), scratch.data_ptr(), CUT_SORT_HINT, None, 0, None, None, st),
+                       "dsr_bin_sort")
+            seg_sorted = None
+        else:
+            scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev) if maxc > lds_cap else None
+            _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
+                              keys.data_ptr(), st), "dsr_bin_scatter")
+            ws = _sort_workspace(lib, V, H, W, maxc, dev)
+            stride = 0
+            seg_sorted = _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, maxc, ws, st,
+                                      lds_cap)
     color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
     outs = (color.data_ptr(), final_T.data_ptr(), n_contrib.data_ptr(), st)
     overflow = None
-    if seg_sorted is not None:
-        overflow = torch.zeros(V * T, dtype=torch.int32, device=dev)
+    if seg_sorted is not None or stride == SEG_ENDS:
+        overflow = torch.zeros(V * T + 1, dtype=torch.int32, device=dev)  # + the any-flag word
     _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
                       _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(), _ptr(seg_sorted),
                       _ptr(overflow), None, *outs), "dsr_render_fwd")
     if overflow is not None:
-        # tiles whose unsorted tail would have blended: sort those in full, render them again
-        # (both launches return at once for unflagged tiles; no host sync)
+        # tiles whose unsorted (or unwritten) tail would have blended: complete them, sort them
+        # in full, render them again (every launch returns at once for unflagged tiles; no sync)
+        if stride == SEG_ENDS:
+            _lib.check(lib.dsr_bin_scatter_cut(G, V, H, W, geom.data_ptr(), seg_count.data_ptr(), keys.data_ptr(),
+                                               cut.data_ptr(), 1, overflow.data_ptr(), st), "dsr_bin_scatter_cut(tail)")
         _lib.check(lib.dsr_bin_sort(G, V, H, W, _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(),
-                                    scratch.data_ptr(), 0, None, 0, seg_sorted.data_ptr(), overflow.data_ptr(), st),
+                                    scratch.data_ptr(), 0, None, 0, _ptr(seg_sorted), overflow.data_ptr(), st),
                    "dsr_bin_sort(overflow)")
         _lib.check(lib.dsr_render_fwd(G, V, H, W, cams.data_ptr(), geom.data_ptr(), _ptr(seg_start),
                                       seg_count.data_ptr(), stride, keys.data_ptr(), None, None, overflow.data_ptr(),
                                       *outs), "dsr_render_fwd(overflow)")
-    _last["counts"] = seg_count
-    return color, RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, seg_sorted,
-                              overflow)
+    state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, seg_sorted, overflow,
+                        tile_count if stride == SEG_ENDS else None)
+    _last["counts"] = state.counts
+    return color, state
 
 
 def _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, max_count, ws, st, lds_cap):

@@ -34,15 +34,24 @@ def hip_forward(sc, st, gpu, use_sh=True, bg=(0.0, 0.0, 0.0)):
 
 
 def _segments(state, V, T):
-    """(start [V*T+1], keys) in the prefix layout, whichever layout the forward used."""
+    """(begin [V*T], end [V*T], keys): the written, sorted part of each segment, whichever
+    layout the forward used (fixed capacity, prefix, or depth-cut ends)."""
     keys = state.keys.cpu().numpy().view(np.uint64)
     if state.seg_stride == 0:
-        return state.seg_start.cpu().numpy().astype(np.int64), keys
+        start = state.seg_start.cpu().numpy().astype(np.int64)
+        return start[:-1], start[1:], keys
+    if state.seg_stride == raster_mod().SEG_ENDS:
+        return (state.seg_start.cpu().numpy().astype(np.int64)[:-1],
+                state.seg_count.cpu().numpy().astype(np.int64), keys)
     cnt = state.seg_count.cpu().numpy().astype(np.int64)
     assert cnt.shape[0] == V * T
-    parts = [keys[s * state.seg_stride: s * state.seg_stride + cnt[s]] for s in range(V * T)]
-    start = np.concatenate([[0], np.cumsum(cnt)])
-    return start, np.concatenate(parts) if parts else keys[:0]
+    begin = np.arange(V * T, dtype=np.int64) * state.seg_stride
+    return begin, begin + cnt, keys
+
+
+def raster_mod():
+    from my_depthsplat_amd import raster
+    return raster
 
 
 @pytest.mark.parametrize("binning", ["fused", "two_phase"])
@@ -61,7 +70,7 @@ def test_preprocess_and_binning_bitexact(gpu, h, w, sh_degree, binning, monkeypa
     radii = state.radii.cpu().numpy()
     gx, gy = (w + 15) // 16, (h + 15) // 16
     T = gx * gy
-    start, keys = _segments(state, len(orcs), T)
+    begin, end, keys = _segments(state, len(orcs), T)
     for v, o in enumerate(orcs):
         og = o.geom()
         np.testing.assert_array_equal(radii[v], og["radii"])
@@ -71,9 +80,9 @@ def test_preprocess_and_binning_bitexact(gpu, h, w, sh_degree, binning, monkeypa
         np.testing.assert_array_equal(geom[v, vis, 2:5], og["conic_opacity"][vis, :3])
         np.testing.assert_array_equal(geom[v, vis, 6:9], og["rgb"][vis])
         okeys, ovals, ranges = o.binning()
-        assert int(start[(v + 1) * T] - start[v * T]) == o.num_rendered
+        assert int(state.counts[v * T:(v + 1) * T].sum()) == o.num_rendered
         for t in range(T):
-            hk = keys[start[v * T + t]:start[v * T + t + 1]]
+            hk = keys[begin[v * T + t]:end[v * T + t]]
             ob, oe = ranges[t]
             # same Gaussians in the same (depth, id) order, same depth bits
             np.testing.assert_array_equal((hk & np.uint64(0xFFFFFFFF)).astype(np.uint32), ovals[ob:oe])
@@ -174,14 +183,18 @@ def _large_tile_scene(opacity_scale=0.05, constant_opacity=None):
 def _check_segments_vs_oracle(state, orcs, V, T):
     """Segment ids vs the oracle's sorted ids: all of them, or with prefix-sorted segments
     the sorted prefix exactly and the unordered tail as a set."""
-    start, keys = _segments(state, V, T)
+    begin, end, keys = _segments(state, V, T)
     srt = None if state.seg_sorted is None else state.seg_sorted.cpu().numpy()
     for v, o in enumerate(orcs):
         okeys, ovals, ranges = o.binning()
         for t in range(T):
             s = v * T + t
-            hk = (keys[start[s]:start[s + 1]] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+            hk = (keys[begin[s]:end[s]] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
             ob, oe = ranges[t]
+            if state.seg_stride == raster_mod().SEG_ENDS:  # depth cut: the head of the sorted list
+                assert len(hk) <= oe - ob
+                np.testing.assert_array_equal(hk, ovals[ob:ob + len(hk)])
+                continue
             if srt is None:
                 np.testing.assert_array_equal(hk, ovals[ob:oe])
                 continue
@@ -205,6 +218,7 @@ def test_large_tiles_sort_paths(gpu, binning, hint, prefix, monkeypatch):
     cap = _lib.load().dsr_sort_lds_capacity()
     if binning == "two_phase":
         monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+        monkeypatch.setattr(raster, "CUT_PREFIX", 0)  # full scatter (the depth cut has its own tests)
     monkeypatch.setattr(raster, "SORT_PREFIX", prefix)
     monkeypatch.setitem(raster._spec, "max_count", {"low": 1, "exact": 12288 + 8, "between": cap + 1}[hint])
     monkeypatch.setattr(raster, "_note_counts", lambda counts: None)  # keep the hint fixed
@@ -231,6 +245,7 @@ def test_prefix_sort_overflow_fixup(gpu, binning, monkeypatch):
     from my_depthsplat_amd import raster
     if binning == "two_phase":
         monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+        monkeypatch.setattr(raster, "CUT_PREFIX", 0)
     monkeypatch.setitem(raster._spec, "max_count", 12288 + 8)
     monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
     sc = _large_tile_scene(constant_opacity=0.0045)
@@ -243,8 +258,9 @@ def test_prefix_sort_overflow_fixup(gpu, binning, monkeypatch):
     st4 = runs[4096][3]
     assert st4.seg_overflow is not None
     big = st4.seg_count.cpu() > 4096
-    flagged = st4.seg_overflow.cpu() != 0
+    flagged = st4.seg_overflow.cpu()[:-1] != 0  # last word: the any-flag
     assert bool(flagged.any()) and not bool(flagged[~big].any())
+    assert int(st4.seg_overflow[-1]) == 1
     assert torch.equal(st4.seg_sorted.cpu()[flagged], st4.seg_count.cpu()[flagged])  # re-sorted in full
     for a, b in zip(runs[4096][:3], runs[0][:3]):
         assert torch.equal(a, b)
@@ -291,6 +307,94 @@ def test_prefix_sort_matches_full_sort(gpu, monkeypatch):
         assert torch.equal(a, b)
     for a, b in zip(fa[3:], fb[3:]):  # gradients: same terms, float atomics add them in any order
         assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max())
+
+
+def _forward_backward(sc, st, gpu):
+    from my_depthsplat_amd import raster
+    means, shs, opac, cov6 = flat_inputs(sc)
+    B, v = sc.target_extrinsics.shape[:2]
+    view_scene = [i // v for i in range(B * v)]
+    h, w = sc.image_shape
+    deg = math.isqrt(shs.shape[2]) - 1
+    cams = packed_cams(st, view_scene, (0.0, 0.0, 0.0)).to(gpu)
+    args = [t.to(gpu) for t in (means, shs, opac, cov6)]
+    color, state = raster.forward_raw(args[0], args[1], True, deg, args[2], args[3], cams, B * v, h, w)
+    dcolor = torch.linspace(-1, 1, color.numel(), device=gpu).view_as(color)
+    grads = raster.backward_raw(args[0], args[1], True, deg, args[2], args[3], cams, view_scene, state, dcolor,
+                                want_mean2d=True)
+    torch.cuda.synchronize()
+    return state, [color.cpu(), state.final_T.cpu(), state.n_contrib.cpu()] + [g.cpu() for g in grads if g is not None]
+
+
+@pytest.mark.parametrize("opacity", ["default", "faint"])
+def test_depth_cut_matches_full_scatter(gpu, opacity, monkeypatch):
+    """Two-phase binning with the depth cut (only the nearest ~CUT_PREFIX entries per tile are
+    written and sorted) vs the full scatter + full sort: forward outputs bit-identical,
+    gradients equal up to float-atomic order, written heads equal to the oracle's sorted
+    lists. default: the heads suffice (some tiles keep an unwritten tail, none is flagged);
+    faint (alpha just above 1/255, no pixel saturates): every cut tile is flagged, its tail
+    appended, the whole list sorted and the tile rendered again."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+    monkeypatch.setattr(raster, "SORT_PREFIX", 0)
+    sc = _large_tile_scene(opacity_scale=1.0) if opacity == "default" else _large_tile_scene(constant_opacity=0.0045)
+    st = settings_for(sc)
+    out = {}
+    for cutp in (1024, 0):
+        monkeypatch.setattr(raster, "CUT_PREFIX", cutp)
+        out[cutp] = _forward_backward(sc, st, gpu)
+    stc = out[1024][0]
+    assert stc.seg_stride == raster.SEG_ENDS and out[0][0].seg_stride == 0
+    written, counts = stc.written().cpu(), stc.counts.cpu().long()
+    flagged = stc.seg_overflow.cpu()[:-1] != 0
+    assert bool((written <= counts).all())
+    if opacity == "default":
+        assert bool((written < counts).any()) and not bool(flagged.any())
+        assert int(stc.seg_overflow[-1]) == 0
+    else:
+        assert bool(flagged.any()) and int(stc.seg_overflow[-1]) == 1
+        assert torch.equal(written[flagged], counts[flagged])  # completed and sorted in full
+        assert torch.equal(written[~flagged], counts[~flagged])  # tiles the cut kept whole
+    fa, fb = out[1024][1], out[0][1]
+    for a, b in zip(fa[:3], fb[:3]):  # forward: bit-identical
+        assert torch.equal(a, b)
+    for a, b in zip(fa[3:], fb[3:]):  # gradients: same terms, float atomics add them in any order
+        assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max())
+    orcs = oracle_views(sc, st)
+    _check_segments_vs_oracle(stc, orcs, 2, 4)
+    for v, o in enumerate(orcs):
+        oc, _, on = o.image()
+        assert float(np.abs(fa[0][v].numpy() - oc).mean()) < 1e-4
+        assert (fa[2][v].numpy() == on).mean() > 0.999
+        o.close()
+
+
+def test_depth_cut_multiview_scene_vs_oracle(gpu, monkeypatch):
+    """A scaled-down 6-view scene (6 x 128x224 context -> G = 172K, ~5K entries per tile):
+    the two-phase path with the depth cut writes a fraction of the entries, and the images,
+    n_contrib and written list heads still match the oracle (and the full scatter exactly)."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+    monkeypatch.setattr(raster, "SORT_PREFIX", 0)
+    sc = scene_inputs(h=128, w=224, n_ctx=6, n_tgt=2, seed=21)
+    st = settings_for(sc)
+    monkeypatch.setattr(raster, "CUT_PREFIX", 0)
+    full, _, _ = hip_forward(sc, st, gpu)
+    monkeypatch.setattr(raster, "CUT_PREFIX", 2048)
+    color, state, _ = hip_forward(sc, st, gpu)
+    assert state.seg_stride == raster.SEG_ENDS
+    written, counts = state.written().cpu(), state.counts.cpu().long()
+    assert int(written.sum()) < 0.8 * int(counts.sum())  # the cut wrote a fraction of the entries
+    assert torch.equal(color.cpu(), full.cpu())
+    orcs = oracle_views(sc, st)
+    gx, gy = (224 + 15) // 16, (128 + 15) // 16
+    _check_segments_vs_oracle(state, orcs, 2, gx * gy)
+    ncon = state.n_contrib.cpu().numpy()
+    for v, o in enumerate(orcs):
+        oc, _, on = o.image()
+        assert float(np.abs(color[v].cpu().numpy() - oc).mean()) < 1e-4
+        assert (ncon[v] == on).mean() > 0.999
+        o.close()
 
 
 def test_empty_and_culled(gpu):
@@ -389,11 +493,11 @@ def test_equal_depth_ties_sorted_by_id(gpu, n_ties):
     st = settings_for(sc)
     color, state, _ = hip_forward(sc, st, gpu)
     orcs = oracle_views(sc, st)
-    start, keys = _segments(state, 2, 16)
+    begin, end, keys = _segments(state, 2, 16)
     for v, o in enumerate(orcs):
         okeys, ovals, ranges = o.binning()
         for t in range(16):
-            hk = keys[start[v * 16 + t]:start[v * 16 + t + 1]]
+            hk = keys[begin[v * 16 + t]:end[v * 16 + t]]
             ob, oe = ranges[t]
             np.testing.assert_array_equal((hk & np.uint64(0xFFFFFFFF)).astype(np.uint32), ovals[ob:oe])
         oc, _, _ = o.image()
