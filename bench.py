@@ -42,8 +42,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--eager", action="store_true", help="time eager launches instead of hipGraph replays")
-    p.add_argument("--extra", default="train,dl3dv",
-                   help="secondary measurements: train (config C step), dl3dv (6-view 448x768 render); '' = none")
+    p.add_argument("--extra", default="train,dl3dv,recon12",
+                   help="secondary measurements: train (config C step), dl3dv (6-view 448x768 render), "
+                        "recon12 (12-view 512x960 reconstruction, 100 views in chunks of 10); '' = none")
     p.add_argument("--extra-steps", type=int, default=10)
     return p.parse_args()
 
@@ -152,6 +153,8 @@ def main():
         extra["train_config_c"] = train_leg(args, dev, rank, world, timed)
     if "dl3dv" in wanted:
         extra["render_config_d"] = dl3dv_leg(args, dev, rank, world, timed)
+    if "recon12" in wanted:
+        extra["recon_config_e"] = recon12_leg(args, dev, rank, world, timed)
     if rank == 0:
         line = {
             "metric": "rendered views/sec + PSNR, 2-view 256x256 RE10K, 1/2/4/8 MI355X",
@@ -267,6 +270,55 @@ def dl3dv_leg(args, dev, rank, world, timed):
     return {"workload": f"6-view {H}x{W} render, G={sc.gaussians.means.shape[1]}, {v} target views/scene, fp32",
             "ms_per_step": round(ms, 3), "views_per_s": round(v * world / (ms * 1e-3), 1), "steps": args.extra_steps,
             "n_gpus": world}
+
+
+def recon12_leg(args, dev, rank, world, timed):
+    """BASELINE.json configs[4]: 12-view 512x960 feed-forward reconstruction (G = 5,898,240
+    Gaussians from the fused adapter), then 100 target views rendered in chunks of 10
+    (render_chunk_size, README.md:198). One step = adapter + 10 decoder calls for one scene.
+    The reference's 0.6 s per scene on an A100 (README.md:105) also includes the encoder
+    network, which is out of scope here, so no ratio is reported. Per GPU; weak scaling."""
+    import torch
+
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg, gaussians_from_head
+    from my_depthsplat_amd.synthetic import context_cameras, target_cameras
+
+    V, H, W, v, chunk = 12, 512, 960, 100, 10
+    g = torch.Generator(device=dev).manual_seed(99 + rank)
+    adapter = GaussianAdapter(GaussianAdapterCfg(1e-10, 3.0, 2)).to(dev)
+    head = torch.randn(1, V, H * W, 3 + adapter.d_in, generator=g, device=dev)
+    depths = torch.rand(1, V, H * W, 1, 1, generator=g, device=dev) * 9 + 1
+    images = torch.rand(1, V, 3, H, W, generator=g, device=dev)
+    K = torch.tensor([[1.0, 0, 0.5], [0, 1.0, 0.5], [0, 0, 1]], device=dev)
+    ctx = context_cameras(V)[None].to(dev)
+    tgt = target_cameras(context_cameras(V), v)[None].to(dev)
+    ctx_k, tgt_k = K.expand(1, V, 3, 3).contiguous(), K.expand(1, v, 3, 3).contiguous()
+    near = torch.full((1, v), 0.5, device=dev)
+    far = torch.full((1, v), 100.0, device=dev)
+    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
+    out = torch.empty(1, v, 3, H, W, device=dev)
+
+    def step():
+        with torch.no_grad():
+            gs = gaussians_from_head(head, depths, images, ctx, ctx_k, adapter)
+            for c in range(0, v, chunk):
+                sl = slice(c, min(v, c + chunk))
+                out[:, sl] = dec(gs, tgt[:, sl], tgt_k[:, sl], near[:, sl], far[:, sl], (H, W)).color
+
+    step()
+    steps = max(2, args.extra_steps // 2)
+    el = timed(step, steps)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    ms = 1e3 * el / steps
+    return {"workload": f"{V}-view {H}x{W} reconstruction, G={V * H * W}, adapter + {v} target views in chunks of "
+                        f"{chunk} (encoder network out of scope), fp32",
+            "ms_per_scene": round(ms, 2), "views_per_s": round(v * world / (ms * 1e-3), 1), "steps": steps,
+            "n_gpus": world, "reference": "0.6 s per scene end to end on an A100 incl. the encoder (README.md:105)"}
 
 
 def cpu_leg(sc, out, args, H, W):

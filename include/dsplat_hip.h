@@ -102,7 +102,8 @@ int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M,
                     void* stream);
 
 /* Exclusive scan of seg_count[V*T] -> seg_start[V*T+1], seg_cursor[V*T] (= seg_start),
- * totals[0] = N (num_rendered over all views), totals[1] = max entries in one tile. */
+ * totals[0] = N (num_rendered over all views), totals[1] = max entries in one tile,
+ * totals[2] = 1 if N reached 2^31 (offsets invalid: render fewer views per call). */
 int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_start,
                  uint32_t* seg_cursor, uint32_t* totals, void* stream);
 

@@ -497,11 +497,12 @@ __global__ __launch_bounds__(1024) void k_scan(int n, const uint32_t* __restrict
                                                uint32_t* __restrict__ cursor,
                                                uint32_t* __restrict__ totals) {
   __shared__ uint32_t s_w[16];
-  __shared__ uint32_t s_carry, s_max;
+  __shared__ uint32_t s_carry, s_max, s_big;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid == 0) {
     s_carry = 0;
     s_max = 0;
+    s_big = 0;
   }
   __syncthreads();
   uint32_t my_max = 0;
@@ -520,7 +521,13 @@ __global__ __launch_bounds__(1024) void k_scan(int n, const uint32_t* __restrict
       cursor[i] = ex;
     }
     __syncthreads();
-    if (tid == 1023) s_carry = ex + x;
+    if (tid == 1023) {
+      const uint64_t c = (uint64_t)s_carry + (s_w[0] + s_w[1] + s_w[2] + s_w[3] + s_w[4] + s_w[5] + s_w[6] + s_w[7] +
+                                              s_w[8] + s_w[9] + s_w[10] + s_w[11] + s_w[12] + s_w[13] + s_w[14] +
+                                              (uint64_t)s_w[15]);
+      if (c >> 31) s_big = 1u;  // offsets past 2^31: the caller must split the batch
+      s_carry = ex + x;
+    }
     __syncthreads();
   }
   atomicMax(&s_max, my_max);
@@ -529,6 +536,7 @@ __global__ __launch_bounds__(1024) void k_scan(int n, const uint32_t* __restrict
     start[n] = s_carry;
     totals[0] = s_carry;
     totals[1] = s_max;
+    totals[2] = s_big;
   }
 }
 

@@ -97,6 +97,30 @@ def render_views(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch
     h, w = image_shape
     n = gaussian_sh_coefficients.shape[-1]
     degree = math.isqrt(n) - 1
+    try:
+        return _render_views(extrinsics, intrinsics, near, far, image_shape, background_color, gaussian_means,
+                             gaussian_covariances, gaussian_sh_coefficients, gaussian_opacities, view_scene,
+                             scale_invariant, use_sh, return_radii, degree)
+    except raster.EntryOverflow:
+        if V == 1:
+            raise
+    # more (view, tile, Gaussian) entries than 32-bit offsets address: render the views in halves
+    k = V // 2
+    parts = [render_views(extrinsics[sl], intrinsics[sl], near[sl], far[sl], image_shape, background_color[sl]
+                          if background_color.dim() > 1 else background_color, gaussian_means, gaussian_covariances,
+                          gaussian_sh_coefficients, gaussian_opacities, list(view_scene[sl]),
+                          scale_invariant=scale_invariant, use_sh=use_sh, return_radii=return_radii)
+             for sl in (slice(0, k), slice(k, V))]
+    if return_radii:
+        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+    return torch.cat(parts)
+
+
+def _render_views(extrinsics, intrinsics, near, far, image_shape, background_color, gaussian_means,
+                  gaussian_covariances, gaussian_sh_coefficients, gaussian_opacities, view_scene, scale_invariant,
+                  use_sh, return_radii, degree):
+    V = extrinsics.shape[0]
+    h, w = image_shape
     # the camera_settings() math, as one device kernel (no torch op chain, no host sync)
     # (it also zeroes the per-(view, tile) counters the binning kernel accumulates into)
     gx, gy = raster.tiles(h, w)

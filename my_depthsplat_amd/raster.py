@@ -125,6 +125,10 @@ def algorithmic_bytes(kernel: str, *, G: int, V: int, N: int, HW: int, T: int | 
     raise KeyError(kernel)
 
 
+class EntryOverflow(_lib.DsplatError):
+    """The batch has too many (view, tile, Gaussian) entries for 32-bit key offsets."""
+
+
 @dataclass
 class RasterState:
     """Everything the backward needs (all device tensors)."""
@@ -342,8 +346,11 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         if torch.cuda.is_current_stream_capturing():
             raise _lib.DsplatError(f"V*G*tiles = {V * G * T} key slots exceed KEY_BUDGET_BYTES: this size needs a "
                                    "host read-back and cannot be captured into a graph")
-        tot = totals[:2].cpu()  # one small read-back: N sizes the key buffer
+        tot = totals[:3].cpu()  # one small read-back: N sizes the key buffer
         N, maxc = int(tot[0]), int(tot[1])
+        if int(tot[2]):
+            raise EntryOverflow(f"{V} views x {G} Gaussians produce >= 2^31 (view, tile, Gaussian) entries: "
+                                "render fewer views per call")
         keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
         if sb > 0:
             # depth cut: write only each tile's nearest entries (cursor ends at their end)
