@@ -155,8 +155,10 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M,
 int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t prefix, uint32_t* cut,
                    void* stream);
 /* As dsr_bin_scatter, restricted by cut: tail = 0 -> entries with bucket <= cut; tail = 1 ->
- * entries with bucket > cut of the segments with seg_overflow[s] != 0 (seg_overflow has
- * V*T + 1 words; the last is the any-flag). seg_cursor advances past what is written. */
+ * entries with bucket > cut of the segments with seg_overflow[s] != 0. seg_overflow here has
+ * V*T + 1 + V*nsb words: tile flags, the any-flag, then per-(view, super-block) flags, all
+ * written by dsr_render_fwd in the DSR_SEG_ENDS layout. seg_cursor advances past what is
+ * written. */
 int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor,
                         uint64_t* keys, const uint32_t* cut, int tail, const uint32_t* seg_overflow,
                         void* stream);
@@ -198,7 +200,9 @@ uint32_t dsr_sort_lds_capacity(void);
  * seg_overflow and seg_sorted = NULL, which renders only those tiles. In the DSR_SEG_ENDS
  * layout (depth-cut binning) with seg_overflow given, a segment whose written end is below
  * seg_start[s+1] is flagged when any of its pixels is still live at that end. seg_overflow
- * has V*T + 1 words: the last one is set to 1 whenever any tile is flagged. */
+ * has V*T + 1 words, word V*T set to 1 whenever any tile is flagged; in the DSR_SEG_ENDS
+ * layout V*T + 1 + V*nsb words, the last V*nsb flagging the super-blocks of flagged tiles
+ * (dsr_preprocess_cut). */
 int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride,
                    const uint64_t* keys, const uint32_t* seg_sorted, uint32_t* seg_overflow,

@@ -588,6 +588,9 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
     __syncthreads();
   }
   const uint32_t* vov = CUT && tail ? seg_overflow + (size_t)v * T : nullptr;
+  const uint32_t* sbov = nullptr;  // flagged super-blocks of this view (tail pass)
+  if constexpr (CUT)
+    if (tail) sbov = seg_overflow + (size_t)V * T + 1 + (size_t)v * nsx * ((gy + sb - 1) / sb);
   // the cut: does the entry (tile t, key) belong to this pass?
   auto keep = [&](int t, int tx, int ty, uint64_t key) -> bool {
     if constexpr (!CUT) {
@@ -617,7 +620,7 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
           for (int sy = sy0; sy < sy1; ++sy)
             for (int sx = sx0; sx < sx1; ++sx) {
               const bool nearer = bk <= (int)s_cut[sy * nsx + sx];
-              any |= tail ? !nearer : nearer;
+              any |= tail ? (!nearer && sbov[sy * nsx + sx] != 0u) : nearer;
             }
           if (!any) r = 0;
         }
@@ -1796,6 +1799,11 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   if (void_tile && lane == 0) {  // the tile's output is void: completed, sorted and re-rendered by the caller
     seg_overflow[seg] = 1u;
     seg_overflow[(size_t)gridDim.z * T] = 1u;  // any-flag
+    if (absent_tail) {  // depth cut: also flag the tile's super-block (the tail scatter's pre-test)
+      const int sb = cut_superblock(gx, T / gx), sbl = __builtin_ctz((unsigned)sb);
+      const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((T / gx + sb - 1) / sb);
+      seg_overflow[(size_t)gridDim.z * T + 1 + (size_t)v * nsb + (blockIdx.y >> sbl) * nsx + (blockIdx.x >> sbl)] = 1u;
+    }
   }
   if (inside) {
     const size_t HW = (size_t)H * W;

@@ -325,7 +325,11 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                   lds_cap)
         _note_counts(seg_count)
     else:
-        sb = lib.dsr_cut_superblock(H, W) if CUT_PREFIX > 0 else 0
+        # the depth cut pays when tile lists are long; the previous two-phase call's largest
+        # list (None on the first call) decides whether this one builds the depth histogram
+        prev = _spec.get("two_phase_max")
+        want_cut = CUT_PREFIX > 0 and (prev is None or prev > 4 * CUT_PREFIX)
+        sb = lib.dsr_cut_superblock(H, W) if want_cut else 0
         if sb > 0:
             nsb = -(-gx // sb) * -(-gy // sb)
             hist = torch.empty(V * nsb * 128, dtype=torch.int32, device=dev)
@@ -348,10 +352,13 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                    "host read-back and cannot be captured into a graph")
         tot = totals[:3].cpu()  # one small read-back: N sizes the key buffer
         N, maxc = int(tot[0]), int(tot[1])
+        _spec["two_phase_max"] = maxc
         if int(tot[2]):
             raise EntryOverflow(f"{V} views x {G} Gaussians produce >= 2^31 (view, tile, Gaussian) entries: "
                                 "render fewer views per call")
         keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
+        if sb > 0 and maxc <= 2 * CUT_PREFIX:  # short lists after all: write everything
+            sb = 0
         if sb > 0:
             # depth cut: write only each tile's nearest entries (cursor ends at their end)
             scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev)  # only big segments touch it
@@ -378,8 +385,10 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
     outs = (color.data_ptr(), final_T.data_ptr(), n_contrib.data_ptr(), st)
     overflow = None
-    if seg_sorted is not None or stride == SEG_ENDS:
+    if seg_sorted is not None:
         overflow = torch.zeros(V * T + 1, dtype=torch.int32, device=dev)  # + the any-flag word
+    elif stride == SEG_ENDS:  # + any-flag + flags per (view, super-block)
+        overflow = torch.zeros(V * T + 1 + V * nsb, dtype=torch.int32, device=dev)
     _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
                       _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(), _ptr(seg_sorted),
                       _ptr(overflow), None, *outs), "dsr_render_fwd")
