@@ -130,12 +130,12 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
  *   1. dsr_preprocess_cut = dsr_preprocess_fwd + a per-(view, super-block) histogram of
  *      depth buckets (DSR_CUT_BUCKETS log-spaced buckets, 16 per octave of view depth from
  *      0.25 near-units, each Gaussian counted once per touched tile);
- *   2. dsr_bin_cutoff picks per (view, super-block) the nearest bucket whose cumulative count
+ *   2. dsr_bin_cutoff picks per (view, super-block) the depth at which the cumulative count
  *      reaches `prefix` entries per tile;
- *   3. dsr_bin_scatter_cut (tail = 0) emits only the entries at or before that bucket into the
+ *   3. dsr_bin_scatter_cut (tail = 0) emits only the entries at or before that depth into the
  *      prefix layout of dsr_bin_scan (full counts): seg_cursor ends at each segment's written
  *      end -> DSR_SEG_ENDS layout for dsr_bin_sort / dsr_render_fwd / dsr_render_bwd.
- * Every emitted entry is nearer than every omitted one (buckets are depth ranges), so the
+ * Every emitted entry is nearer than every omitted one (a depth threshold), so the
  * sorted written part IS the head of the full sorted list. dsr_render_fwd flags a tile whose
  * pixels are not all saturated at the end of its written part (seg_overflow[s] = 1 and
  * seg_overflow[V*T] = 1); dsr_bin_scatter_cut with tail = 1 then appends the omitted entries
@@ -151,11 +151,13 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* opacities, const float* cov6, const dsr_camera* cams,
                        float* geom, int32_t* radii, uint32_t* seg_count, uint32_t* depth_hist,
                        int layout, void* stream);
-/* cut [V, nsb] uint32: last bucket emitted per super-block (DSR_CUT_BUCKETS - 1 = all). */
+/* cut [V, nsb] uint32: per super-block, the largest depth (float bits) emitted: inside the
+ * bucket where the count reaches `prefix` per tile, interpolated by the fraction still
+ * needed (0xffffffff = all). */
 int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t prefix, uint32_t* cut,
                    void* stream);
-/* As dsr_bin_scatter, restricted by cut: tail = 0 -> entries with bucket <= cut; tail = 1 ->
- * entries with bucket > cut of the segments with seg_overflow[s] != 0. seg_overflow here has
+/* As dsr_bin_scatter, restricted by cut: tail = 0 -> entries with depth bits <= cut; tail = 1 ->
+ * the deeper entries of the segments with seg_overflow[s] != 0. seg_overflow here has
  * V*T + 1 + V*nsb words: tile flags, the any-flag, then per-(view, super-block) flags, all
  * written by dsr_render_fwd in the DSR_SEG_ENDS layout. seg_cursor advances past what is
  * written. */

@@ -553,53 +553,24 @@ __device__ __forceinline__ int depth_bucket(uint32_t zbits) {
 __host__ __device__ inline int cut_superblock(int gx, int gy) {
   for (int sb = 4; sb <= 64; sb *= 2) {
     const int nsb = ((gx + sb - 1) / sb) * ((gy + sb - 1) / sb);
-    if (gx * gy + nsb * kCutBuckets <= kCutLdsWords) return sb;
+    if ((gx + 1) * (gy + 1) + nsb * kCutBuckets <= kCutLdsWords) return sb;
   }
   return 0;
 }
 
-// K3: emit (depth, id) keys into their (view, tile) bucket. CUT: only the entries the
-// depth cut keeps (tail == 0: bucket <= cut of the tile's super-block; tail == 1: the others,
-// of flagged segments only).
-template <bool CUT>
+// K3: emit (depth, id) keys into their (view, tile) bucket.
 __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, const float* __restrict__ geom,
                                                 uint32_t* __restrict__ cursor,
-                                                uint64_t* __restrict__ keys, int lds_hist,
-                                                const uint32_t* __restrict__ cut, int tail,
-                                                const uint32_t* __restrict__ seg_overflow) {
+                                                uint64_t* __restrict__ keys, int lds_hist) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
-  __shared__ uint32_t s_cut[CUT ? kCutMaxSB : 1];
   int v, blk;
   if (!xcd_item((G + NT - 1) / NT, V, v, blk)) return;
   const int T = gx * gy;
-  if (CUT && tail && seg_overflow[(size_t)V * T] == 0u) return;  // no tile flagged (uniform)
   const int tid = threadIdx.x;
-  int sb = 1, sbl = 0, nsx = 1;
-  if constexpr (CUT) {
-    sb = cut_superblock(gx, gy);
-    sbl = __builtin_ctz((unsigned)sb);
-    nsx = (gx + sb - 1) / sb;
-    const int nsb = nsx * ((gy + sb - 1) / sb);
-    for (int s = tid; s < nsb; s += NT) s_cut[s] = cut[(size_t)v * nsb + s];
-    if (!lds_hist) __syncthreads();
-  }
   if (lds_hist) {
     for (int t = tid; t < T; t += NT) s_hist[t] = 0;
     __syncthreads();
   }
-  const uint32_t* vov = CUT && tail ? seg_overflow + (size_t)v * T : nullptr;
-  const uint32_t* sbov = nullptr;  // flagged super-blocks of this view (tail pass)
-  if constexpr (CUT)
-    if (tail) sbov = seg_overflow + (size_t)V * T + 1 + (size_t)v * nsx * ((gy + sb - 1) / sb);
-  // the cut: does the entry (tile t, key) belong to this pass?
-  auto keep = [&](int t, int tx, int ty, uint64_t key) -> bool {
-    if constexpr (!CUT) {
-      return true;
-    } else {
-      const bool nearer = depth_bucket((uint32_t)(key >> 32)) <= (int)s_cut[(ty >> sbl) * nsx + (tx >> sbl)];
-      return tail ? (!nearer && vov[t] != 0u) : nearer;
-    }
-  };
   const int g = blk * NT + tid;
   int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
   uint64_t key = 0;
@@ -609,22 +580,6 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
     if (r > 0) {
       tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
       key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
-      if constexpr (CUT) {
-        // whole-Gaussian pre-test over the super-blocks its rect touches (the cut keeps ~10%
-        // of the entries at 6x448x768, and most of the rest belong to Gaussians deeper than
-        // every cut they meet): skip the per-tile expansion when no tile can take it
-        const int sx0 = x0 >> sbl, sx1 = ((x1 - 1) >> sbl) + 1, sy0 = y0 >> sbl, sy1 = ((y1 - 1) >> sbl) + 1;
-        if ((sx1 - sx0) * (sy1 - sy0) <= 16) {
-          const int bk = depth_bucket((uint32_t)(key >> 32));
-          bool any = false;
-          for (int sy = sy0; sy < sy1; ++sy)
-            for (int sx = sx0; sx < sx1; ++sx) {
-              const bool nearer = bk <= (int)s_cut[sy * nsx + sx];
-              any |= tail ? (!nearer && sbov[sy * nsx + sx] != 0u) : nearer;
-            }
-          if (!any) r = 0;
-        }
-      }
     }
   }
   uint32_t* gcur = cursor + (size_t)v * T;
@@ -635,23 +590,83 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
   WaveRects& wr = s_wr[w];
   const uint64_t* wkey = s_key + w * 64;
   if (lds_hist) {
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
-      if (keep(t, tx, ty, wkey[o])) atomicAdd(&s_hist[t], 1u);
-    });
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
     __syncthreads();
     for (int t = tid; t < T; t += NT) {
       const uint32_t c = s_hist[t];
       if (c) s_hist[t] = atomicAdd(&gcur[t], c);
     }
     __syncthreads();
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
-      const uint64_t k = wkey[o];
-      if (keep(t, tx, ty, k)) keys[atomicAdd(&s_hist[t], 1u)] = k;
-    });
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
+                       [&](int t, int o) { keys[atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
   } else {
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
+                       [&](int t, int o) { keys[atomicAdd(&gcur[t], 1u)] = wkey[o]; });
+  }
+}
+
+// K3 under the depth cut (dsr_bin_scatter_cut): only the entries the cut keeps (tail == 0:
+// depth bits <= the threshold of the tile's super-block; tail == 1: the others, of flagged
+// tiles only).
+// Kept entries are few (~4-9 % at 6x448x768 and up), so there is no per-block LDS count /
+// reservation round (whose zero + flush of T counters per 256 Gaussians dominated): each
+// kept entry takes its slot with one global atomic on its segment cursor, and a persistent
+// grid (one view and a run of blocks per workgroup, no workgroup barrier in the loop) walks
+// the Gaussians. A whole-Gaussian pre-test over the super-blocks its rect touches skips the
+// expansion of Gaussians no tile keeps (most of them).
+template <int NTH>
+__global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int gy, const float* __restrict__ geom,
+                                                     uint32_t* __restrict__ cursor, uint64_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ cut, int tail,
+                                                     const uint32_t* __restrict__ seg_overflow, int per_view) {
+  constexpr int NW = NTH / 64;
+  __shared__ uint32_t s_cut[kCutMaxSB];
+  __shared__ WaveRects s_wr[NW];
+  __shared__ uint64_t s_key[NTH];
+  const int T = gx * gy;
+  if (tail && seg_overflow[(size_t)V * T] == 0u) return;  // no tile flagged (uniform)
+  const int v = blockIdx.x / per_view, p = blockIdx.x - v * per_view;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int sb = cut_superblock(gx, gy), sbl = __builtin_ctz((unsigned)sb);
+  const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((gy + sb - 1) / sb);
+  for (int k = tid; k < nsb; k += NTH) s_cut[k] = cut[(size_t)v * nsb + k];
+  __syncthreads();
+  const uint32_t* vov = seg_overflow ? seg_overflow + (size_t)v * T : nullptr;
+  const uint32_t* sbov = seg_overflow ? seg_overflow + (size_t)V * T + 1 + (size_t)v * nsb : nullptr;
+  uint32_t* gcur = cursor + (size_t)v * T;
+  const float* gv = geom + (size_t)v * G * GS;
+  WaveRects& wr = s_wr[w];
+  const uint64_t* wkey = s_key + w * 64;
+  const int nblk = (G + NTH - 1) / NTH;
+  const int b0 = (int)((int64_t)nblk * p / per_view), b1 = (int)((int64_t)nblk * (p + 1) / per_view);
+  for (int blk = b0; blk < b1; ++blk) {
+    const int g = blk * NTH + tid;
+    int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    uint64_t key = 0;
+    if (g < G) {
+      const float* rec = gv + (size_t)g * GS;
+      r = __float_as_int(rec[10]);
+      if (r > 0) {
+        tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
+        key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
+        const int sx0 = x0 >> sbl, sx1 = ((x1 - 1) >> sbl) + 1, sy0 = y0 >> sbl, sy1 = ((y1 - 1) >> sbl) + 1;
+        if ((sx1 - sx0) * (sy1 - sy0) <= 16) {
+          const uint32_t zb = (uint32_t)(key >> 32);
+          bool any = false;
+          for (int sy = sy0; sy < sy1; ++sy)
+            for (int sx = sx0; sx < sx1; ++sx) {
+              const bool nearer = zb <= s_cut[sy * nsx + sx];
+              any |= tail ? (!nearer && sbov[sy * nsx + sx] != 0u) : nearer;
+            }
+          if (!any) r = 0;
+        }
+      }
+    }
+    s_key[tid] = key;
     for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
       const uint64_t k = wkey[o];
-      if (keep(t, tx, ty, k)) keys[atomicAdd(&gcur[t], 1u)] = k;
+      const bool nearer = (uint32_t)(k >> 32) <= s_cut[(ty >> sbl) * nsx + (tx >> sbl)];
+      if (tail ? (!nearer && vov[t] != 0u) : nearer) keys[atomicAdd(&gcur[t], 1u)] = k;
     });
   }
 }
@@ -659,7 +674,10 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
 // K1 + depth histogram (dsr_preprocess_cut). NTH threads per workgroup; each workgroup owns
 // one view and a contiguous run of NTH-Gaussian blocks (a persistent grid sized to the
 // resident capacity), so its LDS count and depth histograms are flushed to HBM once for many
-// blocks instead of once per block. Depth histogram: per super-block of sb x sb tiles, each
+// blocks instead of once per block. Per-tile counts: each Gaussian adds its tile rect to a
+// (gx+1) x (gy+1) difference grid (4 LDS atomics instead of one per touched tile: ~34 at
+// 12x512x960); the flush turns it into counts with a 2D prefix sum. Depth histogram: per
+// super-block of sb x sb tiles, each
 // (Gaussian, touched super-block) adds the number of its tiles inside that super-block to
 // the bucket of its depth (super-blocks, not tiles: at 6x448x768 a 16-tile super-block
 // keeps the whole view's histogram in 43 KiB of LDS).
@@ -682,11 +700,12 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
   const int T = gx * gy;
   const int sb = cut_superblock(gx, gy), sbl = __builtin_ctz((unsigned)sb);
   const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((gy + sb - 1) / sb);
-  uint32_t* s_cnt = s_mem;
-  uint32_t* s_dh = s_mem + T;
+  const int gxp = gx + 1, gyp = gy + 1;
+  uint32_t* s_dif = s_mem;  // [gyp][gxp] difference grid of the tile rects
+  uint32_t* s_dh = s_mem + gxp * gyp;
   const int v = blockIdx.x / per_view, p = blockIdx.x - v * per_view;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int k = tid; k < T + nsb * kCutBuckets; k += NTH) s_mem[k] = 0u;
+  for (int k = tid; k < gxp * gyp + nsb * kCutBuckets; k += NTH) s_mem[k] = 0u;
   __syncthreads();
   const dsr_camera* cam = cams + v;
   const int nblk = (G + NTH - 1) / NTH;
@@ -704,7 +723,12 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
       store_geom(geom, radii, (size_t)v * G + g, rec, r);
       zb = __float_as_uint(rec[9]);
     }
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_cnt[t], 1u); });
+    if (r > 0) {
+      atomicAdd(&s_dif[y0 * gxp + x0], 1u);
+      atomicAdd(&s_dif[y0 * gxp + x1], 0xFFFFFFFFu);
+      atomicAdd(&s_dif[y1 * gxp + x0], 0xFFFFFFFFu);
+      atomicAdd(&s_dif[y1 * gxp + x1], 1u);
+    }
     s_rx[w][lane] = (uint32_t)x0 | ((uint32_t)x1 << 16);
     s_ry[w][lane] = (uint32_t)y0 | ((uint32_t)y1 << 16);
     s_bk[w][lane] = (uint32_t)depth_bucket(zb);
@@ -718,9 +742,28 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
     });
   }
   __syncthreads();
+  // 2D inclusive prefix sum of the difference grid: rows (odd stride gxp: no bank conflicts
+  // when gx is even), then columns -> s_dif[ty][tx] = rects covering tile (tx, ty)
+  for (int y = tid; y < gyp; y += NTH) {
+    uint32_t acc = 0u;
+    for (int x = 0; x < gxp; ++x) {
+      acc += s_dif[y * gxp + x];
+      s_dif[y * gxp + x] = acc;
+    }
+  }
+  __syncthreads();
+  for (int x = tid; x < gxp; x += NTH) {
+    uint32_t acc = 0u;
+    for (int y = 0; y < gyp; ++y) {
+      acc += s_dif[y * gxp + x];
+      s_dif[y * gxp + x] = acc;
+    }
+  }
+  __syncthreads();
   uint32_t* gc = seg_count + (size_t)v * T;
   for (int t = tid; t < T; t += NTH) {
-    const uint32_t c = s_cnt[t];
+    const int ty = t / gx;
+    const uint32_t c = s_dif[ty * gxp + (t - ty * gx)];
     if (c) atomicAdd(&gc[t], c);
   }
   uint32_t* gh = depth_hist + (size_t)v * nsb * kCutBuckets;
@@ -730,8 +773,9 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
   }
 }
 
-// One wave per (view, super-block): the nearest bucket at which the super-block's cumulative
-// entry count reaches `prefix` per tile (kCutBuckets - 1, i.e. everything, if it never does).
+// One wave per (view, super-block): the depth (as float bits) at which the super-block's
+// cumulative entry count reaches `prefix` per tile (0xffffffff, i.e. everything, if it never
+// does).
 __global__ __launch_bounds__(256) void k_bin_cutoff(int V, int gx, int gy, const uint32_t* __restrict__ hist,
                                                     uint32_t prefix, uint32_t* __restrict__ cut) {
   const int sb = cut_superblock(gx, gy);
@@ -747,14 +791,25 @@ __global__ __launch_bounds__(256) void k_bin_cutoff(int V, int gx, int gy, const
   const uint32_t incl = dsplat::wave_incl_scan(a + b, lane);
   const uint32_t before = incl - (a + b);
   const uint64_t reach = __ballot((uint64_t)incl >= target);
-  uint32_t c = kCutBuckets - 1;
+  // the threshold: inside the reaching bucket, interpolated linearly in the depth bits by the
+  // fraction of its count still needed (entries spread about evenly across one 1/16 octave),
+  // so the written heads come out near `prefix` instead of a whole bucket above it
+  uint32_t thr = 0xffffffffu;  // never reached (or the open last bucket): keep everything
   if (reach) {
     const int L = __ffsll((unsigned long long)reach) - 1;
     const uint32_t bL = (uint32_t)__shfl((int)before, L, 64);
     const uint32_t aL = (uint32_t)__shfl((int)a, L, 64);
-    c = 2u * L + ((uint64_t)bL + aL >= target ? 0u : 1u);
+    const uint32_t hL = (uint32_t)__shfl((int)b, L, 64);
+    const bool first = (uint64_t)bL + aL >= target;
+    const int c = 2 * L + (first ? 0 : 1);
+    const uint32_t below = first ? bL : bL + aL, inb = first ? aL : hL;
+    if (c < kCutBuckets - 1) {
+      const float f = fminf(1.f, (float)(target - below) / (float)max(inb, 1u));
+      thr = ((uint32_t)(c + (125 << 4)) << 19) + (uint32_t)(f * 524287.f);
+      if (c == 0) thr = max(thr, 0x3E800000u);  // bucket 0 also holds everything nearer than 0.25
+    }
   }
-  if (lane == 0) cut[item] = c;
+  if (lane == 0) cut[item] = thr;
 }
 
 // ------------------------------------------------------------------------------------
@@ -2407,8 +2462,8 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
   DSPLAT_REQUIRE(geom && seg_cursor, "dsr_bin_scatter: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   const int lds = lds_hist_bytes(gx * gy);
-  k_scatter<false><<<xcd_grid((G + NT - 1) / NT, V), NT, lds, (hipStream_t)stream>>>(
-      G, V, gx, gy, geom, seg_cursor, keys, lds > 0, nullptr, 0, nullptr);
+  k_scatter<<<xcd_grid((G + NT - 1) / NT, V), NT, lds, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor, keys,
+                                                                              lds > 0);
   return dsplat::check_launch("k_scatter");
 }
 
@@ -2436,7 +2491,7 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, 
     if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
   if (int e = dsplat::zero_async(depth_hist, (size_t)V * nsb * kCutBuckets * 4, st, "zero depth_hist")) return e;
   constexpr int kNTH = 512;
-  const size_t lds = (size_t)(T + nsb * kCutBuckets) * 4;
+  const size_t lds = (size_t)((gx + 1) * (gy + 1) + nsb * kCutBuckets) * 4;
   // persistent grid: about the resident workgroup count (LDS-limited), split evenly over views
   const int per_cu = max(1, min(4, (int)((160 * 1024) / (lds + 8 * 1024))));
   const int nblk = (G + kNTH - 1) / kNTH;
@@ -2485,9 +2540,11 @@ int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t*
   DSPLAT_REQUIRE(geom && seg_cursor && keys && cut && (!tail || seg_overflow), "dsr_bin_scatter_cut: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   DSPLAT_REQUIRE(cut_superblock(gx, gy) > 0, "dsr_bin_scatter_cut: %dx%d tiles exceed the LDS histograms", gx, gy);
-  const int lds = lds_hist_bytes(gx * gy);
-  k_scatter<true><<<xcd_grid((G + NT - 1) / NT, V), NT, lds, (hipStream_t)stream>>>(
-      G, V, gx, gy, geom, seg_cursor, keys, lds > 0, cut, tail, seg_overflow);
+  constexpr int kNTH = 256;
+  const int per_view = max(1, min((G + kNTH - 1) / kNTH, (256 * 8) / V));
+  k_scatter_cut<kNTH><<<(unsigned)(V * per_view), kNTH, 0, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor,
+                                                                                  keys, cut, tail, seg_overflow,
+                                                                                  per_view);
   return dsplat::check_launch("k_scatter_cut");
 }
 

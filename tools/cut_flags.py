@@ -43,7 +43,7 @@ gx, gy = raster.tiles(H, W)
 T = gx * gy
 cnt = st.counts.cpu().long()
 wr = st.written().cpu()
-ov = st.seg_overflow.cpu()[:-1].bool() if st.seg_overflow is not None else torch.zeros(n * T, dtype=torch.bool)
+ov = st.seg_overflow.cpu()[:n * T].bool() if st.seg_overflow is not None else torch.zeros(n * T, dtype=torch.bool)
 print(f"N={int(cnt.sum())} per view {int(cnt.sum()) // n}, written {int(wr.sum())} ({float(wr.sum() / cnt.sum()):.3f}), "
       f"flagged tiles {int(ov.sum())} of {n * T}")
 ft = torch.nonzero(ov).flatten()
