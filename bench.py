@@ -143,7 +143,8 @@ def main():
                 "traffic_source": traffic_src,
                 "avg_ms": round(avg_ms, 5), "algorithmic_bytes_per_launch": alg,
                 "launches_timed": launches,
-                "per_kernel_avg_ms_probe": {k: round(v[1], 5) for k, v in sorted(all_kernels.items())}}
+                "per_kernel_avg_ms_probe": {k: round(v[1], 5) for k, v in sorted(all_kernels.items())},
+                "valu_issue": pmc_valu(name, f"{args.context}v{H}x{W}x{args.views}b{args.batch}", avg_ms)}
         psnr, l1, cpu = None, None, None
         if not args.no_cpu_baseline:
             psnr, l1, cpu = cpu_leg(sc, out, args, H, W)
@@ -188,6 +189,25 @@ def pmc_traffic(kernel, workload):
     if d.get("workload") != workload or rec is None:
         return None, None
     return int(rec["hbm_bytes"]), f"profiles/pmc_traffic.json ({d.get('source', '')})"
+
+
+def pmc_valu(kernel, workload, avg_ms):
+    """VALU issue rate of `kernel`: SQ_INSTS_VALU per launch (wave-level instructions, from
+    the committed PMC summary of the same workload) over its live average duration, against
+    the chip's issue peak (256 CUs x 4 SIMDs, a wave64 VALU instruction every 4 cycles of a
+    16-lane SIMD at ~2.4 GHz: 614 G wave-instructions/s). The compositor is issue / latency
+    bound, not HBM bound; this is its roofline on the resource that binds."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    d = json.loads(f.read_text())
+    rec = d.get("kernels", {}).get(kernel)
+    if d.get("workload") != workload or rec is None or "SQ_INSTS_VALU" not in rec:
+        return None
+    peak = 256 * 4 * 2.4e9 / 4 / 1e9  # G wave-instructions / s
+    ach = rec["SQ_INSTS_VALU"] / (avg_ms * 1e-3) / 1e9
+    return {"achieved": round(ach, 1), "peak": peak, "unit": "G wave-instr/s", "frac": round(ach / peak, 4),
+            "valu_instr_per_launch": int(rec["SQ_INSTS_VALU"]), "source": "profiles/pmc_traffic.json"}
 
 
 def train_leg(args, dev, rank, world, timed):

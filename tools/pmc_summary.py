@@ -29,12 +29,14 @@ def summarize(dirs):
 
 def traffic(summary):
     """Per-kernel HBM bytes per launch: FETCH_SIZE (KiB) x 2 (gfx950 reports half of a wide
-    streaming read, MI355X_MICROARCH.md HBM section) + WRITE_SIZE (KiB)."""
+    streaming read, MI355X_MICROARCH.md HBM section) + WRITE_SIZE (KiB); plus the SQ
+    instruction / wave counters per launch when a pass collected them."""
     out = {}
     for k, d in summary.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             fb, wb = 2 * 1024 * d["FETCH_SIZE"], 1024 * d["WRITE_SIZE"]
             out[k] = {"fetch_bytes_corrected": int(fb), "write_bytes": int(wb), "hbm_bytes": int(fb + wb)}
+            out[k].update({c: round(v, 1) for c, v in d.items() if c.startswith("SQ_")})
     return out
 
 

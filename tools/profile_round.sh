@@ -18,7 +18,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv 
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT \
   --output-format csv -d $out/sq -o run -- \
   python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --eager --extra "" > $out/sq.log 2>&1
-python3 tools/pmc_summary.py --json $out/pmc_traffic.json 2v256x256x3b1 "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, $tag" \
-  $out/fetch $out/write
+python3 tools/pmc_summary.py --json $out/pmc_traffic.json 2v256x256x3b1 "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ, $tag" \
+  $out/fetch $out/write $out/sq
 python3 tools/pmc_summary.py $out/fetch $out/write $out/sq > $out/pmc_summary.json
 echo done
