@@ -30,6 +30,15 @@ constexpr uint32_t kSortCap = 8192;           // max keys sorted in LDS (2 x 64 
 #define SORT_NTH 256
 #endif
 constexpr int kSortNT = SORT_NTH;  // threads per segment in the LDS sort
+#ifndef SORT_NBIN_LOG2
+#define SORT_NBIN_LOG2 13
+#endif
+// LDS words of the sort's counter area: the LSD passes' u16 counters (16 per thread) or the
+// counting sort's u16 bins, whichever is larger
+template <int NTH>
+constexpr int sort_cnt_words() {
+  return NTH * 8 > (1 << SORT_NBIN_LOG2) / 2 ? NTH * 8 : (1 << SORT_NBIN_LOG2) / 2;
+}
 constexpr int kHistLdsMax = 32768;            // tiles per view histogrammed in LDS
 
 constexpr float SH_C0 = 0.28209479177387814f;
@@ -1051,50 +1060,16 @@ __device__ bool reg_pass(uint64_t* buf, uint32_t n, int word_shift, uint32_t dba
 // range are common to every key and bits below the window only order keys inside a run, so
 // this is the full (depth, id) order. Runs longer than 32 (depths packed far tighter than the
 // segment's range) fall back to full-width passes: ids, then all 32 depth bits (stable).
+// Runs of keys that agree on ((depth - mn) >> shift) are put in full-key order: thread t
+// walks the runs that start in its KMAX positions and insertion-sorts each (full 64-bit keys;
+// runs may extend past its range). Runs longer than 32 (depths packed far tighter than the
+// window resolves) fall back to full-width LSD passes: ids, then all 32 depth bits (stable).
 template <int KMAX, int NTH = NT>
-__device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, uint32_t* wsum, uint32_t* flag) {
-  const int tid = threadIdx.x;
-  uint32_t mn = 0xffffffffu, mx = 0u;
-  for (uint32_t i = tid; i < n; i += NTH) {
-    const uint32_t d = (uint32_t)(A[padi<KMAX>(i)] >> 32);
-    mn = min(mn, d);
-    mx = max(mx, d);
-  }
-  // block min / max: wave shuffles, then 4 wave results through LDS (flag[0..7])
-  const int lane = tid & 63, w = tid >> 6;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
-    mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
-  }
+__device__ void fix_runs(uint64_t* A, uint32_t n, uint32_t mn, int shift, int id_bits, uint16_t* cnt, uint32_t* wsum,
+                         uint32_t* flag) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr int NW = NTH / 64;
-  if (lane == 0) {
-    flag[w] = mn;
-    flag[NW + w] = mx;
-  }
-  __syncthreads();
-  mn = flag[0];
-  mx = flag[NW];
-#pragma unroll
-  for (int k = 1; k < NW; ++k) {
-    mn = min(mn, flag[k]);
-    mx = max(mx, flag[NW + k]);
-  }
-  __syncthreads();
-  const uint32_t range = mx - mn;
-  const int msb = range ? 31 - __clz(range) : -1;
-  const int lo_shift = max(0, msb - 15);
-#ifdef SORT_DIAG_NOPASS
-  if (n > 100000)
-#endif
-  for (int sh = lo_shift; sh <= msb; sh += 4) reg_pass<KMAX, NTH>(A, n, 32, mn, sh, cnt, wsum);
-#ifdef SORT_DIAG_NOFIX
-  if (n < 100000) return;
-#endif
-#define pref(i) ((((uint32_t)(A[padi<KMAX>(i)] >> 32)) - mn) >> lo_shift)
-  // runs of keys equal on (depth - mn) >> lo_shift: thread t walks the runs that start in
-  // its KMAX positions and insertion-sorts each (full 64-bit keys; runs may extend past its
-  // range); the longest run decides whether the window was too coarse
+#define pref(i) ((((uint32_t)(A[padi<KMAX>(i)] >> 32)) - mn) >> shift)
   uint32_t longest = 0;
   {
     // prefixes of positions i0 - 1 .. i0 + KMAX (independent LDS reads, all in flight)
@@ -1153,6 +1128,153 @@ __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, ui
 #undef pref
 }
 
+// block min / max of the keys' depth words (flag[0 .. 2 NW) scratch; two barriers)
+template <int NTH>
+__device__ __forceinline__ void block_minmax(uint32_t& mn, uint32_t& mx, uint32_t* flag) {
+  constexpr int NW = NTH / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+  }
+  if (lane == 0) {
+    flag[w] = mn;
+    flag[NW + w] = mx;
+  }
+  __syncthreads();
+  mn = flag[0];
+  mx = flag[NW];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) {
+    mn = min(mn, flag[k]);
+    mx = max(mx, flag[NW + k]);
+  }
+  __syncthreads();
+}
+
+// Sort of one segment in LDS. Keys are (depth bits << 32 | id), all distinct. The passes
+// only look at the 16 bits of (depth - min depth) below the highest bit in which the
+// segment's depths differ (4 passes instead of 8); fix_runs then orders keys equal on those bits.
+template <int KMAX, int NTH = NT>
+__device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, uint32_t* wsum, uint32_t* flag) {
+  const int tid = threadIdx.x;
+  uint32_t mn = 0xffffffffu, mx = 0u;
+  for (uint32_t i = tid; i < n; i += NTH) {
+    const uint32_t d = (uint32_t)(A[padi<KMAX>(i)] >> 32);
+    mn = min(mn, d);
+    mx = max(mx, d);
+  }
+  block_minmax<NTH>(mn, mx, flag);
+  const uint32_t range = mx - mn;
+  const int msb = range ? 31 - __clz(range) : -1;
+  const int lo_shift = max(0, msb - 15);
+  for (int sh = lo_shift; sh <= msb; sh += 4) reg_pass<KMAX, NTH>(A, n, 32, mn, sh, cnt, wsum);
+  fix_runs<KMAX, NTH>(A, n, mn, lo_shift, id_bits, cnt, wsum, flag);
+}
+
+// One-pass alternative: a counting sort on the top 12 bits of (depth - min) — a 4096-bin
+// histogram (u16 counts, two per LDS word), its scan, and one scatter — then every key ranks
+// itself inside its bin. With ~3K keys over 4096 bins most bins hold 0-2 keys: 6 barriers
+// and no serial insertion chains (the LSD passes + fix_runs took 35 us per launch at 2x256^2,
+// 21 of them in fix_runs). The keys come in registers (thread t holds keys t + i NTH).
+template <int KMAX, int NTH = NT>
+__device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A, int id_bits, uint16_t* cnt,
+                           uint32_t* wsum, uint32_t* flag) {
+  constexpr int NBIN = 1 << SORT_NBIN_LOG2, BPT = NBIN / NTH;  // bins per thread in the scan
+  static_assert(BPT % 2 == 0 && NTH * KMAX < 65536 && NBIN / 2 <= sort_cnt_words<NTH>(), "u16 bin pairs in cnt");
+  uint32_t* hw = reinterpret_cast<uint32_t*>(cnt);  // NBIN / 2 words (cnt holds NTH * 16 u16)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t mn = 0xffffffffu, mx = 0u;
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i)
+    if (tid + (uint32_t)i * NTH < n) {
+      const uint32_t d = (uint32_t)(tmp[i] >> 32);
+      mn = min(mn, d);
+      mx = max(mx, d);
+    }
+  for (int k = tid; k < NBIN / 2; k += NTH) hw[k] = 0u;
+  block_minmax<NTH>(mn, mx, flag);
+  const uint32_t range = mx - mn;
+  const int shift = max(0, (range ? 31 - __clz(range) : 0) - (SORT_NBIN_LOG2 - 1));
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i)
+    if (tid + (uint32_t)i * NTH < n) {
+      const uint32_t bin = ((uint32_t)(tmp[i] >> 32) - mn) >> shift;
+      atomicAdd(&hw[bin >> 1], 1u << ((bin & 1u) * 16u));
+    }
+  __syncthreads();
+  {
+    uint32_t wd[BPT / 2], tot = 0;
+#pragma unroll
+    for (int q = 0; q < BPT / 2; ++q) {
+      wd[q] = hw[tid * (BPT / 2) + q];
+      tot += (wd[q] & 0xFFFFu) + (wd[q] >> 16);
+    }
+    const uint32_t incl = dsplat::wave_incl_add_dpp(tot);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t off = incl - tot;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+#pragma unroll
+    for (int q = 0; q < BPT / 2; ++q) {
+      const uint32_t lo = wd[q] & 0xFFFFu, hi = wd[q] >> 16;
+      hw[tid * (BPT / 2) + q] = off | ((off + lo) << 16);
+      off += lo + hi;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i)
+    if (tid + (uint32_t)i * NTH < n) {
+      const uint32_t bin = ((uint32_t)(tmp[i] >> 32) - mn) >> shift;
+      const uint32_t s16 = (bin & 1u) * 16u;
+      const uint32_t pos = (atomicAdd(&hw[bin >> 1], 1u << s16) >> s16) & 0xFFFFu;
+      A[padi<KMAX>(pos)] = tmp[i];
+    }
+  __syncthreads();
+#ifdef SORT_DIAG_NOFIX  // timing experiment: skip ordering inside bins
+  return;
+#endif
+  // order inside each bin: the scatter left hw holding every bin's END offset, so bin b is
+  // [end(b - 1), end(b)). A key of a bin of c <= 16 keys counts the smaller keys of its bin
+  // (c independent LDS reads, all lanes in parallel); any larger bin (clustered or equal
+  // depths) sends the whole segment through the LSD passes instead.
+#ifndef SORT_BINMAX
+#define SORT_BINMAX 16
+#endif
+  constexpr uint32_t kBinMax = SORT_BINMAX;
+  auto bin_end = [&](uint32_t b) -> uint32_t {
+    const uint32_t wv = hw[b >> 1];
+    return (b & 1u) ? (wv >> 16) : (wv & 0xFFFFu);
+  };
+  uint32_t dest[KMAX];
+  bool big = false;
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    dest[i] = 0u;
+    if (tid + (uint32_t)i * NTH < n) {
+      const uint32_t bin = ((uint32_t)(tmp[i] >> 32) - mn) >> shift;
+      const uint32_t e = bin_end(bin), st = bin ? bin_end(bin - 1u) : 0u;
+      uint32_t r = 0;
+      if (e - st > kBinMax) {
+        big = true;
+      } else if (e - st > 1u) {
+        for (uint32_t j = st; j < e; ++j) r += A[padi<KMAX>(j)] < tmp[i] ? 1u : 0u;
+      }
+      dest[i] = st + r;
+    }
+  }
+  if (__syncthreads_or(big)) {  // A holds the keys grouped by bin: sort it outright
+    reg_sort<KMAX, NTH>(A, n, id_bits, cnt, wsum, flag);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i)
+    if (tid + (uint32_t)i * NTH < n) A[padi<KMAX>(dest[i])] = tmp[i];
+  __syncthreads();
+}
+
 // One workgroup per (view, tile) segment. n <= 256*KMAX: sort in LDS. Larger: when
 // big_here, sort through HBM (keys <-> scratch) with the ballot-ranked passes; otherwise
 // leave it to the MSD split (k_msd_split + k_sort_groups).
@@ -1171,7 +1293,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(KMAX * NTH 
   uint64_t* A = s_keys;
   uint32_t* aux = reinterpret_cast<uint32_t*>(A + padded);  // 8 KiB counters (u16) / HBM-path histogram
   uint16_t* cnt = reinterpret_cast<uint16_t*>(aux);
-  uint32_t* wsum = aux + NTH * 8;
+  uint32_t* wsum = aux + sort_cnt_words<NTH>();
   uint32_t* flag = wsum + 16;
   const int seg = blockIdx.x;
   if (filter && !filter[seg]) return;
@@ -1192,16 +1314,25 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(KMAX * NTH 
       const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
       tmp[i] = idx < n ? keys[b + idx] : 0ull;
     }
+#ifdef SORT_LSD  // the 4-pass LSD sort (kept for comparison runs)
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
       const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
       if (idx < n) A[padi<KMAX>(idx)] = tmp[i];
     }
-  }
-  __syncthreads();
-#ifndef SORT_DIAG_NOSORT
-  reg_sort<KMAX, NTH>(A, n, id_bits, cnt, wsum, flag);
+    __syncthreads();
+    reg_sort<KMAX, NTH>(A, n, id_bits, cnt, wsum, flag);
+#elif defined(SORT_DIAG_NOSORT)  // timing experiment: load + store only
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
+      if (idx < n) A[padi<KMAX>(idx)] = tmp[i];
+    }
+    __syncthreads();
+#else
+    count_sort<KMAX, NTH>(tmp, n, A, id_bits, cnt, wsum, flag);
 #endif
+  }
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
     const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
@@ -1211,7 +1342,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(KMAX * NTH 
 
 template <int KMAX, int NTH = NT>
 constexpr size_t sort_lds_bytes() {
-  return (size_t)(NTH * KMAX + NTH) * 8 + (size_t)NTH * 32 + 64 * 4;
+  return (size_t)(NTH * KMAX + NTH) * 8 + (size_t)sort_cnt_words<NTH>() * 4 + 64 * 4;
 }
 
 // ---- segments larger than the LDS sort (6-view 448x768 and up: ~30-40K entries per tile) --
