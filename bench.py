@@ -201,10 +201,18 @@ def pmc_traffic(kernel, workload):
     if not f.exists():
         return None, None
     d = json.loads(f.read_text())
-    rec = d.get("kernels", {}).get(kernel)
+    rec = _pmc_record(d, kernel)
     if d.get("workload") != workload or rec is None:
         return None, None
     return int(rec["hbm_bytes"]), f"profiles/pmc_traffic.json ({d.get('source', '')})"
+
+
+def _pmc_record(d, kernel):
+    """The PMC entry of `kernel` (template instantiations are listed as name<args>)."""
+    ks = d.get("kernels", {})
+    if kernel in ks:
+        return ks[kernel]
+    return next((v for k, v in ks.items() if k.startswith(kernel + "<")), None)
 
 
 def pmc_valu(kernel, workload, avg_ms):
@@ -217,7 +225,7 @@ def pmc_valu(kernel, workload, avg_ms):
     if not f.exists():
         return None
     d = json.loads(f.read_text())
-    rec = d.get("kernels", {}).get(kernel)
+    rec = _pmc_record(d, kernel)
     if d.get("workload") != workload or rec is None or "SQ_INSTS_VALU" not in rec:
         return None
     peak = 256 * 4 * 2.4e9 / 4 / 1e9  # G wave-instructions / s

@@ -211,6 +211,16 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
                    const uint32_t* seg_filter, float* out_color, float* final_T, uint32_t* n_contrib,
                    void* stream);
 
+/* dsr_bin_sort + dsr_render_fwd in one launch (no prefix / cut modes): each workgroup sorts its
+ * tile's keys in LDS and composites from that copy; segments above 4096 entries are sorted
+ * through `scratch` (same size as keys) by the same workgroup. The sorted keys are written
+ * back to `keys` only when write_keys != 0 (dsr_render_bwd needs them). Outputs as
+ * dsr_render_fwd. */
+int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
+                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
+                    uint64_t* scratch, int write_keys, float* out_color, float* final_T, uint32_t* n_contrib,
+                    void* stream);
+
 /* ---- rasterizer backward -----------------------------------------------------------
  * Back-to-front per tile (K7). dL_dpix [V,3,H,W]. Accumulates into dgeom [V,G,12]
  * (caller zeroes): [0..1] dL/dxy (ndc scale, as upstream dL_dmean2D), [2..4] dL/dconic,

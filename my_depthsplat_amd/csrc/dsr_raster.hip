@@ -1810,16 +1810,113 @@ __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* 
   return false;
 }
 
+// K6 core: one wave composites its 8x8 sub-tile (pixel (px, py) per lane) front to back
+// over the sorted entries [start, end) of its tile, key_at(e) giving entry e's Gaussian id
+// (from HBM keys, or from the fused sort's LDS). The wave walks the list CH entries at a time
+// (EPL keys + records per lane, the next chunk's records and the chunk after's keys already
+// in flight), keeps the entries that can reach its live pixels in a wave-private LDS list
+// (ballot compaction, list order kept, entry pairs field-interleaved for packed math, 8
+// zero-opacity pad entries after the end), and composites that list four entries per step
+// with the next four read ahead. It returns as soon as its 64 pixels have terminated.
+template <typename KeyAt>
+__device__ __forceinline__ void composite_tile(KeyAt key_at, uint32_t start, uint32_t end, const float* __restrict__ gv,
+                                               float fx0, float fy0, f2v pfx2, f2v pfy2, int lane, uint64_t lt,
+                                               PairRec* plist, float& Tr, f2v& C01, float& C2, uint32_t& last,
+                                               bool& alive) {
+  float4 cq[EPL], cr[EPL];
+  float cb[EPL];
+  uint32_t nid[EPL];
+#pragma unroll
+  for (int u = 0; u < EPL; ++u) {
+    const uint32_t e = start + u * 64 + lane;
+    cq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    cr[u] = cq[u];
+    cb[u] = 0.f;
+    if (e < end) {
+      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)key_at(e) * GS);
+      cq[u] = rec[0];
+      cr[u] = rec[1];
+      cb[u] = rec[2].x;
+    }
+    const uint32_t e1 = e + CH;
+    nid[u] = e1 < end ? key_at(e1) : 0xffffffffu;
+  }
+  for (uint32_t base = start; base < end; base += CH) {
+    const uint64_t live = __ballot(alive);
+    if (!live) break;
+    float lx0, ly0, lx1, ly1;
+    live_rect(live, fx0, fy0, lx0, ly0, lx1, ly1);
+    float4 nq[EPL], nr[EPL];
+    float nb[EPL];
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) {
+      nq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      nr[u] = nq[u];
+      nb[u] = 0.f;
+      if (nid[u] != 0xffffffffu) {
+        const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)nid[u] * GS);
+        nq[u] = rec[0];
+        nr[u] = rec[1];
+        nb[u] = rec[2].x;
+      }
+      const uint32_t e2 = base + 2 * CH + u * 64 + lane;
+      nid[u] = e2 < end ? key_at(e2) : 0xffffffffu;
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) {
+      const uint32_t e = base + u * 64 + lane;
+      const bool mine = e < end && rect_hit(cq[u], cr[u], lx0, ly0, lx1, ly1);
+      const uint64_t bal = __ballot(mine);
+      if (mine) {
+        const float4 sq = scaled_conic_q(cq[u]);  // (x, y, A, B)
+        pair_put(plist, cnt + __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * cr[u].x, sq.w, cr[u].y,
+                 cr[u].z, cr[u].w, cb[u], e - start + 1u);
+      }
+      cnt += __popcll(bal);
+    }
+    if (lane < 8)  // pad up to 8 entries: opacity 0 -> alpha 0 -> never blends
+      pair_put(plist, cnt + lane, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u);
+    __builtin_amdgcn_wave_barrier();
+    {
+      const PairRec* pp = plist;
+      PairRec a0 = pp[0], a1 = pp[1];
+      for (int k = 0; k < cnt; k += 4) {
+        pp += 2;
+        const PairRec b0 = pp[0], b1 = pp[1];  // in bounds: pair k/2 + 3 <= (CH + 8) / 2 - 1
+        composite_pair(a0, pfx2, pfy2, Tr, alive, C01, C2, last);
+        composite_pair(a1, pfx2, pfy2, Tr, alive, C01, C2, last);
+        if (!__any(alive)) break;
+        a0 = b0;
+        a1 = b1;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // list reads of this chunk before the next chunk's writes
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) {
+      cq[u] = nq[u];
+      cr[u] = nr[u];
+      cb[u] = nb[u];
+    }
+  }
+}
+
+__device__ __forceinline__ void store_pixel(float* __restrict__ out, float* __restrict__ finalT,
+                                            uint32_t* __restrict__ ncontrib, const float* bg, int v, int H, int W,
+                                            int px, int py, float Tr, f2v C01, float C2, uint32_t last) {
+  const size_t HW = (size_t)H * W;
+  const size_t pix = (size_t)py * W + px;
+  finalT[v * HW + pix] = Tr;
+  ncontrib[v * HW + pix] = last;
+  out[(size_t)v * 3 * HW + pix] = C01.x + Tr * bg[0];
+  out[(size_t)v * 3 * HW + HW + pix] = C01.y + Tr * bg[1];
+  out[(size_t)v * 3 * HW + 2 * HW + pix] = C2 + Tr * bg[2];
+}
+
 // K6: front-to-back compositing. grid = (gx, gy, V), block = 256 = 4 independent waves;
-// wave w owns the 8x8 sub-tile (w & 1, w >> 1) of the tile. There is no workgroup barrier:
-// each wave walks the tile's list CH entries at a time (EPL keys + records per lane, the
-// next chunk's records and the chunk after's keys already in flight), keeps the entries that
-// can reach its sub-tile in a wave-private LDS list (ballot compaction, list order kept,
-// entry pairs field-interleaved for packed math, 8 zero-opacity pad entries after the end),
-// and composites that list four entries per step with the next four read ahead. A wave
-// retires as soon as its own 64 pixels have terminated (a stopped pixel keeps a negative T
-// whose magnitude is its final T); the waves of a workgroup share the tile's keys/records
-// through L1.
+// wave w owns the 8x8 sub-tile (w & 1, w >> 1) of the tile (composite_tile). There is no
+// workgroup barrier; the waves of a workgroup share the tile's keys/records through L1. A
+// stopped pixel keeps its final T (alive is a lane mask).
 __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, int T,
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
@@ -1846,137 +1943,17 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   if (seg_sorted) end = start + min(seg_sorted[seg], end - start);
   // depth-cut binning: entries past `end` were never written (all deeper than the written ones)
   const bool absent_tail = stride == kSegEnds && seg_overflow != nullptr && end < seg_start[seg + 1];
-  const float pfx = (float)px, pfy = (float)py;
   const float fx0 = (float)sx0, fy0 = (float)sy0;
   const float* gv = geom + (size_t)v * G * GS;
   const uint64_t lt = dsplat::lanemask_lt(lane);
   PairRec* plist = l_pair[w];
-  const f2v pfx2 = {pfx, pfx}, pfy2 = {pfy, pfy};
+  const f2v pfx2 = {(float)px, (float)px}, pfy2 = {(float)py, (float)py};
   f2v C01 = {0.f, 0.f};
-  float Tr = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
+  float Tr = 1.0f, C2 = 0.f;
   bool alive = inside;
   uint32_t last = 0;
-  float4 cq[EPL], cr[EPL];
-  float cb[EPL];
-  uint32_t nid[EPL];
-#pragma unroll
-  for (int u = 0; u < EPL; ++u) {
-    const uint32_t e = start + u * 64 + lane;
-    cq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    cr[u] = cq[u];
-    cb[u] = 0.f;
-    if (e < end) {
-      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)(uint32_t)keys[e] * GS);
-      cq[u] = rec[0];
-      cr[u] = rec[1];
-      cb[u] = rec[2].x;
-    }
-    const uint32_t e1 = e + CH;
-    nid[u] = e1 < end ? (uint32_t)keys[e1] : 0xffffffffu;
-  }
-#ifdef RF_PD2  // records two chunks ahead (c1), keys three ahead
-  float4 c1q[EPL], c1r[EPL];
-  float c1b[EPL];
-#pragma unroll
-  for (int u = 0; u < EPL; ++u) {
-    c1q[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    c1r[u] = c1q[u];
-    c1b[u] = 0.f;
-    if (nid[u] != 0xffffffffu) {
-      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)nid[u] * GS);
-      c1q[u] = rec[0];
-      c1r[u] = rec[1];
-      c1b[u] = rec[2].x;
-    }
-    const uint32_t e2 = start + 2 * CH + u * 64 + lane;
-    nid[u] = e2 < end ? (uint32_t)keys[e2] : 0xffffffffu;
-  }
-#endif
-#ifdef RF_DIAG_WAVESTATS
-  const uint64_t t_begin = wall_clock64();
-  uint32_t d_chunks = 0, d_comp = 0;
-#endif
-  for (uint32_t base = start; base < end; base += CH) {
-    const uint64_t live = __ballot(alive);
-    if (!live) break;
-    float lx0, ly0, lx1, ly1;
-    live_rect(live, fx0, fy0, lx0, ly0, lx1, ly1);
-#ifdef RF_DIAG_WAVESTATS
-    ++d_chunks;
-#endif
-    float4 nq[EPL], nr[EPL];
-    float nb[EPL];
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) {
-      nq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      nr[u] = nq[u];
-      nb[u] = 0.f;
-      if (nid[u] != 0xffffffffu) {
-        const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)nid[u] * GS);
-        nq[u] = rec[0];
-        nr[u] = rec[1];
-        nb[u] = rec[2].x;
-      }
-#ifdef RF_PD2
-      const uint32_t e2 = base + 3 * CH + u * 64 + lane;
-#else
-      const uint32_t e2 = base + 2 * CH + u * 64 + lane;
-#endif
-      nid[u] = e2 < end ? (uint32_t)keys[e2] : 0xffffffffu;
-    }
-    int cnt = 0;
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) {
-      const uint32_t e = base + u * 64 + lane;
-#ifdef RF_FULL_SUBTILE
-      const bool mine = e < end && subtile_hit(cq[u], cr[u], fx0, fy0);
-#else
-      const bool mine = e < end && rect_hit(cq[u], cr[u], lx0, ly0, lx1, ly1);
-#endif
-      const uint64_t bal = __ballot(mine);
-      if (mine) {
-        const float4 sq = scaled_conic_q(cq[u]);  // (x, y, A, B)
-        pair_put(plist, cnt + __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * cr[u].x, sq.w, cr[u].y,
-                 cr[u].z, cr[u].w, cb[u], e - start + 1u);
-      }
-      cnt += __popcll(bal);
-    }
-    if (lane < 8)  // pad up to 8 entries: opacity 0 -> alpha 0 -> never blends
-      pair_put(plist, cnt + lane, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u);
-#ifdef RF_DIAG_WAVESTATS
-    d_comp += cnt;
-#endif
-    __builtin_amdgcn_wave_barrier();
-    {
-      const PairRec* pp = plist;
-      PairRec a0 = pp[0], a1 = pp[1];
-      for (int k = 0; k < cnt; k += 4) {
-        pp += 2;
-        const PairRec b0 = pp[0], b1 = pp[1];  // in bounds: pair k/2 + 3 <= (CH + 8) / 2 - 1
-        composite_pair(a0, pfx2, pfy2, Tr, alive, C01, C2, last);
-        composite_pair(a1, pfx2, pfy2, Tr, alive, C01, C2, last);
-        if (!__any(alive)) break;
-        a0 = b0;
-        a1 = b1;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();  // list reads of this chunk before the next chunk's writes
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) {
-#ifdef RF_PD2
-      cq[u] = c1q[u];
-      cr[u] = c1r[u];
-      cb[u] = c1b[u];
-      c1q[u] = nq[u];
-      c1r[u] = nr[u];
-      c1b[u] = nb[u];
-#else
-      cq[u] = nq[u];
-      cr[u] = nr[u];
-      cb[u] = nb[u];
-#endif
-    }
-  }
+  composite_tile([&](uint32_t e) { return (uint32_t)keys[e]; }, start, end, gv, fx0, fy0, pfx2, pfy2, lane, lt,
+                 plist, Tr, C01, C2, last, alive);
   bool void_tile = false;  // wave-uniform
   if (absent_tail)
     void_tile = __any(alive);  // a pixel still live at the end of the written part: the rest may blend
@@ -1991,24 +1968,75 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
       seg_overflow[(size_t)gridDim.z * T + 1 + (size_t)v * nsb + (blockIdx.y >> sbl) * nsx + (blockIdx.x >> sbl)] = 1u;
     }
   }
-  if (inside) {
-    const size_t HW = (size_t)H * W;
-    const size_t pix = (size_t)py * W + px;
-    const float* bg = cams[v].bg;
-    C0 = C01.x;
-    C1 = C01.y;
-    const float Tf = Tr;
-    finalT[v * HW + pix] = Tf;
-    ncontrib[v * HW + pix] = last;
-#ifdef RF_DIAG_WAVESTATS  // timing experiment: lanes 0-2 report (ticks, chunks, composited entries)
-    if (lane == 0) ncontrib[v * HW + pix] = (uint32_t)(wall_clock64() - t_begin);
-    if (lane == 1) ncontrib[v * HW + pix] = d_chunks;
-    if (lane == 2) ncontrib[v * HW + pix] = d_comp;
-#endif
-    out[(size_t)v * 3 * HW + pix] = C0 + Tf * bg[0];
-    out[(size_t)v * 3 * HW + HW + pix] = C1 + Tf * bg[1];
-    out[(size_t)v * 3 * HW + 2 * HW + pix] = C2 + Tf * bg[2];
+  if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
+}
+
+// K4 + K6 fused: one workgroup per tile sorts the tile's keys in LDS (count_sort) and its 4
+// waves composite straight from the sorted LDS copy (their pair lists reuse the sort's
+// counter area). The sorted keys go back to HBM only when the backward needs them
+// (write_keys), the render never re-reads keys from HBM, and the sort and compositing phases
+// of different tiles overlap inside one launch. A segment above the LDS capacity is sorted
+// through HBM (scratch) by the same workgroup and composited from there.
+template <int KMAX>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) void k_sort_render(
+    int G, int H, int W, int gx, int T, const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
+    const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ seg_count, uint32_t stride,
+    uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits, int write_keys,
+    float* __restrict__ out, float* __restrict__ finalT, uint32_t* __restrict__ ncontrib) {
+  constexpr uint32_t cap = NT * KMAX;
+  constexpr uint32_t padded = cap + cap / KMAX;
+  extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
+  uint64_t* A = s_keys;
+  uint32_t* aux = reinterpret_cast<uint32_t*>(A + padded);
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(aux);
+  uint32_t* wsum = aux + sort_cnt_words<NT>();
+  uint32_t* flag = wsum + 16;
+  static_assert(sizeof(PairRec) * 4 * ((CH + 8) / 2) <= (size_t)sort_cnt_words<NT>() * 4, "pair lists fit the counters");
+  const int v = blockIdx.z;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int seg = v * T + blockIdx.y * gx + blockIdx.x;
+  uint32_t b, e;
+  seg_bounds(seg_start, seg_count, stride, seg, b, e);
+  const uint32_t n = e - b;
+  const bool in_lds = n <= cap;  // uniform
+  if (in_lds) {
+    uint64_t tmp[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      const uint32_t idx = tid + (uint32_t)i * NT;
+      tmp[i] = idx < n ? keys[b + idx] : 0ull;
+    }
+    if (n > 1) {
+      count_sort<KMAX, NT>(tmp, n, A, id_bits, cnt, wsum, flag);
+    } else {
+      if (tid == 0 && n == 1) A[0] = tmp[0];
+      __syncthreads();
+    }
+    if (write_keys)
+      for (uint32_t i = tid; i < n; i += NT) keys[b + i] = A[padi<KMAX>(i)];
+  } else {
+    sort_segment<NT>(keys + b, scratch + b, n, id_bits, aux, wsum, flag, keys + b);
+    __syncthreads();
   }
+  const int sx0 = blockIdx.x * BX + (w & 1) * SUB, sy0 = blockIdx.y * BY + (w >> 1) * SUB;
+  const int px = sx0 + (lane & (SUB - 1));
+  const int py = sy0 + (lane >> 3);
+  const bool inside = px < W && py < H;
+  const float* gv = geom + (size_t)v * G * GS;
+  const uint64_t lt = dsplat::lanemask_lt(lane);
+  PairRec* plist = reinterpret_cast<PairRec*>(aux) + w * ((CH + 8) / 2);
+  const f2v pfx2 = {(float)px, (float)px}, pfy2 = {(float)py, (float)py};
+  f2v C01 = {0.f, 0.f};
+  float Tr = 1.0f, C2 = 0.f;
+  bool alive = inside;
+  uint32_t last = 0;
+  if (in_lds)
+    composite_tile([&](uint32_t i) { return (uint32_t)A[padi<KMAX>(i)]; }, 0u, n, gv, (float)sx0, (float)sy0, pfx2,
+                   pfy2, lane, lt, plist, Tr, C01, C2, last, alive);
+  else
+    composite_tile([&](uint32_t i) { return (uint32_t)keys[i]; }, b, e, gv, (float)sx0, (float)sy0, pfx2, pfy2,
+                   lane, lt, plist, Tr, C01, C2, last, alive);
+  if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2804,6 +2832,33 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
                                                      seg_stride, keys, seg_sorted, seg_overflow, seg_filter,
                                                      out_color, final_T, n_contrib);
   return dsplat::check_launch("k_render_fwd");
+}
+
+int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
+                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
+                    uint64_t* scratch, int write_keys, float* out_color, float* final_T, uint32_t* n_contrib,
+                    void* stream) {
+  DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_sort_render: bad sizes");
+  DSPLAT_REQUIRE(cams && geom && keys && scratch && seg_ptrs_ok(seg_start, seg_count, seg_stride) && out_color &&
+                     final_T && n_contrib,
+                 "dsr_sort_render: null pointer");
+  static bool attr = false;
+  if (!attr) {
+    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_render<16>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      (int)sort_lds_bytes<16>()),
+                                  "hipFuncSetAttribute(k_sort_render)"))
+      return e;
+    attr = true;
+  }
+  int id_bits = 0;
+  while (id_bits < 32 && ((uint64_t)1 << id_bits) < (uint64_t)G) ++id_bits;
+  const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
+  dim3 grid(gx, gy, V);
+  k_sort_render<16><<<grid, NT, sort_lds_bytes<16>(), (hipStream_t)stream>>>(
+      G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count, seg_stride, keys, scratch, id_bits, write_keys,
+      out_color, final_T, n_contrib);
+  return dsplat::check_launch("k_sort_render");
 }
 
 int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,

@@ -122,6 +122,8 @@ def algorithmic_bytes(kernel: str, *, G: int, V: int, N: int, HW: int, T: int | 
         return 16 * N
     if kernel == "k_render_fwd":   # keys; each 36-B compositing record once; RGB + T + n_contrib out
         return 8 * N + 36 * V * G + 20 * V * HW
+    if kernel == "k_sort_render":  # keys in (sorted copy stays in LDS: inference), records, outputs
+        return 8 * N + 36 * V * G + 20 * V * HW
     raise KeyError(kernel)
 
 
@@ -180,6 +182,11 @@ SORT_PREFIX = int(os.environ.get("DSPLAT_SORT_PREFIX", "4096"))
 # not all saturate within them get the rest appended, sorted and rendered again. 0 = off.
 CUT_PREFIX = int(os.environ.get("DSPLAT_CUT_PREFIX", "2048"))
 CUT_SORT_HINT = 4096  # LDS sort size for the written parts (larger ones sort through HBM)
+# Fixed-capacity binning with tile lists up to FUSED_MAX entries (the hint from earlier calls)
+# sorts and composites in one launch (dsr_sort_render); longer lists take dsr_bin_sort +
+# dsr_render_fwd (MSD split, prefix sort). Either is exact for any list length.
+FUSED_SORT_RENDER = os.environ.get("DSPLAT_FUSED_SORT_RENDER", "1") != "0"
+FUSED_MAX = 4096
 SEG_ENDS = 0xFFFFFFFF  # DSR_SEG_ENDS
 _spec = {"max_count": 0}
 _inflight: list = []  # (pinned int32 counts, event) read-backs, consumed without blocking
@@ -280,7 +287,8 @@ def input_layout(feats, cov6, use_sh, channel_major_sh):
     return lay
 
 
-def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0, zeroed_counts=None):
+def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0, zeroed_counts=None,
+                need_state=True):
     """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh; [S,G,3,M] with
     LAYOUT_SH_CHANNEL_MAJOR) or [S,G,3]; opacities [S,G]; cov6 [S,G,6] (or [S,G,3,3] with
     LAYOUT_COV_FULL); cams [V,44]. Returns (color [V,3,H,W], RasterState).
@@ -320,11 +328,15 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             "dsr_project_bin")
         maxc_hint = _spec["max_count"] or lds_cap
         seg_start, stride = None, G
-        ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
-        seg_sorted = _prefix_sort(lib, G, V, H, W, None, seg_count, stride, keys, scratch, maxc_hint, ws, st,
-                                  lds_cap)
+        fused = FUSED_SORT_RENDER and maxc_hint <= FUSED_MAX
+        seg_sorted = None
+        if not fused:
+            ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
+            seg_sorted = _prefix_sort(lib, G, V, H, W, None, seg_count, stride, keys, scratch, maxc_hint, ws, st,
+                                      lds_cap)
         _note_counts(seg_count)
     else:
+        fused = False
         # the depth cut pays when tile lists are long; the previous two-phase call's largest
         # list (None on the first call) decides whether this one builds the depth histogram
         prev = _spec.get("two_phase_max")
@@ -384,6 +396,13 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
     outs = (color.data_ptr(), final_T.data_ptr(), n_contrib.data_ptr(), st)
+    if fused:  # sort + composite in one launch; sorted keys kept only when a backward needs them
+        _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(), None,
+                          seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(), int(bool(need_state)),
+                          *outs), "dsr_sort_render")
+        state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib)
+        _last["counts"] = state.counts
+        return color, state
     overflow = None
     if seg_sorted is not None:
         overflow = torch.zeros(V * T + 1, dtype=torch.int32, device=dev)  # + the any-flag word
@@ -471,7 +490,7 @@ class _RasterizeViews(torch.autograd.Function):
                 zeroed_counts):
         V = len(view_scene)
         color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout,
-                                   zeroed_counts)
+                                   zeroed_counts, need_state=any(ctx.needs_input_grad[:5]))
         ctx.save_for_backward(means, feats, opacities, cov6, cams)
         ctx.state = state
         ctx.meta = (view_scene, use_sh, sh_degree, None if means2d is None else means2d.shape, layout)
