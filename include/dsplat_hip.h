@@ -101,6 +101,18 @@ int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M,
                     float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout,
                     void* stream);
 
+/* dsr_build_cameras + dsr_project_bin in one launch: every workgroup sets up its view's
+ * camera from the render_cuda inputs (as dsr_build_cameras) and the first block of each view
+ * stores it to cams [V] for the later calls. seg_count must come zeroed (DSR_LAYOUT_COUNTS_ZEROED
+ * in layout; e.g. by dsr_sort_render's clear_counts). */
+int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, int M,
+                            const float* means, const float* shs, const float* colors,
+                            const float* opacities, const float* cov6, const float* extrinsics,
+                            const float* intrinsics, const float* near, const float* far,
+                            const float* bg, const int32_t* view_scene, int scale_invariant,
+                            dsr_camera* cams, float* geom, int32_t* radii, uint32_t* seg_count,
+                            uint64_t* keys, int layout, void* stream);
+
 /* Exclusive scan of seg_count[V*T] -> seg_start[V*T+1], seg_cursor[V*T] (= seg_start),
  * totals[0] = N (num_rendered over all views), totals[1] = max entries in one tile,
  * totals[2] = 1 if N reached 2^31 (offsets invalid: render fewer views per call). */
@@ -217,9 +229,11 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
  * back to `keys` only when write_keys != 0 (dsr_render_bwd needs them). Outputs as
  * dsr_render_fwd. */
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
-                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
-                    uint64_t* scratch, int write_keys, float* out_color, float* final_T, uint32_t* n_contrib,
-                    void* stream);
+                    const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
+                    uint64_t* scratch, int write_keys, int clear_counts, float* out_color, float* final_T,
+                    uint32_t* n_contrib, void* stream);
+/* clear_counts != 0 (fixed-capacity layout only): seg_count is zeroed as it is consumed, so
+ * the buffer can serve the next dsr_project_bin_cameras call as already-zeroed counters. */
 
 /* ---- rasterizer backward -----------------------------------------------------------
  * Back-to-front per tile (K7). dL_dpix [V,3,H,W]. Accumulates into dgeom [V,G,12]

@@ -271,6 +271,200 @@ __device__ __forceinline__ void seg_bounds(const uint32_t* __restrict__ start, c
   }
 }
 
+template <typename Real>
+__device__ void inv4(const Real* m, Real* o) {  // row-major 4x4 inverse (cofactors)
+  Real inv[16];
+  inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+  inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+  inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+  inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+  inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+  inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+  inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+  inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+  inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+  inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+  inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+  inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+  inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+  inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+  inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+  inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+  const Real rdet = Real(1) / (m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12]);
+  for (int i = 0; i < 16; ++i) o[i] = inv[i] * rdet;
+}
+
+template <typename Real>
+__device__ void inv3(const Real* k, Real* o) {
+  const Real a = k[0], b = k[1], c = k[2], d = k[3], e = k[4], f = k[5], g = k[6], h = k[7], i = k[8];
+  const Real A = e * i - f * h, B = -(d * i - f * g), C = d * h - e * g;
+  const Real r = Real(1) / (a * A + b * B + c * C);
+  o[0] = A * r; o[1] = -(b * i - c * h) * r; o[2] = (b * f - c * e) * r;
+  o[3] = B * r; o[4] = (a * i - c * g) * r; o[5] = -(a * f - c * d) * r;
+  o[6] = C * r; o[7] = -(a * h - b * g) * r; o[8] = (a * e - b * d) * r;
+}
+
+// tan(fov / 2) for the angle between the rays through two image-edge midpoints (get_fov,
+// projection.py:233-247, takes acos of their normalised dot product; the reference then takes
+// tan of half of it): tan(t / 2) = |u x w| / (|u| |w| + u . w), no transcendental calls.
+template <typename Real>
+__device__ Real edge_tan_half(const Real* ki, Real x0, Real y0, Real x1, Real y1) {
+  Real u[3], w[3];
+  for (int r = 0; r < 3; ++r) {
+    u[r] = ki[3 * r] * x0 + ki[3 * r + 1] * y0 + ki[3 * r + 2];
+    w[r] = ki[3 * r] * x1 + ki[3 * r + 1] * y1 + ki[3 * r + 2];
+  }
+  const Real nu = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+  const Real nw = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+  const Real cx = u[1] * w[2] - u[2] * w[1], cy = u[2] * w[0] - u[0] * w[2], cz = u[0] * w[1] - u[1] * w[0];
+  return sqrt(cx * cx + cy * cy + cz * cz) / (nu * nw + (u[0] * w[0] + u[1] * w[1] + u[2] * w[2]));
+}
+
+// One camera of dsr_build_cameras: the render_cuda set-up (cuda_splatting.py:62-86):
+// scale-invariant rescale, K^-1 and tan(fov / 2) (get_fov), projection matrix, world->camera
+// inverse, and their transposed (column-major) storage. Real = double in dsr_build_cameras;
+// float where every workgroup of the binning kernel sets its camera up (the reference computes
+// all of this in float32 torch; the two agree to ~1e-7 relative).
+template <typename Real>
+__device__ void make_camera(int v, const float* __restrict__ ext, const float* __restrict__ intr,
+                            const float* __restrict__ near, const float* __restrict__ far,
+                            const float* __restrict__ bg, const int32_t* __restrict__ view_scene,
+                            int scale_invariant, dsr_camera& c) {
+  Real E[16], K[9], Ki[9], Wc[16];
+  for (int i = 0; i < 16; ++i) E[i] = ext[16 * v + i];
+  for (int i = 0; i < 9; ++i) K[i] = intr[9 * v + i];
+  Real n = near[v], f = far[v];
+  float sc = 1.f;
+  if (scale_invariant) {
+    sc = 1.0f / near[v];  // float, as the reference's `scale = 1 / near`
+    for (int r = 0; r < 3; ++r) E[4 * r + 3] *= (Real)sc;
+    n *= (Real)sc;
+    f *= (Real)sc;
+  }
+  inv3(K, Ki);
+  const Real tx = edge_tan_half<Real>(Ki, 0, 0.5, 1, 0.5);
+  const Real ty = edge_tan_half<Real>(Ki, 0.5, 0, 0.5, 1);
+  // P (row-major) = get_projection_matrix
+  Real P[16] = {0};
+  const Real top = ty * n, right = tx * n;
+  P[0] = 2 * n / (2 * right);
+  P[5] = 2 * n / (2 * top);
+  P[14] = 1;  // [3][2]
+  P[10] = f / (f - n);
+  P[11] = -(f * n) / (f - n);
+  inv4(E, Wc);  // world -> camera, row-major
+  // viewmatrix storage = (W2C)^T row-major  -> element [r*4 + c] = Wc[c*4 + r]
+  for (int r = 0; r < 4; ++r)
+    for (int q = 0; q < 4; ++q) c.viewmatrix[r * 4 + q] = (float)Wc[q * 4 + r];
+  // projmatrix storage = (P W2C)^T
+  for (int r = 0; r < 4; ++r)
+    for (int q = 0; q < 4; ++q) {
+      Real s = 0;
+      for (int k = 0; k < 4; ++k) s += P[r * 4 + k] * Wc[k * 4 + q];
+      c.projmatrix[q * 4 + r] = (float)s;
+    }
+  c.campos[0] = (float)E[3];
+  c.campos[1] = (float)E[7];
+  c.campos[2] = (float)E[11];
+  c.tanfovx = (float)tx;
+  c.tanfovy = (float)ty;
+  c.bg[0] = bg[3 * v];
+  c.bg[1] = bg[3 * v + 1];
+  c.bg[2] = bg[3 * v + 2];
+  c.scene = view_scene[v];
+  c.scale = sc;
+  c._pad[0] = 0;
+  c._pad[1] = 0;
+}
+
+// render_cuda camera inputs for the in-kernel camera set-up (dsr_project_bin_cameras)
+struct CamIn {
+  const float *ext, *intr, *near, *far, *bg;
+  const int32_t* view_scene;
+  int scale_invariant;
+};
+
+// make_camera in float, spread over one wave so that no lane holds more than a few values
+// (a one-lane set-up inside the binning kernel raised its VGPR count 60 -> 178 and cut its
+// occupancy from 8 to 2 waves/SIMD). Lane i < 16 owns E[i] and the cofactor (r, c) = (i / 4,
+// i % 4) of the 4x4 inverse; lanes 16..24 own K and the cofactors of the 3x3 inverse. Values
+// move between lanes with ds_bpermute (__shfl), which every lane of the wave executes.
+__device__ void make_camera_wave(int v, const CamIn& ci, int lane, dsr_camera& c) {
+  const float sc = ci.scale_invariant ? 1.0f / ci.near[v] : 1.0f;
+  float x = 0.f;
+  if (lane < 16) {
+    x = ci.ext[16 * v + lane];
+    if (ci.scale_invariant && (lane & 3) == 3 && lane < 12) x *= sc;
+  } else if (lane < 25) {
+    x = ci.intr[9 * v + lane - 16];
+  }
+  // cofactor of the element this lane owns, transposed (adjugate entry); 4x4 on lanes 0..15,
+  // 3x3 on lanes 16..24
+  float adj = 0.f;
+  {
+    const bool big = lane < 16;
+    const int j = big ? lane : (lane < 25 ? lane - 16 : 0);
+    const int N = big ? 4 : 3, base = big ? 0 : 16;
+    const int r = j / N, col = j % N;  // adj[r][col] = (-1)^(r+col) * minor(row col, col r)
+    // minor rows skip row `col`, minor columns skip column `r`
+    auto at = [&](int a, int b) { return __shfl(x, base + (a + (a >= col)) * N + (b + (b >= r))); };
+    float d;
+    if (big) {
+      const float m00 = at(0, 0), m01 = at(0, 1), m02 = at(0, 2);
+      const float m10 = at(1, 0), m11 = at(1, 1), m12 = at(1, 2);
+      const float m20 = at(2, 0), m21 = at(2, 1), m22 = at(2, 2);
+      d = m00 * (m11 * m22 - m12 * m21) - m01 * (m10 * m22 - m12 * m20) + m02 * (m10 * m21 - m11 * m20);
+    } else {
+      const float m00 = at(0, 0), m01 = at(0, 1);
+      const float m10 = at(1, 0), m11 = at(1, 1);
+      d = m00 * m11 - m01 * m10;
+    }
+    adj = ((r + col) & 1) ? -d : d;
+  }
+  // determinants: row 0 of the matrix times column 0 of the adjugate
+  const float det4 = __shfl(x, 0) * __shfl(adj, 0) + __shfl(x, 1) * __shfl(adj, 4) +
+                     __shfl(x, 2) * __shfl(adj, 8) + __shfl(x, 3) * __shfl(adj, 12);
+  const float det3 = __shfl(x, 16) * __shfl(adj, 16) + __shfl(x, 17) * __shfl(adj, 19) +
+                     __shfl(x, 18) * __shfl(adj, 22);
+  const float inv = adj * (1.0f / (lane < 16 ? det4 : det3));  // Wc on 0..15, K^-1 on 16..24
+  float ki[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) ki[k] = __shfl(inv, 16 + k);
+  const float tx = edge_tan_half<float>(ki, 0.f, 0.5f, 1.f, 0.5f);
+  const float ty = edge_tan_half<float>(ki, 0.5f, 0.f, 0.5f, 1.f);
+  const float n = ci.near[v] * sc, f = ci.far[v] * sc;
+  const float top = ty * n, right = tx * n;
+  // projmatrix storage = (P W2C)^T: lane o = q*4 + r holds (P W2C)[r][q]; P row r from
+  // get_projection_matrix (only its non-zero terms)
+  const int o = lane & 15, q = o >> 2, r = o & 3;
+  const float w0 = __shfl(inv, q), w1 = __shfl(inv, 4 + q), w2 = __shfl(inv, 8 + q), w3 = __shfl(inv, 12 + q);
+  float pm;
+  if (r == 0) pm = (2 * n / (2 * right)) * w0;
+  else if (r == 1) pm = (2 * n / (2 * top)) * w1;
+  else if (r == 2) pm = (f / (f - n)) * w2 + (-(f * n) / (f - n)) * w3;
+  else pm = w2;
+  const float vm = __shfl(inv, (o & 3) * 4 + (o >> 2));  // viewmatrix storage = W2C^T
+  const float cx = __shfl(x, 3), cy = __shfl(x, 7), cz = __shfl(x, 11);
+  if (lane < 16) {
+    c.viewmatrix[lane] = vm;
+    c.projmatrix[lane] = pm;
+  }
+  if (lane == 0) {
+    c.campos[0] = cx;
+    c.campos[1] = cy;
+    c.campos[2] = cz;
+    c.tanfovx = tx;
+    c.tanfovy = ty;
+    c.bg[0] = ci.bg[3 * v];
+    c.bg[1] = ci.bg[3 * v + 1];
+    c.bg[2] = ci.bg[3 * v + 2];
+    c.scene = ci.view_scene[v];
+    c.scale = sc;
+    c._pad[0] = 0;
+    c._pad[1] = 0;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // K1 building blocks: one Gaussian's scene inputs (loaded once) and its projection into one
 // view (upstream preprocessCUDA, rows A7 of the survey).
@@ -438,20 +632,21 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
 #ifndef PB_WPE
 #define PB_WPE 1
 #endif
-template <int DEG>
+template <int DEG, bool CAM>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
                                                      const float* __restrict__ means,
                                                      const float* __restrict__ shs,
                                                      const float* __restrict__ colors,
                                                      const float* __restrict__ opac,
                                                      const float* __restrict__ cov6,
-                                                     const dsr_camera* __restrict__ cams,
+                                                     dsr_camera* __restrict__ cams,
                                                      float* __restrict__ geom, int32_t* __restrict__ radii,
                                                      uint32_t* __restrict__ seg_count,
-                                                     uint64_t* __restrict__ keys, int layout) {
+                                                     uint64_t* __restrict__ keys, int layout, CamIn ci) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
+  __shared__ dsr_camera s_cam[1];  // CAM only
   int v, blk;
   if (!xcd_item((G + NT - 1) / NT, V, v, blk)) return;
   const dsr_camera* cam = cams + v;
@@ -464,9 +659,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
     for (int t = tid; t < T; t += NT) s_hist[t] = 0;
     int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     uint64_t key = 0;
+    GaussIn<DEG> in;
+    if (g < G) load_gauss<DEG>(in, (size_t)(CAM ? ci.view_scene[v] : cam->scene) * G + g, means, opac, cov6, layout);
+    if constexpr (CAM) {
+      // every workgroup sets up its view's camera while its Gaussians load (no separate
+      // launch); the first block of each view also stores it for the later kernels
+      if (w == 0) make_camera_wave(v, ci, lane, s_cam[0]);
+      __syncthreads();
+      if (blk == 0 && tid < (int)(sizeof(dsr_camera) / 4))
+        reinterpret_cast<uint32_t*>(cams + v)[tid] = reinterpret_cast<const uint32_t*>(s_cam)[tid];
+      cam = s_cam;
+    }
     if (g < G) {
-      GaussIn<DEG> in;
-      load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
       float rec[GS];
       r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
       store_geom(geom, radii, (size_t)v * G + g, rec, r);
@@ -1980,8 +2184,8 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
 template <int KMAX>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) void k_sort_render(
     int G, int H, int W, int gx, int T, const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
-    const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ seg_count, uint32_t stride,
-    uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits, int write_keys,
+    const uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_count, uint32_t stride,
+    uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits, int write_keys, int clear_counts,
     float* __restrict__ out, float* __restrict__ finalT, uint32_t* __restrict__ ncontrib) {
   constexpr uint32_t cap = NT * KMAX;
   constexpr uint32_t padded = cap + cap / KMAX;
@@ -2037,6 +2241,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) 
     composite_tile([&](uint32_t i) { return (uint32_t)keys[i]; }, b, e, gv, (float)sx0, (float)sy0, pfx2, pfy2,
                    lane, lt, plist, Tr, C01, C2, last, alive);
   if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
+  // counts handed back zeroed for the next call's binning (every thread read it before the
+  // sort's first barrier)
+  if (clear_counts && tid == 0) seg_count[seg] = 0u;
 }
 
 // ------------------------------------------------------------------------------------
@@ -2576,25 +2783,35 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   return dsplat::check_launch("k_preprocess");
 }
 
-int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means, const float* shs,
-                    const float* colors, const float* opacities, const float* cov6, const dsr_camera* cams,
-                    float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout, void* stream) {
-  DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_project_bin: bad sizes S=%d G=%d V=%d H=%d W=%d", S, G, V, H, W);
-  DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "dsr_project_bin: exactly one of shs/colors must be given");
+}  // extern "C"
+namespace {
+int project_bin_impl(const char* who, int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
+                     const float* shs, const float* colors, const float* opacities, const float* cov6,
+                     dsr_camera* cams, const CamIn* ci, float* geom, int32_t* radii, uint32_t* seg_count,
+                     uint64_t* keys, int layout, void* stream) {
+  DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "%s: bad sizes S=%d G=%d V=%d H=%d W=%d", who, S, G, V, H, W);
+  DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "%s: exactly one of shs/colors must be given", who);
   DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
-                 "dsr_project_bin: sh_degree=%d M=%d unsupported (degree 0..3, M >= (deg+1)^2)", sh_degree, M);
-  DSPLAT_REQUIRE(means && opacities && cov6 && cams && geom && radii && seg_count && keys, "dsr_project_bin: null pointer");
+                 "%s: sh_degree=%d M=%d unsupported (degree 0..3, M >= (deg+1)^2)", who, sh_degree, M);
+  DSPLAT_REQUIRE(means && opacities && cov6 && cams && geom && radii && seg_count && keys, "%s: null pointer", who);
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H), T = gx * gy;
-  DSPLAT_REQUIRE(T <= kHistLdsMax, "dsr_project_bin: %d tiles per view exceed the LDS histogram (%d)", T, kHistLdsMax);
-  DSPLAT_REQUIRE((uint64_t)V * T * G < (1ull << 32), "dsr_project_bin: V*tiles*G must fit 32-bit key offsets");
+  DSPLAT_REQUIRE(T <= kHistLdsMax, "%s: %d tiles per view exceed the LDS histogram (%d)", who, T, kHistLdsMax);
+  DSPLAT_REQUIRE((uint64_t)V * T * G < (1ull << 32), "%s: V*tiles*G must fit 32-bit key offsets", who);
   hipStream_t st = (hipStream_t)stream;
   if (!(layout & kLayoutCountsZeroed))
     if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
   const unsigned grid = xcd_grid((G + NT - 1) / NT, V);
   const int deg = shs ? sh_degree : -1;
-#define DSR_PB(D)                                                                                             \
-  k_project_emit<D><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, \
-                                             geom, radii, seg_count, keys, layout)
+#define DSR_PB(D)                                                                                              \
+  do {                                                                                                         \
+    if (ci)                                                                                                    \
+      k_project_emit<D, true><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities,   \
+                                                       cov6, cams, geom, radii, seg_count, keys, layout, *ci); \
+    else                                                                                                       \
+      k_project_emit<D, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities,  \
+                                                        cov6, cams, geom, radii, seg_count, keys, layout,      \
+                                                        CamIn{});                                              \
+  } while (0)
   switch (deg) {
     case -1: DSR_PB(-1); break;
     case 0: DSR_PB(0); break;
@@ -2604,6 +2821,28 @@ int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M, con
   }
 #undef DSR_PB
   return dsplat::check_launch("k_project_emit");
+}
+}  // namespace
+extern "C" {
+
+int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means, const float* shs,
+                    const float* colors, const float* opacities, const float* cov6, const dsr_camera* cams,
+                    float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout, void* stream) {
+  return project_bin_impl("dsr_project_bin", S, G, V, H, W, sh_degree, M, means, shs, colors, opacities, cov6,
+                          const_cast<dsr_camera*>(cams), nullptr, geom, radii, seg_count, keys, layout, stream);
+}
+
+int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
+                            const float* shs, const float* colors, const float* opacities, const float* cov6,
+                            const float* extrinsics, const float* intrinsics, const float* near, const float* far,
+                            const float* bg, const int32_t* view_scene, int scale_invariant, dsr_camera* cams,
+                            float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout,
+                            void* stream) {
+  DSPLAT_REQUIRE(extrinsics && intrinsics && near && far && bg && view_scene,
+                 "dsr_project_bin_cameras: null camera input");
+  const CamIn ci{extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant};
+  return project_bin_impl("dsr_project_bin_cameras", S, G, V, H, W, sh_degree, M, means, shs, colors, opacities,
+                          cov6, cams, &ci, geom, radii, seg_count, keys, layout, stream);
 }
 
 int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_start, uint32_t* seg_cursor,
@@ -2835,9 +3074,10 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
 }
 
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
-                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
-                    uint64_t* scratch, int write_keys, float* out_color, float* final_T, uint32_t* n_contrib,
-                    void* stream) {
+                    const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
+                    uint64_t* scratch, int write_keys, int clear_counts, float* out_color, float* final_T,
+                    uint32_t* n_contrib, void* stream) {
+  DSPLAT_REQUIRE(!clear_counts || seg_stride > 0, "dsr_sort_render: clear_counts needs the fixed-capacity layout");
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_sort_render: bad sizes");
   DSPLAT_REQUIRE(cams && geom && keys && scratch && seg_ptrs_ok(seg_start, seg_count, seg_stride) && out_color &&
                      final_T && n_contrib,
@@ -2857,7 +3097,7 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
   dim3 grid(gx, gy, V);
   k_sort_render<16><<<grid, NT, sort_lds_bytes<16>(), (hipStream_t)stream>>>(
       G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count, seg_stride, keys, scratch, id_bits, write_keys,
-      out_color, final_T, n_contrib);
+      clear_counts, out_color, final_T, n_contrib);
   return dsplat::check_launch("k_sort_render");
 }
 
@@ -2916,49 +3156,6 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
 // =====================================================================================
 namespace {
 
-__device__ void inv4(const double* m, double* o) {  // row-major 4x4 inverse (cofactors)
-  double inv[16];
-  inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
-  inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
-  inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
-  inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
-  inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
-  inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
-  inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
-  inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
-  inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
-  inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
-  inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
-  inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
-  inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
-  inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
-  inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
-  inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
-  const double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
-  for (int i = 0; i < 16; ++i) o[i] = inv[i] / det;
-}
-
-__device__ void inv3(const double* k, double* o) {
-  const double a = k[0], b = k[1], c = k[2], d = k[3], e = k[4], f = k[5], g = k[6], h = k[7], i = k[8];
-  const double A = e * i - f * h, B = -(d * i - f * g), C = d * h - e * g;
-  const double det = a * A + b * B + c * C;
-  o[0] = A / det; o[1] = -(b * i - c * h) / det; o[2] = (b * f - c * e) / det;
-  o[3] = B / det; o[4] = (a * i - c * g) / det; o[5] = -(a * f - c * d) / det;
-  o[6] = C / det; o[7] = -(a * h - b * g) / det; o[8] = (a * e - b * d) / det;
-}
-
-__device__ double edge_angle(const double* ki, double x0, double y0, double x1, double y1) {
-  double u[3], w[3];
-  for (int r = 0; r < 3; ++r) {
-    u[r] = ki[3 * r] * x0 + ki[3 * r + 1] * y0 + ki[3 * r + 2];
-    w[r] = ki[3 * r] * x1 + ki[3 * r + 1] * y1 + ki[3 * r + 2];
-  }
-  const double nu = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
-  const double nw = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-  double dot = (u[0] * w[0] + u[1] * w[1] + u[2] * w[2]) / (nu * nw);
-  dot = fmin(1.0, fmax(-1.0, dot));
-  return acos(dot);
-}
 
 __global__ void k_cameras(int V, const float* __restrict__ ext, const float* __restrict__ intr,
                           const float* __restrict__ near, const float* __restrict__ far,
@@ -2969,55 +3166,8 @@ __global__ void k_cameras(int V, const float* __restrict__ ext, const float* __r
   // the next kernels' per-(view, tile) counters, zeroed here to save them a launch
   for (uint32_t i = (uint32_t)v; i < n_zero; i += gridDim.x * blockDim.x) zero[i] = 0u;
   if (v >= V) return;
-  double E[16], K[9], Ki[9], Wc[16];
-  for (int i = 0; i < 16; ++i) E[i] = ext[16 * v + i];
-  for (int i = 0; i < 9; ++i) K[i] = intr[9 * v + i];
-  double n = near[v], f = far[v];
-  float sc = 1.f;
-  if (scale_invariant) {
-    sc = 1.0f / near[v];  // float, as the reference's `scale = 1 / near`
-    for (int r = 0; r < 3; ++r) E[4 * r + 3] *= (double)sc;
-    n *= (double)sc;
-    f *= (double)sc;
-  }
-  inv3(K, Ki);
-  const double fovx = edge_angle(Ki, 0.0, 0.5, 1.0, 0.5);
-  const double fovy = edge_angle(Ki, 0.5, 0.0, 0.5, 1.0);
-  const double tx = tan(0.5 * fovx), ty = tan(0.5 * fovy);
-  // P (row-major) = get_projection_matrix
-  double P[16] = {0};
-  const double top = ty * n, right = tx * n;
-  P[0] = 2 * n / (2 * right);
-  P[5] = 2 * n / (2 * top);
-  P[14] = 1.0;  // [3][2]
-  P[10] = f / (f - n);
-  P[11] = -(f * n) / (f - n);
-  inv4(E, Wc);  // world -> camera, row-major
-  dsr_camera& c = cams[v];
-  // viewmatrix storage = (W2C)^T row-major  -> element [r*4 + c] = Wc[c*4 + r]
-  for (int r = 0; r < 4; ++r)
-    for (int q = 0; q < 4; ++q) c.viewmatrix[r * 4 + q] = (float)Wc[q * 4 + r];
-  // projmatrix storage = (P W2C)^T
-  for (int r = 0; r < 4; ++r)
-    for (int q = 0; q < 4; ++q) {
-      double s = 0;
-      for (int k = 0; k < 4; ++k) s += P[r * 4 + k] * Wc[k * 4 + q];
-      c.projmatrix[q * 4 + r] = (float)s;
-    }
-  c.campos[0] = (float)E[3];
-  c.campos[1] = (float)E[7];
-  c.campos[2] = (float)E[11];
-  c.tanfovx = (float)tx;
-  c.tanfovy = (float)ty;
-  c.bg[0] = bg[3 * v];
-  c.bg[1] = bg[3 * v + 1];
-  c.bg[2] = bg[3 * v + 2];
-  c.scene = view_scene[v];
-  c.scale = sc;
-  c._pad[0] = 0;
-  c._pad[1] = 0;
+  make_camera<double>(v, ext, intr, near, far, bg, view_scene, scale_invariant, cams[v]);
 }
-
 }  // namespace
 
 extern "C" int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, const float* near,

@@ -121,20 +121,18 @@ def _render_views(extrinsics, intrinsics, near, far, image_shape, background_col
                   use_sh, return_radii, degree):
     V = extrinsics.shape[0]
     h, w = image_shape
-    # the camera_settings() math, as one device kernel (no torch op chain, no host sync)
-    # (it also zeroes the per-(view, tile) counters the binning kernel accumulates into)
-    gx, gy = raster.tiles(h, w)
-    counts = torch.empty(V * gx * gy, dtype=torch.int32, device=extrinsics.device)
-    cams = raster.build_cameras(extrinsics, intrinsics, near, far, background_color.expand(V, 3), view_scene,
-                                scale_invariant, zero_counts=counts)
+    # the camera_settings() math runs on the device (no torch op chain, no host sync): in one
+    # launch that also zeroes the binning counters, or, for eager inference, inside the
+    # binning kernel itself
+    cams = raster.camera_inputs(extrinsics, intrinsics, near, far, background_color.expand(V, 3), view_scene,
+                                scale_invariant)
     # The kernels read the decoder's layouts directly: harmonics [S,G,3,d_sh] (no
     # "b g xyz n -> b g n xyz" copy) and full covariances through the triu gather (no
     # [S,G,6] copy); gradients come back in the same layouts (upper triangle for cov).
     feats = gaussian_sh_coefficients if use_sh else gaussian_sh_coefficients[..., 0]
     color, radii = raster.rasterize_views(
         gaussian_means, feats, gaussian_opacities, gaussian_covariances, cams, view_scene,
-        use_sh=use_sh, sh_degree=degree, image_height=h, image_width=w, channel_major_sh=True,
-        zeroed_counts=counts)
+        use_sh=use_sh, sh_degree=degree, image_height=h, image_width=w, channel_major_sh=True)
     return (color, radii) if return_radii else color
 
 

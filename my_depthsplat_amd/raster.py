@@ -91,8 +91,12 @@ def set_timer(t: KernelTimer | None) -> None:
 def last_stats() -> dict:
     """(num_rendered, max tile count) of the last forward (reads the device: syncs)."""
     c = _last["counts"]
-    if c is None:
-        return {"num_rendered": 0, "max_count": 0}
+    if c is None:  # consumed on the device (inference fast path): the newest pinned copy
+        hc = _last.get("host_counts")
+        if hc is None:
+            return {"num_rendered": 0, "max_count": 0}
+        hc[1].synchronize()
+        c = hc[0]
     n, m = int(c.sum()), int(c.max())
     _spec["max_count"] = m
     return {"num_rendered": n, "max_count": m}
@@ -145,6 +149,7 @@ class RasterState:
     seg_sorted: torch.Tensor | None = None    # [V*T] sorted entries per segment (prefix-sort mode)
     seg_overflow: torch.Tensor | None = None  # [V*T(+1)] tiles re-sorted in full and re-rendered
     tile_count: torch.Tensor | None = None    # [V*T] all entries per tile (depth-cut mode: seg_count = ends)
+    cams: torch.Tensor | None = None          # [V, 44] dsr_camera array the forward used
 
     @property
     def counts(self) -> torch.Tensor:
@@ -208,6 +213,7 @@ def _note_counts(counts: torch.Tensor) -> None:
         ev = torch.cuda.Event()
         ev.record()
         _inflight.append((host, ev))
+        _last["host_counts"] = (host, ev)
 
 
 def _key_capacity(V, G, T):
@@ -254,6 +260,71 @@ def _dense_bg(bg: torch.Tensor) -> torch.Tensor:
     return t
 
 
+@dataclass
+class CameraInputs:
+    """render_cuda's camera inputs, turned into dsr_camera structs by the first kernel that
+    needs them (dsr_build_cameras, or inside dsr_project_bin_cameras: no launch of its own).
+    extrinsics [V,4,4] c2w, intrinsics [V,3,3] normalised, near/far [V], bg [V,3] dense,
+    view_scene [V] int32 (device)."""
+    extrinsics: torch.Tensor
+    intrinsics: torch.Tensor
+    near: torch.Tensor
+    far: torch.Tensor
+    bg: torch.Tensor
+    view_scene: torch.Tensor
+    scale_invariant: bool
+
+    @property
+    def V(self) -> int:
+        return self.extrinsics.shape[0]
+
+
+def camera_inputs(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True) -> CameraInputs:
+    dev = extrinsics.device
+    _lib.require_gpu(extrinsics, intrinsics, near, far, bg)
+    vs = view_scene.to(device=dev, dtype=torch.int32) if isinstance(view_scene, torch.Tensor) \
+        else device_index(view_scene, dev)
+    f = lambda t: t.detach().contiguous().float()  # noqa: E731
+    return CameraInputs(f(extrinsics), f(intrinsics), f(near), f(far), _dense_bg(bg), vs, bool(scale_invariant))
+
+
+# Per-(device, size) counter buffers that are zero once the work of their last user is done:
+# dsr_sort_render(clear_counts=1) zeroes each counter as it consumes it, so the next inference
+# forward needs no zeroing launch (dsr_project_bin_cameras takes them as zeroed). A buffer is
+# reused on the stream that last used it (stream order), or on another stream once an event
+# recorded after its last use has completed. A buffer taken while a stream is captured into
+# a graph belongs to that graph from then on (each replay leaves it zeroed again).
+_clean_counts: dict = {}
+_graph_owned: list = []
+
+
+def _take_clean_counts(n: int, dev, stream) -> torch.Tensor | None:
+    key = (str(dev), n)
+    ent = _clean_counts.get(key)
+    capturing = torch.cuda.is_current_stream_capturing()
+    if ent is not None:
+        t, last_stream, ev = ent
+        # (events cannot be queried during capture: graphs.GraphedCall synchronizes the device
+        # before capturing, so the buffer's last user has finished by then)
+        if capturing or last_stream == int(stream) or ev.query():
+            del _clean_counts[key]
+            return t
+    if capturing:
+        return None  # a zeroing node inside the graph would cost what the fast path saves
+    return torch.zeros(n, dtype=torch.int32, device=dev)
+
+
+def _give_back_clean_counts(t: torch.Tensor, dev, stream) -> None:
+    if torch.cuda.is_current_stream_capturing():
+        _graph_owned.append(t)  # the captured graph keeps using (and re-zeroing) it
+        return
+    ev = torch.cuda.Event()
+    ev.record()
+    if len(_clean_counts) > 64:
+        _clean_counts.clear()
+    _clean_counts[(str(dev), t.numel())] = (t, int(stream), ev)
+
+
 def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True,
                   zero_counts: torch.Tensor | None = None) -> torch.Tensor:
     """Device-side camera set-up (dsr_build_cameras) -> [V, 44] float32 dsr_camera array.
@@ -298,7 +369,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     kernel (no scan, no second pass over the geometry, no host sync); otherwise the
     two-phase path counts, scans (one 8-byte read-back of N), scatters."""
     lib = _lib.load()
-    _lib.require_gpu(means, feats, opacities, cov6, cams)
+    cam_in = cams if isinstance(cams, CameraInputs) else None
+    _lib.require_gpu(means, feats, opacities, cov6, None if cam_in is not None else cams)
     S, G = means.shape[0], means.shape[1]
     M = (feats.shape[3] if layout & LAYOUT_SH_CHANNEL_MAJOR else feats.shape[2]) if use_sh else 0
     dev = means.device
@@ -310,25 +382,49 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     col_p = None if use_sh else feats.data_ptr()
     geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
     radii = torch.empty((V, G), dtype=torch.int32, device=dev)
-    if zeroed_counts is not None:  # zeroed by dsr_build_cameras (one launch fewer)
+    lds_cap = lib.dsr_sort_lds_capacity()
+    cap = _key_capacity(V, G, T)
+    fixed = cap is not None and T <= 32768 and V * T * G < (1 << 32)
+    maxc_hint = _spec["max_count"] or lds_cap
+    fused = fixed and FUSED_SORT_RENDER and maxc_hint <= FUSED_MAX
+    # eager inference fast path: cameras set up inside the binning kernel, counters taken zeroed
+    # from the previous call's sort + composite (two launches per forward)
+    fast = fused and cam_in is not None and not need_state and zeroed_counts is None
+    clean = _take_clean_counts(V * T, dev, st) if fast else None
+    fast = clean is not None
+    if fast:
+        seg_count = clean
+        layout |= LAYOUT_COUNTS_ZEROED
+        cams = torch.empty((V, CAM_FLOATS), dtype=torch.float32, device=dev)
+    elif zeroed_counts is not None:  # zeroed by dsr_build_cameras (one launch fewer)
         assert zeroed_counts.numel() == V * T and zeroed_counts.dtype == torch.int32
         seg_count = zeroed_counts
         layout |= LAYOUT_COUNTS_ZEROED
     else:
         seg_count = torch.empty(V * T, dtype=torch.int32, device=dev)
-    lds_cap = lib.dsr_sort_lds_capacity()
-    cap = _key_capacity(V, G, T)
-    if cap is not None and T <= 32768 and V * T * G < (1 << 32):
+    if cam_in is not None and not fast:  # one launch: cameras + zeroed counters
+        cams = build_cameras(cam_in.extrinsics, cam_in.intrinsics, cam_in.near, cam_in.far, cam_in.bg,
+                             cam_in.view_scene, cam_in.scale_invariant,
+                             zero_counts=None if layout & LAYOUT_COUNTS_ZEROED else seg_count)
+        layout |= LAYOUT_COUNTS_ZEROED
+    if fixed:
         keys = torch.empty(V * T * G, dtype=torch.int64, device=dev)
         # scratch for segments above the LDS sort (their size is unknown before the sort)
         scratch = torch.empty(V * T * G, dtype=torch.int64, device=dev)
-        _lib.check(_timed("k_project_emit", lib.dsr_project_bin,
-            S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-            cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout, st),
-            "dsr_project_bin")
-        maxc_hint = _spec["max_count"] or lds_cap
+        if fast:
+            ci = cam_in
+            _lib.check(_timed("k_project_emit", lib.dsr_project_bin_cameras,
+                S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+                ci.extrinsics.data_ptr(), ci.intrinsics.data_ptr(), ci.near.data_ptr(), ci.far.data_ptr(),
+                ci.bg.data_ptr(), ci.view_scene.data_ptr(), int(ci.scale_invariant), cams.data_ptr(),
+                geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout, st),
+                "dsr_project_bin_cameras")
+        else:
+            _lib.check(_timed("k_project_emit", lib.dsr_project_bin,
+                S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout,
+                st), "dsr_project_bin")
         seg_start, stride = None, G
-        fused = FUSED_SORT_RENDER and maxc_hint <= FUSED_MAX
         seg_sorted = None
         if not fused:
             ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
@@ -336,7 +432,6 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                       lds_cap)
         _note_counts(seg_count)
     else:
-        fused = False
         # the depth cut pays when tile lists are long; the previous two-phase call's largest
         # list (None on the first call) decides whether this one builds the depth histogram
         prev = _spec.get("two_phase_max")
@@ -399,9 +494,12 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     if fused:  # sort + composite in one launch; sorted keys kept only when a backward needs them
         _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(), None,
                           seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(), int(bool(need_state)),
-                          *outs), "dsr_sort_render")
-        state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib)
-        _last["counts"] = state.counts
+                          int(fast), *outs), "dsr_sort_render")
+        state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, cams=cams)
+        if fast:  # the counters are zero again once the launch above has run
+            _give_back_clean_counts(seg_count, dev, st)
+            state.seg_count = None  # consumed (no backward in this mode)
+        _last["counts"] = None if fast else state.counts
         return color, state
     overflow = None
     if seg_sorted is not None:
@@ -424,7 +522,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                       seg_count.data_ptr(), stride, keys.data_ptr(), None, None, overflow.data_ptr(),
                                       *outs), "dsr_render_fwd(overflow)")
     state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, seg_sorted, overflow,
-                        tile_count if stride == SEG_ENDS else None)
+                        tile_count if stride == SEG_ENDS else None, cams=cams)
     _last["counts"] = state.counts
     return color, state
 
@@ -491,7 +589,7 @@ class _RasterizeViews(torch.autograd.Function):
         V = len(view_scene)
         color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout,
                                    zeroed_counts, need_state=any(ctx.needs_input_grad[:5]))
-        ctx.save_for_backward(means, feats, opacities, cov6, cams)
+        ctx.save_for_backward(means, feats, opacities, cov6, state.cams)
         ctx.state = state
         ctx.meta = (view_scene, use_sh, sh_degree, None if means2d is None else means2d.shape, layout)
         ctx.mark_non_differentiable(state.radii)
@@ -521,8 +619,9 @@ def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.T
     view_scene[v] = scene index of view v. zeroed_counts: optional [V*tiles] int32 buffer already
     zeroed (build_cameras(zero_counts=...)). Returns color [V,3,H,W] and radii [V,G] (int32)."""
     S = means.shape[0]
-    if len(view_scene) != cams.shape[0]:
-        raise ValueError(f"view_scene has {len(view_scene)} entries for {cams.shape[0]} cameras")
+    n_cams = cams.V if isinstance(cams, CameraInputs) else cams.shape[0]
+    if len(view_scene) != n_cams:
+        raise ValueError(f"view_scene has {len(view_scene)} entries for {n_cams} cameras")
     if any(not (0 <= s < S) for s in view_scene):
         raise ValueError(f"view_scene entries must be in [0, {S})")
     n_coef = (feats.shape[3] if channel_major_sh else feats.shape[2]) if use_sh else 0
@@ -532,7 +631,8 @@ def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.T
         raise ValueError("image size must be positive")
     f = lambda t: t.contiguous().float()  # noqa: E731
     layout = input_layout(feats, cov6, use_sh, channel_major_sh)
-    return _RasterizeViews.apply(f(means), f(feats), f(opacities), f(cov6), means2d, cams.contiguous(),
+    return _RasterizeViews.apply(f(means), f(feats), f(opacities), f(cov6), means2d,
+                                 cams if isinstance(cams, CameraInputs) else cams.contiguous(),
                                  list(view_scene), use_sh, int(sh_degree), int(image_height), int(image_width),
                                  layout, zeroed_counts)
 
