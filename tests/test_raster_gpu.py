@@ -568,3 +568,45 @@ def test_graph_capture_replay_matches_eager(gpu):
     want = step().color.clone()
     assert torch.equal(g().color, want)
     assert not torch.equal(want, eager)
+
+
+def test_inference_fast_path_matches_state_path(gpu):
+    """Eager inference (no grad): cameras built inside the binning kernel by one wave, counters
+    re-zeroed by the fused sort + composite and reused by the next call. Repeated calls with
+    alternating sizes must keep matching the stateful path (device cameras in double), and the
+    in-kernel camera block must match dsr_build_cameras."""
+    from my_depthsplat_amd import raster
+    from my_depthsplat_amd.cuda_splatting import _cov6, render_views
+    from my_depthsplat_amd.synthetic import make_scene
+    scenes = {hw: make_scene(batch=1, n_context=2, n_targets=3, height=hw[0], width=hw[1], seed=21, device=gpu)
+              for hw in ((48, 64), (64, 96))}
+    refs = {}
+    for hw, sc in scenes.items():
+        g = sc.gaussians
+        bg = torch.rand(3, 3, device=gpu)
+        cams = raster.build_cameras(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0], bg,
+                                    [0, 0, 0], True)
+        img, _ = raster.rasterize_views(g.means, g.harmonics.transpose(-1, -2), g.opacities, _cov6(g.covariances),
+                                        cams, [0, 0, 0], use_sh=True, sh_degree=2, image_height=hw[0],
+                                        image_width=hw[1])
+        refs[hw] = (img, bg, cams)
+    for hw in ((48, 64), (64, 96), (48, 64), (48, 64), (64, 96)):
+        sc, (ref, bg, cams_ref) = scenes[hw], refs[hw]
+        g = sc.gaussians
+        with torch.no_grad():
+            img = render_views(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0], hw, bg,
+                               g.means, g.covariances, g.harmonics, g.opacities, [0, 0, 0])
+        torch.cuda.synchronize()
+        assert float((img - ref).abs().mean()) < 1e-5, hw
+        assert float((img - ref).abs().max()) < 2e-2, hw
+    # camera block of the fast path (the last call's state keeps it) vs the double-precision one
+    ci = raster.camera_inputs(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0], bg,
+                              [0, 0, 0], True)
+    with torch.no_grad():
+        _, st = raster.forward_raw(g.means, g.harmonics, True, 2, g.opacities, g.covariances, ci, 3, hw[0], hw[1],
+                                   raster.input_layout(g.harmonics, g.covariances, True, True), need_state=False)
+    torch.cuda.synchronize()
+    assert st.seg_count is None  # the two-launch path ran (counters consumed)
+    c_fast, c_ref = st.cams.view(3, -1)[:, :42], cams_ref.view(3, -1)[:, :42]
+    assert torch.allclose(c_fast, c_ref, rtol=1e-5, atol=1e-5), float((c_fast - c_ref).abs().max())
+    assert torch.equal(st.cams.view(3, -1)[:, 42:], cams_ref.view(3, -1)[:, 42:])
