@@ -42,8 +42,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--eager", action="store_true", help="time eager launches only (no hipGraph capture)")
-    p.add_argument("--launch", choices=["auto", "hipgraph", "eager"], default="auto",
-                   help="launch mode of the timed region (auto: the faster of a short calibration of both)")
+    p.add_argument("--launch", choices=["auto", "hipgraph", "hipgraph2", "hipgraph3", "hipgraph4", "eager"], default="auto",
+                   help="launch mode of the timed region (auto: the fastest in a short calibration of all)")
     p.add_argument("--extra", default="train,dl3dv,recon12",
                    help="secondary measurements: train (config C step), dl3dv (6-view 448x768 render), "
                         "recon12 (12-view 512x960 reconstruction, 100 views in chunks of 10); '' = none")
@@ -110,25 +110,44 @@ def main():
     # eagerly (the host runs ahead of the device, so launch gaps hide either way; on the
     # MI355X boxes eager measured ~2 % faster: graph kernel nodes are separated by heavier
     # barriers). A short calibration of both picks the mode; every kernel runs in both.
-    runner, mode = step, "eager"
+    # "hipgraphN" (N = 2..4): N such graphs (own buffers each) replayed in turn on N HIP
+    # streams, so consecutive scenes overlap — one scene's compositing tail shares the chip with the
+    # next scene's binning. Every step still renders its whole scene; only the overlap differs.
+    runner, mode, cal = step, "eager", None
     if not args.eager:
         from my_depthsplat_amd.graphs import GraphedCall
         graphed = GraphedCall(step, warmup=2)
         out = graphed()
+        graphs = [graphed] + [GraphedCall(step, warmup=2) for _ in range(3)]
+        lanes = [torch.cuda.Stream(device=dev) for _ in graphs]
+        turn = [0]
+
+        def multi_stream(n):
+            def run():
+                i = turn[0] % n
+                turn[0] += 1
+                with torch.cuda.stream(lanes[i]):
+                    return graphs[i]()
+            return run
+
+        modes = {"hipgraph": graphed, **{f"hipgraph{n}": multi_stream(n) for n in (2, 3, 4)}, "eager": step}
         if args.launch == "auto":
             ncal = max(10, min(50, args.steps))
-            t_graph, t_eager = timed(graphed, ncal), timed(step, ncal)
+            cal = {m: timed(fn, ncal) for m, fn in modes.items()}
             if world > 1:  # every rank takes the same decision
-                t = torch.tensor([t_graph, t_eager], device=dev, dtype=torch.float64)
+                t = torch.tensor(list(cal.values()), device=dev, dtype=torch.float64)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                t_graph, t_eager = (float(x) for x in t.tolist())
-            use_graph = t_graph <= t_eager
+                cal = dict(zip(cal, t.tolist()))
+            mode = min(cal, key=cal.get)
+            cal = {m: round(1e3 * t / ncal, 4) for m, t in cal.items()}
         else:
-            use_graph = args.launch == "hipgraph"
-        if use_graph:
-            runner, mode = graphed, "hipgraph"
+            mode = args.launch
+        runner = modes[mode]
     # timed region 1 (value): exactly K steps in the chosen mode
     elapsed = timed(runner, args.steps)
+    if mode.startswith("hipgraph") and mode != "hipgraph":  # the captures in use rendered the same scene
+        used = graphs[:int(mode[len("hipgraph"):])]
+        assert all(torch.equal(graphed.out.color, g.out.color) for g in used), f"{mode} captures disagree"
     # timed region 2: the same K steps launched eagerly, with HIP events recorded around the
     # dominant kernel on its launch stream (its average duration feeds the roofline)
     ev = raster.KernelTimer(only=[dominant])
@@ -177,13 +196,14 @@ def main():
             "metric": "rendered views/sec + PSNR, 2-view 256x256 RE10K, 1/2/4/8 MI355X",
             "value": round(value, 2), "unit": "views/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
-            "launch_mode": mode,
+            "launch_mode": mode, "launch_calibration_ms_per_step": cal,
             "ms_per_step_eager": round(1e3 * elapsed_eager / args.steps, 4),
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.context}-view {H}x{W} RE10K feed-forward render, 1 Gaussian/pixel "
                                    f"(G={G}), {args.views} target views/scene, fp32",
                        "global_batch": args.batch * world, "views_per_scene": args.views, "gaussians": G,
-                       "num_rendered_per_step": n_rendered, "parallelism": f"dp{world} (per-scene, no collective)"},
+                       "num_rendered_per_step": n_rendered, "parallelism": f"dp{world} (per-scene, no collective)",
+                       "scenes_in_flight_per_gpu": int(mode[len("hipgraph"):] or 1) if mode.startswith("hipgraph") else 1},
             "psnr_vs_oracle_db": psnr, "l1_vs_oracle": l1,
             "roofline": roof, "cpu_baseline": cpu,
             **extra,

@@ -2199,6 +2199,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) 
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int seg = v * T + blockIdx.y * gx + blockIdx.x;
+#ifdef SR_TIMING  // diagnostics (tools/wg_timing.py): per-workgroup start / end / size / placement
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef SR_PRIO
+  {
+    const int L = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    const int pr = min(L >> 8, 3);
+    if (pr == 1) __builtin_amdgcn_s_setprio(1);
+    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+    else if (pr == 3) __builtin_amdgcn_s_setprio(3);
+  }
+#endif
   uint32_t b, e;
   seg_bounds(seg_start, seg_count, stride, seg, b, e);
   const uint32_t n = e - b;
@@ -2244,6 +2256,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) 
   // counts handed back zeroed for the next call's binning (every thread read it before the
   // sort's first barrier)
   if (clear_counts && tid == 0) seg_count[seg] = 0u;
+#ifdef SR_TIMING
+  __syncthreads();
+  if (tid == 0) {
+    scratch[4 * seg] = t_start;
+    scratch[4 * seg + 1] = __builtin_amdgcn_s_memrealtime();
+    scratch[4 * seg + 2] = n;
+    scratch[4 * seg + 3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                           ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------

@@ -86,6 +86,15 @@ def main():
                     return rc
                 return lib.dsr_bin_sort(G, V, H, W, None, cnt2.data_ptr(), a.stride or G, keys2.data_ptr(),
                                         scratch2.data_ptr(), state.max_count, ws_p, 0, None, None, st)
+        elif a.kernel == "sort_render":  # fused sort + composite (keys already sorted: same work)
+            assert stride > 0, "fused layout expected"
+            out = [torch.empty_like(color), torch.empty_like(state.final_T), torch.empty_like(state.n_contrib)]
+            scr4 = torch.empty_like(state.keys)
+
+            def launch():
+                return lib.dsr_sort_render(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), None, sc_p, stride,
+                                           state.keys.data_ptr(), scr4.data_ptr(), 0, 0, out[0].data_ptr(),
+                                           out[1].data_ptr(), out[2].data_ptr(), st)
         elif a.kernel == "scatter":  # two-phase key scatter from the scan's segment starts
             assert stride == 0, "two-phase layout expected (--two-phase)"
             cur = torch.empty_like(state.seg_start)
