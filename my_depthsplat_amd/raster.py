@@ -192,6 +192,9 @@ CUT_SORT_HINT = 4096  # LDS sort size for the written parts (larger ones sort th
 # dsr_render_fwd (MSD split, prefix sort). Either is exact for any list length.
 FUSED_SORT_RENDER = os.environ.get("DSPLAT_FUSED_SORT_RENDER", "1") != "0"
 FUSED_MAX = 4096
+# inference fast path (cameras inside the binning kernel, self-zeroing counters); env
+# DSPLAT_INKERNEL_CAMERAS=0 keeps the separate camera launch (experiments)
+INKERNEL_CAMERAS = os.environ.get("DSPLAT_INKERNEL_CAMERAS", "1") != "0"
 SEG_ENDS = 0xFFFFFFFF  # DSR_SEG_ENDS
 _spec = {"max_count": 0}
 _inflight: list = []  # (pinned int32 counts, event) read-backs, consumed without blocking
@@ -389,7 +392,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     fused = fixed and FUSED_SORT_RENDER and maxc_hint <= FUSED_MAX
     # eager inference fast path: cameras set up inside the binning kernel, counters taken zeroed
     # from the previous call's sort + composite (two launches per forward)
-    fast = fused and cam_in is not None and not need_state and zeroed_counts is None
+    fast = fused and INKERNEL_CAMERAS and cam_in is not None and not need_state and zeroed_counts is None
     clean = _take_clean_counts(V * T, dev, st) if fast else None
     fast = clean is not None
     if fast:

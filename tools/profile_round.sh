@@ -9,8 +9,13 @@ tag=${1:-r01}
 export TMPDIR=/tmp
 out=gpurun_out/prof_$tag
 mkdir -p $out
+# (--launch hipgraph: one scene in flight, so the per-kernel averages are the kernels' own
+# durations, comparable with the roofline's eager single-stream HIP-event timing; with N
+# scenes in flight the kernels share the chip and their durations stretch)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats -o run -- \
-  python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --extra "" > $out/stats.log 2>&1
+  python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --extra "" --launch hipgraph > $out/stats.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_default -o run -- \
+  python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --extra "" > $out/stats_default.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- \
   python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --eager --extra "" > $out/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- \
