@@ -111,8 +111,8 @@ struct WaveRects {
 // marks (DPP, no dependent LDS search); the tile comes from (j - ex) / width with a hardware
 // reciprocal and exact integer fix-ups. f(tile, owner lane[, tile x, tile y]).
 template <typename F>
-__device__ __forceinline__ void for_each_rect_tile(WaveRects& wr, int lane, int x0, int y0, int x1, int y1,
-                                                   bool has, int gx, F f) {
+__device__ __forceinline__ uint32_t for_each_rect_tile(WaveRects& wr, int lane, int x0, int y0, int x1, int y1,
+                                                       bool has, int gx, F f) {
   const uint32_t area = has ? (uint32_t)((x1 - x0) * (y1 - y0)) : 0u;
   const uint32_t incl = dsplat::wave_incl_add_dpp(area);
   const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -147,6 +147,7 @@ __device__ __forceinline__ void for_each_rect_tile(WaveRects& wr, int lane, int 
     }
     __builtin_amdgcn_wave_barrier();
   }
+  return total;
 }
 
 struct Cov2D {
@@ -632,6 +633,13 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
 #ifndef PB_WPE
 #define PB_WPE 1
 #endif
+// pair cache of the count pass (PE_CAPW (tile, rank, owner) words per wave in LDS)
+#ifndef PE_CACHE
+#define PE_CACHE 1
+#endif
+#ifndef PE_CAPW
+#define PE_CAPW 768
+#endif
 template <int DEG, bool CAM>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
                                                      const float* __restrict__ means,
@@ -647,6 +655,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
   __shared__ dsr_camera s_cam[1];  // CAM only
+#if PE_CACHE
+  __shared__ uint32_t s_pairs[NT / 64][PE_CAPW];
+  __shared__ uint32_t s_ovf;
+#endif
   int v, blk;
   if (!xcd_item((G + NT - 1) / NT, V, v, blk)) return;
   const dsr_camera* cam = cams + v;
@@ -677,8 +689,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
       key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
     }
     s_key[tid] = key;
+#if PE_CACHE
+    if (tid == 0) s_ovf = 0u;
+#endif
     __syncthreads();
+#if PE_CACHE
+    // count pass; each pair's rank among the workgroup's entries of its tile (the LDS atomic's
+    // return value) is kept with the tile and the owner lane, so the emission pass below is a
+    // plain walk over the kept pairs instead of a second rect expansion
+    uint32_t* wp = s_pairs[w];
+    uint32_t stp = 0;
+    const uint32_t wtotal = for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o) {
+      const uint32_t rk = atomicAdd(&s_hist[t], 1u);
+      const uint32_t j = stp++ * 64u + (uint32_t)lane;
+      if (j < (uint32_t)PE_CAPW) wp[j] = (uint32_t)t | (rk << 16) | ((uint32_t)o << 24);
+    });
+    if (lane == 0 && wtotal > (uint32_t)PE_CAPW) s_ovf = 1u;
+#else
     for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
+#endif
     __syncthreads();
     uint32_t* gcount = seg_count + (size_t)v * T;
     for (int t = tid; t < T; t += NT) {
@@ -696,6 +725,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
                        [&](int t, int o) { vkeys[(size_t)t * PB_STRIDE + atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
 #else
     uint64_t* vkeys = keys + (size_t)v * T * G;
+#if PE_CACHE
+    if (!s_ovf) {  // workgroup-uniform
+      for (uint32_t j = (uint32_t)lane; j < wtotal; j += 64u) {
+        const uint32_t p = wp[j];
+        const uint32_t t = p & 0xFFFFu;
+        vkeys[(size_t)t * G + s_hist[t] + ((p >> 16) & 0xFFu)] = wkey[p >> 24];
+      }
+      return;
+    }
+#endif
     for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
                        [&](int t, int o) { vkeys[(size_t)t * G + atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
 #endif

@@ -646,3 +646,25 @@ def test_inference_fast_path_matches_state_path(gpu):
     c_fast, c_ref = st.cams.view(3, -1)[:, :42], cams_ref.view(3, -1)[:, :42]
     assert torch.allclose(c_fast, c_ref, rtol=1e-5, atol=1e-5), float((c_fast - c_ref).abs().max())
     assert torch.equal(st.cams.view(3, -1)[:, 42:], cams_ref.view(3, -1)[:, 42:])
+
+
+@pytest.mark.parametrize("cov_scale", [1.0, 30.0, 100.0])
+def test_emit_pair_cache_and_overflow(gpu, cov_scale):
+    """k_project_emit keeps each count-pass pair (tile, rank, owner) in LDS, 768 per wave, and
+    emits keys from that list; a workgroup with a wave over the cap re-expands its rects
+    instead. Growing the Gaussians moves workgroups from the first path to the second (both
+    occur at 30x); the segments must equal the oracle's sorted lists either way."""
+    from my_depthsplat_amd import raster
+    sc = scene_inputs(h=128, w=128, seed=7, n_ctx=2)
+    sc.gaussians.covariances = sc.gaussians.covariances * cov_scale
+    st = settings_for(sc)
+    color, state, _ = hip_forward(sc, st, gpu)
+    assert state.seg_stride > 0  # fixed-capacity binning (the kernel under test)
+    B, v = sc.target_extrinsics.shape[:2]
+    gx, gy = raster.tiles(128, 128)
+    orcs = oracle_views(sc, st)
+    _check_segments_vs_oracle(state, orcs, B * v, gx * gy)
+    for i, o in enumerate(orcs):
+        oc, _, _ = o.image()
+        assert float(np.abs(color[i].cpu().numpy() - oc).mean()) < 1e-4
+        o.close()
