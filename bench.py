@@ -33,8 +33,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec); 6.29 TB/s 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=500)  # ~30 ms timed at ~60 us per scene
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=1, help="scenes per step per GPU (reference test loop: 1)")
     p.add_argument("--views", type=int, default=3, help="target views per scene (RE10K eval: 3)")
     p.add_argument("--size", type=int, default=256)

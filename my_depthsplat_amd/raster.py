@@ -177,7 +177,7 @@ class RasterState:
 # that fits KEY_BUDGET_BYTES (1.6 GB at 2x256^2 x 3 views: cheap on a 288 GB part, and
 # untouched pages cost no bandwidth); the whole forward then runs with NO host sync.
 # Larger problems fall back to one 8-byte read of (N, max tile count) after the scan.
-KEY_BUDGET_BYTES = 8 << 30
+KEY_BUDGET_BYTES = int(float(os.environ.get("DSPLAT_KEY_BUDGET_GB", "8")) * (1 << 30))
 # Segments larger than this many entries (only when some exceed the LDS sort) get only their
 # nearest SORT_PREFIX entries put in order (dsr_bin_sort prefix mode): at 6x448x768 the
 # compositor uses at most ~1.2K of 30-40K entries per tile. 0 sorts everything.
