@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--eager", action="store_true", help="time eager launches only (no hipGraph capture)")
-    p.add_argument("--launch", choices=["auto", "hipgraph", "hipgraph2", "hipgraph3", "hipgraph4", "eager"], default="auto",
+    p.add_argument("--launch", choices=["auto", "hipgraph", "eager"] + [f"hipgraph{n}" for n in range(2, 9)], default="auto",
                    help="launch mode of the timed region (auto: the fastest in a short calibration of all)")
     p.add_argument("--extra", default="train,dl3dv,recon12",
                    help="secondary measurements: train (config C step), dl3dv (6-view 448x768 render), "
@@ -118,7 +118,8 @@ def main():
         from my_depthsplat_amd.graphs import GraphedCall
         graphed = GraphedCall(step, warmup=2)
         out = graphed()
-        graphs = [graphed] + [GraphedCall(step, warmup=2) for _ in range(3)]
+        max_lanes = int(os.environ.get("DSPLAT_BENCH_MAX_LANES", "4"))
+        graphs = [graphed] + [GraphedCall(step, warmup=2) for _ in range(max_lanes - 1)]
         lanes = [torch.cuda.Stream(device=dev) for _ in graphs]
         turn = [0]
 
@@ -130,7 +131,8 @@ def main():
                     return graphs[i]()
             return run
 
-        modes = {"hipgraph": graphed, **{f"hipgraph{n}": multi_stream(n) for n in (2, 3, 4)}, "eager": step}
+        modes = {"hipgraph": graphed, **{f"hipgraph{n}": multi_stream(n) for n in range(2, max_lanes + 1)},
+                 "eager": step}
         if args.launch == "auto":
             ncal = max(10, min(50, args.steps))
             cal = {m: timed(fn, ncal) for m, fn in modes.items()}
