@@ -8,12 +8,14 @@ the library shares torch's streams and device allocations.
 from __future__ import annotations
 
 import ctypes
+import os
 from ctypes import c_float, c_int, c_uint32, c_void_p
 from pathlib import Path
 
 import torch  # noqa: F401  (must be loaded before the HIP library)
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libdsplat_hip.so"
+# (DSPLAT_LIB: another build of the same ABI, e.g. a tools/variants.py experiment)
+LIB_PATH = Path(os.environ.get("DSPLAT_LIB") or Path(__file__).resolve().parent / "lib" / "libdsplat_hip.so")
 
 # name -> (restype, argtypes); mirrors include/dsplat_hip.h exactly.
 _P = c_void_p
