@@ -668,3 +668,34 @@ def test_emit_pair_cache_and_overflow(gpu, cov_scale):
         oc, _, _ = o.image()
         assert float(np.abs(color[i].cpu().numpy() - oc).mean()) < 1e-4
         o.close()
+
+
+@pytest.mark.parametrize("case", ["ragged", "culled", "one_view"])
+def test_inference_fast_path_edge_cases(gpu, case):
+    """The two-launch inference path on a ragged image (50x70: partial edge tiles), a scene
+    whose Gaussians are all behind the camera (background only), and a single view; each
+    against the stateful path with device cameras, called twice (counters reused)."""
+    from my_depthsplat_amd import raster
+    from my_depthsplat_amd.cuda_splatting import _cov6, render_views
+    from my_depthsplat_amd.synthetic import make_scene
+    h, w = (50, 70) if case == "ragged" else (48, 64)
+    n_tgt = 1 if case == "one_view" else 2
+    sc = make_scene(batch=1, n_context=2, n_targets=n_tgt, height=h, width=w, seed=23, device=gpu)
+    g = sc.gaussians
+    if case == "culled":
+        g.means = g.means * torch.tensor([1.0, 1.0, -1.0], device=gpu)
+    vs = [0] * n_tgt
+    bg = torch.tensor([[0.25, 0.5, 0.75]], device=gpu).expand(n_tgt, 3).contiguous()
+    cams = raster.build_cameras(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0], bg, vs, True)
+    ref, _ = raster.rasterize_views(g.means, g.harmonics.transpose(-1, -2), g.opacities, _cov6(g.covariances), cams,
+                                    vs, use_sh=True, sh_degree=2, image_height=h, image_width=w)
+    for _ in range(2):
+        with torch.no_grad():
+            img = render_views(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0], (h, w), bg,
+                               g.means, g.covariances, g.harmonics, g.opacities, vs)
+        torch.cuda.synchronize()
+        assert img.shape == (n_tgt, 3, h, w)
+        assert float((img - ref).abs().mean()) < 1e-5
+        if case == "culled":
+            want = bg[:, :, None, None].expand_as(img)
+            assert torch.equal(img, want)
