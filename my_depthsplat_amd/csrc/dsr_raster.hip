@@ -890,8 +890,9 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
   WaveRects& wr = s_wr[w];
   const uint64_t* wkey = s_key + w * 64;
   const int nblk = (G + NTH - 1) / NTH;
-  const int b0 = (int)((int64_t)nblk * p / per_view), b1 = (int)((int64_t)nblk * (p + 1) / per_view);
-  for (int blk = b0; blk < b1; ++blk) {
+  // blocks dealt round-robin (p, p + per_view, ...): neighbouring blocks (context-image rows)
+  // carry similar loads, so contiguous runs left some workgroups with several times the work
+  for (int blk = p; blk < nblk; blk += per_view) {
     const int g = blk * NTH + tid;
     int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     uint64_t key = 0;
@@ -961,9 +962,8 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
   __syncthreads();
   const dsr_camera* cam = cams + v;
   const int nblk = (G + NTH - 1) / NTH;
-  const int b0 = (int)((int64_t)nblk * p / per_view), b1 = (int)((int64_t)nblk * (p + 1) / per_view);
   WaveRects& wr = s_wr[w];
-  for (int blk = b0; blk < b1; ++blk) {
+  for (int blk = p; blk < nblk; blk += per_view) {  // round-robin blocks (see k_scatter_cut)
     const int g = blk * NTH + tid;
     int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     uint32_t zb = 0u;
