@@ -110,9 +110,14 @@ struct WaveRects {
 // holds j, found per window by marking each run's first slot and a wave max-scan of the
 // marks (DPP, no dependent LDS search); the tile comes from (j - ex) / width with a hardware
 // reciprocal and exact integer fix-ups. f(tile, owner lane[, tile x, tile y]).
-template <typename F>
+// pre(owner) runs on every lane of each 64-pair window before f, outside the j < total
+// branch, so it may use cross-lane operations (ds_bpermute needs its source lanes active).
+struct NoPre {
+  __device__ void operator()(int) const {}
+};
+template <typename F, typename P = NoPre>
 __device__ __forceinline__ uint32_t for_each_rect_tile(WaveRects& wr, int lane, int x0, int y0, int x1, int y1,
-                                                       bool has, int gx, F f) {
+                                                       bool has, int gx, F f, P pre = P{}) {
   const uint32_t area = has ? (uint32_t)((x1 - x0) * (y1 - y0)) : 0u;
   const uint32_t incl = dsplat::wave_incl_add_dpp(area);
   const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -130,6 +135,7 @@ __device__ __forceinline__ uint32_t for_each_rect_tile(WaveRects& wr, int lane, 
     if (lane == 0) m = max(m, carry);
     const uint32_t own = dsplat::wave_incl_max_dpp(m);
     carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
+    pre(max((int)own - 1, 0));
     const uint32_t j = base + (uint32_t)lane;
     if (j < total) {
       const int o = (int)own - 1;
@@ -622,6 +628,77 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
   }
 }
 
+// Exact tile test of the inference binning (PE_EXACT): can the alpha >= 1/255 ellipse of a
+// Gaussian reach a pixel centre of the tile box [x0, x0 + BX - 1] x [y0, y0 + BY - 1]? The
+// same continuous-box minimum of the conic as the compositor's rect_hit (defined with it
+// below), with the per-Gaussian terms computed once by the owner lane (TileEll) and moved to
+// the pair's lane by ds_bpermute. A tile it rejects is one where the compositor's per-pixel
+// test fails at every pixel, so dropping the pair leaves every blend unchanged.
+struct TileEll {
+  float x, y, a, b, c, t2, ia, ic;  // t2 < 0: opacity below 1/255 (reaches nothing)
+};
+__device__ __forceinline__ TileEll tile_ell(const float* rec, int r) {
+  TileEll e;
+  e.x = rec[0];
+  e.y = rec[1];
+  e.a = rec[2];
+  e.b = rec[3];
+  e.c = rec[4];
+  const float op = rec[5];
+  e.t2 = (r > 0 && op >= 1.0f / 255.0f) ? 2.0f * __logf(255.0f * op) * 1.002f + 0.02f : -1.0f;
+  e.ia = 1.0f / e.a;
+  e.ic = 1.0f / e.c;
+  return e;
+}
+__device__ __forceinline__ TileEll tile_ell_of(const TileEll& e, int o) {
+  return TileEll{__shfl(e.x, o), __shfl(e.y, o), __shfl(e.a, o), __shfl(e.b, o),
+                 __shfl(e.c, o), __shfl(e.t2, o), __shfl(e.ia, o), __shfl(e.ic, o)};
+}
+__device__ __forceinline__ bool tile_reach(const TileEll& e, int tx, int ty) {
+  if (!(e.t2 >= 0.f)) return false;
+  const float a = e.a, b = e.b, c = e.c;
+  if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;  // degenerate / NaN: keep
+  const float lx = (float)(tx * BX) - e.x, hx = lx + (float)(BX - 1);
+  const float ly = (float)(ty * BY) - e.y, hy = ly + (float)(BY - 1);
+  if (lx <= 0.f && hx >= 0.f && ly <= 0.f && hy >= 0.f) return true;
+  float m = 3.4e38f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float dx = k ? hx : lx;
+    const float dy = fminf(fmaxf(-b * dx * e.ic, ly), hy);
+    m = fminf(m, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float dy = k ? hy : ly;
+    const float dx = fminf(fmaxf(-b * dy * e.ia, lx), hx);
+    m = fminf(m, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
+  }
+  return !(m > e.t2);
+}
+// Tile rect of the alpha >= 1/255 ellipse's bounding box (half extents sqrt(t2 c / det),
+// sqrt(t2 a / det), padded), intersected with the 3-sigma rect [x0, x1) x [y0, y1): fewer
+// pairs to expand before tile_reach. Degenerate / NaN conics keep the 3-sigma rect.
+__device__ __forceinline__ void tile_rect_alpha(const TileEll& e, int& x0, int& y0, int& x1, int& y1) {
+  if (!(e.t2 >= 0.f)) {
+    x1 = x0;
+    y1 = y0;
+    return;
+  }
+  const float det = e.a * e.c - e.b * e.b;
+  const float hx = sqrtf(e.t2 * e.c / det) * 1.002f + 0.05f, hy = sqrtf(e.t2 * e.a / det) * 1.002f + 0.05f;
+  if (!(e.a > 0.f && e.c > 0.f && det > 0.f) || !(hx == hx) || !(hy == hy)) return;
+  const float lim = 65536.f;
+  x0 = max(x0, (int)floorf(fminf(fmaxf((e.x - hx) * (1.0f / BX), -1.f), lim)));
+  x1 = min(x1, (int)floorf(fminf(fmaxf((e.x + hx) * (1.0f / BX), -1.f), lim)) + 1);
+  y0 = max(y0, (int)floorf(fminf(fmaxf((e.y - hy) * (1.0f / BY), -1.f), lim)));
+  y1 = min(y1, (int)floorf(fminf(fmaxf((e.y + hy) * (1.0f / BY), -1.f), lim)) + 1);
+  if (x1 <= x0 || y1 <= y0) {
+    x1 = x0;
+    y1 = y0;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // K1+K3 fused (fixed-capacity binning): one workgroup per (256 Gaussians, view) projects
 // them, counts the block's (view, tile) entries in an LDS histogram, reserves a contiguous
@@ -639,6 +716,11 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
 #endif
 #ifndef PE_CAPW
 #define PE_CAPW 768
+#endif
+// exact ellipse-vs-tile test in the inference binning (CAM path only: the stateful path keeps
+// the reference's rect lists, which the backward and the oracle list tests follow)
+#ifndef PE_EXACT
+#define PE_EXACT 1
 #endif
 template <int DEG, bool CAM>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
@@ -671,6 +753,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
     for (int t = tid; t < T; t += NT) s_hist[t] = 0;
     int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     uint64_t key = 0;
+    constexpr bool EXACT = CAM && PE_EXACT;
+    TileEll ell{0.f, 0.f, 0.f, 0.f, 0.f, -1.f, 0.f, 0.f};
     GaussIn<DEG> in;
     if (g < G) load_gauss<DEG>(in, (size_t)(CAM ? ci.view_scene[v] : cam->scene) * G + g, means, opac, cov6, layout);
     if constexpr (CAM) {
@@ -687,25 +771,40 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
       r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
       store_geom(geom, radii, (size_t)v * G + g, rec, r);
       key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
+      if constexpr (EXACT) {
+        ell = tile_ell(rec, r);
+        if (r > 0) tile_rect_alpha(ell, x0, y0, x1, y1);
+      }
     }
     s_key[tid] = key;
 #if PE_CACHE
     if (tid == 0) s_ovf = 0u;
 #endif
     __syncthreads();
+    TileEll oe = ell;  // the owner's ellipse terms for the current pair (EXACT)
+    const auto fetch = [&](int o) {
+      if constexpr (EXACT) oe = tile_ell_of(ell, o);
+    };
 #if PE_CACHE
     // count pass; each pair's rank among the workgroup's entries of its tile (the LDS atomic's
     // return value) is kept with the tile and the owner lane, so the emission pass below is a
     // plain walk over the kept pairs instead of a second rect expansion
     uint32_t* wp = s_pairs[w];
     uint32_t stp = 0;
-    const uint32_t wtotal = for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o) {
-      const uint32_t rk = atomicAdd(&s_hist[t], 1u);
+    const uint32_t wtotal = for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
       const uint32_t j = stp++ * 64u + (uint32_t)lane;
+      if constexpr (EXACT) {
+        if (!tile_reach(oe, tx, ty)) {  // dropped pair: a hole in the list
+          if (j < (uint32_t)PE_CAPW) wp[j] = 0xFFFFFFFFu;
+          return;
+        }
+      }
+      const uint32_t rk = atomicAdd(&s_hist[t], 1u);
       if (j < (uint32_t)PE_CAPW) wp[j] = (uint32_t)t | (rk << 16) | ((uint32_t)o << 24);
-    });
+    }, fetch);
     if (lane == 0 && wtotal > (uint32_t)PE_CAPW) s_ovf = 1u;
 #else
+    static_assert(!EXACT, "PE_EXACT needs the pair cache");
     for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
 #endif
     __syncthreads();
@@ -729,14 +828,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
     if (!s_ovf) {  // workgroup-uniform
       for (uint32_t j = (uint32_t)lane; j < wtotal; j += 64u) {
         const uint32_t p = wp[j];
+        if (EXACT && p == 0xFFFFFFFFu) continue;
         const uint32_t t = p & 0xFFFFu;
         vkeys[(size_t)t * G + s_hist[t] + ((p >> 16) & 0xFFu)] = wkey[p >> 24];
       }
       return;
     }
 #endif
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
-                       [&](int t, int o) { vkeys[(size_t)t * G + atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
+      if constexpr (EXACT) {
+        if (!tile_reach(oe, tx, ty)) return;  // same decision as the count pass
+      }
+      vkeys[(size_t)t * G + atomicAdd(&s_hist[t], 1u)] = wkey[o];
+    }, fetch);
 #endif
   }
 }

@@ -699,3 +699,40 @@ def test_inference_fast_path_edge_cases(gpu, case):
         if case == "culled":
             want = bg[:, :, None, None].expand_as(img)
             assert torch.equal(img, want)
+
+
+@pytest.mark.parametrize("case", ["large", "anisotropic", "low_opacity"])
+def test_inference_exact_tile_binning(gpu, case):
+    """The inference binning (k_project_emit with in-kernel cameras) keeps a (Gaussian, tile)
+    pair only when the Gaussian's alpha >= 1/255 ellipse reaches a pixel centre of the tile
+    (opacity-aware box, then the exact conic minimum over the tile); the stateful path keeps
+    the reference's 3-sigma rects. Dropped pairs never blend, so the images must agree on
+    Gaussians that are large, strongly anisotropic, or near / below the 1/255 opacity floor."""
+    from my_depthsplat_amd import raster
+    from my_depthsplat_amd.cuda_splatting import _cov6, render_views
+    from my_depthsplat_amd.synthetic import make_scene
+    h, w = 64, 96
+    sc = make_scene(batch=1, n_context=2, n_targets=2, height=h, width=w, seed=29, device=gpu)
+    g = sc.gaussians
+    gen = torch.Generator(device="cpu").manual_seed(5)
+    if case == "large":
+        g.covariances = g.covariances * 30.0
+    elif case == "anisotropic":
+        s = torch.tensor([6.0, 0.15, 1.0], device=gpu)
+        g.covariances = g.covariances * 20.0 * s[:, None] * s[None, :]
+    else:
+        u = torch.rand(g.opacities.shape, generator=gen).to(gpu)
+        g.opacities = torch.where(u < 0.3, torch.full_like(u, 0.5 / 255.0),
+                                  torch.where(u < 0.6, torch.full_like(u, 1.5 / 255.0), g.opacities))
+        g.covariances = g.covariances * 10.0
+    vs = [0, 0]
+    bg = torch.tensor([[0.1, 0.2, 0.3]], device=gpu).expand(2, 3).contiguous()
+    cams = raster.build_cameras(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0], bg, vs, True)
+    ref, _ = raster.rasterize_views(g.means, g.harmonics.transpose(-1, -2), g.opacities, _cov6(g.covariances), cams,
+                                    vs, use_sh=True, sh_degree=2, image_height=h, image_width=w)
+    with torch.no_grad():
+        img = render_views(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0], (h, w), bg,
+                           g.means, g.covariances, g.harmonics, g.opacities, vs)
+    torch.cuda.synchronize()
+    assert float((img - ref).abs().mean()) < 1e-5, case
+    assert float((img - ref).abs().max()) < 2e-2, case
