@@ -6,20 +6,26 @@ per pixel (G = 131,072), fp32, rendered into v = 3 target views (the RE10K evalu
 index: 2 context, 3 target views per scene). One "step" = one DecoderSplattingCUDA
 forward of one scene batch (B scenes x v views) with the Gaussians already resident in
 HBM — the `decoder` timer of the reference test loop (model_wrapper.py:432-484).
-Synthetic inputs through the Gaussian adapter (my_depthsplat_amd.synthetic).
+Synthetic inputs through the Gaussian adapter (my_depthsplat_amd.synthetic); every
+in-flight lane renders its own scene.
 
 N GPUs: one process per GPU (torchrun), each rank renders its own scenes (per-scene data
 parallel, no collective on the data path) -> scaling "weak"; value = all views / max time.
 
-Extra fields: roofline of the dominant kernel (HIP events around its launches on the
-stream it runs on; algorithmic bytes per launch in DESIGN.md §4), cpu_baseline (the CPU
-oracle on the host, rank 0, bounded sample), psnr_vs_oracle_db (parity PSNR of one view).
+Extra fields: the same throughput with the reference's 3-sigma tile binning, the roofline
+of the dominant kernel (HIP events around its launches on the stream it runs on;
+algorithmic bytes per launch in DESIGN.md §4) and its VALU issue rate, cpu_baseline (the
+CPU oracle on the host, rank 0, bounded samples, one thread and the box's CPU share),
+parity of every view vs the oracle, and the secondary legs (config C training step,
+6-view 448x768 render, 12-view reconstruction, plane-sweep cost volume on the matrix cores,
+config D data-parallel training step with the RCCL gradient all-reduce).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 from pathlib import Path
@@ -28,6 +34,10 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec); 6.29 TB/s measured copy
+# wave64 VALU issue: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave instruction per 2 cycles
+# (MI355X_MICROARCH.md "Wave scheduling": a wave issues each VALU instruction over 2 cycles)
+VALU_PEAK_GWI = 256 * 4 * 2.4e9 / 2 / 1e9
+FP32_MATRIX_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32, dense (spec)
 
 
 def parse():
@@ -39,14 +49,15 @@ def parse():
     p.add_argument("--views", type=int, default=3, help="target views per scene (RE10K eval: 3)")
     p.add_argument("--size", type=int, default=256)
     p.add_argument("--context", type=int, default=2)
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU-baseline sample per thread count")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--eager", action="store_true", help="time eager launches only (no hipGraph capture)")
     p.add_argument("--launch", choices=["auto", "hipgraph", "eager"] + [f"hipgraph{n}" for n in range(2, 9)], default="auto",
                    help="launch mode of the timed region (auto: the fastest in a short calibration of all)")
-    p.add_argument("--extra", default="train,dl3dv,recon12",
+    p.add_argument("--extra", default="train,dl3dv,recon12,costvol,train_d",
                    help="secondary measurements: train (config C step), dl3dv (6-view 448x768 render), "
-                        "recon12 (12-view 512x960 reconstruction, 100 views in chunks of 10); '' = none")
+                        "recon12 (12-view 512x960 reconstruction, 100 views in chunks of 10), costvol (plane-sweep "
+                        "cost volume, configs A / B shapes), train_d (config D data-parallel training step); '' = none")
     p.add_argument("--extra-steps", type=int, default=10)
     return p.parse_args()
 
@@ -72,15 +83,21 @@ def main():
 
     _lib.load()
     H = W = args.size
-    sc = make_scene(batch=args.batch, n_context=args.context, n_targets=args.views, height=H, width=W,
-                    seed=1000 + rank, device=dev)
+    max_lanes = 1 if args.eager else int(os.environ.get("DSPLAT_BENCH_MAX_LANES", "4"))
+    # one resident scene per in-flight lane (distinct Gaussians: the lanes do not share inputs)
+    scenes = [make_scene(batch=args.batch, n_context=args.context, n_targets=args.views, height=H, width=W,
+                         seed=1000 + 16 * rank + lane, device=dev) for lane in range(max_lanes)]
+    sc = scenes[0]
     dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
-    dec = dec.to(dev)
 
-    def step():
-        with torch.no_grad():
-            return dec(sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near, sc.far, (H, W))
+    def step_of(s):
+        def step():
+            with torch.no_grad():
+                return dec(s.gaussians, s.target_extrinsics, s.target_intrinsics, s.near, s.far, (H, W))
+        return step
 
+    steps = [step_of(s) for s in scenes]
+    step = steps[0]
     for _ in range(args.warmup):
         out = step()
     torch.cuda.synchronize()
@@ -94,32 +111,32 @@ def main():
     dominant = max(probe.summary().items(), key=lambda kv: kv[1][0] * kv[1][1])[0]
     all_kernels = probe.summary()
 
-    def timed(fn, steps):
+    def timed(fn, nsteps):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
+        for _ in range(nsteps):
             fn()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         return time.perf_counter() - t0
 
+    def max_over_ranks(*vals):
+        if world == 1:
+            return vals
+        t = torch.tensor(vals, device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return tuple(float(x) for x in t.tolist())
+
     # launch mode: the whole decoder call replayed as ONE hipGraph per step, or launched
-    # eagerly (the host runs ahead of the device, so launch gaps hide either way; on the
-    # MI355X boxes eager measured ~2 % faster: graph kernel nodes are separated by heavier
-    # barriers). A short calibration of both picks the mode; every kernel runs in both.
-    # "hipgraphN" (N = 2..4): N such graphs (own buffers each) replayed in turn on N HIP
-    # streams, so consecutive scenes overlap — one scene's compositing tail shares the chip with the
-    # next scene's binning. Every step still renders its whole scene; only the overlap differs.
-    runner, mode, cal = step, "eager", None
-    if not args.eager:
+    # eagerly; "hipgraphN" (N = 2..4): N captures, one per lane (own scene, own buffers),
+    # replayed in turn on N HIP streams so consecutive scenes overlap — one scene's compositing
+    # tail shares the chip with the next scene's binning. Every step renders a whole scene.
+    def build_modes():
         from my_depthsplat_amd.graphs import GraphedCall
-        graphed = GraphedCall(step, warmup=2)
-        out = graphed()
-        max_lanes = int(os.environ.get("DSPLAT_BENCH_MAX_LANES", "4"))
-        graphs = [graphed] + [GraphedCall(step, warmup=2) for _ in range(max_lanes - 1)]
+        graphs = [GraphedCall(fn, warmup=2) for fn in steps]
         lanes = [torch.cuda.Stream(device=dev) for _ in graphs]
         turn = [0]
 
@@ -130,41 +147,60 @@ def main():
                 with torch.cuda.stream(lanes[i]):
                     return graphs[i]()
             return run
-
-        modes = {"hipgraph": graphed, **{f"hipgraph{n}": multi_stream(n) for n in range(2, max_lanes + 1)},
+        modes = {"hipgraph": graphs[0], **{f"hipgraph{n}": multi_stream(n) for n in range(2, len(graphs) + 1)},
                  "eager": step}
+        return modes, graphs
+
+    runner, mode, cal, graphs = step, "eager", None, []
+    if not args.eager:
+        modes, graphs = build_modes()
         if args.launch == "auto":
             ncal = max(10, min(50, args.steps))
-            cal = {m: timed(fn, ncal) for m, fn in modes.items()}
-            if world > 1:  # every rank takes the same decision
-                t = torch.tensor(list(cal.values()), device=dev, dtype=torch.float64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                cal = dict(zip(cal, t.tolist()))
-            mode = min(cal, key=cal.get)
+            names = list(modes)
+            cal = dict(zip(names, max_over_ranks(*[timed(modes[m], ncal) for m in names])))
+            mode = min(cal, key=cal.get)  # every rank takes the same decision
             cal = {m: round(1e3 * t / ncal, 4) for m, t in cal.items()}
         else:
             mode = args.launch
         runner = modes[mode]
+    lanes_used = int(mode[len("hipgraph"):] or 1) if mode.startswith("hipgraph") else 1
     # timed region 1 (value): exactly K steps in the chosen mode
     elapsed = timed(runner, args.steps)
-    if mode.startswith("hipgraph") and mode != "hipgraph":  # the captures in use rendered the same scene
-        used = graphs[:int(mode[len("hipgraph"):])]
-        assert all(torch.equal(graphed.out.color, g.out.color) for g in used), f"{mode} captures disagree"
-    # timed region 2: the same K steps launched eagerly, with HIP events recorded around the
+    # every capture in use rendered its own scene exactly as an eager call does
+    for i in range(lanes_used if graphs else 0):
+        assert torch.equal(graphs[i].out.color, steps[i]().color), f"lane {i} of {mode} differs from eager"
+    # timed region 2: the same K steps in the same mode with the reference's 3-sigma tile
+    # binning (DSR_LAYOUT_RECT_BINNING) instead of the exact alpha test — the throughput the
+    # reference's lists give on the same kernels
+    raster.EXACT_BINNING = False
+    runner_ref, graphs_ref = step, []
+    try:
+        if not args.eager:
+            modes_ref, graphs_ref = build_modes()
+            runner_ref = modes_ref[mode]
+        elapsed_ref = timed(runner_ref, args.steps)
+        step()
+        torch.cuda.synchronize()
+        n_rendered_ref = raster.last_stats()["num_rendered"]
+        if graphs_ref:
+            assert torch.equal(graphs_ref[0].out.color, graphs[0].out.color), "binning modes disagree"
+    finally:
+        raster.EXACT_BINNING = True
+    del runner_ref, graphs_ref
+    # timed region 3: the same K steps launched eagerly, with HIP events recorded around the
     # dominant kernel on its launch stream (its average duration feeds the roofline)
     ev = raster.KernelTimer(only=[dominant])
     raster.set_timer(ev)
     elapsed_eager = timed(step, args.steps)
     raster.set_timer(None)
     ktimes = ev.summary()  # name -> (launches, avg_ms)
-    if world > 1:
-        t = torch.tensor([elapsed, elapsed_eager], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, elapsed_eager = (float(x) for x in t.tolist())
+    elapsed, elapsed_eager, elapsed_ref = max_over_ranks(elapsed, elapsed_eager, elapsed_ref)
     views_per_step = args.batch * args.views
     total_views = views_per_step * args.steps * world
     value = total_views / elapsed
 
+    roof = psnr = cpu = None
+    workload_tag = f"{args.context}v{H}x{W}x{args.views}b{args.batch}"
     if rank == 0:
         G = sc.gaussians.means.shape[1]
         V = views_per_step
@@ -174,25 +210,28 @@ def main():
         launches, avg_ms = ktimes[name]
         alg = raster.algorithmic_bytes(name, G=G, V=V, N=n_rendered, HW=HW)
         achieved = alg / (avg_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(name, f"{args.context}v{H}x{W}x{args.views}b{args.batch}")
+        traffic, traffic_src = pmc_traffic(name, workload_tag)
         roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "traffic_source": traffic_src,
                 "avg_ms": round(avg_ms, 5), "algorithmic_bytes_per_launch": alg,
                 "launches_timed": launches,
                 "per_kernel_avg_ms_probe": {k: round(v[1], 5) for k, v in sorted(all_kernels.items())},
-                "valu_issue": pmc_valu(name, f"{args.context}v{H}x{W}x{args.views}b{args.batch}", avg_ms)}
-        psnr, l1, cpu = None, None, None
+                "valu_issue": pmc_valu(name, workload_tag, avg_ms)}
         if not args.no_cpu_baseline:
-            psnr, l1, cpu = cpu_leg(sc, out, args, H, W)
+            psnr, cpu = cpu_leg(sc, out, args, H, W)
     extra = {}
     wanted = [e for e in args.extra.split(",") if e]
     if "train" in wanted:
-        extra["train_config_c"] = train_leg(args, dev, rank, world, timed)
+        extra["train_config_c"] = train_leg(args, dev, rank, world, timed, max_over_ranks)
     if "dl3dv" in wanted:
-        extra["render_config_d"] = dl3dv_leg(args, dev, rank, world, timed)
+        extra["render_config_d"] = dl3dv_leg(args, dev, rank, world, timed, max_over_ranks)
     if "recon12" in wanted:
-        extra["recon_config_e"] = recon12_leg(args, dev, rank, world, timed)
+        extra["recon_config_e"] = recon12_leg(args, dev, rank, world, timed, max_over_ranks)
+    if "costvol" in wanted:
+        extra["cost_volume"] = costvol_leg(args, dev, rank, world, max_over_ranks)
+    if "train_d" in wanted:
+        extra["train_config_d_dp"] = train_d_leg(args, dev, rank, world, timed, max_over_ranks)
     if rank == 0:
         line = {
             "metric": "rendered views/sec + PSNR, 2-view 256x256 RE10K, 1/2/4/8 MI355X",
@@ -200,13 +239,19 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
             "launch_mode": mode, "launch_calibration_ms_per_step": cal,
             "ms_per_step_eager": round(1e3 * elapsed_eager / args.steps, 4),
+            "reference_binning": {"value": round(total_views / elapsed_ref, 2), "unit": "views/s",
+                                  "ms_per_step": round(1e3 * elapsed_ref / args.steps, 4),
+                                  "num_rendered_per_step": n_rendered_ref,
+                                  "note": "same kernels and launch mode, the reference's 3-sigma tile lists "
+                                          "(DSR_LAYOUT_RECT_BINNING); images bit-identical to the headline's"},
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.context}-view {H}x{W} RE10K feed-forward render, 1 Gaussian/pixel "
-                                   f"(G={G}), {args.views} target views/scene, fp32",
-                       "global_batch": args.batch * world, "views_per_scene": args.views, "gaussians": G,
-                       "num_rendered_per_step": n_rendered, "parallelism": f"dp{world} (per-scene, no collective)",
-                       "scenes_in_flight_per_gpu": int(mode[len("hipgraph"):] or 1) if mode.startswith("hipgraph") else 1},
-            "psnr_vs_oracle_db": psnr, "l1_vs_oracle": l1,
+                                   f"(G={sc.gaussians.means.shape[1]}), {args.views} target views/scene, fp32",
+                       "global_batch": args.batch * world, "views_per_scene": args.views,
+                       "gaussians": sc.gaussians.means.shape[1], "num_rendered_per_step": n_rendered,
+                       "parallelism": f"dp{world} (per-scene, no collective)",
+                       "scenes_in_flight_per_gpu": lanes_used, "distinct_scenes_per_gpu": lanes_used},
+            "parity_vs_oracle": psnr,
             "roofline": roof, "cpu_baseline": cpu,
             **extra,
         }
@@ -215,16 +260,18 @@ def main():
         dist.destroy_process_group()
 
 
+def _pmc_file():
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    return json.loads(f.read_text()) if f.exists() else None
+
+
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same
     workload (profiles/pmc_traffic.json, written by tools/pmc_summary.py --json: FETCH_SIZE
     x2 per the gfx950 correction + WRITE_SIZE, separate --pmc passes). None if absent."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
-    if not f.exists():
-        return None, None
-    d = json.loads(f.read_text())
-    rec = _pmc_record(d, kernel)
-    if d.get("workload") != workload or rec is None:
+    d = _pmc_file()
+    rec = None if d is None else _pmc_record(d, kernel)
+    if d is None or d.get("workload") != workload or rec is None:
         return None, None
     return int(rec["hbm_bytes"]), f"profiles/pmc_traffic.json ({d.get('source', '')})"
 
@@ -240,23 +287,19 @@ def _pmc_record(d, kernel):
 def pmc_valu(kernel, workload, avg_ms):
     """VALU issue rate of `kernel`: SQ_INSTS_VALU per launch (wave-level instructions, from
     the committed PMC summary of the same workload) over its live average duration, against
-    the chip's issue peak (256 CUs x 4 SIMDs, a wave64 VALU instruction every 4 cycles of a
-    16-lane SIMD at ~2.4 GHz: 614 G wave-instructions/s). The compositor is issue / latency
-    bound, not HBM bound; this is its roofline on the resource that binds."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
-    if not f.exists():
+    the chip's wave64 issue peak (VALU_PEAK_GWI: 256 CUs x 4 SIMD-32, one wave instruction per
+    2 cycles at 2.4 GHz = 1,229 G wave-instructions/s)."""
+    d = _pmc_file()
+    rec = None if d is None else _pmc_record(d, kernel)
+    if d is None or d.get("workload") != workload or rec is None or "SQ_INSTS_VALU" not in rec:
         return None
-    d = json.loads(f.read_text())
-    rec = _pmc_record(d, kernel)
-    if d.get("workload") != workload or rec is None or "SQ_INSTS_VALU" not in rec:
-        return None
-    peak = 256 * 4 * 2.4e9 / 4 / 1e9  # G wave-instructions / s
     ach = rec["SQ_INSTS_VALU"] / (avg_ms * 1e-3) / 1e9
-    return {"achieved": round(ach, 1), "peak": peak, "unit": "G wave-instr/s", "frac": round(ach / peak, 4),
-            "valu_instr_per_launch": int(rec["SQ_INSTS_VALU"]), "source": "profiles/pmc_traffic.json"}
+    return {"achieved": round(ach, 1), "peak": VALU_PEAK_GWI, "unit": "G wave-instr/s",
+            "frac": round(ach / VALU_PEAK_GWI, 4), "valu_instr_per_launch": int(rec["SQ_INSTS_VALU"]),
+            "source": "profiles/pmc_traffic.json"}
 
 
-def train_leg(args, dev, rank, world, timed):
+def train_leg(args, dev, rank, world, timed, max_over_ranks):
     """Config C (BASELINE.json configs[2]): 2-view 256x256, 16 scenes x 4 target views per
     step, Gaussians from the adapter (head outputs are the trainable leaf), rasterizer forward
     + backward of an L1 + MSE colour loss, SGD update of the head. Per GPU; weak scaling."""
@@ -295,12 +338,7 @@ def train_leg(args, dev, rank, world, timed):
 
     for _ in range(2):
         step()
-    el = timed(step, args.extra_steps)
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t)
+    (el,) = max_over_ranks(timed(step, args.extra_steps))
     ms = 1e3 * el / args.extra_steps
     return {"workload": "config C: 2-view 256x256, 16 scenes x 4 target views, adapter + raster fwd+bwd, "
                         "L1+MSE loss, SGD on head outputs (no encoder network: out of scope)",
@@ -308,7 +346,7 @@ def train_leg(args, dev, rank, world, timed):
             "n_gpus": world}
 
 
-def dl3dv_leg(args, dev, rank, world, timed):
+def dl3dv_leg(args, dev, rank, world, timed, max_over_ranks):
     """6-view 448x768 (north_star's second input), 1 Gaussian per pixel (G = 2,064,384),
     8 target views per scene, forward render through the decoder. Per GPU; weak scaling."""
     import torch
@@ -326,19 +364,14 @@ def dl3dv_leg(args, dev, rank, world, timed):
 
     for _ in range(2):
         step()
-    el = timed(step, args.extra_steps)
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t)
+    (el,) = max_over_ranks(timed(step, args.extra_steps))
     ms = 1e3 * el / args.extra_steps
     return {"workload": f"6-view {H}x{W} render, G={sc.gaussians.means.shape[1]}, {v} target views/scene, fp32",
             "ms_per_step": round(ms, 3), "views_per_s": round(v * world / (ms * 1e-3), 1), "steps": args.extra_steps,
             "n_gpus": world}
 
 
-def recon12_leg(args, dev, rank, world, timed):
+def recon12_leg(args, dev, rank, world, timed, max_over_ranks):
     """BASELINE.json configs[4]: 12-view 512x960 feed-forward reconstruction (G = 5,898,240
     Gaussians from the fused adapter), then 100 target views rendered in chunks of 10
     (render_chunk_size, README.md:198). One step = adapter + 10 decoder calls for one scene.
@@ -374,12 +407,7 @@ def recon12_leg(args, dev, rank, world, timed):
 
     step()
     steps = max(2, args.extra_steps // 2)
-    el = timed(step, steps)
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t)
+    (el,) = max_over_ranks(timed(step, steps))
     ms = 1e3 * el / steps
     return {"workload": f"{V}-view {H}x{W} reconstruction, G={V * H * W}, adapter + {v} target views in chunks of "
                         f"{chunk} (encoder network out of scope), fp32",
@@ -387,8 +415,173 @@ def recon12_leg(args, dev, rank, world, timed):
             "n_gpus": world, "reference": "0.6 s per scene end to end on an A100 incl. the encoder (README.md:105)"}
 
 
+def costvol_leg(args, dev, rank, world, max_over_ranks):
+    """Fused plane-sweep warp + correlation (matching.py:24-90 + mv_unimatch.py:494-505) at
+    BASELINE configs[0]'s shape (2 views, C = 128, D = 128, 32x32) and config B's scale 0
+    (2 views, C = 128, D = 128, 64x64): HIP time per call from HIP events on the launch stream,
+    FLOP rate against the FP32 matrix-core peak (the correlation runs on
+    v_mfma_f32_16x16x4_f32), algorithmic HBM bytes, and the same call on the host CPU through
+    the torch restatement (oracle/cost_volume.py, rank 0). FLOPs = 2 BV J C D H W."""
+    import torch
+
+    from my_depthsplat_amd.matching import plane_sweep_cost_volume
+
+    res = {}
+    for tag, (BV, J, C, Hc, Wc, D) in {"config_a_32x32": (2, 1, 128, 32, 32, 128),
+                                       "config_b_scale0_64x64": (2, 1, 128, 64, 64, 128)}.items():
+        g = torch.Generator(device=dev).manual_seed(5 + rank)
+        ref = torch.randn(BV, C, Hc, Wc, generator=g, device=dev)
+        tgt = torch.randn(BV, J, C, Hc, Wc, generator=g, device=dev)
+        K = torch.tensor([[Wc * 1.0, 0, Wc / 2], [0, Hc * 1.0, Hc / 2], [0, 0, 1]], device=dev).expand(BV, J, 3, 3)
+        pose = torch.eye(4, device=dev).repeat(BV, J, 1, 1)
+        pose[:, :, 0, 3] = 0.1
+        depth = (1.0 / torch.linspace(1 / 0.5, 1 / 100.0, D, device=dev)).expand(BV, D).contiguous()
+        K = K.contiguous()
+
+        def call():
+            return plane_sweep_cost_volume(ref, tgt, K, pose, depth)
+
+        for _ in range(3):
+            call()
+        n = 50
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            call()
+        e1.record()
+        torch.cuda.synchronize()
+        (ms,) = max_over_ranks(e0.elapsed_time(e1) / n)
+        flops = 2.0 * BV * J * C * D * Hc * Wc
+        nbytes = 4.0 * (BV * C * Hc * Wc * (1 + J) + BV * D * Hc * Wc)
+        tf = flops / (ms * 1e-3) / 1e12
+        ent = {"shape": {"BV": BV, "J": J, "C": C, "H": Hc, "W": Wc, "D": D}, "ms_per_call": round(ms, 5),
+               "tflops": round(tf, 3), "peak_tflops": FP32_MATRIX_PEAK_TFLOPS,
+               "frac": round(tf / FP32_MATRIX_PEAK_TFLOPS, 4), "gbps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+               "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+               "mfma_busy": pmc_mfma(tag)}
+        if rank == 0 and not args.no_cpu_baseline:
+            ent["cpu"] = costvol_cpu(ref, tgt, K, pose, depth)
+        res[tag] = ent
+    res["note"] = ("fp32 in / fp32 accumulate on the matrix cores (exact f32); FLOP rate vs the dense FP32-matrix "
+                   "peak; CPU = oracle/cost_volume.py (torch grid_sample restatement of the reference) on the host")
+    return res
+
+
+def pmc_mfma(tag):
+    """SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CU_CYCLES-based CU cycles) from the committed PMC
+    summary of the cost-volume kernels (profiles/pmc_costvol.json), if present."""
+    f = ROOT / "profiles" / "pmc_costvol.json"
+    if not f.exists():
+        return None
+    return json.loads(f.read_text()).get(tag)
+
+
+def _cpu_share() -> tuple[int, dict]:
+    """Threads for the all-core CPU sample: the CPUs this process may run on (affinity),
+    capped by the cgroup CPU quota and by the box's declared share (OMP_NUM_THREADS, 16 per
+    GPU on the MI355X boxes). Also the machine's nproc and CPU model."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    share = min(x for x in (aff, quota, env or None) if x)
+    model = platform.processor() or ""
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return share, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
+                   "omp_num_threads_env": env or None, "cpu_model": model}
+
+
+def _set_omp_threads(n: int) -> None:
+    import ctypes
+    try:
+        ctypes.CDLL("libgomp.so.1").omp_set_num_threads(int(n))
+    except OSError:
+        os.environ["OMP_NUM_THREADS"] = str(n)
+
+
+def costvol_cpu(ref, tgt, K, pose, depth):
+    import torch
+
+    from oracle import cost_volume as ocv
+    share, _ = _cpu_share()
+    r, t, k, p, d = (x.cpu() for x in (ref, tgt, K, pose, depth))
+    out = {}
+    prev = torch.get_num_threads()
+    for label, nt in (("1_thread", 1), ("all_share", share)):
+        torch.set_num_threads(nt)
+        ocv.cost_volume(r, t, k, p, d)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 1.5 or n < 2:
+            ocv.cost_volume(r, t, k, p, d)
+            n += 1
+        out[label] = {"ms_per_call": round(1e3 * (time.perf_counter() - t0) / n, 2), "threads": nt, "calls": n}
+    torch.set_num_threads(prev)
+    return out
+
+
+def train_d_leg(args, dev, rank, world, timed, max_over_ranks):
+    """BASELINE.json configs[3]: 6-view 448x768 training, 4 scenes per GPU (batch 32 at 8
+    GPUs), 8 target views per scene. One step (my_depthsplat_amd.training.TrainStep): the
+    trainable head (vitb-sized stand-in for the Gaussian regressor + head) -> fused adapter ->
+    batched rasterizer forward + backward -> fused L1 + MSE -> ONE flat fp32 all-reduce of the
+    head gradients over RCCL (xGMI) -> clip 0.5 -> AdamW. Every rank builds only its shard of
+    the global batch. Per GPU work fixed: weak scaling."""
+    import torch
+    import torch.distributed as dist
+
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg
+    from my_depthsplat_amd.loss import l1_mse_loss
+    from my_depthsplat_amd.parallel import allreduce_gradients, shard
+    from my_depthsplat_amd.training import GaussianHead, TrainStep, synthetic_batch
+
+    per_rank, V, v, H, W = 4, 6, 8, 448, 768
+    n_global = per_rank * world
+    batch = synthetic_batch(n_global, V, v, H, W, seed=4242, scene_ids=shard(n_global, rank, world)).to(dev)
+    adapter = GaussianAdapter(GaussianAdapterCfg(1e-10, 3.0, 2)).to(dev)
+    torch.manual_seed(0)  # identical initial weights on every rank
+    head = GaussianHead(3 + adapter.d_in).to(dev)
+    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
+    step = TrainStep(head, adapter, lambda gs, e, k, n, f, hw: dec(gs, e, k, n, f, hw).color,
+                     lambda p, t: l1_mse_loss(p, t, 1.0, 1.0), lr=1e-4, world=world)
+    for _ in range(2):
+        step(batch)
+    n_steps = max(3, args.extra_steps // 2)
+    (el,) = max_over_ranks(timed(lambda: step(batch), n_steps))
+    ms = 1e3 * el / n_steps
+    # the collective alone (same bucket), for the share of the step it takes
+    for p in head.parameters():
+        p.grad = torch.zeros_like(p)
+    (ar,) = max_over_ranks(timed(lambda: allreduce_gradients(list(head.parameters()), world), 20))
+    for p in head.parameters():
+        p.grad = None
+    nparam = sum(p.numel() for p in head.parameters())
+    return {"workload": f"config D shape: {V}-view {H}x{W} context (G={V * H * W}/scene), {per_rank} scenes x {v} "
+                        "target views per GPU, head -> fused adapter -> raster fwd+bwd -> L1+MSE -> one-bucket "
+                        "RCCL all-reduce -> clip -> AdamW (dense encoder out of scope)",
+            "ms_per_step": round(ms, 3), "views_per_s": round(n_global * v / (ms * 1e-3), 1),
+            "scenes_per_s": round(n_global / (ms * 1e-3), 2), "global_batch": n_global, "steps": n_steps,
+            "n_gpus": world, "world_size_seen": dist.get_world_size() if dist.is_initialized() else 1,
+            "backend": dist.get_backend() if dist.is_initialized() else None,
+            "trainable_params": nparam, "allreduce_bucket_bytes": step.bucket_bytes,
+            "allreduce_ms": round(1e3 * ar / 20, 4)}
+
+
 def cpu_leg(sc, out, args, H, W):
-    """CPU oracle on the host: parity PSNR/L1 of view 0 + a bounded throughput sample."""
+    """CPU oracle on the host: parity of every view + bounded throughput samples with one
+    thread and with the box's CPU share; the fused adapter's CPU restatement at config B."""
     import numpy as np
     import torch
 
@@ -405,29 +598,63 @@ def cpu_leg(sc, out, args, H, W):
     cov6 = _cov6(g.covariances[0]).contiguous().cpu().numpy()
     bg = np.zeros(3, np.float32)
     deg = int(round(shs.shape[1] ** 0.5)) - 1
+    share, sysinfo = _cpu_share()
 
     def one(i):
         return orc.render_settings(means, shs, None, opac, cov6, npst, i, bg, H, W, deg)
 
-    o = one(0)
-    ref, _, _ = o.image()
-    o.close()
-    hip = out.color[0, 0].float().cpu().numpy()
-    l1 = float(np.abs(hip - ref).mean())
-    mse = float(np.mean((np.clip(hip, 0, 1) - np.clip(ref, 0, 1)) ** 2))
-    psnr = None if mse == 0 else round(-10 * np.log10(mse), 3)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        o = one(n % args.views)
+    _set_omp_threads(share)
+    views = []
+    for i in range(args.views):  # parity of every target view of scene 0 (headline path)
+        o = one(i)
+        ref, _, _ = o.image()
         o.close()
+        hip = out.color[0, i].float().cpu().numpy()
+        l1 = float(np.abs(hip - ref).mean())
+        mse = float(np.mean((np.clip(hip, 0, 1) - np.clip(ref, 0, 1)) ** 2))
+        views.append({"view": i, "l1": l1, "max_abs": float(np.abs(hip - ref).max()),
+                      "psnr_db": None if mse == 0 else round(-10 * np.log10(mse), 3)})
+    parity = {"views": views, "max_l1": max(v["l1"] for v in views),
+              "min_psnr_db": min((v["psnr_db"] for v in views if v["psnr_db"] is not None), default=None),
+              "oracle": "oracle/dsr_oracle.cpp (parity unpinned vs the absent CUDA library: DESIGN.md §3)"}
+    samples = {}
+    for label, nt in (("1_thread", 1), ("all_share", share)):
+        _set_omp_threads(nt)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            o = one(n % args.views)
+            o.close()
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds and n >= 2:
+                break
+        samples[label] = {"views_per_s": round(n / el, 3), "threads": nt, "views": n, "seconds": round(el, 2)}
+    _set_omp_threads(share)
+    # the adapter's CPU restatement (torch, all threads of the share) at the same scene size
+    from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg, gaussians_from_head_torch
+    from my_depthsplat_amd.synthetic import context_cameras
+    torch.set_num_threads(share)
+    ad = GaussianAdapter(GaussianAdapterCfg(1e-10, 3.0, 2))
+    gen = torch.Generator().manual_seed(0)
+    Vc = args.context
+    head = torch.randn(1, Vc, H * W, 3 + ad.d_in, generator=gen)
+    dep = torch.rand(1, Vc, H * W, 1, 1, generator=gen) * 9 + 1
+    img = torch.rand(1, Vc, 3, H, W, generator=gen)
+    K = torch.tensor([[1.0, 0, 0.5], [0, 1.0, 0.5], [0, 0, 1]]).expand(1, Vc, 3, 3)
+    ext = context_cameras(Vc)[None]
+    gaussians_from_head_torch(head, dep, img, ext, K, ad)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 2.0 or n < 2:
+        gaussians_from_head_torch(head, dep, img, ext, K, ad)
         n += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds and n >= 2:
-            break
-    return psnr, l1, {"value": round(n / el, 3), "unit": "views/s", "cores": threads, "kind": "port",
-                      "sample": f"{n} target views of the same {H}x{W} scene (G={means.shape[0]}) rendered by "
-                                f"oracle/dsr_oracle.cpp (OpenMP, {threads} threads) in {el:.1f}s"}
+    adapter_ms = 1e3 * (time.perf_counter() - t0) / n
+    cpu = {"value": samples["all_share"]["views_per_s"], "unit": "views/s", "cores": share, "kind": "port",
+           "sample": f"{samples['all_share']['views']} target views of one {H}x{W} scene (G={means.shape[0]}) rendered "
+                     f"by oracle/dsr_oracle.cpp (OpenMP, {share} threads) in {samples['all_share']['seconds']}s; "
+                     f"1 thread: {samples['1_thread']['views']} views in {samples['1_thread']['seconds']}s",
+           "single_thread_views_per_s": samples["1_thread"]["views_per_s"], **sysinfo,
+           "adapter_cpu_ms_per_scene": round(adapter_ms, 1)}
+    return parity, cpu
 
 
 if __name__ == "__main__":

@@ -82,6 +82,8 @@ int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, c
 #define DSR_LAYOUT_SH_CHANNEL_MAJOR 1  /* shs given as [S,G,3,M] (Gaussians.harmonics)      */
 #define DSR_LAYOUT_COV_FULL 2          /* covariance given as [S,G,3,3]; grads: upper triangle */
 #define DSR_LAYOUT_COUNTS_ZEROED 4     /* seg_count already zeroed (dsr_build_cameras)       */
+#define DSR_LAYOUT_RECT_BINNING 8      /* dsr_project_bin_cameras only: keep the reference's 3-sigma
+                                          tile rects instead of the exact alpha >= 1/255 test       */
 int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,
@@ -91,9 +93,11 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
 /* Fused alternative to dsr_preprocess_fwd + dsr_bin_scan + dsr_bin_scatter (K1 + K3) for
  * problems whose fixed-capacity key buffer fits: the same projection, plus the keys of every
  * (gaussian, touched tile) written straight into segment (v, t) = keys[(v*T + t) * G ...]
- * (a gaussian touches a tile at most once). Inputs load once per scene and project into
- * every view of that scene. keys must hold V*T*G entries (only V*T segments' prefixes are
- * written); seg_count [V*T] receives the entry counts (zeroed by this call). Consumers take
+ * (a gaussian touches a tile at most once). One workgroup per (256 gaussians, view); the
+ * workgroups of one gaussian block for all views of its scene are placed on one XCD, back
+ * to back, so the scene inputs come from HBM once and from that XCD's L2 for the other
+ * views. keys must hold V*T*G entries (only V*T segments' prefixes are written);
+ * seg_count [V*T] receives the entry counts (zeroed by this call). Consumers take
  * seg_stride = G. Requires T <= 32768 and V*T*G < 2^32. */
 int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M,
                     const float* means, const float* shs, const float* colors,
@@ -101,10 +105,15 @@ int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M,
                     float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout,
                     void* stream);
 
-/* dsr_build_cameras + dsr_project_bin in one launch: every workgroup sets up its view's
- * camera from the render_cuda inputs (as dsr_build_cameras) and the first block of each view
- * stores it to cams [V] for the later calls. seg_count must come zeroed (DSR_LAYOUT_COUNTS_ZEROED
- * in layout; e.g. by dsr_sort_render's clear_counts). */
+/* dsr_build_cameras + dsr_project_bin in one launch (the inference fast path): every
+ * workgroup sets up its view's camera from the render_cuda inputs (as dsr_build_cameras, in
+ * float) and the first block of each view stores it to cams [V] for the later calls.
+ * seg_count must come zeroed (DSR_LAYOUT_COUNTS_ZEROED in layout; e.g. by dsr_sort_render's
+ * clear_counts). Binning: a (gaussian, tile) pair is kept only when the gaussian's
+ * alpha >= 1/255 ellipse reaches the tile (exact conic minimum over the tile box), so each
+ * segment is an order-preserving subsequence of the reference's 3-sigma list holding every
+ * entry that can blend at a pixel of the tile; images are identical, n_contrib counts
+ * positions in the shorter list. DSR_LAYOUT_RECT_BINNING keeps the reference's lists. */
 int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, int M,
                             const float* means, const float* shs, const float* colors,
                             const float* opacities, const float* cov6, const float* extrinsics,
@@ -323,6 +332,31 @@ int dga_adapter_bwd(int B, int V, int H, int W, int d_sh, int C, const float* he
                     const float* dharmonics, const float* dopacities, float* dhead, float* ddepths,
                     void* stream);
 
+/* The reference operator itself: GaussianAdapter.forward(extrinsics, intrinsics, coordinates,
+ * depths, opacities, raw_gaussians, image_shape, eps, point_cloud, input_images)
+ * (gaussian_adapter.py:49-102; called at encoder_depthsplat.py:300-314). Rows n = ((bv * H*W
+ * + pixel) * S + s) for BV = b*v views and S Gaussians per pixel (surfaces x spp):
+ *   raw [N, C] (C >= 7 + 3*d_sh: scales 3, rotation 4, sh 3*d_sh channel-major),
+ *   coordinates [N, 2] normalised image xy, depths [N], images [BV,3,H,W],
+ *   cams [BV,104] (dga_adapter_cameras), eps: the quaternion normaliser's epsilon.
+ * out: means [N,3], covariances [N,3,3], harmonics [N,3,d_sh], and, when non-NULL, the
+ * activated scales [N,3] and normalised rotations [N,4] (AdapterGaussians.scales /
+ * .rotations). Opacities pass through unchanged (no kernel work). */
+int dga_adapter_forward(int BV, int H, int W, int S, int d_sh, int C, const float* raw,
+                        const float* coordinates, const float* depths, const float* images,
+                        const float* cams, float scale_min, float scale_max, const float* sh_mask,
+                        float eps, float* means, float* covariances, float* harmonics, float* scales,
+                        float* rotations, void* stream);
+/* Backward of dga_adapter_forward: output gradients may be NULL (zero). draw [N, C]
+ * overwritten (unused channels 0); dcoordinates [N, 2] and ddepths [N] when non-NULL.
+ * Cameras and images get no gradient. */
+int dga_adapter_backward(int BV, int H, int W, int S, int d_sh, int C, const float* raw,
+                         const float* coordinates, const float* depths, const float* cams,
+                         float scale_min, float scale_max, const float* sh_mask, float eps,
+                         const float* dmeans, const float* dcovariances, const float* dharmonics,
+                         const float* dscales, const float* drotations, float* draw,
+                         float* dcoordinates, float* ddepths, void* stream);
+
 /* ---- loss / metric (the step after the rasterizer) ------------------------------------
  * One pass over n_images images of n_per_image floats: loss[0] = w_l1 mean|p - t| +
  * w_mse mean (p - t)^2 (loss_mse.py:33-44), grad (optional) = dloss/dp, psnr (optional)
@@ -332,6 +366,32 @@ size_t dls_loss_workspace_size(int n_images, int64_t n_per_image);
 int dls_l1_mse_psnr(int n_images, int64_t n_per_image, const float* pred, const float* target,
                     float w_l1, float w_mse, float* loss, float* grad, float* psnr, void* workspace,
                     void* stream);
+
+/* ---- buffer sizing -------------------------------------------------------------------
+ * Bytes of every caller-owned buffer of one rasterizer call sequence over V views of
+ * W x H pixels and G gaussians per scene (T = ceil(W/16) * ceil(H/16) tiles per view), so a
+ * host that is not the Python layer can allocate them (the library never allocates).
+ * key_budget: largest key buffer the caller accepts for the sync-free fixed-capacity layout
+ * (the Python layer uses 8 GiB). fixed_capacity = 1: dsr_project_bin(_cameras) applies and
+ * keys / scratch are sized V*T*G; 0: the two-phase layout (dsr_preprocess_fwd / _cut, scan,
+ * scatter), whose keys / scratch hold N = totals[0] of dsr_bin_scan entries (known only
+ * after the scan: keys_bytes is then 0 here). Forward outputs: color [V,3,H,W], final_T
+ * [V,H,W], n_contrib [V,H,W]; backward: dgeom [V,G,12]. */
+typedef struct dsr_workspace {
+    uint64_t cams_bytes;        /* dsr_camera [V]                                   */
+    uint64_t geom_bytes;        /* [V,G,12] f32                                     */
+    uint64_t radii_bytes;       /* [V,G] i32                                        */
+    uint64_t seg_count_bytes;   /* [V*T] u32                                        */
+    uint64_t seg_start_bytes;   /* [V*T+1] u32 (two-phase layout)                   */
+    uint64_t keys_bytes;        /* u64 keys (fixed capacity: V*T*G)                 */
+    uint64_t scratch_bytes;     /* same size as keys: segments above the LDS sort   */
+    uint64_t sort_ws_bytes;     /* dsr_bin_sort_workspace_size at the worst case    */
+    uint64_t color_bytes, final_T_bytes, n_contrib_bytes, dgeom_bytes;
+    uint64_t total_bytes;       /* sum of the above                                 */
+    int32_t tiles;              /* T                                                */
+    int32_t fixed_capacity;     /* 1: fixed-capacity layout under key_budget        */
+} dsr_workspace;
+int dsr_workspace_size(int G, int H, int W, int n_views, uint64_t key_budget, dsr_workspace* out);
 
 /* ---- misc ------------------------------------------------------------------------- */
 const char* dsplat_last_error(void);

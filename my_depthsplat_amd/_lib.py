@@ -32,6 +32,7 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_bin_scatter_cut": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),
     "dsr_bin_sort": (_I, [_I, _I, _I, _I, _P, _P, c_uint32, _P, _P, c_uint32, _P, c_uint32, _P, _P, _P]),
     "dsr_bin_sort_workspace_size": (ctypes.c_size_t, [_I, _I, _I, c_uint32]),
+    "dsr_workspace_size": (_I, [_I, _I, _I, _I, ctypes.c_uint64, _P]),
     "dsr_sort_lds_capacity": (c_uint32, []),
     "dsr_render_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dsr_sort_render": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _I, _I, _P, _P, _P, _P]),
@@ -49,11 +50,23 @@ SIGNATURES: dict[str, tuple] = {
     "dga_adapter_fwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, c_float, _P, _P, _P, _P, _P, _P]),
     "dga_adapter_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
                              _P]),
+    "dga_adapter_forward": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, c_float, _P, c_float, _P, _P, _P,
+                                 _P, _P, _P]),
+    "dga_adapter_backward": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, c_float, _P, c_float, _P, _P, _P,
+                                  _P, _P, _P, _P, _P, _P]),
     "dls_loss_workspace_size": (ctypes.c_size_t, [_I, ctypes.c_int64]),
     "dls_l1_mse_psnr": (_I, [_I, ctypes.c_int64, _P, _P, c_float, c_float, _P, _P, _P, _P, _P]),
     "dsplat_last_error": (ctypes.c_char_p, []),
     "dsplat_abi_version": (_I, []),
 }
+
+class Workspace(ctypes.Structure):
+    """dsr_workspace (include/dsplat_hip.h): bytes of every caller-owned buffer."""
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "cams_bytes", "geom_bytes", "radii_bytes", "seg_count_bytes", "seg_start_bytes", "keys_bytes",
+        "scratch_bytes", "sort_ws_bytes", "color_bytes", "final_T_bytes", "n_contrib_bytes", "dgeom_bytes",
+        "total_bytes")] + [("tiles", ctypes.c_int32), ("fixed_capacity", ctypes.c_int32)]
+
 
 _lib = None
 

@@ -1,10 +1,18 @@
-"""Fused Gaussian adapter on the device (dga_adapter_fwd / dga_adapter_bwd).
+"""Fused Gaussian adapter on the device.
 
-Replaces the encoder glue + GaussianAdapter + rotate_sh chain (encoder_depthsplat.py:224-346,
-gaussian_adapter.py:49-102, gaussians.py:8-44, sh_rotation.py:10-30) — ~30 torch kernels and
-batched 3x3 GEMMs per call — by one kernel per direction. Per-view constants (c2w rotation
-and translation, K^-1, Wigner-D blocks of the rotation) are built here with the same torch
-functions the reference path uses, so both paths rotate SH with identical matrices.
+Two entries, one kernel per direction each:
+  * `adapter_forward_hip` — the reference operator `GaussianAdapter.forward(extrinsics,
+    intrinsics, coordinates, depths, opacities, raw_gaussians, image_shape, eps, point_cloud,
+    input_images)` (gaussian_adapter.py:49-102, called at encoder_depthsplat.py:300-314) on
+    dga_adapter_forward / dga_adapter_backward; `GaussianAdapter.forward` routes device
+    tensors here.
+  * `fused_gaussians_from_head` — the encoder glue fused in front of it (opacity sigmoid,
+    pixel offsets: encoder_depthsplat.py:224-346) on dga_adapter_fwd / dga_adapter_bwd,
+    producing the decoder's Gaussians straight from the head channels.
+Both replace ~30 torch kernels and batched 3x3 GEMMs per call (build_covariance,
+get_world_rays, rotate_sh: gaussians.py:8-44, projection.py:91-114, sh_rotation.py:10-30).
+Per-view constants (c2w rotation and translation, K^-1, Wigner-D blocks of the rotation) come
+from dga_adapter_cameras, which solves the Wigner-D blocks exactly as sh_rotation.wigner_d.
 """
 from __future__ import annotations
 
@@ -117,3 +125,99 @@ def fused_gaussians_from_head(head, depths, images, extrinsics, intrinsics, adap
         adapter.cfg.gaussian_scale_min, adapter.cfg.gaussian_scale_max,
         adapter.sh_mask.to(head.device).float().contiguous(), d_sh)
     return Gaussians(means, cov, harm, opac)
+
+
+class _RefAdapter(torch.autograd.Function):
+    """GaussianAdapter.forward on dga_adapter_forward / dga_adapter_backward. Gradients reach
+    raw_gaussians, coordinates and depths; cameras and images get none (as in the fused
+    encoder path; the reference's extrinsics / intrinsics / images are data)."""
+
+    @staticmethod
+    def forward(ctx, raw, coords, depths, images, cams, sh_mask, meta):
+        lib = _lib.load()
+        BV, H, W, S, d_sh, smin, smax, eps = meta
+        N, C = raw.shape
+        dev = raw.device
+        means = torch.empty((N, 3), dtype=torch.float32, device=dev)
+        cov = torch.empty((N, 3, 3), dtype=torch.float32, device=dev)
+        harm = torch.empty((N, 3, d_sh), dtype=torch.float32, device=dev)
+        scales = torch.empty((N, 3), dtype=torch.float32, device=dev)
+        rots = torch.empty((N, 4), dtype=torch.float32, device=dev)
+        _lib.check(lib.dga_adapter_forward(BV, H, W, S, d_sh, C, raw.data_ptr(), coords.data_ptr(), depths.data_ptr(),
+                                           images.data_ptr(), cams.data_ptr(), float(smin), float(smax),
+                                           sh_mask.data_ptr(), float(eps), means.data_ptr(), cov.data_ptr(),
+                                           harm.data_ptr(), scales.data_ptr(), rots.data_ptr(), _lib.stream_of(dev)),
+                   "dga_adapter_forward")
+        ctx.save_for_backward(raw, coords, depths, cams, sh_mask)
+        ctx.meta = meta
+        return means, cov, harm, scales, rots
+
+    @staticmethod
+    def backward(ctx, dmeans, dcov, dharm, dscales, drots):
+        lib = _lib.load()
+        raw, coords, depths, cams, sh_mask = ctx.saved_tensors
+        BV, H, W, S, d_sh, smin, smax, eps = ctx.meta
+        N, C = raw.shape
+        f = lambda t: None if t is None else t.contiguous().float()  # noqa: E731
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        g = [f(t) for t in (dmeans, dcov, dharm, dscales, drots)]
+        draw = torch.empty_like(raw)
+        dcoords = torch.empty_like(coords) if ctx.needs_input_grad[1] else None
+        ddepth = torch.empty_like(depths) if ctx.needs_input_grad[2] else None
+        _lib.check(lib.dga_adapter_backward(BV, H, W, S, d_sh, C, raw.data_ptr(), coords.data_ptr(), depths.data_ptr(),
+                                            cams.data_ptr(), float(smin), float(smax), sh_mask.data_ptr(), float(eps),
+                                            *[p(t) for t in g], draw.data_ptr(), p(dcoords), p(ddepth),
+                                            _lib.stream_of(raw.device)), "dga_adapter_backward")
+        return draw, dcoords, ddepth, None, None, None, None
+
+
+def _per_view(t: torch.Tensor, b: int, v: int, tail: tuple, name: str) -> torch.Tensor:
+    """[b, v, 1, ..., 1, *tail] (the reference's "b v i j -> b v () () () i j") -> [b*v, *tail]."""
+    if t.dim() < 2 + len(tail) or tuple(t.shape[-len(tail):]) != tail:
+        raise ValueError(f"{name} must end in {tail}; got {tuple(t.shape)}")
+    lead = t.shape[:-len(tail)]
+    if lead[:2] != (b, v) or any(d != 1 for d in lead[2:]):
+        raise ValueError(f"{name} {tuple(t.shape)}: the fused adapter takes one camera per (batch, view), "
+                         f"shaped [{b}, {v}, 1, ..., 1, {', '.join(map(str, tail))}]")
+    return t.reshape(b * v, *tail)
+
+
+def adapter_forward_hip(adapter, extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians, image_shape,
+                        eps: float = 1e-8, input_images=None):
+    """GaussianAdapter.forward (gaussian_adapter.py:49-102) for device tensors. Batch shape =
+    opacities.shape = [b, v, h*w, *rest] (rest: surfaces x Gaussians per pixel)."""
+    from .gaussian_adapter import AdapterGaussians
+
+    if input_images is None:
+        raise ValueError("GaussianAdapter.forward needs input_images (gaussian_adapter.py:69)")
+    if intrinsics is None:
+        raise ValueError("GaussianAdapter.forward needs intrinsics for the pixel rays")
+    _lib.require_gpu(extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians, input_images)
+    batch = tuple(opacities.shape)
+    if len(batch) < 3:
+        raise ValueError(f"opacities {batch}: expected [b, v, h*w, ...]")
+    b, v, r = batch[:3]
+    h, w = image_shape
+    if r != h * w or tuple(input_images.shape) != (b, v, 3, h, w):
+        raise ValueError(f"rays {r} / images {tuple(input_images.shape)} do not match image_shape {image_shape}")
+    S = 1
+    for d in batch[3:]:
+        S *= d
+    d_sh = adapter.d_sh
+    C = raw_gaussians.shape[-1]
+    if C < 7 + 3 * d_sh:
+        raise ValueError(f"raw_gaussians has {C} channels; the adapter needs {adapter.d_in}")
+    N = b * v * r * S
+    f = lambda t: t.contiguous().float()  # noqa: E731
+    raw = f(raw_gaussians.expand(*batch, C)).reshape(N, C)
+    coords = f(coordinates.expand(*batch, 2)).reshape(N, 2)
+    dep = f(depths.expand(*batch)).reshape(N)
+    ext = _per_view(extrinsics, b, v, (4, 4), "extrinsics")
+    K = _per_view(intrinsics, b, v, (3, 3), "intrinsics")
+    cams = adapter_cameras(ext.view(b, v, 4, 4), K.view(b, v, 3, 3), adapter.cfg.sh_degree)
+    meta = (b * v, h, w, S, d_sh, adapter.cfg.gaussian_scale_min, adapter.cfg.gaussian_scale_max, float(eps))
+    means, cov, harm, scales, rots = _RefAdapter.apply(raw, coords, dep, f(input_images.detach()), cams,
+                                                       adapter.sh_mask.to(raw.device).float().contiguous(), meta)
+    return AdapterGaussians(means=means.view(*batch, 3), covariances=cov.view(*batch, 3, 3),
+                            scales=scales.view(*batch, 3), rotations=rots.view(*batch, 4),
+                            harmonics=harm.view(*batch, 3, d_sh), opacities=opacities)

@@ -74,23 +74,36 @@ __device__ __forceinline__ void mmt3(const float* A, const float* B, float* C) {
     for (int c = 0; c < 3; ++c) C[a * 3 + c] = (A[a] * B[c] + A[3 + a] * B[3 + c]) + A[6 + a] * B[6 + c];
 }
 
-struct Pix {
-  int b, v, p, i, j;
-  size_t n;   // flat (b, v, p)
-  size_t bg;  // b * G + v * HW + p (scene-major output index)
+// One launch's inputs. GLUE (the encoder glue fused in, dga_adapter_fwd): rows are head
+// channels [opacity logit, 2 offset logits, raw...] per (b, v, pixel). Otherwise (the
+// reference GaussianAdapter.forward signature, dga_adapter_forward): rows are the adapter's
+// raw_gaussians [scales 3, rotation 4, sh 3 d_sh] and the normalised coordinates come in
+// `coords` [N, 2]; S rows share one pixel (surfaces x Gaussians per pixel, innermost).
+struct AdIn {
+  const float* rows;    // [N, C]
+  const float* coords;  // [N, 2] (reference signature only)
+  const float* depths;  // [N]
+  const float* images;  // [B*V, 3, H, W]
+  const float* cams;    // [B*V, kCamFloats]
+  const float* sh_mask; // [d_sh]
+  float smin, smax, eps;
+  int C, BV, H, W, S;
 };
 
-__device__ __forceinline__ bool pixel_of(size_t n, int B, int V, int H, int W, Pix& px) {
-  const size_t HW = (size_t)H * W;
-  if (n >= (size_t)B * V * HW) return false;
+struct Pix {
+  size_t n;   // row
+  size_t bv;  // camera / image index
+  int p, i, j;
+};
+
+__device__ __forceinline__ bool pixel_of(size_t n, const AdIn& a, Pix& px) {
+  const size_t HW = (size_t)a.H * a.W, per = HW * (size_t)a.S;
+  if (n >= (size_t)a.BV * per) return false;
   px.n = n;
-  const size_t bv = n / HW;
-  px.p = (int)(n - bv * HW);
-  px.b = (int)(bv / V);
-  px.v = (int)(bv - (size_t)px.b * V);
-  px.i = px.p / W;
-  px.j = px.p - px.i * W;
-  px.bg = (size_t)px.b * V * HW + (size_t)px.v * HW + px.p;
+  px.bv = n / per;
+  px.p = (int)((n / (size_t)a.S) % HW);
+  px.i = px.p / a.W;
+  px.j = px.p - px.i * a.W;
   return true;
 }
 
@@ -111,72 +124,84 @@ __device__ __forceinline__ const float* dblock(const float* cam, int l) {
   return cam + (l == 1 ? kOffD1 : l == 2 ? kOffD2 : kOffD3);
 }
 
-// Per-thread copies of one pixel's row (staged through LDS; kHead = channels used).
-template <int NSH>
+// row channels used: GLUE adds the opacity logit and the two offset logits in front
+template <int NSH, bool GLUE>
 struct Rows {
-  static constexpr int kHead = 10 + 3 * NSH;
+  static constexpr int kOff = GLUE ? 3 : 0;            // first raw_gaussians channel
+  static constexpr int kHead = kOff + 7 + 3 * NSH;
 };
 
-template <int NSH>
-__global__ __launch_bounds__(NT) void k_adapter_fwd(int B, int V, int H, int W, int C, const float* __restrict__ head,
-                                                    const float* __restrict__ depths,
-                                                    const float* __restrict__ images,
-                                                    const float* __restrict__ cams, float smin, float smax,
-                                                    const float* __restrict__ sh_mask, float* __restrict__ means,
-                                                    float* __restrict__ covs, float* __restrict__ harm,
-                                                    float* __restrict__ opac) {
-  constexpr int KH = Rows<NSH>::kHead;
-  extern __shared__ float lds[];  // NT * max(C, 3 * NSH) floats
-  const size_t total = (size_t)B * V * H * W;
+// normalised image coordinates of a row: pixel centre + offset (GLUE) or given (reference)
+template <bool GLUE>
+__device__ __forceinline__ void row_xy(const AdIn& a, const Pix& px, const float* h, float& x, float& y, float& s1,
+                                       float& s2) {
+  if constexpr (GLUE) {
+    s1 = sigmoidf(h[1]);
+    s2 = sigmoidf(h[2]);
+    x = ((float)px.j + 0.5f) / (float)a.W + (s1 - 0.5f) * (1.0f / (float)a.W);
+    y = ((float)px.i + 0.5f) / (float)a.H + (s2 - 0.5f) * (1.0f / (float)a.H);
+  } else {
+    s1 = s2 = 0.f;
+    x = a.coords[2 * px.n];
+    y = a.coords[2 * px.n + 1];
+  }
+}
+
+template <int NSH, bool GLUE>
+__global__ __launch_bounds__(NT) void k_adapter_fwd(AdIn a, float* __restrict__ means, float* __restrict__ covs,
+                                                    float* __restrict__ harm, float* __restrict__ opac,
+                                                    float* __restrict__ scales_out, float* __restrict__ rot_out) {
+  constexpr int KH = Rows<NSH, GLUE>::kHead, O = Rows<NSH, GLUE>::kOff;
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // NT * max(C, 3 * NSH, 9) floats
+  const size_t total = (size_t)a.BV * a.H * a.W * a.S;
   const size_t n0 = (size_t)blockIdx.x * NT;
   const int nrows = (int)min((size_t)NT, total - n0);
   const int tid = threadIdx.x;
+  const int C = a.C;
   Pix px;
-  const bool valid = pixel_of(n0 + tid, B, V, H, W, px);  // px.bg == px.n: outputs share the row order
-  dsplat::stage_in<NT>(head + n0 * C, (size_t)nrows * C, lds);
+  const bool valid = pixel_of(n0 + tid, a, px);  // outputs share the row order
+  dsplat::stage_in<NT>(a.rows + n0 * C, (size_t)nrows * C, lds);
   __syncthreads();
   float h[KH];
 #pragma unroll
   for (int k = 0; k < KH; ++k) h[k] = valid ? lds[tid * C + k] : 0.f;
   __syncthreads();
-  const size_t HW = (size_t)H * W;
-  float mo[3], Cw[9], ho[3 * NSH];
+  const size_t HW = (size_t)a.H * a.W;
+  float mo[3], Cw[9], ho[3 * NSH], sc[3], q[4];
   if (valid) {
-    const float* cam = cams + ((size_t)px.b * V + px.v) * kCamFloats;
-    opac[px.n] = sigmoidf(h[0]);
-    // position: xy from the pixel centre and the offset logits, then the camera ray
-    const float x = ((float)px.j + 0.5f) / (float)W + (sigmoidf(h[1]) - 0.5f) * (1.0f / (float)W);
-    const float y = ((float)px.i + 0.5f) / (float)H + (sigmoidf(h[2]) - 0.5f) * (1.0f / (float)H);
+    const float* cam = a.cams + px.bv * kCamFloats;
+    if constexpr (GLUE) opac[px.n] = sigmoidf(h[0]);
+    // position: the camera ray through the row's image coordinates, scaled by the depth
+    float x, y, s1, s2;
+    row_xy<GLUE>(a, px, h, x, y, s1, s2);
     float u[3], d[3], dw[3];
     ray(cam, x, y, u, d, dw);
-    const float z = depths[px.n];
+    const float z = a.depths[px.n];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) mo[a] = cam[kOffT + a] + dw[a] * z;
+    for (int k = 0; k < 3; ++k) mo[k] = cam[kOffT + k] + dw[k] * z;
     // covariance
-    float sc[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) sc[k] = fminf(fmaxf(softplusf(h[3 + k] - 4.0f), smin), smax);
-    float q[4];
-    const float L = sqrtf(((h[6] * h[6] + h[7] * h[7]) + h[8] * h[8]) + h[9] * h[9]);
+    for (int k = 0; k < 3; ++k) sc[k] = fminf(fmaxf(softplusf(h[O + k] - 4.0f), a.smin), a.smax);
+    const float L = sqrtf(((h[O + 3] * h[O + 3] + h[O + 4] * h[O + 4]) + h[O + 5] * h[O + 5]) + h[O + 6] * h[O + 6]);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = h[6 + k] / (L + 1e-8f);
+    for (int k = 0; k < 4; ++k) q[k] = h[O + 3 + k] / (L + a.eps);
     QuatR qr;
     quat_to_R(q, qr);
     float M[9], Cl[9], T1[9];
 #pragma unroll
-    for (int a = 0; a < 3; ++a)
+    for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) M[a * 3 + k] = (qr.R[a * 3 + k] * sc[k]) * sc[k];
+      for (int k = 0; k < 3; ++k) M[r * 3 + k] = (qr.R[r * 3 + k] * sc[k]) * sc[k];
     mm3t(M, qr.R, Cl);          // (R S S^T) R^T
     mm3(cam + kOffR, Cl, T1);   // Rc C
     mm3t(T1, cam + kOffR, Cw);  // (Rc C) Rc^T
     // harmonics: masked raw SH + the image colour in the DC term, rotated per degree block
-    const float* img = images + ((size_t)px.b * V + px.v) * 3 * HW + px.p;
+    const float* img = a.images + px.bv * 3 * HW + px.p;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       float sh[NSH];
 #pragma unroll
-      for (int k = 0; k < NSH; ++k) sh[k] = h[10 + c * NSH + k] * sh_mask[k];
+      for (int k = 0; k < NSH; ++k) sh[k] = h[O + 7 + c * NSH + k] * a.sh_mask[k];
       sh[0] = sh[0] + (img[c * HW] - 0.5f) / kC0;
       float* o = ho + c * NSH;
       o[0] = sh[0];
@@ -195,98 +220,78 @@ __global__ __launch_bounds__(NT) void k_adapter_fwd(int B, int V, int H, int W, 
     }
   }
   // coalesced row writes through LDS
-  if (valid)
-#pragma unroll
-    for (int k = 0; k < 3 * NSH; ++k) lds[tid * 3 * NSH + k] = ho[k];
-  __syncthreads();
-  dsplat::stage_out<NT>(harm + n0 * 3 * NSH, (size_t)nrows * 3 * NSH, lds);
-  __syncthreads();
-  if (valid)
-#pragma unroll
-    for (int k = 0; k < 9; ++k) lds[tid * 9 + k] = Cw[k];
-  __syncthreads();
-  dsplat::stage_out<NT>(covs + n0 * 9, (size_t)nrows * 9, lds);
-  __syncthreads();
-  if (valid)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) lds[tid * 3 + k] = mo[k];
-  __syncthreads();
-  dsplat::stage_out<NT>(means + n0 * 3, (size_t)nrows * 3, lds);
+  const auto put = [&](float* dst, const float* v, int width) {
+    if (valid)
+      for (int k = 0; k < width; ++k) lds[tid * width + k] = v[k];
+    __syncthreads();
+    dsplat::stage_out<NT>(dst + n0 * width, (size_t)nrows * width, lds);
+    __syncthreads();
+  };
+  put(harm, ho, 3 * NSH);
+  put(covs, Cw, 9);
+  put(means, mo, 3);
+  if constexpr (!GLUE) {
+    if (scales_out) put(scales_out, sc, 3);
+    if (rot_out) put(rot_out, q, 4);
+  }
 }
 
-template <int NSH>
-__global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, int C, const float* __restrict__ head,
-                                                    const float* __restrict__ depths,
-                                                    const float* __restrict__ cams, float smin, float smax,
-                                                    const float* __restrict__ sh_mask,
-                                                    const float* __restrict__ dmeans,
+template <int NSH, bool GLUE>
+__global__ __launch_bounds__(NT) void k_adapter_bwd(AdIn a, const float* __restrict__ dmeans,
                                                     const float* __restrict__ dcovs,
                                                     const float* __restrict__ dharm,
-                                                    const float* __restrict__ dopac, float* __restrict__ dhead,
-                                                    float* __restrict__ ddepth) {
-  constexpr int KH = Rows<NSH>::kHead;
-  extern __shared__ float lds[];  // NT * max(C, 3 * NSH) floats
-  const size_t total = (size_t)B * V * H * W;
+                                                    const float* __restrict__ dopac,
+                                                    const float* __restrict__ dscales,
+                                                    const float* __restrict__ drot, float* __restrict__ drows,
+                                                    float* __restrict__ ddepth, float* __restrict__ dcoords) {
+  constexpr int KH = Rows<NSH, GLUE>::kHead, O = Rows<NSH, GLUE>::kOff;
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // NT * max(C, 3 * NSH, 9) floats
+  const size_t total = (size_t)a.BV * a.H * a.W * a.S;
   const size_t n0 = (size_t)blockIdx.x * NT;
   const int nrows = (int)min((size_t)NT, total - n0);
   const int tid = threadIdx.x;
+  const int C = a.C;
   Pix px;
-  const bool valid = pixel_of(n0 + tid, B, V, H, W, px);
+  const bool valid = pixel_of(n0 + tid, a, px);
   // rows in: head, then the output gradients (each staged through the same LDS buffer)
-  float h[KH], gh[3 * NSH], gCw[9], gm[3];
-  dsplat::stage_in<NT>(head + n0 * C, (size_t)nrows * C, lds);
+  const auto get = [&](const float* src, float* v, int width) {
+    if (!src) {
+      for (int k = 0; k < width; ++k) v[k] = 0.f;
+      return;
+    }
+    dsplat::stage_in<NT>(src + n0 * width, (size_t)nrows * width, lds);
+    __syncthreads();
+    for (int k = 0; k < width; ++k) v[k] = valid ? lds[tid * width + k] : 0.f;
+    __syncthreads();
+  };
+  float h[KH], gh[3 * NSH], gCw[9], gm[3], gsc[3], grot[4];
+  dsplat::stage_in<NT>(a.rows + n0 * C, (size_t)nrows * C, lds);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < KH; ++k) h[k] = valid ? lds[tid * C + k] : 0.f;
   __syncthreads();
-  if (dharm) {
-    dsplat::stage_in<NT>(dharm + n0 * 3 * NSH, (size_t)nrows * 3 * NSH, lds);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 3 * NSH; ++k) gh[k] = valid ? lds[tid * 3 * NSH + k] : 0.f;
-    __syncthreads();
-  } else {
-#pragma unroll
-    for (int k = 0; k < 3 * NSH; ++k) gh[k] = 0.f;
-  }
-  if (dcovs) {
-    dsplat::stage_in<NT>(dcovs + n0 * 9, (size_t)nrows * 9, lds);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 9; ++k) gCw[k] = valid ? lds[tid * 9 + k] : 0.f;
-    __syncthreads();
-  } else {
-#pragma unroll
-    for (int k = 0; k < 9; ++k) gCw[k] = 0.f;
-  }
-  if (dmeans) {
-    dsplat::stage_in<NT>(dmeans + n0 * 3, (size_t)nrows * 3, lds);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 3; ++k) gm[k] = valid ? lds[tid * 3 + k] : 0.f;
-    __syncthreads();
-  } else {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) gm[k] = 0.f;
-  }
+  get(dharm, gh, 3 * NSH);
+  get(dcovs, gCw, 9);
+  get(dmeans, gm, 3);
+  get(GLUE ? nullptr : dscales, gsc, 3);
+  get(GLUE ? nullptr : drot, grot, 4);
   float dh[KH];
 #pragma unroll
   for (int k = 0; k < KH; ++k) dh[k] = 0.f;
+  float gxy[2] = {0.f, 0.f};
   if (valid) {
-    const float* cam = cams + ((size_t)px.b * V + px.v) * kCamFloats;
-    // opacity
-    {
+    const float* cam = a.cams + px.bv * kCamFloats;
+    if constexpr (GLUE) {  // opacity
       const float sg = sigmoidf(h[0]);
       dh[0] = dopac ? dopac[px.n] * sg * (1.0f - sg) : 0.0f;
     }
-    // mean -> depth, offsets
+    // mean -> depth, image coordinates (-> offset logits)
     {
-      const float s1 = sigmoidf(h[1]), s2 = sigmoidf(h[2]);
-      const float x = ((float)px.j + 0.5f) / (float)W + (s1 - 0.5f) * (1.0f / (float)W);
-      const float y = ((float)px.i + 0.5f) / (float)H + (s2 - 0.5f) * (1.0f / (float)H);
+      float x, y, s1, s2;
+      row_xy<GLUE>(a, px, h, x, y, s1, s2);
       float u[3], d[3], dw[3];
       ray(cam, x, y, u, d, dw);
-      const float z = depths[px.n];
+      const float z = a.depths[px.n];
       if (ddepth) ddepth[px.n] = (gm[0] * dw[0] + gm[1] * dw[1]) + gm[2] * dw[2];
       const float* Rc = cam + kOffR;
       float gd[3];  // d L / d d = Rc^T (z gm)
@@ -302,25 +307,27 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
       for (int b = 0; b < 3; ++b) gu[b] = gd[b] * inv;
       gu[2] -= dot * inv * inv;
       const float* Ki = cam + kOffKinv;
-      const float gx = (Ki[0] * gu[0] + Ki[3] * gu[1]) + Ki[6] * gu[2];
-      const float gy = (Ki[1] * gu[0] + Ki[4] * gu[1]) + Ki[7] * gu[2];
-      dh[1] = gx * (1.0f / (float)W) * s1 * (1.0f - s1);
-      dh[2] = gy * (1.0f / (float)H) * s2 * (1.0f - s2);
+      gxy[0] = (Ki[0] * gu[0] + Ki[3] * gu[1]) + Ki[6] * gu[2];
+      gxy[1] = (Ki[1] * gu[0] + Ki[4] * gu[1]) + Ki[7] * gu[2];
+      if constexpr (GLUE) {
+        dh[1] = gxy[0] * (1.0f / (float)a.W) * s1 * (1.0f - s1);
+        dh[2] = gxy[1] * (1.0f / (float)a.H) * s2 * (1.0f - s2);
+      }
     }
     // covariance -> scales, rotation
     {
       float sc[3], sraw[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        sraw[k] = softplusf(h[3 + k] - 4.0f);
-        sc[k] = fminf(fmaxf(sraw[k], smin), smax);
+        sraw[k] = softplusf(h[O + k] - 4.0f);
+        sc[k] = fminf(fmaxf(sraw[k], a.smin), a.smax);
       }
       float r[4], q[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) r[k] = h[6 + k];
+      for (int k = 0; k < 4; ++k) r[k] = h[O + 3 + k];
       const float L = sqrtf(((r[0] * r[0] + r[1] * r[1]) + r[2] * r[2]) + r[3] * r[3]);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) q[k] = r[k] / (L + 1e-8f);
+      for (int k = 0; k < 4; ++k) q[k] = r[k] / (L + a.eps);
       QuatR qr;
       quat_to_R(q, qr);
       float T[9], gC[9];
@@ -332,18 +339,18 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
       for (int k = 0; k < 9; ++k) gS[k] = gC[k] + gC[(k % 3) * 3 + k / 3];
       float RS2[9];
 #pragma unroll
-      for (int a = 0; a < 3; ++a)
+      for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) RS2[a * 3 + k] = qr.R[a * 3 + k] * (sc[k] * sc[k]);
+        for (int k = 0; k < 3; ++k) RS2[i * 3 + k] = qr.R[i * 3 + k] * (sc[k] * sc[k]);
       mm3(gS, RS2, gR);
       float GR[9];
       mm3(gC, qr.R, GR);  // gC R
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const float dsig = (qr.R[k] * GR[k] + qr.R[3 + k] * GR[3 + k]) + qr.R[6 + k] * GR[6 + k];
-        const float ds = 2.0f * sc[k] * dsig;
-        const bool pass = sraw[k] >= smin && sraw[k] <= smax;  // torch.clamp gradient mask
-        dh[3 + k] = pass ? ds * softplus_grad(h[3 + k] - 4.0f) : 0.0f;
+        const float ds = 2.0f * sc[k] * dsig + gsc[k];  // + the scales output's own gradient
+        const bool pass = sraw[k] >= a.smin && sraw[k] <= a.smax;  // torch.clamp gradient mask
+        dh[O + k] = pass ? ds * softplus_grad(h[O + k] - 4.0f) : 0.0f;
       }
       // R(q) = I + s2 P(q), s2 = 2 / (|q|^2 + eps)
       const float i = q[0], j = q[1], kk = q[2], w = q[3], s2 = qr.s2;
@@ -361,13 +368,13 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
       gq[2] = s2 * (-2.f * g * kk - g01 * w + g02 * i + g10 * w - 2.f * g11 * kk + g12 * j + g20 * i + g21 * j);
       gq[3] = s2 * (-g01 * kk + g02 * j + g10 * kk - g12 * i - g20 * j + g21 * i);
 #pragma unroll
-      for (int m = 0; m < 4; ++m) gq[m] -= gs2 * s2 * s2 * q[m];
+      for (int m = 0; m < 4; ++m) gq[m] = gq[m] - gs2 * s2 * s2 * q[m] + grot[m];  // + rotations output grad
       // q = r / (|r| + eps)
-      const float Le = L + 1e-8f;
+      const float Le = L + a.eps;
       const float dqr = ((gq[0] * r[0] + gq[1] * r[1]) + gq[2] * r[2]) + gq[3] * r[3];
       const float c2 = L > 0.f ? dqr / (L * Le * Le) : 0.f;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) dh[6 + m] = gq[m] / Le - c2 * r[m];
+      for (int m = 0; m < 4; ++m) dh[O + 3 + m] = gq[m] / Le - c2 * r[m];
     }
     // harmonics -> raw SH: D^T per degree block, then the mask
 #pragma unroll
@@ -383,22 +390,33 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(int B, int V, int H, int W, 
         for (int k = 0; k < n; ++k) {
           float acc = 0.f;
 #pragma unroll
-          for (int a = 0; a < n; ++a) acc += D[a * n + k] * g2[b0 + a];
+          for (int i2 = 0; i2 < n; ++i2) acc += D[i2 * n + k] * g2[b0 + i2];
           gs[b0 + k] = acc;
         }
       }
 #pragma unroll
-      for (int k = 0; k < NSH; ++k) dh[10 + c * NSH + k] = gs[k] * sh_mask[k];
+      for (int k = 0; k < NSH; ++k) dh[O + 7 + c * NSH + k] = gs[k] * a.sh_mask[k];
     }
   }
-  // dhead rows out through LDS (channels past 10 + 3 d_sh are 0)
+  // drows out through LDS (channels past the used ones are 0)
   if (valid) {
 #pragma unroll
     for (int k = 0; k < KH; ++k) lds[tid * C + k] = dh[k];
     for (int k = KH; k < C; ++k) lds[tid * C + k] = 0.f;
   }
   __syncthreads();
-  dsplat::stage_out<NT>(dhead + n0 * C, (size_t)nrows * C, lds);
+  dsplat::stage_out<NT>(drows + n0 * C, (size_t)nrows * C, lds);
+  if constexpr (!GLUE) {
+    if (dcoords) {
+      __syncthreads();
+      if (valid) {
+        lds[tid * 2] = gxy[0];
+        lds[tid * 2 + 1] = gxy[1];
+      }
+      __syncthreads();
+      dsplat::stage_out<NT>(dcoords + n0 * 2, (size_t)nrows * 2, lds);
+    }
+  }
 }
 
 // Per-view constant blocks (dga_adapter_cameras): R, t of c2w, K^-1 (double, adjugate) and
@@ -484,6 +502,41 @@ __global__ void k_adapter_cams(int BV, const float* __restrict__ ext, const floa
 
 }  // namespace
 
+namespace {
+size_t adapter_lds(int C, int d_sh) { return (size_t)NT * (size_t)max(max(C, 3 * d_sh), 9) * sizeof(float); }
+
+template <int NS, bool GLUE>
+int launch_fwd(const AdIn& a, float* means, float* covs, float* harm, float* opac, float* scales, float* rots,
+               hipStream_t st) {
+  const size_t n = (size_t)a.BV * a.H * a.W * a.S;
+  const size_t lds = adapter_lds(a.C, NS);
+  if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_adapter_fwd<NS, GLUE>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return dsplat::check_launch("hipFuncSetAttribute(k_adapter_fwd)");
+  k_adapter_fwd<NS, GLUE><<<(unsigned)((n + NT - 1) / NT), NT, lds, st>>>(a, means, covs, harm, opac, scales, rots);
+  return dsplat::check_launch("k_adapter_fwd");
+}
+template <int NS, bool GLUE>
+int launch_bwd(const AdIn& a, const float* dmeans, const float* dcovs, const float* dharm, const float* dopac,
+               const float* dscales, const float* drot, float* drows, float* ddepth, float* dcoords, hipStream_t st) {
+  const size_t n = (size_t)a.BV * a.H * a.W * a.S;
+  const size_t lds = adapter_lds(a.C, NS);
+  if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_adapter_bwd<NS, GLUE>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return dsplat::check_launch("hipFuncSetAttribute(k_adapter_bwd)");
+  k_adapter_bwd<NS, GLUE><<<(unsigned)((n + NT - 1) / NT), NT, lds, st>>>(a, dmeans, dcovs, dharm, dopac, dscales,
+                                                                           drot, drows, ddepth, dcoords);
+  return dsplat::check_launch("k_adapter_bwd");
+}
+#define DGA_DISPATCH(d_sh, CALL) \
+  switch (d_sh) {                \
+    case 1: return CALL(1);      \
+    case 4: return CALL(4);      \
+    case 9: return CALL(9);      \
+    default: return CALL(16);    \
+  }
+}  // namespace
+
 extern "C" {
 
 int dga_adapter_cameras(int BV, const float* extrinsics, const float* intrinsics, int sh_degree, const double* probes,
@@ -494,6 +547,7 @@ int dga_adapter_cameras(int BV, const float* extrinsics, const float* intrinsics
   return dsplat::check_launch("k_adapter_cams");
 }
 
+
 int dga_adapter_fwd(int B, int V, int H, int W, int d_sh, int C, const float* head, const float* depths,
                     const float* images, const float* cams, float scale_min, float scale_max, const float* sh_mask,
                     float* means, float* covariances, float* harmonics, float* opacities, void* stream) {
@@ -502,25 +556,12 @@ int dga_adapter_fwd(int B, int V, int H, int W, int d_sh, int C, const float* he
   DSPLAT_REQUIRE(C >= 10 + 3 * d_sh, "dga_adapter_fwd: %d head channels < 10 + 3*d_sh", C);
   DSPLAT_REQUIRE(head && depths && images && cams && sh_mask && means && covariances && harmonics && opacities,
                  "dga_adapter_fwd: null pointer");
-  const size_t n = (size_t)B * V * H * W;
-  const unsigned grid = (unsigned)((n + NT - 1) / NT);
-  const size_t lds = (size_t)NT * (size_t)max(C, 3 * d_sh) * sizeof(float);
-  DSPLAT_REQUIRE(lds <= 160 * 1024, "dga_adapter_fwd: %d head channels exceed the LDS row staging", C);
+  DSPLAT_REQUIRE(adapter_lds(C, d_sh) <= 160 * 1024, "dga_adapter_fwd: %d head channels exceed the LDS row staging", C);
+  const AdIn a{head, nullptr, depths, images, cams, sh_mask, scale_min, scale_max, 1e-8f, C, B * V, H, W, 1};
   hipStream_t st = (hipStream_t)stream;
-#define DGA_F(NS)                                                                                     \
-  if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_adapter_fwd<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                             (int)lds) != hipSuccess)                                            \
-    return dsplat::check_launch("hipFuncSetAttribute(k_adapter_fwd)");                                                  \
-  k_adapter_fwd<NS><<<grid, NT, lds, st>>>(B, V, H, W, C, head, depths, images, cams, scale_min, scale_max, \
-                                         sh_mask, means, covariances, harmonics, opacities)
-  switch (d_sh) {
-    case 1: DGA_F(1); break;
-    case 4: DGA_F(4); break;
-    case 9: DGA_F(9); break;
-    default: DGA_F(16); break;
-  }
+#define DGA_F(NS) launch_fwd<NS, true>(a, means, covariances, harmonics, opacities, nullptr, nullptr, st)
+  DGA_DISPATCH(d_sh, DGA_F)
 #undef DGA_F
-  return dsplat::check_launch("k_adapter_fwd");
 }
 
 int dga_adapter_bwd(int B, int V, int H, int W, int d_sh, int C, const float* head, const float* depths,
@@ -531,25 +572,48 @@ int dga_adapter_bwd(int B, int V, int H, int W, int d_sh, int C, const float* he
   DSPLAT_REQUIRE(d_sh == 1 || d_sh == 4 || d_sh == 9 || d_sh == 16, "dga_adapter_bwd: d_sh=%d (1, 4, 9, 16)", d_sh);
   DSPLAT_REQUIRE(C >= 10 + 3 * d_sh, "dga_adapter_bwd: %d head channels < 10 + 3*d_sh", C);
   DSPLAT_REQUIRE(head && depths && cams && sh_mask && dhead, "dga_adapter_bwd: null pointer");
-  const size_t n = (size_t)B * V * H * W;
-  const unsigned grid = (unsigned)((n + NT - 1) / NT);
-  const size_t lds = (size_t)NT * (size_t)max(C, 3 * d_sh) * sizeof(float);
-  DSPLAT_REQUIRE(lds <= 160 * 1024, "dga_adapter_bwd: %d head channels exceed the LDS row staging", C);
+  DSPLAT_REQUIRE(adapter_lds(C, d_sh) <= 160 * 1024, "dga_adapter_bwd: %d head channels exceed the LDS row staging", C);
+  const AdIn a{head, nullptr, depths, nullptr, cams, sh_mask, scale_min, scale_max, 1e-8f, C, B * V, H, W, 1};
   hipStream_t st = (hipStream_t)stream;
-#define DGA_B(NS)                                                                                     \
-  if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_adapter_bwd<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                             (int)lds) != hipSuccess)                                            \
-    return dsplat::check_launch("hipFuncSetAttribute(k_adapter_bwd)");                                                  \
-  k_adapter_bwd<NS><<<grid, NT, lds, st>>>(B, V, H, W, C, head, depths, cams, scale_min, scale_max, sh_mask, \
-                                         dmeans, dcovariances, dharmonics, dopacities, dhead, ddepths)
-  switch (d_sh) {
-    case 1: DGA_B(1); break;
-    case 4: DGA_B(4); break;
-    case 9: DGA_B(9); break;
-    default: DGA_B(16); break;
-  }
+#define DGA_B(NS) \
+  launch_bwd<NS, true>(a, dmeans, dcovariances, dharmonics, dopacities, nullptr, nullptr, dhead, ddepths, nullptr, st)
+  DGA_DISPATCH(d_sh, DGA_B)
 #undef DGA_B
-  return dsplat::check_launch("k_adapter_bwd");
+}
+
+int dga_adapter_forward(int BV, int H, int W, int S, int d_sh, int C, const float* raw, const float* coordinates,
+                        const float* depths, const float* images, const float* cams, float scale_min,
+                        float scale_max, const float* sh_mask, float eps, float* means, float* covariances,
+                        float* harmonics, float* scales, float* rotations, void* stream) {
+  DSPLAT_REQUIRE(BV > 0 && H > 0 && W > 0 && S > 0, "dga_adapter_forward: bad sizes");
+  DSPLAT_REQUIRE(d_sh == 1 || d_sh == 4 || d_sh == 9 || d_sh == 16, "dga_adapter_forward: d_sh=%d (1, 4, 9, 16)", d_sh);
+  DSPLAT_REQUIRE(C >= 7 + 3 * d_sh, "dga_adapter_forward: %d raw channels < 7 + 3*d_sh", C);
+  DSPLAT_REQUIRE(raw && coordinates && depths && images && cams && sh_mask && means && covariances && harmonics,
+                 "dga_adapter_forward: null pointer");
+  DSPLAT_REQUIRE(adapter_lds(C, d_sh) <= 160 * 1024, "dga_adapter_forward: %d channels exceed the LDS row staging", C);
+  const AdIn a{raw, coordinates, depths, images, cams, sh_mask, scale_min, scale_max, eps, C, BV, H, W, S};
+  hipStream_t st = (hipStream_t)stream;
+#define DGA_F(NS) launch_fwd<NS, false>(a, means, covariances, harmonics, nullptr, scales, rotations, st)
+  DGA_DISPATCH(d_sh, DGA_F)
+#undef DGA_F
+}
+
+int dga_adapter_backward(int BV, int H, int W, int S, int d_sh, int C, const float* raw, const float* coordinates,
+                         const float* depths, const float* cams, float scale_min, float scale_max,
+                         const float* sh_mask, float eps, const float* dmeans, const float* dcovariances,
+                         const float* dharmonics, const float* dscales, const float* drotations, float* draw,
+                         float* dcoordinates, float* ddepths, void* stream) {
+  DSPLAT_REQUIRE(BV > 0 && H > 0 && W > 0 && S > 0, "dga_adapter_backward: bad sizes");
+  DSPLAT_REQUIRE(d_sh == 1 || d_sh == 4 || d_sh == 9 || d_sh == 16, "dga_adapter_backward: d_sh=%d", d_sh);
+  DSPLAT_REQUIRE(C >= 7 + 3 * d_sh, "dga_adapter_backward: %d raw channels < 7 + 3*d_sh", C);
+  DSPLAT_REQUIRE(raw && coordinates && depths && cams && sh_mask && draw, "dga_adapter_backward: null pointer");
+  DSPLAT_REQUIRE(adapter_lds(C, d_sh) <= 160 * 1024, "dga_adapter_backward: %d channels exceed the LDS row staging", C);
+  const AdIn a{raw, coordinates, depths, nullptr, cams, sh_mask, scale_min, scale_max, eps, C, BV, H, W, S};
+  hipStream_t st = (hipStream_t)stream;
+#define DGA_B(NS) \
+  launch_bwd<NS, false>(a, dmeans, dcovariances, dharmonics, nullptr, dscales, drotations, draw, ddepths, dcoordinates, st)
+  DGA_DISPATCH(d_sh, DGA_B)
+#undef DGA_B
 }
 
 }  // extern "C"

@@ -80,19 +80,17 @@ int zero_async(void* p, size_t bytes, hipStream_t st, const char* what);
 // contiguous span, so it moves as 16-byte vectors (coalesced) and each thread then reads /
 // writes its own row in LDS (odd row lengths are bank-conflict free). Per-thread rows of
 // 9 / 27 / 37 floats accessed directly make every load instruction touch ~64 cache lines.
+// The LDS side moves 16 B per lane too (ds_write_b128 / ds_read_b128: consecutive lanes,
+// consecutive 16-B slots, no bank conflict; four scalar ds ops at a 16-B lane stride were a
+// 4-way conflict each). `lds` must be 16-byte aligned.
 template <int NTH>
 __device__ __forceinline__ void stage_in(const float* __restrict__ src, size_t nfloat, float* lds) {
   const uintptr_t addr = reinterpret_cast<uintptr_t>(src);
   if ((addr & 15) == 0) {
     const size_t n4 = nfloat / 4;
     const float4* s4 = reinterpret_cast<const float4*>(src);
-    for (size_t i = threadIdx.x; i < n4; i += NTH) {
-      const float4 v = s4[i];
-      lds[4 * i] = v.x;
-      lds[4 * i + 1] = v.y;
-      lds[4 * i + 2] = v.z;
-      lds[4 * i + 3] = v.w;
-    }
+    float4* l4 = reinterpret_cast<float4*>(lds);
+    for (size_t i = threadIdx.x; i < n4; i += NTH) l4[i] = s4[i];
     for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NTH) lds[i] = src[i];
   } else {
     for (size_t i = threadIdx.x; i < nfloat; i += NTH) lds[i] = src[i];
@@ -104,8 +102,8 @@ __device__ __forceinline__ void stage_out(float* __restrict__ dst, size_t nfloat
   if ((addr & 15) == 0) {
     const size_t n4 = nfloat / 4;
     float4* d4 = reinterpret_cast<float4*>(dst);
-    for (size_t i = threadIdx.x; i < n4; i += NTH)
-      d4[i] = make_float4(lds[4 * i], lds[4 * i + 1], lds[4 * i + 2], lds[4 * i + 3]);
+    const float4* l4 = reinterpret_cast<const float4*>(lds);
+    for (size_t i = threadIdx.x; i < n4; i += NTH) d4[i] = l4[i];
     for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NTH) dst[i] = lds[i];
   } else {
     for (size_t i = threadIdx.x; i < nfloat; i += NTH) dst[i] = lds[i];

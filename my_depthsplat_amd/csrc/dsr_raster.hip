@@ -233,7 +233,8 @@ __device__ __forceinline__ float sh_eval(const float* sh, int ch, float x, float
 // decoder's Gaussians.harmonics) instead of the rasterizer's coefficient-major [S,G,M,3];
 // bit 1: full covariance [S,G,3,3] instead of cov6 — the upper triangle is read, exactly
 // what cuda_splatting.py:114,122's triu gather hands the rasterizer.
-constexpr int kLayoutShChannelMajor = 1, kLayoutCovFull = 2, kLayoutCountsZeroed = 4;
+constexpr int kLayoutShChannelMajor = DSR_LAYOUT_SH_CHANNEL_MAJOR, kLayoutCovFull = DSR_LAYOUT_COV_FULL,
+              kLayoutCountsZeroed = DSR_LAYOUT_COUNTS_ZEROED, kLayoutRectBinning = DSR_LAYOUT_RECT_BINNING;
 __device__ __forceinline__ float load_cov(const float* cov, size_t sg, int k, int layout) {
   if (layout & kLayoutCovFull) {
     constexpr int idx[6] = {0, 1, 2, 4, 5, 8};
@@ -244,10 +245,6 @@ __device__ __forceinline__ float load_cov(const float* cov, size_t sg, int k, in
 template <int NC>
 __device__ __forceinline__ void load_sh(const float* shs, size_t sg, int M, int layout, float* out) {
   const float* p = shs + sg * (size_t)M * 3;
-#ifdef PP_NOSH
-  for (int k = 0; k < NC * 3; ++k) out[k] = 0.01f * k + (float)(sg & 7);
-  return;
-#endif
   if (layout & kLayoutShChannelMajor) {
 #pragma unroll
     for (int k = 0; k < NC; ++k)
@@ -628,7 +625,7 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
   }
 }
 
-// Exact tile test of the inference binning (PE_EXACT): can the alpha >= 1/255 ellipse of a
+// Exact tile test of the inference binning (k_project_emit EXACT): can the alpha >= 1/255 ellipse of a
 // Gaussian reach a pixel centre of the tile box [x0, x0 + BX - 1] x [y0, y0 + BY - 1]? The
 // same continuous-box minimum of the conic as the compositor's rect_hit (defined with it
 // below), with the per-Gaussian terms computed once by the owner lane (TileEll) and moved to
@@ -704,25 +701,35 @@ __device__ __forceinline__ void tile_rect_alpha(const TileEll& e, int& x0, int& 
 // them, counts the block's (view, tile) entries in an LDS histogram, reserves a contiguous
 // range per touched tile with one global atomic, and writes the (depth, id) keys into
 // segment (v, t), which starts at (v*T + t) * G (a Gaussian touches a tile at most once, so
-// G slots suffice). No global scan is needed before the keys exist. (One workgroup per
-// view, re-reading the scene's inputs through L2, beats one per scene looping over its
-// views: 3x the waves in flight hide the load and atomic latencies.)
+// G slots suffice). No global scan is needed before the keys exist. The V workgroups of one
+// Gaussian block run back to back on one XCD (xcd_item_views), so the scene's 148 B per
+// Gaussian come from HBM once and from that XCD's L2 for the other views (one workgroup per
+// scene looping over its views would hold 3x fewer waves in flight to hide the load and
+// atomic latencies).
 #ifndef PB_WPE
 #define PB_WPE 1
 #endif
 // pair cache of the count pass (PE_CAPW (tile, rank, owner) words per wave in LDS)
-#ifndef PE_CACHE
-#define PE_CACHE 1
-#endif
 #ifndef PE_CAPW
 #define PE_CAPW 768
 #endif
-// exact ellipse-vs-tile test in the inference binning (CAM path only: the stateful path keeps
-// the reference's rect lists, which the backward and the oracle list tests follow)
-#ifndef PE_EXACT
-#define PE_EXACT 1
-#endif
-template <int DEG, bool CAM>
+// Workgroup -> (view, block) placement for k_project_emit: the items are (block, view) in
+// block-major order, cut into 8 contiguous ranges, one per XCD (dispatch is round-robin over
+// the XCDs: workgroup i runs on XCD i % 8). A block's V views then sit in consecutive slots
+// of one XCD and re-read the block's inputs from its L2.
+__device__ __forceinline__ bool xcd_item_views(int blocks_per_view, int V, int& v, int& blk) {
+  const int items = blocks_per_view * V;
+  const int per = (items + 7) >> 3;
+  const int item = (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
+  if ((int)(blockIdx.x >> 3) >= per || item >= items) return false;
+  blk = item / V;
+  v = item - blk * V;
+  return true;
+}
+// EXACT (inference binning, CAM only): a pair is kept only when tile_reach says the
+// alpha >= 1/255 ellipse reaches the tile; the stateful / training path keeps the reference's
+// rect lists, which the backward and the oracle list tests follow.
+template <int DEG, bool CAM, bool EXACT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
                                                      const float* __restrict__ means,
                                                      const float* __restrict__ shs,
@@ -733,116 +740,97 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
                                                      float* __restrict__ geom, int32_t* __restrict__ radii,
                                                      uint32_t* __restrict__ seg_count,
                                                      uint64_t* __restrict__ keys, int layout, CamIn ci) {
+  static_assert(CAM || !EXACT, "exact binning is an inference-path (CAM) mode");
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
   __shared__ dsr_camera s_cam[1];  // CAM only
-#if PE_CACHE
   __shared__ uint32_t s_pairs[NT / 64][PE_CAPW];
   __shared__ uint32_t s_ovf;
-#endif
   int v, blk;
-  if (!xcd_item((G + NT - 1) / NT, V, v, blk)) return;
+  if (!xcd_item_views((G + NT - 1) / NT, V, v, blk)) return;
   const dsr_camera* cam = cams + v;
   const int T = gx * gy;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = blk * NT + tid;
   WaveRects& wr = s_wr[w];
   const uint64_t* wkey = s_key + w * 64;
-  {
-    for (int t = tid; t < T; t += NT) s_hist[t] = 0;
-    int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    uint64_t key = 0;
-    constexpr bool EXACT = CAM && PE_EXACT;
-    TileEll ell{0.f, 0.f, 0.f, 0.f, 0.f, -1.f, 0.f, 0.f};
-    GaussIn<DEG> in;
-    if (g < G) load_gauss<DEG>(in, (size_t)(CAM ? ci.view_scene[v] : cam->scene) * G + g, means, opac, cov6, layout);
-    if constexpr (CAM) {
-      // every workgroup sets up its view's camera while its Gaussians load (no separate
-      // launch); the first block of each view also stores it for the later kernels
-      if (w == 0) make_camera_wave(v, ci, lane, s_cam[0]);
-      __syncthreads();
-      if (blk == 0 && tid < (int)(sizeof(dsr_camera) / 4))
-        reinterpret_cast<uint32_t*>(cams + v)[tid] = reinterpret_cast<const uint32_t*>(s_cam)[tid];
-      cam = s_cam;
-    }
-    if (g < G) {
-      float rec[GS];
-      r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
-      store_geom(geom, radii, (size_t)v * G + g, rec, r);
-      key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
-      if constexpr (EXACT) {
-        ell = tile_ell(rec, r);
-        if (r > 0) tile_rect_alpha(ell, x0, y0, x1, y1);
-      }
-    }
-    s_key[tid] = key;
-#if PE_CACHE
-    if (tid == 0) s_ovf = 0u;
-#endif
+  for (int t = tid; t < T; t += NT) s_hist[t] = 0;
+  int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+  uint64_t key = 0;
+  TileEll ell{0.f, 0.f, 0.f, 0.f, 0.f, -1.f, 0.f, 0.f};
+  GaussIn<DEG> in;
+  if (g < G) load_gauss<DEG>(in, (size_t)(CAM ? ci.view_scene[v] : cam->scene) * G + g, means, opac, cov6, layout);
+  if constexpr (CAM) {
+    // every workgroup sets up its view's camera while its Gaussians load (no separate
+    // launch); the first block of each view also stores it for the later kernels
+    if (w == 0) make_camera_wave(v, ci, lane, s_cam[0]);
     __syncthreads();
-    TileEll oe = ell;  // the owner's ellipse terms for the current pair (EXACT)
-    const auto fetch = [&](int o) {
-      if constexpr (EXACT) oe = tile_ell_of(ell, o);
-    };
-#if PE_CACHE
-    // count pass; each pair's rank among the workgroup's entries of its tile (the LDS atomic's
-    // return value) is kept with the tile and the owner lane, so the emission pass below is a
-    // plain walk over the kept pairs instead of a second rect expansion
-    uint32_t* wp = s_pairs[w];
-    uint32_t stp = 0;
-    const uint32_t wtotal = for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
-      const uint32_t j = stp++ * 64u + (uint32_t)lane;
-      if constexpr (EXACT) {
-        if (!tile_reach(oe, tx, ty)) {  // dropped pair: a hole in the list
-          if (j < (uint32_t)PE_CAPW) wp[j] = 0xFFFFFFFFu;
-          return;
-        }
-      }
-      const uint32_t rk = atomicAdd(&s_hist[t], 1u);
-      if (j < (uint32_t)PE_CAPW) wp[j] = (uint32_t)t | (rk << 16) | ((uint32_t)o << 24);
-    }, fetch);
-    if (lane == 0 && wtotal > (uint32_t)PE_CAPW) s_ovf = 1u;
-#else
-    static_assert(!EXACT, "PE_EXACT needs the pair cache");
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
-#endif
-    __syncthreads();
-    uint32_t* gcount = seg_count + (size_t)v * T;
-    for (int t = tid; t < T; t += NT) {
-      const uint32_t c = s_hist[t];
-#ifdef PB_DIAG_NORES
-      s_hist[t] = 0;
-#else
-      if (c) s_hist[t] = atomicAdd(&gcount[t], c);
-#endif
-    }
-    __syncthreads();
-#ifdef PB_STRIDE  // layout experiment: segment stride PB_STRIDE instead of G (no overflow check)
-    uint64_t* vkeys = keys + (size_t)v * T * PB_STRIDE;
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
-                       [&](int t, int o) { vkeys[(size_t)t * PB_STRIDE + atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
-#else
-    uint64_t* vkeys = keys + (size_t)v * T * G;
-#if PE_CACHE
-    if (!s_ovf) {  // workgroup-uniform
-      for (uint32_t j = (uint32_t)lane; j < wtotal; j += 64u) {
-        const uint32_t p = wp[j];
-        if (EXACT && p == 0xFFFFFFFFu) continue;
-        const uint32_t t = p & 0xFFFFu;
-        vkeys[(size_t)t * G + s_hist[t] + ((p >> 16) & 0xFFu)] = wkey[p >> 24];
-      }
-      return;
-    }
-#endif
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
-      if constexpr (EXACT) {
-        if (!tile_reach(oe, tx, ty)) return;  // same decision as the count pass
-      }
-      vkeys[(size_t)t * G + atomicAdd(&s_hist[t], 1u)] = wkey[o];
-    }, fetch);
-#endif
+    if (blk == 0 && tid < (int)(sizeof(dsr_camera) / 4))
+      reinterpret_cast<uint32_t*>(cams + v)[tid] = reinterpret_cast<const uint32_t*>(s_cam)[tid];
+    cam = s_cam;
   }
+  if (g < G) {
+    float rec[GS];
+    r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
+    store_geom(geom, radii, (size_t)v * G + g, rec, r);
+    key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
+    if constexpr (EXACT) {
+      ell = tile_ell(rec, r);
+      if (r > 0) tile_rect_alpha(ell, x0, y0, x1, y1);
+    }
+  }
+  s_key[tid] = key;
+  if (tid == 0) s_ovf = 0u;
+  __syncthreads();
+  TileEll oe = ell;  // the owner's ellipse terms for the current pair (EXACT)
+  const auto fetch = [&](int o) {
+    if constexpr (EXACT) oe = tile_ell_of(ell, o);
+  };
+  // count pass; each pair's rank among the workgroup's entries of its tile (the LDS atomic's
+  // return value) is kept with the tile and the owner lane, so the emission pass below is a
+  // plain walk over the kept pairs instead of a second rect expansion
+  uint32_t* wp = s_pairs[w];
+  uint32_t stp = 0;
+  const uint32_t wtotal = for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
+    const uint32_t j = stp++ * 64u + (uint32_t)lane;
+    if constexpr (EXACT) {
+      if (!tile_reach(oe, tx, ty)) {  // dropped pair: a hole in the list
+        if (j < (uint32_t)PE_CAPW) wp[j] = 0xFFFFFFFFu;
+        return;
+      }
+    }
+    const uint32_t rk = atomicAdd(&s_hist[t], 1u);
+    if (j < (uint32_t)PE_CAPW) wp[j] = (uint32_t)t | (rk << 16) | ((uint32_t)o << 24);
+  }, fetch);
+  if (lane == 0 && wtotal > (uint32_t)PE_CAPW) s_ovf = 1u;
+  __syncthreads();
+  uint32_t* gcount = seg_count + (size_t)v * T;
+  for (int t = tid; t < T; t += NT) {
+    const uint32_t c = s_hist[t];
+    if (c) s_hist[t] = atomicAdd(&gcount[t], c);
+  }
+  __syncthreads();
+  uint64_t* vkeys = keys + (size_t)v * T * G;
+  if (!s_ovf) {  // workgroup-uniform
+    for (uint32_t j = (uint32_t)lane; j < wtotal; j += 64u) {
+      const uint32_t p = wp[j];
+      if (EXACT && p == 0xFFFFFFFFu) continue;
+      const uint32_t t = p & 0xFFFFu;
+      vkeys[(size_t)t * G + s_hist[t] + ((p >> 16) & 0xFFu)] = wkey[p >> 24];
+    }
+    return;
+  }
+  // a wave of this workgroup had more than PE_CAPW pairs: re-expand the rects. The keep test
+  // is the same inlined code on the same operands (oe from the same owner lane, same tile
+  // coordinates) as in the count pass, so both passes keep exactly the same pairs and the
+  // emission fills the ranges reserved above (tests: test_inference_emit_overflow).
+  for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
+    if constexpr (EXACT) {
+      if (!tile_reach(oe, tx, ty)) return;
+    }
+    vkeys[(size_t)t * G + atomicAdd(&s_hist[t], 1u)] = wkey[o];
+  }, fetch);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1580,9 +1568,6 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
       A[padi<KMAX>(pos)] = tmp[i];
     }
   __syncthreads();
-#ifdef SORT_DIAG_NOFIX  // timing experiment: skip ordering inside bins
-  return;
-#endif
   // order inside each bin: the scatter left hw holding every bin's END offset, so bin b is
   // [end(b - 1), end(b)). A key of a bin of c <= 16 keys counts the smaller keys of its bin
   // (c independent LDS reads, all lanes in parallel); any larger bin (clustered or equal
@@ -1661,24 +1646,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(KMAX * NTH 
       const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
       tmp[i] = idx < n ? keys[b + idx] : 0ull;
     }
-#ifdef SORT_LSD  // the 4-pass LSD sort (kept for comparison runs)
-#pragma unroll
-    for (int i = 0; i < KMAX; ++i) {
-      const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
-      if (idx < n) A[padi<KMAX>(idx)] = tmp[i];
-    }
-    __syncthreads();
-    reg_sort<KMAX, NTH>(A, n, id_bits, cnt, wsum, flag);
-#elif defined(SORT_DIAG_NOSORT)  // timing experiment: load + store only
-#pragma unroll
-    for (int i = 0; i < KMAX; ++i) {
-      const uint32_t idx = threadIdx.x + (uint32_t)i * NTH;
-      if (idx < n) A[padi<KMAX>(idx)] = tmp[i];
-    }
-    __syncthreads();
-#else
     count_sort<KMAX, NTH>(tmp, n, A, id_bits, cnt, wsum, flag);
-#endif
   }
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
@@ -2342,18 +2310,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) 
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int seg = v * T + blockIdx.y * gx + blockIdx.x;
-#ifdef SR_TIMING  // diagnostics (tools/wg_timing.py): per-workgroup start / end / size / placement
-  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef SR_PRIO
-  {
-    const int L = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
-    const int pr = min(L >> 8, 3);
-    if (pr == 1) __builtin_amdgcn_s_setprio(1);
-    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-    else if (pr == 3) __builtin_amdgcn_s_setprio(3);
-  }
-#endif
   uint32_t b, e;
   seg_bounds(seg_start, seg_count, stride, seg, b, e);
   const uint32_t n = e - b;
@@ -2399,16 +2355,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) 
   // counts handed back zeroed for the next call's binning (every thread read it before the
   // sort's first barrier)
   if (clear_counts && tid == 0) seg_count[seg] = 0u;
-#ifdef SR_TIMING
-  __syncthreads();
-  if (tid == 0) {
-    scratch[4 * seg] = t_start;
-    scratch[4 * seg + 1] = __builtin_amdgcn_s_memrealtime();
-    scratch[4 * seg + 2] = n;
-    scratch[4 * seg + 3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
-                           ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
-  }
-#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -2615,11 +2561,7 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
     for (int i = lane; i < cnt * 9; i += 64) {
       const float a = acc[i];
       const int k = i / 9;
-#ifdef BWD_DIAG_NOFLUSH
-      if (a == 12345.f)
-#else
       if (a != 0.f)
-#endif
         atomicAdd(&dgv[(size_t)list[k].id * GS + (i - k * 9)], a);
     }
     __builtin_amdgcn_wave_barrier();
@@ -2637,7 +2579,7 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
     float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D, int layout) {
   constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
-  extern __shared__ float lds[];  // NT * max(3 M, 9) floats: row staging
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // NT * max(3 M, 9) floats: row staging
   const int s = blockIdx.y;
   const int tid = threadIdx.x;
   const int g0 = blockIdx.x * NT;
@@ -2969,13 +2911,18 @@ int project_bin_impl(const char* who, int S, int G, int V, int H, int W, int sh_
   const int deg = shs ? sh_degree : -1;
 #define DSR_PB(D)                                                                                              \
   do {                                                                                                         \
-    if (ci)                                                                                                    \
-      k_project_emit<D, true><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities,   \
-                                                       cov6, cams, geom, radii, seg_count, keys, layout, *ci); \
+    if (ci && !(layout & kLayoutRectBinning))                                                                  \
+      k_project_emit<D, true, true><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,         \
+                                                             opacities, cov6, cams, geom, radii, seg_count,     \
+                                                             keys, layout, *ci);                                \
+    else if (ci)                                                                                               \
+      k_project_emit<D, true, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,        \
+                                                              opacities, cov6, cams, geom, radii, seg_count,    \
+                                                              keys, layout, *ci);                               \
     else                                                                                                       \
-      k_project_emit<D, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities,  \
-                                                        cov6, cams, geom, radii, seg_count, keys, layout,      \
-                                                        CamIn{});                                              \
+      k_project_emit<D, false, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,       \
+                                                               opacities, cov6, cams, geom, radii, seg_count,   \
+                                                               keys, layout, CamIn{});                          \
   } while (0)
   switch (deg) {
     case -1: DSR_PB(-1); break;
@@ -3115,6 +3062,35 @@ size_t dsr_bin_sort_workspace_size(int V, int H, int W, uint32_t max_count) {
   if (max_count <= kSortCap) return 0;
   const size_t nseg = (size_t)V * dsplat::tiles_x(W) * dsplat::tiles_y(H);
   return nseg * (size_t)split_groups(max_count) * 2 * sizeof(uint32_t);
+}
+
+int dsr_workspace_size(int G, int H, int W, int n_views, uint64_t key_budget, dsr_workspace* out) {
+  DSPLAT_REQUIRE(G > 0 && H > 0 && W > 0 && n_views > 0 && out, "dsr_workspace_size: bad arguments");
+  const uint64_t V = (uint64_t)n_views, T = (uint64_t)dsplat::tiles_x(W) * dsplat::tiles_y(H);
+  const uint64_t HW = (uint64_t)H * W;
+  dsr_workspace ws{};
+  ws.tiles = (int32_t)T;
+  ws.cams_bytes = V * sizeof(dsr_camera);
+  ws.geom_bytes = V * G * GS * 4;
+  ws.radii_bytes = V * G * 4;
+  ws.seg_count_bytes = V * T * 4;
+  ws.seg_start_bytes = (V * T + 1) * 4;
+  // the same test as the Python layer (raster.forward_raw): worst case V*T*G keys + as much
+  // scratch within the budget, tiles within the LDS histogram, offsets within 32 bits
+  const uint64_t worst = V * T * (uint64_t)G;
+  ws.fixed_capacity = (worst * 16 <= key_budget && T <= (uint64_t)kHistLdsMax && worst < (1ull << 32)) ? 1 : 0;
+  ws.keys_bytes = ws.fixed_capacity ? worst * 8 : 0;
+  ws.scratch_bytes = ws.keys_bytes;
+  ws.sort_ws_bytes = dsr_bin_sort_workspace_size(n_views, H, W, (uint32_t)G);
+  ws.color_bytes = V * 3 * HW * 4;
+  ws.final_T_bytes = V * HW * 4;
+  ws.n_contrib_bytes = V * HW * 4;
+  ws.dgeom_bytes = ws.geom_bytes;
+  ws.total_bytes = ws.cams_bytes + ws.geom_bytes + ws.radii_bytes + ws.seg_count_bytes + ws.seg_start_bytes +
+                   ws.keys_bytes + ws.scratch_bytes + ws.sort_ws_bytes + ws.color_bytes + ws.final_T_bytes +
+                   ws.n_contrib_bytes + ws.dgeom_bytes;
+  *out = ws;
+  return 0;
 }
 
 }  // extern "C"

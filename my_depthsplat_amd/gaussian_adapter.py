@@ -2,10 +2,13 @@
 gaussians.py (GaussianAdapterCfg, GaussianAdapter, RGB2SH, quaternion_to_matrix,
 build_covariance) plus the encoder glue of encoder_depthsplat.py:258-273.
 
-Same names, config fields, argument meaning and output shapes as the reference. The
-per-Gaussian math is batched torch on the device (it is elementwise and fuses poorly
-into the rasterizer, which consumes world-space Gaussians per SCENE, not per view);
-the fused HIP adapter kernel is SURVEY §8f rank 2 (next).
+Same names, config fields, argument meaning and output shapes as the reference. On the
+device, `GaussianAdapter.forward` runs the fused HIP kernel (dga_adapter_forward/backward:
+one launch per direction; adapter_hip.py) and `gaussians_from_head` the same kernel with the
+encoder glue fused in (dga_adapter_fwd/bwd). The torch composition below is what host
+tensors run: the fp32 reference the kernels are tested against (tests/test_adapter_gpu.py)
+and the synthetic-data builder for the CPU oracle. It is pinned by tests/golden/adapter.npz,
+recorded from the reference modules (identity rotations: e3nn is absent offline).
 """
 from __future__ import annotations
 
@@ -84,6 +87,16 @@ class GaussianAdapter(nn.Module):
 
     def forward(self, extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians, image_shape,
                 eps: float = 1e-8, point_cloud=None, input_images=None) -> AdapterGaussians:
+        if raw_gaussians.is_cuda:  # the fused HIP kernel (no torch fallback on the device)
+            from .adapter_hip import adapter_forward_hip
+            return adapter_forward_hip(self, extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians,
+                                       image_shape, eps, input_images)
+        return self.forward_torch(extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians,
+                                  image_shape, eps, point_cloud, input_images)
+
+    def forward_torch(self, extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians, image_shape,
+                      eps: float = 1e-8, point_cloud=None, input_images=None) -> AdapterGaussians:
+        """The reference's torch composition (host tensors; the kernels' fp32 reference)."""
         scales, rotations, sh = raw_gaussians.split((3, 4, 3 * self.d_sh), dim=-1)
         scales = torch.clamp(F.softplus(scales - 4.0), min=self.cfg.gaussian_scale_min,
                              max=self.cfg.gaussian_scale_max)
@@ -139,8 +152,8 @@ def gaussians_from_head_torch(head: torch.Tensor, depths: torch.Tensor, images: 
     pixel = 1 / torch.tensor((w, h), dtype=torch.float32, device=head.device)
     xy_ray = xy_ray + (raw[..., :2].sigmoid() - 0.5) * pixel   # [B, V, HW, 1, 2]
     e = lambda t: t[:, :, None, None, None]  # noqa: E731  "b v i j -> b v () () () i j"
-    out = adapter(e(extrinsics), e(intrinsics), xy_ray[..., None, :], depths, opac, raw[..., None, 2:], (h, w),
-                  input_images=images)
+    out = adapter.forward_torch(e(extrinsics), e(intrinsics), xy_ray[..., None, :], depths, opac, raw[..., None, 2:],
+                                (h, w), input_images=images)
     G = V * h * w
     return Gaussians(out.means.reshape(B, G, 3), out.covariances.reshape(B, G, 3, 3),
                      out.harmonics.reshape(B, G, 3, adapter.d_sh), out.opacities.reshape(B, G))

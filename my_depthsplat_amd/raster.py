@@ -150,6 +150,9 @@ class RasterState:
     seg_overflow: torch.Tensor | None = None  # [V*T(+1)] tiles re-sorted in full and re-rendered
     tile_count: torch.Tensor | None = None    # [V*T] all entries per tile (depth-cut mode: seg_count = ends)
     cams: torch.Tensor | None = None          # [V, 44] dsr_camera array the forward used
+    # inference fast path with exact binning: the lists hold only entries whose alpha >= 1/255
+    # ellipse reaches the tile, and n_contrib counts positions in those shorter lists
+    pruned_lists: bool = False
 
     @property
     def counts(self) -> torch.Tensor:
@@ -195,6 +198,15 @@ FUSED_MAX = 4096
 # inference fast path (cameras inside the binning kernel, self-zeroing counters); env
 # DSPLAT_INKERNEL_CAMERAS=0 keeps the separate camera launch (experiments)
 INKERNEL_CAMERAS = os.environ.get("DSPLAT_INKERNEL_CAMERAS", "1") != "0"
+# Binning of the inference fast path: exact (a (Gaussian, tile) pair is kept only when the
+# alpha >= 1/255 ellipse reaches the tile; same images, shorter lists) or the reference's
+# 3-sigma rects (DSR_LAYOUT_RECT_BINNING; bench.py reports both throughputs).
+EXACT_BINNING = os.environ.get("DSPLAT_EXACT_BINNING", "1") != "0"
+LAYOUT_RECT_BINNING = 8
+# Test hook (tests/test_fullsize_parity.py): the fast path also snapshots its per-tile counts
+# and writes its sorted keys back, so its lists can be compared with the oracle's. It adds a
+# copy and the key stores; the product never sets it.
+DEBUG_KEEP_FAST_LISTS = False
 SEG_ENDS = 0xFFFFFFFF  # DSR_SEG_ENDS
 _spec = {"max_count": 0}
 _inflight: list = []  # (pinned int32 counts, event) read-backs, consumed without blocking
@@ -219,9 +231,22 @@ def _note_counts(counts: torch.Tensor) -> None:
         _last["host_counts"] = (host, ev)
 
 
-def _key_capacity(V, G, T):
-    worst = V * G * T
-    return worst if worst * 16 <= KEY_BUDGET_BYTES else None
+_ws_cache: dict = {}
+
+
+def workspace(G: int, H: int, W: int, V: int) -> _lib.Workspace:
+    """dsr_workspace_size: the bytes of every buffer of one call sequence and whether the
+    sync-free fixed-capacity layout fits KEY_BUDGET_BYTES (the C ABI's own sizing rule)."""
+    key = (G, H, W, V, KEY_BUDGET_BYTES)
+    ws = _ws_cache.get(key)
+    if ws is None:
+        ws = _lib.Workspace()
+        _lib.check(_lib.load().dsr_workspace_size(G, H, W, V, KEY_BUDGET_BYTES, _lib.ctypes.byref(ws)),
+                   "dsr_workspace_size")
+        if len(_ws_cache) > 256:
+            _ws_cache.clear()
+        _ws_cache[key] = ws
+    return ws
 
 
 _index_cache: dict = {}
@@ -386,8 +411,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
     radii = torch.empty((V, G), dtype=torch.int32, device=dev)
     lds_cap = lib.dsr_sort_lds_capacity()
-    cap = _key_capacity(V, G, T)
-    fixed = cap is not None and T <= 32768 and V * T * G < (1 << 32)
+    fixed = bool(workspace(G, H, W, V).fixed_capacity)
     maxc_hint = _spec["max_count"] or lds_cap
     fused = fixed and FUSED_SORT_RENDER and maxc_hint <= FUSED_MAX
     # eager inference fast path: cameras set up inside the binning kernel, counters taken zeroed
@@ -398,6 +422,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     if fast:
         seg_count = clean
         layout |= LAYOUT_COUNTS_ZEROED
+        if not EXACT_BINNING:
+            layout |= LAYOUT_RECT_BINNING
         cams = torch.empty((V, CAM_FLOATS), dtype=torch.float32, device=dev)
     elif zeroed_counts is not None:  # zeroed by dsr_build_cameras (one launch fewer)
         assert zeroed_counts.numel() == V * T and zeroed_counts.dtype == torch.int32
@@ -495,13 +521,17 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
     outs = (color.data_ptr(), final_T.data_ptr(), n_contrib.data_ptr(), st)
     if fused:  # sort + composite in one launch; sorted keys kept only when a backward needs them
+        snap = seg_count.clone() if (fast and DEBUG_KEEP_FAST_LISTS) else None
         _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(), None,
-                          seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(), int(bool(need_state)),
-                          int(fast), *outs), "dsr_sort_render")
+                          seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(),
+                          int(bool(need_state) or snap is not None), int(fast), *outs), "dsr_sort_render")
         state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, cams=cams)
         if fast:  # the counters are zero again once the launch above has run
             _give_back_clean_counts(seg_count, dev, st)
-            state.seg_count = None  # consumed (no backward in this mode)
+            # consumed (no backward in this mode); with exact binning n_contrib counts positions
+            # in the pruned lists (a subsequence of the reference's), not in the 3-sigma lists
+            state.seg_count = snap
+            state.pruned_lists = not (layout & LAYOUT_RECT_BINNING)
         _last["counts"] = None if fast else state.counts
         return color, state
     overflow = None

@@ -250,12 +250,60 @@ def gen_adapter():
     np.savez_compressed(OUT / "adapter.npz", **{k: t2n(v) for k, v in out.items()})
 
 
+def _candidate_block():
+    """The depth-candidate lines of MultiViewUniMatch.forward (mv_unimatch.py:416-475), read
+    from the reference source at generation time and run as they stand: the class itself
+    cannot be built offline (its __init__ fetches DINOv2 through torch.hub)."""
+    src = (REF / "src/model/encoder/unimatch/mv_unimatch.py").read_text().splitlines()
+    a = next(i for i, ln in enumerate(src) if "num_depth_candidates = self.num_depth_candidates // (4**scale_idx)" in ln)
+    b = next(i for i in range(a, len(src)) if "intrinsics_input = torch.stack(intrinsics_curr" in src[i])
+    import textwrap
+    return compile(textwrap.dedent("\n".join(src[a:b])), "mv_unimatch.py:depth-candidates", "exec")
+
+
+def gen_matching():
+    """batch_features_camera_parameters with an nn_matrix (mv_transformer.py:653-747) and the
+    per-scale depth candidates (mv_unimatch.py:416-475) -> matching.npz."""
+    mvt = importlib.import_module("src.model.encoder.unimatch.mv_transformer")
+    g = torch.Generator().manual_seed(3)
+    out = {}
+    B, V, C, H, W = 2, 4, 4, 3, 5
+    feats = [torch.randn(B, C, H, W, generator=g) for _ in range(V)]
+    intr = [torch.rand(B, 3, 3, generator=g) for _ in range(V)]
+    extr = [torch.randn(B, 4, 4, generator=g) for _ in range(V)]
+    nn = torch.stack([torch.stack([torch.tensor([i] + [(i + k) % V for k in (1, 3)]) for i in range(V)]),
+                      torch.stack([torch.tensor([i] + [(i + k) % V for k in (2, 1)]) for i in range(V)])])
+    res = mvt.batch_features_camera_parameters(feats, intr, extr, nn_matrix=nn)
+    out.update({"nn_feats": torch.stack(feats, 1), "nn_intr": torch.stack(intr, 1), "nn_extr": torch.stack(extr, 1),
+                "nn_matrix": nn})
+    for k, t in zip(("ref", "ref_k", "ref_e", "tgt", "tgt_k", "tgt_e"), res):
+        out[f"nn_{k}"] = t
+    code = _candidate_block()
+    BV, J, h, w, D = 3, 2, 4, 6, 128
+    min_depth = 1.0 / (5 + 5 * torch.rand(BV, generator=g))   # inverse depths, as the caller passes
+    max_depth = 1.0 / (0.2 + 0.5 * torch.rand(BV, generator=g))
+    for s in (0, 1, 2):
+        depth = min_depth.view(-1, 1, 1, 1) + torch.rand(BV, 1, h, w, generator=g) * (max_depth - min_depth).view(-1, 1, 1, 1)
+        self = types.SimpleNamespace(num_depth_candidates=D)
+        env = {"torch": torch, "self": self, "scale_idx": s, "min_depth": min_depth, "max_depth": max_depth,
+               "depth": depth, "features_list_cnn": [torch.zeros(1)], "tgt_features": torch.zeros(BV, J, 1, h, w),
+               "h": h, "w": w}
+        exec(code, env)
+        out[f"cand{s}_depth"] = depth
+        out[f"cand{s}_candidates"] = env["depth_candidates"]
+        out[f"cand{s}_candidates_curr"] = env["depth_candidates_curr"]
+    out["cand_min"], out["cand_max"] = min_depth, max_depth
+    np.savez_compressed(OUT / "matching.npz", **{k: t2n(v) for k, v in out.items()})
+
+
 if __name__ == "__main__":
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     setup_imports()
     torch.set_default_dtype(torch.float32)
-    gen_cuda_splatting()
-    gen_cost_volume()
-    gen_adapter()
+    only = sys.argv[1:]  # e.g. `make_golden.py matching` regenerates one fixture file
+    for name, fn in (("cuda_splatting", gen_cuda_splatting), ("cost_volume", gen_cost_volume),
+                     ("adapter", gen_adapter), ("matching", gen_matching)):
+        if not only or name in only:
+            fn()
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)

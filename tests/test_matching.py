@@ -1,0 +1,78 @@
+"""Cost-volume plumbing vs fixtures recorded from the reference (CPU):
+batch_features_camera_parameters (mv_transformer.py:653-747), with and without an nn_matrix,
+the relative pose (mv_unimatch.py:405-407) and the depth candidates of every scale
+(mv_unimatch.py:416-475; tests/golden/matching.npz runs that block of the reference)."""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from my_depthsplat_amd.matching import batch_features_camera_parameters, depth_candidates
+
+GOLD = Path(__file__).parent / "golden"
+CV = np.load(GOLD / "cost_volume.npz")
+MT = np.load(GOLD / "matching.npz")
+
+
+@pytest.mark.parametrize("tag", ["s0", "s1"])
+def test_batch_features_all_other_views(tag):
+    """Every view as reference, all others as sources; relative pose tgt_c2w^-1 ref_c2w."""
+    feats = torch.from_numpy(CV[f"{tag}_feats"])    # [B, V, C, H, W]
+    extr = torch.from_numpy(CV[f"{tag}_extr"])      # [B, V, 4, 4]
+    B, V, C, H, W = feats.shape
+    K = torch.tensor([[W * 0.9, 0, W / 2], [0, H * 0.9, H / 2], [0, 0, 1.0]])
+    ref, ref_k, ref_e, tgt, tgt_k, tgt_e = batch_features_camera_parameters(
+        list(feats.unbind(1)), [K.expand(B, 3, 3).clone() for _ in range(V)], list(extr.unbind(1)))
+    np.testing.assert_array_equal(ref.numpy(), CV[f"{tag}_ref"])
+    np.testing.assert_array_equal(tgt.numpy(), CV[f"{tag}_tgt"])
+    np.testing.assert_array_equal(ref_k.numpy(), CV[f"{tag}_intr"])
+    pose = torch.matmul(tgt_e.inverse(), ref_e.unsqueeze(1))
+    np.testing.assert_allclose(pose.numpy(), CV[f"{tag}_pose"], rtol=1e-6, atol=1e-7)
+    assert tgt_k.shape == (B * V, V - 1, 3, 3)
+
+
+def test_batch_features_nn_matrix():
+    """Source views picked by an nn_matrix (gather path), all six outputs."""
+    feats = list(torch.from_numpy(MT["nn_feats"]).unbind(1))
+    intr = list(torch.from_numpy(MT["nn_intr"]).unbind(1))
+    extr = list(torch.from_numpy(MT["nn_extr"]).unbind(1))
+    out = batch_features_camera_parameters(feats, intr, extr, nn_matrix=torch.from_numpy(MT["nn_matrix"]))
+    for k, t in zip(("ref", "ref_k", "ref_e", "tgt", "tgt_k", "tgt_e"), out):
+        np.testing.assert_array_equal(t.numpy(), MT[f"nn_{k}"], err_msg=k)
+
+
+def test_batch_features_no_batch_lists():
+    feats = list(torch.from_numpy(MT["nn_feats"]).unbind(1))
+    intr = list(torch.from_numpy(MT["nn_intr"]).unbind(1))
+    extr = list(torch.from_numpy(MT["nn_extr"]).unbind(1))
+    q, qk, qe, kv, kvk, kve = batch_features_camera_parameters(feats, intr, extr, no_batch=True)
+    assert len(q) == len(kv) == 4 and kv[0].shape[1] == 3
+    assert torch.equal(kv[2][:, 0], feats[0]) and torch.equal(kv[2][:, 2], feats[3])
+
+
+@pytest.mark.parametrize("scale", [0, 1, 2])
+def test_depth_candidates_vs_reference(scale):
+    """Inverse-depth hypotheses: scale 0 a per-image linspace of 128; scale s a per-pixel
+    window of 128 / 4^s around the previous scale's depth, clamped to [min, max]. Also the
+    [BV*(V-1), D, H, W] layout the warp receives (the reference repeats per source view)."""
+    mn, mx = torch.from_numpy(MT["cand_min"]), torch.from_numpy(MT["cand_max"])
+    depth = torch.from_numpy(MT[f"cand{scale}_depth"])
+    cand = depth_candidates(mn, mx, 128, scale, None if scale == 0 else depth)
+    want = MT[f"cand{scale}_candidates"]
+    np.testing.assert_allclose(cand.numpy(), want, rtol=1e-6, atol=1e-7)
+    curr = MT[f"cand{scale}_candidates_curr"]
+    J, (h, w) = curr.shape[0] // cand.shape[0], depth.shape[-2:]
+    rep = cand.unsqueeze(1).expand(cand.shape[0], J, cand.shape[1], h, w).reshape(-1, cand.shape[1], h, w)
+    np.testing.assert_allclose(rep.numpy(), curr, rtol=1e-6, atol=1e-7)
+
+
+def test_depth_candidates_scale0_match_cost_volume_fixture():
+    """The s0 cost-volume fixture's depths are 1 / (linspace of inverse depths)."""
+    BV, D = CV["s0_depth"].shape[:2]
+    inv_min, inv_max = torch.full((BV,), 1 / 10.0), torch.full((BV,), 1 / 0.5)
+    cand = depth_candidates(inv_min, inv_max, D, 0)
+    np.testing.assert_allclose((1.0 / cand).expand(BV, D, *CV["s0_depth"].shape[2:]).numpy(), CV["s0_depth"],
+                               rtol=1e-6)

@@ -64,3 +64,84 @@ def test_allreduce_gradients_gloo_world2():
     assert (e0 == 0.5).all() and (e1 == 0.5).all()
     assert n0 == n1 == (15 + 3 + 4) * 4
     assert t0 == t1 == 2.0
+
+
+# ---------------------------------------------------------------- the data-parallel training step
+
+def _dense_render(gs, ext, K, near, far, image_shape):
+    """Decoder-signature renderer on the dense torch restatement (tests/dense_raster.py):
+    the per-scene Gaussians seen from each target view, reference camera set-up."""
+    from dense_raster import render
+
+    from my_depthsplat_amd.cuda_splatting import _cov6, camera_settings
+    B, v = ext.shape[:2]
+    H, W = image_shape
+    out = []
+    for b in range(B):
+        st = camera_settings(ext[b], K[b], near[b], far[b])
+        views = []
+        for j in range(v):
+            s = st["scale"][j]
+            views.append(render(gs.means[b] * s, gs.harmonics[b].transpose(-1, -2), gs.opacities[b],
+                                _cov6(gs.covariances[b]) * s * s, st["viewmatrix"][j].reshape(-1),
+                                st["projmatrix"][j].reshape(-1), st["campos"][j], float(st["tanfovx"][j]),
+                                float(st["tanfovy"][j]), torch.zeros(3), H, W))
+        out.append(torch.stack(views))
+    return torch.stack(out)
+
+
+def _train_setup(seed_batch=5):
+    from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg
+    from my_depthsplat_amd.training import GaussianHead, synthetic_batch
+    adapter = GaussianAdapter(GaussianAdapterCfg(1e-10, 3.0, 1))
+    torch.manual_seed(0)  # identical head initialisation on every rank
+    head = GaussianHead(3 + adapter.d_in, width=8, down=4)
+    batch = synthetic_batch(4, 2, 1, 16, 16, seed=seed_batch)
+    return adapter, head, batch
+
+
+def _train_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from my_depthsplat_amd.training import TrainStep, rank_batch, torch_l1_mse
+    adapter, head, batch = _train_setup()
+    mine = rank_batch(batch, rank, world)
+    step = TrainStep(head, adapter, _dense_render, torch_l1_mse, lr=1e-3, world=world)
+    loss = step.forward_backward(mine)
+    nbytes = allreduce_gradients(list(head.parameters()), world)
+    grads = [p.grad.clone().numpy() for p in head.parameters()]
+    step.opt.zero_grad(set_to_none=True)
+    step(mine)  # full step: all-reduce, clip, AdamW
+    params = [p.detach().clone().numpy() for p in head.parameters()]
+    q.put((rank, mine.n_scenes, float(loss), grads, params, nbytes))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_training_step_gloo_world2_matches_full_batch():
+    """world 2 (gloo): each rank takes its half of a 4-scene batch (parallel.shard), runs head
+    -> adapter -> dense rasterizer -> loss -> backward and ONE bucketed all-reduce. The
+    averaged gradient equals the single-process gradient of the whole batch, and after the
+    optimizer step both ranks hold identical parameters."""
+    from my_depthsplat_amd.training import TrainStep, torch_l1_mse
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, n0, l0, g0, p0, b0), (_, n1, l1, g1, p1, b1) = res
+    assert n0 == n1 == 2
+    adapter, head, batch = _train_setup()
+    assert b0 == b1 == 4 * sum(p.numel() for p in head.parameters())
+    TrainStep(head, adapter, _dense_render, torch_l1_mse, world=1).forward_backward(batch)
+    for a, b, ref in zip(g0, g1, [p.grad.numpy() for p in head.parameters()]):
+        assert abs(a - b).max() == 0
+        assert abs(a - ref).max() <= 1e-4 * (abs(ref).max() + 1e-12) + 1e-7
+    for a, b in zip(p0, p1):
+        assert (a == b).all()
+    assert abs((l0 + l1) / 2) > 0
