@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--context", type=int, default=2)
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU-baseline sample per thread count")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-reference-binning", action="store_true",
+                   help="skip the 3-sigma-binning timed region (profiling passes: one kernel variant per name)")
     p.add_argument("--eager", action="store_true", help="time eager launches only (no hipGraph capture)")
     p.add_argument("--launch", choices=["auto", "hipgraph", "eager"] + [f"hipgraph{n}" for n in range(2, 9)], default="auto",
                    help="launch mode of the timed region (auto: the fastest in a short calibration of all)")
@@ -174,14 +176,18 @@ def main():
     # reference's lists give on the same kernels
     raster.EXACT_BINNING = False
     runner_ref, graphs_ref = step, []
+    elapsed_ref, n_rendered_ref = float("nan"), None
     try:
-        if not args.eager:
+        if args.no_reference_binning:
+            pass
+        elif not args.eager:
             modes_ref, graphs_ref = build_modes()
             runner_ref = modes_ref[mode]
-        elapsed_ref = timed(runner_ref, args.steps)
-        step()
-        torch.cuda.synchronize()
-        n_rendered_ref = raster.last_stats()["num_rendered"]
+        if not args.no_reference_binning:
+            elapsed_ref = timed(runner_ref, args.steps)
+            step()
+            torch.cuda.synchronize()
+            n_rendered_ref = raster.last_stats()["num_rendered"]
         if graphs_ref:
             assert torch.equal(graphs_ref[0].out.color, graphs[0].out.color), "binning modes disagree"
     finally:
@@ -239,7 +245,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
             "launch_mode": mode, "launch_calibration_ms_per_step": cal,
             "ms_per_step_eager": round(1e3 * elapsed_eager / args.steps, 4),
-            "reference_binning": {"value": round(total_views / elapsed_ref, 2), "unit": "views/s",
+            "reference_binning": None if args.no_reference_binning else {
+                                  "value": round(total_views / elapsed_ref, 2), "unit": "views/s",
                                   "ms_per_step": round(1e3 * elapsed_ref / args.steps, 4),
                                   "num_rendered_per_step": n_rendered_ref,
                                   "note": "same kernels and launch mode, the reference's 3-sigma tile lists "

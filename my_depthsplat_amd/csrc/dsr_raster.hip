@@ -1513,12 +1513,25 @@ __device__ void reg_sort(uint64_t* A, uint32_t n, int id_bits, uint16_t* cnt, ui
 // itself inside its bin. With ~3K keys over 4096 bins most bins hold 0-2 keys: 6 barriers
 // and no serial insertion chains (the LSD passes + fix_runs took 35 us per launch at 2x256^2,
 // 21 of them in fix_runs). The keys come in registers (thread t holds keys t + i NTH).
+// Bin-pair word w of the counting sort lives at LDS word bin_word<R>(w): each thread's scan
+// row of R words is read / written as R/4 16-byte chunks (ds_read_b128 / ds_write_b128) and
+// the chunks are XOR-rotated by (thread / 4) mod (R/4), so the 16 lanes of one b128 lane
+// group touch 16 different 4-bank slots. Unswizzled, rows of 16 words at a 64-byte lane
+// stride put 4 lanes of a group on each slot (4-way conflicts in every scan access).
+template <int R>
+__device__ __forceinline__ uint32_t bin_word(uint32_t w) {
+  static_assert(R >= 4 && (R & (R - 1)) == 0, "rows of whole 16-byte chunks");
+  constexpr int RL = R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : R == 32 ? 5 : 6;
+  return w ^ ((((w >> RL) >> 2) & (uint32_t)(R / 4 - 1)) << 2);
+}
+
 template <int KMAX, int NTH = NT>
 __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A, int id_bits, uint16_t* cnt,
                            uint32_t* wsum, uint32_t* flag) {
   constexpr int NBIN = 1 << SORT_NBIN_LOG2, BPT = NBIN / NTH;  // bins per thread in the scan
-  static_assert(BPT % 2 == 0 && NTH * KMAX < 65536 && NBIN / 2 <= sort_cnt_words<NTH>(), "u16 bin pairs in cnt");
-  uint32_t* hw = reinterpret_cast<uint32_t*>(cnt);  // NBIN / 2 words (cnt holds NTH * 16 u16)
+  constexpr int R = BPT / 2;                                    // scan row: bin-pair words per thread
+  static_assert(BPT % 8 == 0 && NTH * KMAX < 65536 && NBIN / 2 <= sort_cnt_words<NTH>(), "u16 bin pairs in cnt");
+  uint32_t* hw = reinterpret_cast<uint32_t*>(cnt);  // NBIN / 2 words (cnt holds NTH * 16 u16), 16-B aligned
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t mn = 0xffffffffu, mx = 0u;
 #pragma unroll
@@ -1528,7 +1541,10 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
       mn = min(mn, d);
       mx = max(mx, d);
     }
-  for (int k = tid; k < NBIN / 2; k += NTH) hw[k] = 0u;
+  {
+    uint4* h4 = reinterpret_cast<uint4*>(hw);
+    for (int k = tid; k < NBIN / 8; k += NTH) h4[k] = make_uint4(0u, 0u, 0u, 0u);
+  }
   block_minmax<NTH>(mn, mx, flag);
   const uint32_t range = mx - mn;
   const int shift = max(0, (range ? 31 - __clz(range) : 0) - (SORT_NBIN_LOG2 - 1));
@@ -1536,27 +1552,36 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
   for (int i = 0; i < KMAX; ++i)
     if (tid + (uint32_t)i * NTH < n) {
       const uint32_t bin = ((uint32_t)(tmp[i] >> 32) - mn) >> shift;
-      atomicAdd(&hw[bin >> 1], 1u << ((bin & 1u) * 16u));
+      atomicAdd(&hw[bin_word<R>(bin >> 1)], 1u << ((bin & 1u) * 16u));
     }
   __syncthreads();
   {
-    uint32_t wd[BPT / 2], tot = 0;
+    uint4* row = reinterpret_cast<uint4*>(hw) + tid * (R / 4);
+    const int rot = (tid >> 2) & (R / 4 - 1);
+    uint32_t wd[R], tot = 0;
 #pragma unroll
-    for (int q = 0; q < BPT / 2; ++q) {
-      wd[q] = hw[tid * (BPT / 2) + q];
-      tot += (wd[q] & 0xFFFFu) + (wd[q] >> 16);
+    for (int c = 0; c < R / 4; ++c) {
+      const uint4 x = row[c ^ rot];
+      wd[4 * c] = x.x;
+      wd[4 * c + 1] = x.y;
+      wd[4 * c + 2] = x.z;
+      wd[4 * c + 3] = x.w;
     }
+#pragma unroll
+    for (int q = 0; q < R; ++q) tot += (wd[q] & 0xFFFFu) + (wd[q] >> 16);
     const uint32_t incl = dsplat::wave_incl_add_dpp(tot);
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
     uint32_t off = incl - tot;
     for (int k = 0; k < w; ++k) off += wsum[k];
 #pragma unroll
-    for (int q = 0; q < BPT / 2; ++q) {
+    for (int q = 0; q < R; ++q) {
       const uint32_t lo = wd[q] & 0xFFFFu, hi = wd[q] >> 16;
-      hw[tid * (BPT / 2) + q] = off | ((off + lo) << 16);
+      wd[q] = off | ((off + lo) << 16);
       off += lo + hi;
     }
+#pragma unroll
+    for (int c = 0; c < R / 4; ++c) row[c ^ rot] = make_uint4(wd[4 * c], wd[4 * c + 1], wd[4 * c + 2], wd[4 * c + 3]);
   }
   __syncthreads();
 #pragma unroll
@@ -1564,7 +1589,7 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
     if (tid + (uint32_t)i * NTH < n) {
       const uint32_t bin = ((uint32_t)(tmp[i] >> 32) - mn) >> shift;
       const uint32_t s16 = (bin & 1u) * 16u;
-      const uint32_t pos = (atomicAdd(&hw[bin >> 1], 1u << s16) >> s16) & 0xFFFFu;
+      const uint32_t pos = (atomicAdd(&hw[bin_word<R>(bin >> 1)], 1u << s16) >> s16) & 0xFFFFu;
       A[padi<KMAX>(pos)] = tmp[i];
     }
   __syncthreads();
@@ -1577,7 +1602,7 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
 #endif
   constexpr uint32_t kBinMax = SORT_BINMAX;
   auto bin_end = [&](uint32_t b) -> uint32_t {
-    const uint32_t wv = hw[b >> 1];
+    const uint32_t wv = hw[bin_word<R>(b >> 1)];
     return (b & 1u) ? (wv >> 16) : (wv & 0xFFFFu);
   };
   uint32_t dest[KMAX];

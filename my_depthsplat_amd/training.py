@@ -14,7 +14,8 @@ AdamW (model_wrapper.py:1104-1158). This module is that step, MI355X-first:
 The dense network in front of the adapter (PromptDA / DINOv2 / DPT; frozen in this fork,
 promptda.py:66-73) is out of scope. `GaussianHead` stands in for the trainable Gaussian
 regressor + head (encoder_depthsplat.py:96-122) with the vitb head's parameter count
-(~0.77 M: a 3.1 MB gradient bucket), so the all-reduce moves what the reference's would.
+(0.77 M at d_out = 37: a 3.1 MB gradient bucket), so the all-reduce moves what the
+reference's would.
 The renderer and the loss are arguments, so tests can swap the HIP rasterizer for a dense
 torch one (tests/test_parallel.py).
 """
@@ -35,7 +36,7 @@ class GaussianHead(nn.Module):
     per-pixel head channels [B, V, H*W, d_out] (d_out = 1 opacity + 2 offsets + adapter.d_in).
     Works at 1/`down` resolution and pixel-shuffles back to full resolution."""
 
-    def __init__(self, d_out: int, width: int = 160, down: int = 8):
+    def __init__(self, d_out: int, width: int = 108, down: int = 8):
         super().__init__()
         self.down = down
         self.d_out = d_out

@@ -57,10 +57,13 @@ def timeit(fn, n=20):
     return a.elapsed_time(b) / n
 
 
+SHAPES = {"a": (2, 1, 128, 32, 32, 128, False, "config A (2v, 32^2, C128, D128)"),
+          "b0": (2, 1, 128, 64, 64, 128, False, "config B scale 0 (2v, 64^2, C128, D128)"),
+          "b1": (2, 1, 64, 128, 128, 32, True, "config B scale 1 (per-pixel D32)"),
+          "d0": (6, 2, 128, 56, 96, 128, False, "config D scale 0 (6v, 2 nbrs, 56x96)")}
 dev = torch.device("cuda:0")
-for (B, J, C, H, W, D, pp, name) in [(2, 1, 128, 64, 64, 128, False, "config B scale 0 (2v, 64^2, C128, D128)"),
-                                     (2, 1, 64, 128, 128, 32, True, "config B scale 1 (per-pixel D32)"),
-                                     (6, 2, 128, 56, 96, 128, False, "config D scale 0 (6v, 2 nbrs, 56x96)")]:
+pick = sys.argv[1:] or ["b0", "b1", "d0"]  # e.g. `python tools/cv_bench.py a` (one shape per profile pass)
+for (B, J, C, H, W, D, pp, name) in [SHAPES[k] for k in pick]:
     ref, tgt, K, pose, depth = case(B, J, C, H, W, D, pp, dev)
     hip = plane_sweep_cost_volume(ref, tgt, K, pose, depth)
     tr = torch_cost(ref, tgt, K, pose, depth)
