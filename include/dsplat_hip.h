@@ -274,7 +274,12 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
  * projection of pixel (x,y) at depth[b,d,y,x] through K[b,j] and pose[b,j].
  *   ref [B,C,H,W]  tgt [B,J,C,H,W]  intr [B,J,3,3] (pixel units)  pose [B,J,4,4]
  *   depth [B,D,H,W] when depth_per_pixel else [B,D]   ->   cost [B,D,H,W]
- * tgt_hwc: workspace [B,J,H,W,C] (filled here: channel-last copy of tgt).          */
+ * C in {16, 32, 64, 128}: one workgroup per (16 reference pixels of a row, 64 depths)
+ * correlates its pixels with the bounding box of the target pixels its samples tap as one
+ * GEMM on the matrix cores (v_mfma_f32_16x16x4_f32, exact f32), reading ref and tgt in
+ * their given layouts. tgt_hwc: workspace [B,J,H,W,C]; NULL allowed for those C (filled
+ * with the channel-last copy of tgt when given: dcv_cost_volume_bwd reads it); required
+ * for other C. */
 int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel,
                         const float* ref, const float* tgt, const float* intr, const float* pose,
                         const float* depth, float clamp_min_depth, float* tgt_hwc, float* cost,

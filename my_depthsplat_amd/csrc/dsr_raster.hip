@@ -99,6 +99,21 @@ __device__ __forceinline__ bool xcd_item(int blocks_per_view, int V, int& v, int
 __host__ __device__ constexpr unsigned xcd_grid(int blocks_per_view, int V) {
   return 8u * (unsigned)((blocks_per_view * V + 7) / 8);
 }
+// Placement that keeps the views of one Gaussian block together instead: the items are
+// (major, minor) pairs in major-major order (major = Gaussian block, minor = view), cut into 8
+// contiguous per-XCD ranges as above. The V views of a block then run in consecutive slots
+// of one XCD and read the block's 148 B per Gaussian from HBM once, from that XCD's L2 after
+// (project / preprocess kernels; k_project_emit at config B: 95 -> 54 MB of HBM traffic per
+// launch). Same grid size as xcd_grid(n_major, n_minor).
+__device__ __forceinline__ bool xcd_pair(int n_major, int n_minor, int& major, int& minor) {
+  const int items = n_major * n_minor;
+  const int per = (items + 7) >> 3;
+  const int item = (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
+  if ((int)(blockIdx.x >> 3) >= per || item >= items) return false;
+  major = item / n_minor;
+  minor = item - major * n_minor;
+  return true;
+}
 
 struct WaveRects {
   uint32_t ex[64];    // exclusive scan of areas
@@ -590,7 +605,7 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
                                                    uint32_t* __restrict__ seg_count, int lds_hist, int layout) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
   int v, blk;
-  if (!xcd_item((G + NT - 1) / NT, V, v, blk)) return;
+  if (!xcd_pair((G + NT - 1) / NT, V, blk, v)) return;
   const int T = gx * gy;
   const int tid = threadIdx.x;
   const dsr_camera* cam = cams + v;
@@ -702,7 +717,7 @@ __device__ __forceinline__ void tile_rect_alpha(const TileEll& e, int& x0, int& 
 // range per touched tile with one global atomic, and writes the (depth, id) keys into
 // segment (v, t), which starts at (v*T + t) * G (a Gaussian touches a tile at most once, so
 // G slots suffice). No global scan is needed before the keys exist. The V workgroups of one
-// Gaussian block run back to back on one XCD (xcd_item_views), so the scene's 148 B per
+// Gaussian block run back to back on one XCD (xcd_pair), so the scene's 148 B per
 // Gaussian come from HBM once and from that XCD's L2 for the other views (one workgroup per
 // scene looping over its views would hold 3x fewer waves in flight to hide the load and
 // atomic latencies).
@@ -713,19 +728,6 @@ __device__ __forceinline__ void tile_rect_alpha(const TileEll& e, int& x0, int& 
 #ifndef PE_CAPW
 #define PE_CAPW 768
 #endif
-// Workgroup -> (view, block) placement for k_project_emit: the items are (block, view) in
-// block-major order, cut into 8 contiguous ranges, one per XCD (dispatch is round-robin over
-// the XCDs: workgroup i runs on XCD i % 8). A block's V views then sit in consecutive slots
-// of one XCD and re-read the block's inputs from its L2.
-__device__ __forceinline__ bool xcd_item_views(int blocks_per_view, int V, int& v, int& blk) {
-  const int items = blocks_per_view * V;
-  const int per = (items + 7) >> 3;
-  const int item = (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
-  if ((int)(blockIdx.x >> 3) >= per || item >= items) return false;
-  blk = item / V;
-  v = item - blk * V;
-  return true;
-}
 // EXACT (inference binning, CAM only): a pair is kept only when tile_reach says the
 // alpha >= 1/255 ellipse reaches the tile; the stateful / training path keeps the reference's
 // rect lists, which the backward and the oracle list tests follow.
@@ -748,7 +750,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
   __shared__ uint32_t s_pairs[NT / 64][PE_CAPW];
   __shared__ uint32_t s_ovf;
   int v, blk;
-  if (!xcd_item_views((G + NT - 1) / NT, V, v, blk)) return;
+  if (!xcd_pair((G + NT - 1) / NT, V, blk, v)) return;
   const dsr_camera* cam = cams + v;
   const int T = gx * gy;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1048,7 +1050,10 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
   const int gxp = gx + 1, gyp = gy + 1;
   uint32_t* s_dif = s_mem;  // [gyp][gxp] difference grid of the tile rects
   uint32_t* s_dh = s_mem + gxp * gyp;
-  const int v = blockIdx.x / per_view, p = blockIdx.x - v * per_view;
+  // (run p, view v): the V workgroups of run p sit on one XCD (xcd_pair) and walk the same
+  // blocks, so each block's inputs come from HBM once and from L2 for the other views
+  int v, p;
+  if (!xcd_pair(per_view, V, p, v)) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int k = tid; k < gxp * gyp + nsb * kCutBuckets; k += NTH) s_mem[k] = 0u;
   __syncthreads();
@@ -3043,7 +3048,7 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, 
         return e;                                                                                            \
       attr = true;                                                                                           \
     }                                                                                                        \
-    k_preprocess_cut<D, kNTH><<<(unsigned)(V * per_view), kNTH, lds, st>>>(                                  \
+    k_preprocess_cut<D, kNTH><<<xcd_grid(per_view, V), kNTH, lds, st>>>(                                     \
         G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, geom, radii, seg_count, depth_hist, \
         per_view, layout);                                                                                   \
   } while (0)

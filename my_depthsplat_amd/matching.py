@@ -77,11 +77,14 @@ class _CostVolume(torch.autograd.Function):
         D = depth.shape[1]
         dev = ref.device
         st = _lib.stream_of(dev)
-        tgt_hwc = torch.empty((B, J, H, W, C), dtype=torch.float32, device=dev)
+        # the channel-last copy of the targets is only made for the backward (and for channel
+        # counts the band kernel does not take); inference reads [B,J,C,H,W] directly
+        need_hwc = ctx.needs_input_grad[0] or ctx.needs_input_grad[1] or C not in (16, 32, 64, 128)
+        tgt_hwc = torch.empty((B, J, H, W, C), dtype=torch.float32, device=dev) if need_hwc else None
         cost = torch.empty((B, D, H, W), dtype=torch.float32, device=dev)
         _lib.check(lib.dcv_cost_volume_fwd(B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), tgt.data_ptr(),
                                            intrinsics.data_ptr(), pose.data_ptr(), depth.data_ptr(), clamp,
-                                           tgt_hwc.data_ptr(), cost.data_ptr(), st), "dcv_cost_volume_fwd")
+                                           _lib.ptr(tgt_hwc), cost.data_ptr(), st), "dcv_cost_volume_fwd")
         ctx.save_for_backward(ref, tgt_hwc, intrinsics, pose, depth)
         ctx.meta = (B, J, C, H, W, D, per_pixel, clamp)
         return cost
