@@ -649,7 +649,8 @@ __global__ __launch_bounds__(256) void k_cost_mfma_bwd(int J, int C, int H, int 
 constexpr int BTP = 16;                       // reference pixels per workgroup
 constexpr int BDCH = 64;                      // depth hypotheses per workgroup
 constexpr int BSPT = BTP * BDCH / 256;        // samples per thread
-constexpr int kBandMax = 1024;                // box pixels whose correlations fit in LDS
+constexpr int kBandMax = 512;                 // box pixels whose correlations fit in LDS (33 KB:
+                                              // 4 workgroups per CU, all of config B's in one round)
 constexpr int kCorrStride = kBandMax + 1;     // odd row stride: the gather's lanes spread over banks
 
 __device__ __forceinline__ int wave_min_i(int v) {
@@ -776,12 +777,17 @@ __global__ __launch_bounds__(256) void k_cost_band(int J, int H, int W, int D, i
           const float* bp = tg + (size_t)(lane >> 4) * HW + (q < 0 ? 0 : q);
 #pragma unroll
           for (int s = 0; s < NK; ++s) bv[s] = q >= 0 ? bp[(size_t)4 * s * HW] : 0.f;
-          f32x4 c4 = {0.f, 0.f, 0.f, 0.f};
+          // four independent accumulation chains (a dependent v_mfma_f32_16x16x4f32 waits ~40
+          // cycles for its accumulator), summed at the end
+          f32x4 c4[4];
 #pragma unroll
-          for (int s = 0; s < NK; ++s) c4 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bv[s], c4, 0, 0, 0);
+          for (int k = 0; k < 4; ++k) c4[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < NK; ++s) c4[s & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bv[s], c4[s & 3], 0, 0, 0);
+          c4[0] = (c4[0] + c4[1]) + (c4[2] + c4[3]);
           // D[row][col]: col = lane & 15 (box pixel u), row = 4 (lane >> 4) + r (reference pixel)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s_corr[(4 * (lane >> 4) + r) * kCorrStride + u] = c4[r];
+          for (int r = 0; r < 4; ++r) s_corr[(4 * (lane >> 4) + r) * kCorrStride + u] = c4[0][r];
         }
         __syncthreads();
         const float* crow = s_corr + i * kCorrStride;
