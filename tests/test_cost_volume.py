@@ -34,11 +34,13 @@ def test_oracle_matches_reference(tag):
     ref, tgt, K, pose, depth = case(tag)
     BV, J = tgt.shape[:2]
     cost = ocv.cost_volume(ref, tgt, K, pose, depth)
-    rel_close(cost, G[f"{tag}_cost"], 1e-6)
+    # 5e-6: torch's CPU grid_sample / reductions reorder fp32 sums by host ISA (up to 2.1e-6
+    # seen on the GPU boxes' EPYC hosts; ~1e-7 on the host that recorded the fixture)
+    rel_close(cost, G[f"{tag}_cost"], 5e-6)
     warped = ocv.warp(tgt.reshape(BV * J, *tgt.shape[2:]), K[:, None].expand(BV, J, 3, 3).reshape(-1, 3, 3),
                       pose.reshape(-1, 4, 4), depth[:, None].expand(BV, J, *depth.shape[1:]).reshape(BV * J,
                                                                                                    *depth.shape[1:]))
-    rel_close(warped.reshape(G[f"{tag}_warped"].shape), G[f"{tag}_warped"], 1e-6)
+    rel_close(warped.reshape(G[f"{tag}_warped"].shape), G[f"{tag}_warped"], 5e-6)
 
 
 @pytest.mark.parametrize("tag", TAGS)
