@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--stride", type=int, default=0, help="fused-layout stride override (experiments)")
     ap.add_argument("--two-phase", action="store_true", help="force the two-phase binning layout")
+    ap.add_argument("--exact", action="store_true", help="replay the inference path's exact-binning lists")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -43,8 +44,18 @@ def main():
     layout = raster.input_layout(g.harmonics, g.covariances, True, True)
     if a.two_phase:
         raster.KEY_BUDGET_BYTES = 0
-    color, state = raster.forward_raw(g.means, g.harmonics, True, 2, g.opacities, g.covariances, cams, V, H, W,
-                                      layout)
+    if a.exact:  # the inference fast path's lists (exact binning), snapshotted for replay
+        raster.DEBUG_KEEP_FAST_LISTS = True
+        raster._spec["max_count"] = 2048
+        ci = raster.camera_inputs(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0], bg,
+                                  [0] * V, True)
+        with torch.no_grad():
+            color, state = raster.forward_raw(g.means, g.harmonics, True, 2, g.opacities, g.covariances, ci, V, H,
+                                              W, layout, need_state=False)
+        cams = state.cams
+    else:
+        color, state = raster.forward_raw(g.means, g.harmonics, True, 2, g.opacities, g.covariances, cams, V, H, W,
+                                          layout)
     G = g.means.shape[1]
     torch.cuda.synchronize()
     print(f"G={G} V={V} {H}x{W} N={state.num_rendered}", flush=True)
@@ -86,6 +97,25 @@ def main():
                     return rc
                 return lib.dsr_bin_sort(G, V, H, W, None, cnt2.data_ptr(), a.stride or G, keys2.data_ptr(),
                                         scratch2.data_ptr(), state.max_count, ws_p, 0, None, None, st)
+        elif a.kernel == "project_cam":  # the inference path's binning (in-kernel cameras, exact binning)
+            assert stride > 0, "fused layout expected"
+            geom2, radii2 = torch.empty_like(state.geom), torch.empty_like(state.radii)
+            cnt2 = torch.zeros_like(state.seg_count)
+            keys2 = torch.empty_like(state.keys)
+            cams2 = torch.empty_like(cams)
+            ext, K = sc.target_extrinsics[0].contiguous(), sc.target_intrinsics[0].contiguous()
+            near, far = sc.near[0].contiguous(), sc.far[0].contiguous()
+            vs = torch.zeros(V, dtype=torch.int32, device=dev)
+            out = [geom2]
+
+            def launch():
+                cnt2.zero_()
+                return lib.dsr_project_bin_cameras(1, G, V, H, W, 2, g.harmonics.shape[-1], g.means.data_ptr(),
+                                                   g.harmonics.data_ptr(), None, g.opacities.data_ptr(),
+                                                   g.covariances.data_ptr(), ext.data_ptr(), K.data_ptr(),
+                                                   near.data_ptr(), far.data_ptr(), bg.data_ptr(), vs.data_ptr(), 1,
+                                                   cams2.data_ptr(), geom2.data_ptr(), radii2.data_ptr(),
+                                                   cnt2.data_ptr(), keys2.data_ptr(), layout | 4, st)
         elif a.kernel == "sort_render":  # fused sort + composite (keys already sorted: same work)
             assert stride > 0, "fused layout expected"
             out = [torch.empty_like(color), torch.empty_like(state.final_T), torch.empty_like(state.n_contrib)]
