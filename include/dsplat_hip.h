@@ -236,7 +236,8 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
  * tile's keys in LDS and composites from that copy; segments above 4096 entries are sorted
  * through `scratch` (same size as keys) by the same workgroup. The sorted keys are written
  * back to `keys` only when write_keys != 0 (dsr_render_bwd needs them). Outputs as
- * dsr_render_fwd. */
+ * dsr_render_fwd; n_contrib may be NULL (an inference call with no backward: the compositor
+ * then does not track the last blended position). */
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                     const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
                     uint64_t* scratch, int write_keys, int clear_counts, float* out_color, float* final_T,

@@ -26,18 +26,14 @@ constexpr int BX = DSR_TILE, BY = DSR_TILE;
 constexpr int NT = BX * BY;  // 256 threads = 4 waves per tile
 constexpr int GS = DSR_GEOM_STRIDE;
 constexpr uint32_t kSortCap = 8192;           // max keys sorted in LDS (2 x 64 KiB)
-#ifndef SORT_NTH
-#define SORT_NTH 256
-#endif
-constexpr int kSortNT = SORT_NTH;  // threads per segment in the LDS sort
-#ifndef SORT_NBIN_LOG2
-#define SORT_NBIN_LOG2 13
-#endif
+constexpr int kSortNT = 256;       // threads per segment in the LDS sort
+constexpr int kSortNBinLog2 = 13;  // counting-sort depth bins (8192)
+constexpr int kSortWPE = 3;        // waves per EU of the sort kernels: all config-B segments resident
 // LDS words of the sort's counter area: the LSD passes' u16 counters (16 per thread) or the
 // counting sort's u16 bins, whichever is larger
 template <int NTH>
 constexpr int sort_cnt_words() {
-  return NTH * 8 > (1 << SORT_NBIN_LOG2) / 2 ? NTH * 8 : (1 << SORT_NBIN_LOG2) / 2;
+  return NTH * 8 > (1 << kSortNBinLog2) / 2 ? NTH * 8 : (1 << kSortNBinLog2) / 2;
 }
 constexpr int kHistLdsMax = 32768;            // tiles per view histogrammed in LDS
 
@@ -721,18 +717,14 @@ __device__ __forceinline__ void tile_rect_alpha(const TileEll& e, int& x0, int& 
 // Gaussian come from HBM once and from that XCD's L2 for the other views (one workgroup per
 // scene looping over its views would hold 3x fewer waves in flight to hide the load and
 // atomic latencies).
-#ifndef PB_WPE
-#define PB_WPE 1
-#endif
-// pair cache of the count pass (PE_CAPW (tile, rank, owner) words per wave in LDS)
-#ifndef PE_CAPW
-#define PE_CAPW 768
-#endif
+constexpr int kProjectWPE = 1;
+// pair cache of the count pass (kPairCapW (tile, rank, owner) words per wave in LDS)
+constexpr int kPairCapW = 768;
 // EXACT (inference binning, CAM only): a pair is kept only when tile_reach says the
 // alpha >= 1/255 ellipse reaches the tile; the stateful / training path keeps the reference's
 // rect lists, which the backward and the oracle list tests follow.
 template <int DEG, bool CAM, bool EXACT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE))) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
                                                      const float* __restrict__ means,
                                                      const float* __restrict__ shs,
                                                      const float* __restrict__ colors,
@@ -747,7 +739,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
   __shared__ dsr_camera s_cam[1];  // CAM only
-  __shared__ uint32_t s_pairs[NT / 64][PE_CAPW];
+  __shared__ uint32_t s_pairs[NT / 64][kPairCapW];
   __shared__ uint32_t s_ovf;
   int v, blk;
   if (!xcd_pair((G + NT - 1) / NT, V, blk, v)) return;
@@ -798,14 +790,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
     const uint32_t j = stp++ * 64u + (uint32_t)lane;
     if constexpr (EXACT) {
       if (!tile_reach(oe, tx, ty)) {  // dropped pair: a hole in the list
-        if (j < (uint32_t)PE_CAPW) wp[j] = 0xFFFFFFFFu;
+        if (j < (uint32_t)kPairCapW) wp[j] = 0xFFFFFFFFu;
         return;
       }
     }
     const uint32_t rk = atomicAdd(&s_hist[t], 1u);
-    if (j < (uint32_t)PE_CAPW) wp[j] = (uint32_t)t | (rk << 16) | ((uint32_t)o << 24);
+    if (j < (uint32_t)kPairCapW) wp[j] = (uint32_t)t | (rk << 16) | ((uint32_t)o << 24);
   }, fetch);
-  if (lane == 0 && wtotal > (uint32_t)PE_CAPW) s_ovf = 1u;
+  if (lane == 0 && wtotal > (uint32_t)kPairCapW) s_ovf = 1u;
   __syncthreads();
   uint32_t* gcount = seg_count + (size_t)v * T;
   for (int t = tid; t < T; t += NT) {
@@ -823,7 +815,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PB_WPE))) vo
     }
     return;
   }
-  // a wave of this workgroup had more than PE_CAPW pairs: re-expand the rects. The keep test
+  // a wave of this workgroup had more than kPairCapW pairs: re-expand the rects. The keep test
   // is the same inlined code on the same operands (oe from the same owner lane, same tile
   // coordinates) as in the count pass, so both passes keep exactly the same pairs and the
   // emission fills the ranges reserved above (tests: test_inference_emit_overflow).
@@ -1533,7 +1525,7 @@ __device__ __forceinline__ uint32_t bin_word(uint32_t w) {
 template <int KMAX, int NTH = NT>
 __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A, int id_bits, uint16_t* cnt,
                            uint32_t* wsum, uint32_t* flag) {
-  constexpr int NBIN = 1 << SORT_NBIN_LOG2, BPT = NBIN / NTH;  // bins per thread in the scan
+  constexpr int NBIN = 1 << kSortNBinLog2, BPT = NBIN / NTH;  // bins per thread in the scan
   constexpr int R = BPT / 2;                                    // scan row: bin-pair words per thread
   static_assert(BPT % 8 == 0 && NTH * KMAX < 65536 && NBIN / 2 <= sort_cnt_words<NTH>(), "u16 bin pairs in cnt");
   uint32_t* hw = reinterpret_cast<uint32_t*>(cnt);  // NBIN / 2 words (cnt holds NTH * 16 u16), 16-B aligned
@@ -1552,7 +1544,7 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
   }
   block_minmax<NTH>(mn, mx, flag);
   const uint32_t range = mx - mn;
-  const int shift = max(0, (range ? 31 - __clz(range) : 0) - (SORT_NBIN_LOG2 - 1));
+  const int shift = max(0, (range ? 31 - __clz(range) : 0) - (kSortNBinLog2 - 1));
 #pragma unroll
   for (int i = 0; i < KMAX; ++i)
     if (tid + (uint32_t)i * NTH < n) {
@@ -1602,10 +1594,7 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
   // [end(b - 1), end(b)). A key of a bin of c <= 16 keys counts the smaller keys of its bin
   // (c independent LDS reads, all lanes in parallel); any larger bin (clustered or equal
   // depths) sends the whole segment through the LSD passes instead.
-#ifndef SORT_BINMAX
-#define SORT_BINMAX 16
-#endif
-  constexpr uint32_t kBinMax = SORT_BINMAX;
+  constexpr uint32_t kBinMax = 16;
   auto bin_end = [&](uint32_t b) -> uint32_t {
     const uint32_t wv = hw[bin_word<R>(b >> 1)];
     return (b & 1u) ? (wv >> 16) : (wv & 0xFFFFu);
@@ -1640,11 +1629,8 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
 // One workgroup per (view, tile) segment. n <= 256*KMAX: sort in LDS. Larger: when
 // big_here, sort through HBM (keys <-> scratch) with the ballot-ranked passes; otherwise
 // leave it to the MSD split (k_msd_split + k_sort_groups).
-#ifndef SORT_WPE
-#define SORT_WPE 3
-#endif
 template <int KMAX, int NTH = NT>
-__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(KMAX * NTH >= 8192 ? 1 : SORT_WPE))) void k_sort_lds(const uint32_t* __restrict__ seg_start,
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(KMAX * NTH >= 8192 ? 1 : kSortWPE))) void k_sort_lds(const uint32_t* __restrict__ seg_start,
                                                  const uint32_t* __restrict__ seg_count, uint32_t stride,
                                                  uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
                                                  int id_bits, int big_here, const uint32_t* __restrict__ filter,
@@ -1911,7 +1897,7 @@ __global__ __launch_bounds__(NTH) void k_msd_split(const uint32_t* __restrict__ 
 // Sort every group produced by k_msd_split into `keys` (from scratch, or from keys when the
 // segment was not split). grid = nseg * gmax.
 template <int KMAX>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) void k_sort_groups(
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kSortWPE))) void k_sort_groups(
     const uint32_t* __restrict__ groups, uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits) {
   constexpr uint32_t cap = NT * KMAX;
   constexpr uint32_t padded = cap + cap / KMAX;
@@ -2053,11 +2039,12 @@ __device__ __forceinline__ void live_rect(uint64_t live, float fx0, float fy0, f
   x1 = fx0 + (float)(31 - __builtin_clz(cb));
 }
 
-#ifndef RF_EPL
-#define RF_EPL 1
-#endif
-constexpr int EPL = RF_EPL;      // list entries per lane per chunk
-constexpr int CH = 64 * EPL;     // entries per chunk
+constexpr int CH = 64;  // list entries per chunk (one per lane)
+// Chunks whose records a wave gathers in one batch before compositing. A record gather is a
+// random read that mostly hits the MALL (the views' geometry does not fit one XCD's L2), and a
+// wave walks ~160 entries (p99 ~280, 3-5 chunks) of its tile at config B, so with only the
+// next chunk prefetched the walk was a chain of one memory round trip per chunk.
+constexpr int PD = 4;
 // Two consecutive list entries with their fields interleaved, so the falloff of both runs
 // as packed FP32 (v_pk_fma/mul/add) with no operand shuffling; per-element results are the
 // same IEEE operations as falloff_p2 (the backward's decisions still agree).
@@ -2075,10 +2062,18 @@ __device__ __forceinline__ void pair_put(PairRec* l, int k, float x, float y, fl
   d.x[j] = x; d.y[j] = y; d.A[j] = A; d.C[j] = C; d.B[j] = B; d.o[j] = o;
   d.rg[j] = f2v{r, g}; d.b[j] = b; d.pos[j] = pos;
 }
-// alive: the pixel has not stopped (and lies in the image); a lane mask, so the stop logic
-// is scalar mask arithmetic and T keeps its value for the final_T output.
-__device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v pfy2, float& Tr, bool& alive,
-                                               f2v& C01, float& C2, uint32_t& last) {
+// Front-to-back step over two entries. A pixel's state is its transmittance with the sign
+// as the stop flag (Tr < 0: stopped or outside the image, |Tr| the final T), so the chain
+// T -> test T -> stop -> T is vector compares and selects (VCC) only: no per-pixel lane mask
+// round-trips through SALU ops at every entry. Per entry, exactly as the reference: skip
+// unless power <= 0 and alpha = min(.99, o G) >= 1/255; test T = T (1 - alpha); stop
+// (without blending) when test T < 1e-4; else colour += rgb alpha T, T = test T, last =
+// position. A skipped entry gets alpha 0, which leaves T bit-identical (T * 1) and adds +0
+// colour; a stopped pixel fails the stop test at every later entry (T (1 - alpha) <= 0).
+// LAST: track the last blended position (n_contrib, which only a backward reads).
+template <bool LAST>
+__device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v pfy2, float& Tr, f2v& C01, float& C2,
+                                               uint32_t& last) {
   const f2v dx = P.x - pfx2, dy = P.y - pfy2;
   const f2v Adx = P.A * dx, Cdy = P.C * dy, Bdx = P.B * dx;
   const f2v Bdxdy = Bdx * dy;
@@ -2087,23 +2082,30 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v p
   G.x = __builtin_amdgcn_exp2f(p2.x);
   G.y = __builtin_amdgcn_exp2f(p2.y);
   const f2v oG = P.o * G;
+  f2v alpha;
+  alpha.x = fminf(0.99f, oG.x);
+  alpha.y = fminf(0.99f, oG.y);
+  // ok <=> min(0 - p2, alpha - 1/255) >= 0 (0 - p2 turns p2 = -0 into +0; each difference
+  // has the exact sign of its comparison)
+  const f2v np2 = f2v{0.f, 0.f} - p2;
+  const f2v over = alpha - f2v{1.0f / 255.0f, 1.0f / 255.0f};
+  f2v a;
+  a.x = fminf(np2.x, over.x) >= 0.f ? alpha.x : 0.f;
+  a.y = fminf(np2.y, over.y) >= 0.f ? alpha.y : 0.f;
+  const f2v om = f2v{1.f, 1.f} - a;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const float alpha = fminf(0.99f, oG[j]);
-    const bool ok = alive && p2[j] <= 0.0f && alpha >= 1.0f / 255.0f;
-    const float testT = Tr * (1 - alpha);
-    const bool stop = ok && testT < 0.0001f;
-    const bool blend = ok && !stop;
-    alive = alive && !stop;
-    const float wgt = blend ? alpha * Tr : 0.0f;
+    const float testT = Tr * om[j];
+    const bool stop = testT < 0.0001f;  // always once stopped (test T <= 0)
+    const float wgt = stop ? 0.f : a[j] * Tr;
     const f2v rg = P.rg[j];
     f2v w2;
     w2.x = wgt;
     w2.y = wgt;
     C01 = __builtin_elementwise_fma(rg, w2, C01);
     C2 = fmaf(P.b[j], wgt, C2);
-    Tr = blend ? testT : Tr;
-    last = blend ? P.pos[j] : last;
+    Tr = stop ? -fabsf(Tr) : testT;
+    if (LAST) last = wgt > 0.f ? P.pos[j] : last;  // blended <=> wgt > 0 (alpha >= 1/255, T >= 1e-4)
   }
 }
 
@@ -2155,95 +2157,120 @@ __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* 
   return false;
 }
 
+// One chunk of the walk: keep the entries of [base, base + CH) (this lane's record q, r, b)
+// whose alpha >= 1/255 region reaches the live pixels' box in the wave's LDS list (ballot
+// compaction, list order kept, entry pairs field-interleaved for packed math, 8 zero-opacity
+// pad entries after the end), then composite that list four entries per step with the next
+// four read ahead.
+template <bool LAST>
+__device__ __forceinline__ void composite_chunk(uint32_t base, uint32_t start, uint32_t end, float4 q, float4 r,
+                                                float b, float lx0, float ly0, float lx1, float ly1, f2v pfx2,
+                                                f2v pfy2, int lane, uint64_t lt, PairRec* plist, float& Tr, f2v& C01,
+                                                float& C2, uint32_t& last) {
+  const uint32_t e = base + lane;
+  const bool mine = e < end && rect_hit(q, r, lx0, ly0, lx1, ly1);
+  const uint64_t bal = __ballot(mine);
+  if (mine) {
+    const float4 sq = scaled_conic_q(q);  // (x, y, A, B)
+    pair_put(plist, __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * r.x, sq.w, r.y, r.z, r.w, b,
+             e - start + 1u);
+  }
+  const int cnt = __popcll(bal);
+  if (lane < 8)  // pad up to 8 entries: opacity 0 -> alpha 0 -> never blends
+    pair_put(plist, cnt + lane, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u);
+  __builtin_amdgcn_wave_barrier();
+  const PairRec* pp = plist;
+  PairRec a0 = pp[0], a1 = pp[1];
+  for (int k = 0; k < cnt; k += 4) {
+    pp += 2;
+    const PairRec b0 = pp[0], b1 = pp[1];  // in bounds: pair k/2 + 3 <= (CH + 8) / 2 - 1
+    composite_pair<LAST>(a0, pfx2, pfy2, Tr, C01, C2, last);
+    composite_pair<LAST>(a1, pfx2, pfy2, Tr, C01, C2, last);
+    if (!__any(Tr > 0.f)) break;
+    a0 = b0;
+    a1 = b1;
+  }
+  __builtin_amdgcn_wave_barrier();  // list reads of this chunk before the next chunk's writes
+}
+
 // K6 core: one wave composites its 8x8 sub-tile (pixel (px, py) per lane) front to back
 // over the sorted entries [start, end) of its tile, key_at(e) giving entry e's Gaussian id
-// (from HBM keys, or from the fused sort's LDS). The wave walks the list CH entries at a time
-// (EPL keys + records per lane, the next chunk's records and the chunk after's keys already
-// in flight), keeps the entries that can reach its live pixels in a wave-private LDS list
-// (ballot compaction, list order kept, entry pairs field-interleaved for packed math, 8
-// zero-opacity pad entries after the end), and composites that list four entries per step
-// with the next four read ahead. It returns as soon as its 64 pixels have terminated.
-template <typename KeyAt>
+// (from HBM keys, or from the fused sort's LDS), CH entries at a time (composite_chunk), and
+// returns as soon as its 64 pixels have terminated. The records of the first PD chunks are
+// gathered up front in one batch (straight-line code, so each chunk waits only for its own
+// loads); past them the walk keeps the next chunk's records and the keys of the chunk after
+// in flight.
+template <bool LAST, typename KeyAt>
+__device__ __forceinline__ void composite_walk(KeyAt key_at, uint32_t start, uint32_t end, const float* __restrict__ gv,
+                                               float fx0, float fy0, f2v pfx2, f2v pfy2, int lane, uint64_t lt,
+                                               PairRec* plist, float& Tr, f2v& C01, float& C2, uint32_t& last) {
+  if (start >= end) return;
+  // unconditional key reads (clamped index), so HBM key loads need no wait each; entries past
+  // the end read record 0 (a valid address) and are masked by the chunk's e < end test
+  auto id_of = [&](uint32_t e) -> uint32_t {
+    const uint32_t k = key_at(min(e, end - 1u));
+    return e < end ? k : 0u;
+  };
+  float4 q[PD], r[PD];
+  float b[PD];
+  uint32_t ids[PD];
+#pragma unroll
+  for (int s = 0; s < PD; ++s) ids[s] = id_of(start + s * CH + lane);  // HBM keys: one batch too
+#pragma unroll
+  for (int s = 0; s < PD; ++s) {
+    const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)ids[s] * GS);
+    q[s] = rec[0];
+    r[s] = rec[1];
+    b[s] = rec[2].x;
+  }
+  uint32_t nid = id_of(start + PD * CH + lane);
+#pragma unroll
+  for (int s = 0; s < PD; ++s) {
+    const uint32_t base = start + s * CH;
+    if (base >= end) return;
+    const uint64_t live = __ballot(Tr > 0.f);
+    if (!live) return;
+    float lx0, ly0, lx1, ly1;
+    live_rect(live, fx0, fy0, lx0, ly0, lx1, ly1);
+    composite_chunk<LAST>(base, start, end, q[s], r[s], b[s], lx0, ly0, lx1, ly1, pfx2, pfy2, lane, lt, plist, Tr, C01, C2,
+                    last);
+  }
+  float4 cq = make_float4(0.f, 0.f, 0.f, 0.f), cr = cq;
+  float cb = 0.f;
+  {
+    const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)nid * GS);
+    cq = rec[0];
+    cr = rec[1];
+    cb = rec[2].x;
+  }
+  nid = id_of(start + (PD + 1) * CH + lane);
+  for (uint32_t base = start + PD * CH; base < end; base += CH) {
+    const uint64_t live = __ballot(Tr > 0.f);
+    if (!live) break;
+    float lx0, ly0, lx1, ly1;
+    live_rect(live, fx0, fy0, lx0, ly0, lx1, ly1);
+    const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)nid * GS);
+    const float4 nq = rec[0], nr = rec[1];
+    const float nb = rec[2].x;
+    nid = id_of(base + 2 * CH + lane);
+    composite_chunk<LAST>(base, start, end, cq, cr, cb, lx0, ly0, lx1, ly1, pfx2, pfy2, lane, lt, plist, Tr, C01, C2, last);
+    cq = nq;
+    cr = nr;
+    cb = nb;
+  }
+}
+
+// composite_walk with the kernels' state: alive (the pixel lies in the image and has not
+// stopped) and T = the pixel's transmittance (the final T once stopped).
+template <bool LAST, typename KeyAt>
 __device__ __forceinline__ void composite_tile(KeyAt key_at, uint32_t start, uint32_t end, const float* __restrict__ gv,
                                                float fx0, float fy0, f2v pfx2, f2v pfy2, int lane, uint64_t lt,
                                                PairRec* plist, float& Tr, f2v& C01, float& C2, uint32_t& last,
                                                bool& alive) {
-  float4 cq[EPL], cr[EPL];
-  float cb[EPL];
-  uint32_t nid[EPL];
-#pragma unroll
-  for (int u = 0; u < EPL; ++u) {
-    const uint32_t e = start + u * 64 + lane;
-    cq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    cr[u] = cq[u];
-    cb[u] = 0.f;
-    if (e < end) {
-      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)key_at(e) * GS);
-      cq[u] = rec[0];
-      cr[u] = rec[1];
-      cb[u] = rec[2].x;
-    }
-    const uint32_t e1 = e + CH;
-    nid[u] = e1 < end ? key_at(e1) : 0xffffffffu;
-  }
-  for (uint32_t base = start; base < end; base += CH) {
-    const uint64_t live = __ballot(alive);
-    if (!live) break;
-    float lx0, ly0, lx1, ly1;
-    live_rect(live, fx0, fy0, lx0, ly0, lx1, ly1);
-    float4 nq[EPL], nr[EPL];
-    float nb[EPL];
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) {
-      nq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      nr[u] = nq[u];
-      nb[u] = 0.f;
-      if (nid[u] != 0xffffffffu) {
-        const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)nid[u] * GS);
-        nq[u] = rec[0];
-        nr[u] = rec[1];
-        nb[u] = rec[2].x;
-      }
-      const uint32_t e2 = base + 2 * CH + u * 64 + lane;
-      nid[u] = e2 < end ? key_at(e2) : 0xffffffffu;
-    }
-    int cnt = 0;
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) {
-      const uint32_t e = base + u * 64 + lane;
-      const bool mine = e < end && rect_hit(cq[u], cr[u], lx0, ly0, lx1, ly1);
-      const uint64_t bal = __ballot(mine);
-      if (mine) {
-        const float4 sq = scaled_conic_q(cq[u]);  // (x, y, A, B)
-        pair_put(plist, cnt + __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * cr[u].x, sq.w, cr[u].y,
-                 cr[u].z, cr[u].w, cb[u], e - start + 1u);
-      }
-      cnt += __popcll(bal);
-    }
-    if (lane < 8)  // pad up to 8 entries: opacity 0 -> alpha 0 -> never blends
-      pair_put(plist, cnt + lane, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u);
-    __builtin_amdgcn_wave_barrier();
-    {
-      const PairRec* pp = plist;
-      PairRec a0 = pp[0], a1 = pp[1];
-      for (int k = 0; k < cnt; k += 4) {
-        pp += 2;
-        const PairRec b0 = pp[0], b1 = pp[1];  // in bounds: pair k/2 + 3 <= (CH + 8) / 2 - 1
-        composite_pair(a0, pfx2, pfy2, Tr, alive, C01, C2, last);
-        composite_pair(a1, pfx2, pfy2, Tr, alive, C01, C2, last);
-        if (!__any(alive)) break;
-        a0 = b0;
-        a1 = b1;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();  // list reads of this chunk before the next chunk's writes
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) {
-      cq[u] = nq[u];
-      cr[u] = nr[u];
-      cb[u] = nb[u];
-    }
-  }
+  Tr = alive ? Tr : -Tr;
+  composite_walk<LAST>(key_at, start, end, gv, fx0, fy0, pfx2, pfy2, lane, lt, plist, Tr, C01, C2, last);
+  alive = Tr > 0.f;
+  Tr = fabsf(Tr);
 }
 
 __device__ __forceinline__ void store_pixel(float* __restrict__ out, float* __restrict__ finalT,
@@ -2252,7 +2279,7 @@ __device__ __forceinline__ void store_pixel(float* __restrict__ out, float* __re
   const size_t HW = (size_t)H * W;
   const size_t pix = (size_t)py * W + px;
   finalT[v * HW + pix] = Tr;
-  ncontrib[v * HW + pix] = last;
+  if (ncontrib) ncontrib[v * HW + pix] = last;
   out[(size_t)v * 3 * HW + pix] = C01.x + Tr * bg[0];
   out[(size_t)v * 3 * HW + HW + pix] = C01.y + Tr * bg[1];
   out[(size_t)v * 3 * HW + 2 * HW + pix] = C2 + Tr * bg[2];
@@ -2297,7 +2324,7 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   float Tr = 1.0f, C2 = 0.f;
   bool alive = inside;
   uint32_t last = 0;
-  composite_tile([&](uint32_t e) { return (uint32_t)keys[e]; }, start, end, gv, fx0, fy0, pfx2, pfy2, lane, lt,
+  composite_tile<true>([&](uint32_t e) { return (uint32_t)keys[e]; }, start, end, gv, fx0, fy0, pfx2, pfy2, lane, lt,
                  plist, Tr, C01, C2, last, alive);
   bool void_tile = false;  // wave-uniform
   if (absent_tail)
@@ -2322,8 +2349,8 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
 // (write_keys), the render never re-reads keys from HBM, and the sort and compositing phases
 // of different tiles overlap inside one launch. A segment above the LDS capacity is sorted
 // through HBM (scratch) by the same workgroup and composited from there.
-template <int KMAX>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) void k_sort_render(
+template <int KMAX, bool LAST>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kSortWPE))) void k_sort_render(
     int G, int H, int W, int gx, int T, const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
     const uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_count, uint32_t stride,
     uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits, int write_keys, int clear_counts,
@@ -2376,10 +2403,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SORT_WPE))) 
   bool alive = inside;
   uint32_t last = 0;
   if (in_lds)
-    composite_tile([&](uint32_t i) { return (uint32_t)A[padi<KMAX>(i)]; }, 0u, n, gv, (float)sx0, (float)sy0, pfx2,
+    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)A[padi<KMAX>(i)]; }, 0u, n, gv, (float)sx0, (float)sy0, pfx2,
                    pfy2, lane, lt, plist, Tr, C01, C2, last, alive);
   else
-    composite_tile([&](uint32_t i) { return (uint32_t)keys[i]; }, b, e, gv, (float)sx0, (float)sy0, pfx2, pfy2,
+    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)keys[i]; }, b, e, gv, (float)sx0, (float)sy0, pfx2, pfy2,
                    lane, lt, plist, Tr, C01, C2, last, alive);
   if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
   // counts handed back zeroed for the next call's binning (every thread read it before the
@@ -3251,22 +3278,23 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
   DSPLAT_REQUIRE(!clear_counts || seg_stride > 0, "dsr_sort_render: clear_counts needs the fixed-capacity layout");
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_sort_render: bad sizes");
   DSPLAT_REQUIRE(cams && geom && keys && scratch && seg_ptrs_ok(seg_start, seg_count, seg_stride) && out_color &&
-                     final_T && n_contrib,
+                     final_T,
                  "dsr_sort_render: null pointer");
   static bool attr = false;
   if (!attr) {
-    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_render<16>,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)sort_lds_bytes<16>()),
-                                  "hipFuncSetAttribute(k_sort_render)"))
-      return e;
+    for (const void* f : {(const void*)k_sort_render<16, true>, (const void*)k_sort_render<16, false>})
+      if (int e = dsplat::check_hip(
+              hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sort_lds_bytes<16>()),
+              "hipFuncSetAttribute(k_sort_render)"))
+        return e;
     attr = true;
   }
   int id_bits = 0;
   while (id_bits < 32 && ((uint64_t)1 << id_bits) < (uint64_t)G) ++id_bits;
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
-  k_sort_render<16><<<grid, NT, sort_lds_bytes<16>(), (hipStream_t)stream>>>(
+  auto kern = n_contrib ? k_sort_render<16, true> : k_sort_render<16, false>;  // n_contrib is optional
+  kern<<<grid, NT, sort_lds_bytes<16>(), (hipStream_t)stream>>>(
       G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count, seg_stride, keys, scratch, id_bits, write_keys,
       clear_counts, out_color, final_T, n_contrib);
   return dsplat::check_launch("k_sort_render");

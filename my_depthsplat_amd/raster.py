@@ -126,8 +126,8 @@ def algorithmic_bytes(kernel: str, *, G: int, V: int, N: int, HW: int, T: int | 
         return 16 * N
     if kernel == "k_render_fwd":   # keys; each 36-B compositing record once; RGB + T + n_contrib out
         return 8 * N + 36 * V * G + 20 * V * HW
-    if kernel == "k_sort_render":  # keys in (sorted copy stays in LDS: inference), records, outputs
-        return 8 * N + 36 * V * G + 20 * V * HW
+    if kernel == "k_sort_render":  # keys in (sorted copy stays in LDS: inference), records, RGB + T
+        return 8 * N + 36 * V * G + 16 * V * HW  # (no n_contrib on the inference path)
     raise KeyError(kernel)
 
 
@@ -145,7 +145,7 @@ class RasterState:
     seg_stride: int           # 0: prefix layout; > 0: segment s starts at s * seg_stride
     keys: torch.Tensor        # int64 (uint64 keys, sorted per segment)
     final_T: torch.Tensor     # [V, H, W]
-    n_contrib: torch.Tensor   # [V, H, W] int32
+    n_contrib: torch.Tensor | None  # [V, H, W] int32 (None on the inference fast path)
     seg_sorted: torch.Tensor | None = None    # [V*T] sorted entries per segment (prefix-sort mode)
     seg_overflow: torch.Tensor | None = None  # [V*T(+1)] tiles re-sorted in full and re-rendered
     tile_count: torch.Tensor | None = None    # [V*T] all entries per tile (depth-cut mode: seg_count = ends)
@@ -518,8 +518,11 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                       lds_cap)
     color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
-    n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev)
-    outs = (color.data_ptr(), final_T.data_ptr(), n_contrib.data_ptr(), st)
+    # n_contrib (the last blended position, read only by the backward) is skipped on the
+    # inference fast path: not tracking it takes ~4 VALU instructions off every (pixel, entry)
+    keep_nc = not fast or need_state or DEBUG_KEEP_FAST_LISTS
+    n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev) if keep_nc else None
+    outs = (color.data_ptr(), final_T.data_ptr(), _ptr(n_contrib), st)
     if fused:  # sort + composite in one launch; sorted keys kept only when a backward needs them
         snap = seg_count.clone() if (fast and DEBUG_KEEP_FAST_LISTS) else None
         _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(), None,

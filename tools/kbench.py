@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--stride", type=int, default=0, help="fused-layout stride override (experiments)")
     ap.add_argument("--two-phase", action="store_true", help="force the two-phase binning layout")
     ap.add_argument("--exact", action="store_true", help="replay the inference path's exact-binning lists")
+    ap.add_argument("--no-ncontrib", action="store_true", help="sort_render without n_contrib (inference)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -118,13 +119,15 @@ def main():
                                                    cnt2.data_ptr(), keys2.data_ptr(), layout | 4, st)
         elif a.kernel == "sort_render":  # fused sort + composite (keys already sorted: same work)
             assert stride > 0, "fused layout expected"
-            out = [torch.empty_like(color), torch.empty_like(state.final_T), torch.empty_like(state.n_contrib)]
+            out = [torch.empty_like(color), torch.empty_like(state.final_T)]
+            if not a.no_ncontrib:
+                out.append(torch.empty_like(state.n_contrib))
             scr4 = torch.empty_like(state.keys)
 
             def launch():
                 return lib.dsr_sort_render(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), None, sc_p, stride,
                                            state.keys.data_ptr(), scr4.data_ptr(), 0, 0, out[0].data_ptr(),
-                                           out[1].data_ptr(), out[2].data_ptr(), st)
+                                           out[1].data_ptr(), out[2].data_ptr() if len(out) > 2 else None, st)
         elif a.kernel == "scatter":  # two-phase key scatter from the scan's segment starts
             assert stride == 0, "two-phase layout expected (--two-phase)"
             cur = torch.empty_like(state.seg_start)
