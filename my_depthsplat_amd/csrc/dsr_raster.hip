@@ -1527,6 +1527,7 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
                            uint32_t* wsum, uint32_t* flag) {
   constexpr int NBIN = 1 << kSortNBinLog2, BPT = NBIN / NTH;  // bins per thread in the scan
   constexpr int R = BPT / 2;                                    // scan row: bin-pair words per thread
+  constexpr uint32_t kBinMax = 16;  // larger bins (clustered / equal depths): LSD passes instead
   static_assert(BPT % 8 == 0 && NTH * KMAX < 65536 && NBIN / 2 <= sort_cnt_words<NTH>(), "u16 bin pairs in cnt");
   uint32_t* hw = reinterpret_cast<uint32_t*>(cnt);  // NBIN / 2 words (cnt holds NTH * 16 u16), 16-B aligned
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1545,12 +1546,19 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
   block_minmax<NTH>(mn, mx, flag);
   const uint32_t range = mx - mn;
   const int shift = max(0, (range ? 31 - __clz(range) : 0) - (kSortNBinLog2 - 1));
+  // count pass: the atomic's return value is the key's rank among the keys of its bin that
+  // got there first, so the scatter needs no second atomic pass (u16 halves never carry:
+  // n < 65536)
+  uint32_t rk[KMAX];
 #pragma unroll
-  for (int i = 0; i < KMAX; ++i)
+  for (int i = 0; i < KMAX; ++i) {
+    rk[i] = 0u;
     if (tid + (uint32_t)i * NTH < n) {
       const uint32_t bin = ((uint32_t)(tmp[i] >> 32) - mn) >> shift;
-      atomicAdd(&hw[bin_word<R>(bin >> 1)], 1u << ((bin & 1u) * 16u));
+      const uint32_t s16 = (bin & 1u) * 16u;
+      rk[i] = (atomicAdd(&hw[bin_word<R>(bin >> 1)], 1u << s16) >> s16) & 0xFFFFu;
     }
+  }
   __syncthreads();
   {
     uint4* row = reinterpret_cast<uint4*>(hw) + tid * (R / 4);
@@ -1574,55 +1582,50 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const uint32_t lo = wd[q] & 0xFFFFu, hi = wd[q] >> 16;
-      wd[q] = off | ((off + lo) << 16);
+      wd[q] = off | ((off + lo) << 16);  // start offsets of bins 2q, 2q + 1
       off += lo + hi;
     }
 #pragma unroll
     for (int c = 0; c < R / 4; ++c) row[c ^ rot] = make_uint4(wd[4 * c], wd[4 * c + 1], wd[4 * c + 2], wd[4 * c + 3]);
   }
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < KMAX; ++i)
-    if (tid + (uint32_t)i * NTH < n) {
-      const uint32_t bin = ((uint32_t)(tmp[i] >> 32) - mn) >> shift;
-      const uint32_t s16 = (bin & 1u) * 16u;
-      const uint32_t pos = (atomicAdd(&hw[bin_word<R>(bin >> 1)], 1u << s16) >> s16) & 0xFFFFu;
-      A[padi<KMAX>(pos)] = tmp[i];
-    }
-  __syncthreads();
-  // order inside each bin: the scatter left hw holding every bin's END offset, so bin b is
-  // [end(b - 1), end(b)). A key of a bin of c <= 16 keys counts the smaller keys of its bin
-  // (c independent LDS reads, all lanes in parallel); any larger bin (clustered or equal
-  // depths) sends the whole segment through the LSD passes instead.
-  constexpr uint32_t kBinMax = 16;
-  auto bin_end = [&](uint32_t b) -> uint32_t {
+  // bin b is [start(b), start(b + 1)), the last bin ending at n
+  auto bin_start = [&](uint32_t b) -> uint32_t {
+    if (b >= (uint32_t)NBIN) return n;
     const uint32_t wv = hw[bin_word<R>(b >> 1)];
     return (b & 1u) ? (wv >> 16) : (wv & 0xFFFFu);
   };
-  uint32_t dest[KMAX];
+  uint32_t multi = 0u;  // bit i: key i shares its bin (its final place needs the in-bin rank)
   bool big = false;
 #pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    dest[i] = 0u;
+  for (int i = 0; i < KMAX; ++i)
     if (tid + (uint32_t)i * NTH < n) {
       const uint32_t bin = ((uint32_t)(tmp[i] >> 32) - mn) >> shift;
-      const uint32_t e = bin_end(bin), st = bin ? bin_end(bin - 1u) : 0u;
-      uint32_t r = 0;
-      if (e - st > kBinMax) {
-        big = true;
-      } else if (e - st > 1u) {
-        for (uint32_t j = st; j < e; ++j) r += A[padi<KMAX>(j)] < tmp[i] ? 1u : 0u;
-      }
-      dest[i] = st + r;
+      const uint32_t st = bin_start(bin), c = bin_start(bin + 1u) - st;
+      A[padi<KMAX>(st + rk[i])] = tmp[i];
+      big |= c > kBinMax;
+      if (c > 1u) multi |= 1u << i;
+      rk[i] = st | (c << 16);
     }
-  }
-  if (__syncthreads_or(big)) {  // A holds the keys grouped by bin: sort it outright
+  if (__syncthreads_or(big)) {  // a clustered segment: A holds the keys grouped by bin, sort it outright
     reg_sort<KMAX, NTH>(A, n, id_bits, cnt, wsum, flag);
     return;
   }
+  // order inside each shared bin (<= kBinMax keys): count the smaller keys of the bin (c
+  // independent LDS reads, all lanes in parallel); single-key bins are already in place
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    if (multi & (1u << i)) {
+      const uint32_t st = rk[i] & 0xFFFFu, e = st + (rk[i] >> 16);
+      uint32_t r = 0;
+      for (uint32_t j = st; j < e; ++j) r += A[padi<KMAX>(j)] < tmp[i] ? 1u : 0u;
+      rk[i] = st + r;
+    }
+  }
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < KMAX; ++i)
-    if (tid + (uint32_t)i * NTH < n) A[padi<KMAX>(dest[i])] = tmp[i];
+    if (multi & (1u << i)) A[padi<KMAX>(rk[i])] = tmp[i];
   __syncthreads();
 }
 
@@ -2285,6 +2288,18 @@ __device__ __forceinline__ void store_pixel(float* __restrict__ out, float* __re
   out[(size_t)v * 3 * HW + 2 * HW + pix] = C2 + Tr * bg[2];
 }
 
+// Tile of this compositing workgroup (grid = (gx, gy, V)). The dispatcher places workgroups
+// L, L + 256, L + 512, ... (linear ids) on one CU (measured: round-robin over the 8 XCDs, then
+// over an XCD's 32 CUs), i.e. at config B the same tile position of the 3 views, and centre
+// tiles carry ~1.8x the entries of border ones. Shifting each view's tile grid by a third of
+// it along both axes gives a CU tiles from different parts of the image, so the CUs' loads
+// even out (tools/sr_timing.py: per-CU finish times).
+__device__ __forceinline__ void tile_of(int gx, int gy, int& tx, int& ty) {
+  const int v = blockIdx.z;
+  tx = (int)((blockIdx.x + (unsigned)v * (unsigned)((gx + 2) / 3)) % (unsigned)gx);
+  ty = (int)((blockIdx.y + (unsigned)v * (unsigned)((gy + 2) / 3)) % (unsigned)gy);
+}
+
 // K6: front-to-back compositing. grid = (gx, gy, V), block = 256 = 4 independent waves;
 // wave w owns the 8x8 sub-tile (w & 1, w >> 1) of the tile (composite_tile). There is no
 // workgroup barrier; the waves of a workgroup share the tile's keys/records through L1. A
@@ -2303,11 +2318,13 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   __shared__ PairRec l_pair[4][(CH + 8) / 2];
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int sx0 = blockIdx.x * BX + (w & 1) * SUB, sy0 = blockIdx.y * BY + (w >> 1) * SUB;
+  int tx, ty;
+  tile_of(gx, T / gx, tx, ty);
+  const int sx0 = tx * BX + (w & 1) * SUB, sy0 = ty * BY + (w >> 1) * SUB;
   const int px = sx0 + (lane & (SUB - 1));
   const int py = sy0 + (lane >> 3);
   const bool inside = px < W && py < H;
-  const int seg = v * T + blockIdx.y * gx + blockIdx.x;
+  const int seg = v * T + ty * gx + tx;
   if (seg_filter && !seg_filter[seg]) return;
   uint32_t start, end;
   seg_bounds(seg_start, seg_count, stride, seg, start, end);
@@ -2337,7 +2354,7 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
     if (absent_tail) {  // depth cut: also flag the tile's super-block (the tail scatter's pre-test)
       const int sb = cut_superblock(gx, T / gx), sbl = __builtin_ctz((unsigned)sb);
       const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((T / gx + sb - 1) / sb);
-      seg_overflow[(size_t)gridDim.z * T + 1 + (size_t)v * nsb + (blockIdx.y >> sbl) * nsx + (blockIdx.x >> sbl)] = 1u;
+      seg_overflow[(size_t)gridDim.z * T + 1 + (size_t)v * nsb + (ty >> sbl) * nsx + (tx >> sbl)] = 1u;
     }
   }
   if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
@@ -2366,7 +2383,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kSortWPE))) 
   static_assert(sizeof(PairRec) * 4 * ((CH + 8) / 2) <= (size_t)sort_cnt_words<NT>() * 4, "pair lists fit the counters");
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int seg = v * T + blockIdx.y * gx + blockIdx.x;
+  int tx, ty;
+  tile_of(gx, T / gx, tx, ty);
+  const int seg = v * T + ty * gx + tx;
   uint32_t b, e;
   seg_bounds(seg_start, seg_count, stride, seg, b, e);
   const uint32_t n = e - b;
@@ -2390,7 +2409,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kSortWPE))) 
     sort_segment<NT>(keys + b, scratch + b, n, id_bits, aux, wsum, flag, keys + b);
     __syncthreads();
   }
-  const int sx0 = blockIdx.x * BX + (w & 1) * SUB, sy0 = blockIdx.y * BY + (w >> 1) * SUB;
+  const int sx0 = tx * BX + (w & 1) * SUB, sy0 = ty * BY + (w >> 1) * SUB;
   const int px = sx0 + (lane & (SUB - 1));
   const int py = sy0 + (lane >> 3);
   const bool inside = px < W && py < H;
@@ -2480,11 +2499,13 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
   __shared__ float l_acc[4][BCH * 9];
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int sx0 = blockIdx.x * BX + (w & 1) * SUB, sy0 = blockIdx.y * BY + (w >> 1) * SUB;
+  int tx, ty;
+  tile_of(gx, T / gx, tx, ty);
+  const int sx0 = tx * BX + (w & 1) * SUB, sy0 = ty * BY + (w >> 1) * SUB;
   const int px = sx0 + (lane & (SUB - 1));
   const int py = sy0 + (lane >> 3);
   const bool inside = px < W && py < H;
-  const int seg = v * T + blockIdx.y * gx + blockIdx.x;
+  const int seg = v * T + ty * gx + tx;
   uint32_t start, end;
   seg_bounds(seg_start, seg_count, stride, seg, start, end);
   const size_t HW = (size_t)H * W;

@@ -42,8 +42,11 @@ for _ in range(20):
 torch.cuda.synchronize()
 nt = st.seg_count.numel()
 t = scr[: nt * 32].view(nt, 4, 8).cpu().numpy().astype(np.int64)
-t0, t1, t2, n = t[..., 0], t[..., 1], t[..., 2], t[:, 0, 3]
-cf, cc, nch, nent = t[..., 4], t[..., 5], t[..., 6], t[..., 7]
+t0, t1, t2, n = t[..., 0], t[..., 1], t[..., 2], t[:, 0, 3] & 0xFFFFFFFF
+cf, cc, nch, nent = t[..., 4], t[..., 5], t[..., 6] & 0xFFFFFFFF, t[..., 7]
+hwid, xcc = t[:, 0, 3] >> 32, t[:, 0, 6] >> 32
+# HW_ID (gfx9): CU_ID [11:8], SH_ID [12], SE_ID [15:13]; XCC_ID [3:0]
+cu = (xcc & 0xF) * 1000 + ((hwid >> 13) & 7) * 100 + ((hwid >> 12) & 1) * 16 + ((hwid >> 8) & 0xF)
 base = t0.min()
 us = lambda x: x * 0.01  # noqa: E731  (100 MHz ticks -> us)
 q = lambda a: f"mean={a.mean():6.2f} p10={np.percentile(a, 10):6.2f} p50={np.percentile(a, 50):6.2f} " \
@@ -60,3 +63,15 @@ print(f"comp kcyc     {q(cc.reshape(-1) / 1e3)}  per entry {cc.sum() / max(nent.
 lo, hi = np.argsort(n)[: nt // 10], np.argsort(n)[-nt // 10:]
 print(f"sort light/heavy tiles (n {n[lo].mean():.0f} / {n[hi].mean():.0f}): "
       f"{us(t1[lo, 0] - t0[lo, 0]).mean():.2f} / {us(t1[hi, 0] - t0[hi, 0]).mean():.2f} us")
+
+ends = us(t2.max(1) - base)
+cus = {}
+for i in range(nt):
+    cus.setdefault(int(cu[i]), []).append(i)
+print(f"{len(cus)} distinct CUs; tiles per CU: {sorted(set(len(v) for v in cus.values()))}")
+loads = np.array([n[v].sum() for v in cus.values()])
+cu_end = np.array([ends[v].max() for v in cus.values()])
+print(f"entries per CU {q(loads.astype(float))}; CU end {q(cu_end)}")
+gx = (W + 15) // 16
+ex = list(cus.values())[:6]
+print("example CU tile sets (seg = view, ty, tx; n):", [[(i // (nt // V), (i % (nt // V)) // gx, i % gx, int(n[i])) for i in v] for v in ex])

@@ -26,26 +26,24 @@ PATCHES = [
      "  const uint64_t pt2 = __builtin_amdgcn_s_memtime();\n"
      "  if (lane == 0) { const int w = threadIdx.x >> 6; s_prof[w][0] += pt1 - pt0; s_prof[w][1] += pt2 - pt1;"
      " s_prof[w][2] += 1; s_prof[w][3] += cnt; }\n}"),
-    ("  const int seg = v * T + blockIdx.y * gx + blockIdx.x;\n  uint32_t b, e;\n  seg_bounds(seg_start, seg_count, "
-     "stride, seg, b, e);\n  const uint32_t n = e - b;\n  const bool in_lds",
+    ("  uint32_t b, e;\n  seg_bounds(seg_start, seg_count, stride, seg, b, e);\n  const uint32_t n = e - b;\n"
+     "  const bool in_lds",
      "  const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();\n"
      "  if (lane == 0) { s_prof[w][0] = 0; s_prof[w][1] = 0; s_prof[w][2] = 0; s_prof[w][3] = 0; }\n"
-     "  const int seg = v * T + blockIdx.y * gx + blockIdx.x;\n  uint32_t b, e;\n  seg_bounds(seg_start, seg_count, "
-     "stride, seg, b, e);\n  const uint32_t n = e - b;\n  const bool in_lds"),
-    ("  const int sx0 = blockIdx.x * BX + (w & 1) * SUB, sy0 = blockIdx.y * BY + (w >> 1) * SUB;\n"
-     "  const int px = sx0 + (lane & (SUB - 1));\n  const int py = sy0 + (lane >> 3);\n  const bool inside = px < W && "
-     "py < H;\n  const float* gv = geom + (size_t)v * G * GS;\n  const uint64_t lt = dsplat::lanemask_lt(lane);\n"
-     "  PairRec* plist = reinterpret_cast<PairRec*>(aux)",
-     "  const uint64_t t_1 = __builtin_amdgcn_s_memrealtime();\n"
-     "  const int sx0 = blockIdx.x * BX + (w & 1) * SUB, sy0 = blockIdx.y * BY + (w >> 1) * SUB;\n"
-     "  const int px = sx0 + (lane & (SUB - 1));\n  const int py = sy0 + (lane >> 3);\n  const bool inside = px < W && "
-     "py < H;\n  const float* gv = geom + (size_t)v * G * GS;\n  const uint64_t lt = dsplat::lanemask_lt(lane);\n"
+     "  uint32_t b, e;\n  seg_bounds(seg_start, seg_count, stride, seg, b, e);\n  const uint32_t n = e - b;\n"
+     "  const bool in_lds"),
+    ("  const bool inside = px < W && py < H;\n  const float* gv = geom + (size_t)v * G * GS;\n"
+     "  const uint64_t lt = dsplat::lanemask_lt(lane);\n  PairRec* plist = reinterpret_cast<PairRec*>(aux)",
+     "  const bool inside = px < W && py < H;\n  const float* gv = geom + (size_t)v * G * GS;\n"
+     "  const uint64_t lt = dsplat::lanemask_lt(lane);\n  const uint64_t t_1 = __builtin_amdgcn_s_memrealtime();\n"
      "  PairRec* plist = reinterpret_cast<PairRec*>(aux)"),
     ("  if (clear_counts && tid == 0) seg_count[seg] = 0u;",
      "  if (clear_counts && tid == 0) seg_count[seg] = 0u;\n"
      "  const uint64_t t_2 = __builtin_amdgcn_s_memrealtime();\n"
      "  if (lane == 0) { uint64_t* o = scratch + ((size_t)seg * 4 + w) * 8; o[0] = t_0; o[1] = t_1; o[2] = t_2;"
-     " o[3] = n; o[4] = s_prof[w][0]; o[5] = s_prof[w][1]; o[6] = s_prof[w][2]; o[7] = s_prof[w][3]; }"),
+     " o[3] = n | ((uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) << 32); o[4] = s_prof[w][0];"
+     " o[5] = s_prof[w][1]; o[6] = s_prof[w][2] | ((uint64_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);"
+     " o[7] = s_prof[w][3]; }"),
 ]
 
 
