@@ -84,6 +84,9 @@ int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, c
 #define DSR_LAYOUT_COUNTS_ZEROED 4     /* seg_count already zeroed (dsr_build_cameras)       */
 #define DSR_LAYOUT_RECT_BINNING 8      /* dsr_project_bin_cameras only: keep the reference's 3-sigma
                                           tile rects instead of the exact alpha >= 1/255 test       */
+#define DSR_LAYOUT_EXACT_BINNING 16    /* dsr_project_bin / dsr_preprocess_fwd / dsr_bin_scatter:
+                                          exact alpha >= 1/255 tile test (as dsr_project_bin_cameras;
+                                          the count and scatter calls of one forward must agree)    */
 int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,
@@ -132,7 +135,9 @@ int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_s
  * grouped by segment (v, t) at seg_start; order inside a segment is arbitrary here and
  * fixed by dsr_bin_sort. keys must hold N entries. Replaces duplicateWithKeys (K3). */
 int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor,
-                    uint64_t* keys, void* stream);
+                    uint64_t* keys, int layout, void* stream);
+/* layout: DSR_LAYOUT_EXACT_BINNING when the dsr_preprocess_fwd call that counted the entries
+ * had it (other bits ignored). */
 
 /* Segment layout used by the sort and compositing calls:
  *   seg_stride == 0: prefix layout, segment s = keys[seg_start[s] .. seg_start[s+1])

@@ -24,7 +24,7 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_build_cameras": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _P, _P, c_uint32, _P]),
     "dsr_preprocess_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dsr_bin_scan": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
-    "dsr_bin_scatter": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
+    "dsr_bin_scatter": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P]),
     "dsr_project_bin": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dsr_cut_superblock": (_I, [_I, _I]),
     "dsr_preprocess_cut": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),

@@ -245,7 +245,8 @@ __device__ __forceinline__ float sh_eval(const float* sh, int ch, float x, float
 // bit 1: full covariance [S,G,3,3] instead of cov6 — the upper triangle is read, exactly
 // what cuda_splatting.py:114,122's triu gather hands the rasterizer.
 constexpr int kLayoutShChannelMajor = DSR_LAYOUT_SH_CHANNEL_MAJOR, kLayoutCovFull = DSR_LAYOUT_COV_FULL,
-              kLayoutCountsZeroed = DSR_LAYOUT_COUNTS_ZEROED, kLayoutRectBinning = DSR_LAYOUT_RECT_BINNING;
+              kLayoutCountsZeroed = DSR_LAYOUT_COUNTS_ZEROED, kLayoutRectBinning = DSR_LAYOUT_RECT_BINNING,
+              kLayoutExactBinning = DSR_LAYOUT_EXACT_BINNING;
 __device__ __forceinline__ float load_cov(const float* cov, size_t sg, int k, int layout) {
   if (layout & kLayoutCovFull) {
     constexpr int idx[6] = {0, 1, 2, 4, 5, 8};
@@ -587,55 +588,6 @@ __device__ __forceinline__ void store_geom(float* __restrict__ geom, int32_t* __
   radii[vg] = r;
 }
 
-// K1: preprocess + per-(view, tile) entry counts (two-phase binning path).
-// grid = (ceil(G/256), V), block = 256. DEG = -1 -> colors_precomp path.
-template <int DEG>
-__global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, int gx, int gy, int M,
-                                                   const float* __restrict__ means,
-                                                   const float* __restrict__ shs,
-                                                   const float* __restrict__ colors,
-                                                   const float* __restrict__ opac,
-                                                   const float* __restrict__ cov6,
-                                                   const dsr_camera* __restrict__ cams,
-                                                   float* __restrict__ geom, int32_t* __restrict__ radii,
-                                                   uint32_t* __restrict__ seg_count, int lds_hist, int layout) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
-  int v, blk;
-  if (!xcd_pair((G + NT - 1) / NT, V, blk, v)) return;
-  const int T = gx * gy;
-  const int tid = threadIdx.x;
-  const dsr_camera* cam = cams + v;
-  if (lds_hist) {
-    for (int t = tid; t < T; t += NT) s_hist[t] = 0;
-    __syncthreads();
-  }
-  const int g = blk * NT + tid;
-  int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-  if (g < G) {
-    GaussIn<DEG> in;
-    load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
-    float rec[GS];
-    r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
-    store_geom(geom, radii, (size_t)v * G + g, rec, r);
-  }
-  uint32_t* gcount = seg_count + (size_t)v * T;
-  __shared__ WaveRects s_wr[NT / 64];
-  const int lane = tid & 63;
-  if (lds_hist)
-    for_each_rect_tile(s_wr[tid >> 6], lane, x0, y0, x1, y1, r > 0, gx,
-                       [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
-  else
-    for_each_rect_tile(s_wr[tid >> 6], lane, x0, y0, x1, y1, r > 0, gx,
-                       [&](int t, int) { atomicAdd(&gcount[t], 1u); });
-  if (lds_hist) {
-    __syncthreads();
-    for (int t = tid; t < T; t += NT) {
-      const uint32_t c = s_hist[t];
-      if (c) atomicAdd(&gcount[t], c);
-    }
-  }
-}
-
 // Exact tile test of the inference binning (k_project_emit EXACT): can the alpha >= 1/255 ellipse of a
 // Gaussian reach a pixel centre of the tile box [x0, x0 + BX - 1] x [y0, y0 + BY - 1]? The
 // same continuous-box minimum of the conic as the compositor's rect_hit (defined with it
@@ -707,6 +659,64 @@ __device__ __forceinline__ void tile_rect_alpha(const TileEll& e, int& x0, int& 
   }
 }
 
+// K1: preprocess + per-(view, tile) entry counts (two-phase binning path).
+// grid = (ceil(G/256), V), block = 256. DEG = -1 -> colors_precomp path.
+template <int DEG, bool EXACT>
+__global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, int gx, int gy, int M,
+                                                   const float* __restrict__ means,
+                                                   const float* __restrict__ shs,
+                                                   const float* __restrict__ colors,
+                                                   const float* __restrict__ opac,
+                                                   const float* __restrict__ cov6,
+                                                   const dsr_camera* __restrict__ cams,
+                                                   float* __restrict__ geom, int32_t* __restrict__ radii,
+                                                   uint32_t* __restrict__ seg_count, int lds_hist, int layout) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+  int v, blk;
+  if (!xcd_pair((G + NT - 1) / NT, V, blk, v)) return;
+  const int T = gx * gy;
+  const int tid = threadIdx.x;
+  const dsr_camera* cam = cams + v;
+  if (lds_hist) {
+    for (int t = tid; t < T; t += NT) s_hist[t] = 0;
+    __syncthreads();
+  }
+  const int g = blk * NT + tid;
+  int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+  TileEll ell{0.f, 0.f, 0.f, 0.f, 0.f, -1.f, 0.f, 0.f};
+  if (g < G) {
+    GaussIn<DEG> in;
+    load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
+    float rec[GS];
+    r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
+    store_geom(geom, radii, (size_t)v * G + g, rec, r);
+    if constexpr (EXACT) {  // same terms as k_scatter<true> recomputes from the stored record
+      ell = tile_ell(rec, r);
+      if (r > 0) tile_rect_alpha(ell, x0, y0, x1, y1);
+    }
+  }
+  uint32_t* gcount = seg_count + (size_t)v * T;
+  __shared__ WaveRects s_wr[NT / 64];
+  const int lane = tid & 63;
+  uint32_t* hist = lds_hist ? s_hist : gcount;
+  TileEll oe = ell;
+  for_each_rect_tile(s_wr[tid >> 6], lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int, int tx, int ty) {
+    if constexpr (EXACT) {
+      if (!tile_reach(oe, tx, ty)) return;
+    }
+    atomicAdd(&hist[t], 1u);
+  }, [&](int o) {
+    if constexpr (EXACT) oe = tile_ell_of(ell, o);
+  });
+  if (lds_hist) {
+    __syncthreads();
+    for (int t = tid; t < T; t += NT) {
+      const uint32_t c = s_hist[t];
+      if (c) atomicAdd(&gcount[t], c);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // K1+K3 fused (fixed-capacity binning): one workgroup per (256 Gaussians, view) projects
 // them, counts the block's (view, tile) entries in an LDS histogram, reserves a contiguous
@@ -720,9 +730,9 @@ __device__ __forceinline__ void tile_rect_alpha(const TileEll& e, int& x0, int& 
 constexpr int kProjectWPE = 1;
 // pair cache of the count pass (kPairCapW (tile, rank, owner) words per wave in LDS)
 constexpr int kPairCapW = 768;
-// EXACT (inference binning, CAM only): a pair is kept only when tile_reach says the
-// alpha >= 1/255 ellipse reaches the tile; the stateful / training path keeps the reference's
-// rect lists, which the backward and the oracle list tests follow.
+// EXACT: a pair is kept only when tile_reach says the alpha >= 1/255 ellipse reaches the tile
+// (the inference path by default, the stateful path with DSR_LAYOUT_EXACT_BINNING); else the
+// reference's 3-sigma rect lists, which the oracle list tests follow.
 template <int DEG, bool CAM, bool EXACT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE))) void k_project_emit(int G, int V, int H, int W, int gx, int gy, int M,
                                                      const float* __restrict__ means,
@@ -734,7 +744,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
                                                      float* __restrict__ geom, int32_t* __restrict__ radii,
                                                      uint32_t* __restrict__ seg_count,
                                                      uint64_t* __restrict__ keys, int layout, CamIn ci) {
-  static_assert(CAM || !EXACT, "exact binning is an inference-path (CAM) mode");
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
@@ -896,7 +905,9 @@ __host__ __device__ inline int cut_superblock(int gx, int gy) {
   return 0;
 }
 
-// K3: emit (depth, id) keys into their (view, tile) bucket.
+// K3: emit (depth, id) keys into their (view, tile) bucket. EXACT: keep the pairs
+// k_preprocess<DEG, true> counted (same tile test on the stored record).
+template <bool EXACT>
 __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, const float* __restrict__ geom,
                                                 uint32_t* __restrict__ cursor,
                                                 uint64_t* __restrict__ keys, int lds_hist) {
@@ -912,14 +923,23 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
   const int g = blk * NT + tid;
   int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
   uint64_t key = 0;
+  TileEll ell{0.f, 0.f, 0.f, 0.f, 0.f, -1.f, 0.f, 0.f};
   if (g < G) {
     const float* rec = geom + ((size_t)v * G + g) * GS;
     r = __float_as_int(rec[10]);
     if (r > 0) {
       tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
       key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
+      if constexpr (EXACT) {
+        ell = tile_ell(rec, r);
+        tile_rect_alpha(ell, x0, y0, x1, y1);
+      }
     }
   }
+  TileEll oe = ell;
+  const auto fetch = [&](int o) {
+    if constexpr (EXACT) oe = tile_ell_of(ell, o);
+  };
   uint32_t* gcur = cursor + (size_t)v * T;
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
@@ -927,19 +947,27 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
   s_key[tid] = key;
   WaveRects& wr = s_wr[w];
   const uint64_t* wkey = s_key + w * 64;
+  const auto keep = [&](int tx, int ty) {
+    if constexpr (EXACT) return tile_reach(oe, tx, ty);
+    return true;
+  };
   if (lds_hist) {
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int) { atomicAdd(&s_hist[t], 1u); });
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int, int tx, int ty) {
+      if (keep(tx, ty)) atomicAdd(&s_hist[t], 1u);
+    }, fetch);
     __syncthreads();
     for (int t = tid; t < T; t += NT) {
       const uint32_t c = s_hist[t];
       if (c) s_hist[t] = atomicAdd(&gcur[t], c);
     }
     __syncthreads();
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
-                       [&](int t, int o) { keys[atomicAdd(&s_hist[t], 1u)] = wkey[o]; });
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
+      if (keep(tx, ty)) keys[atomicAdd(&s_hist[t], 1u)] = wkey[o];
+    }, fetch);
   } else {
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx,
-                       [&](int t, int o) { keys[atomicAdd(&gcur[t], 1u)] = wkey[o]; });
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
+      if (keep(tx, ty)) keys[atomicAdd(&gcur[t], 1u)] = wkey[o];
+    }, fetch);
   }
 }
 
@@ -2954,9 +2982,15 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   const int lds = lds_hist_bytes(T);
   const unsigned grid = xcd_grid((G + NT - 1) / NT, V);
   const int deg = shs ? sh_degree : -1;
-#define DSR_PRE(D)                                                                                        \
-  k_preprocess<D><<<grid, NT, lds, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, \
-                                         geom, radii, seg_count, lds > 0, layout)
+#define DSR_PRE(D)                                                                                              \
+  do {                                                                                                         \
+    if (layout & kLayoutExactBinning)                                                                          \
+      k_preprocess<D, true><<<grid, NT, lds, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, \
+                                                   cams, geom, radii, seg_count, lds > 0, layout);             \
+    else                                                                                                       \
+      k_preprocess<D, false><<<grid, NT, lds, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities,      \
+                                                    cov6, cams, geom, radii, seg_count, lds > 0, layout);      \
+  } while (0)
   switch (deg) {
     case -1: DSR_PRE(-1); break;
     case 0: DSR_PRE(0); break;
@@ -2997,6 +3031,10 @@ int project_bin_impl(const char* who, int S, int G, int V, int H, int W, int sh_
       k_project_emit<D, true, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,        \
                                                               opacities, cov6, cams, geom, radii, seg_count,    \
                                                               keys, layout, *ci);                               \
+    else if (layout & kLayoutExactBinning)                                                                     \
+      k_project_emit<D, false, true><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,        \
+                                                              opacities, cov6, cams, geom, radii, seg_count,    \
+                                                              keys, layout, CamIn{});                           \
     else                                                                                                       \
       k_project_emit<D, false, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,       \
                                                                opacities, cov6, cams, geom, radii, seg_count,   \
@@ -3045,13 +3083,16 @@ int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_s
 }
 
 int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor, uint64_t* keys,
-                    void* stream) {
+                    int layout, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_scatter: bad sizes");
   DSPLAT_REQUIRE(geom && seg_cursor, "dsr_bin_scatter: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   const int lds = lds_hist_bytes(gx * gy);
-  k_scatter<<<xcd_grid((G + NT - 1) / NT, V), NT, lds, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor, keys,
-                                                                              lds > 0);
+  const unsigned grid = xcd_grid((G + NT - 1) / NT, V);
+  if (layout & kLayoutExactBinning)
+    k_scatter<true><<<grid, NT, lds, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor, keys, lds > 0);
+  else
+    k_scatter<false><<<grid, NT, lds, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor, keys, lds > 0);
   return dsplat::check_launch("k_scatter");
 }
 

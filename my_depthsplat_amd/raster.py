@@ -203,6 +203,14 @@ INKERNEL_CAMERAS = os.environ.get("DSPLAT_INKERNEL_CAMERAS", "1") != "0"
 # 3-sigma rects (DSR_LAYOUT_RECT_BINNING; bench.py reports both throughputs).
 EXACT_BINNING = os.environ.get("DSPLAT_EXACT_BINNING", "1") != "0"
 LAYOUT_RECT_BINNING = 8
+# The same exact test on the stateful (training) path, in the fixed-capacity and plain
+# two-phase layouts (DSR_LAYOUT_EXACT_BINNING; the depth-cut layout keeps 3-sigma rects): the
+# lists are order-preserving subsequences of the reference's, the dropped pairs fail the
+# per-pixel alpha test at every pixel of their tile, so images and gradients are unchanged
+# (tests/test_raster_gpu.py) while the sort, the forward and the backward walk about half the
+# entries. Off: the reference's lists exactly (the oracle list tests switch it off).
+STATEFUL_EXACT_BINNING = os.environ.get("DSPLAT_STATEFUL_EXACT_BINNING", "1") != "0"
+LAYOUT_EXACT_BINNING = 16
 # Test hook (tests/test_fullsize_parity.py): the fast path also snapshots its per-tile counts
 # and writes its sorted keys back, so its lists can be compared with the oracle's. It adds a
 # copy and the key stores; the product never sets it.
@@ -449,6 +457,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                 geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout, st),
                 "dsr_project_bin_cameras")
         else:
+            if STATEFUL_EXACT_BINNING:
+                layout |= LAYOUT_EXACT_BINNING
             _lib.check(_timed("k_project_emit", lib.dsr_project_bin,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                 cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout,
@@ -474,6 +484,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                 cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), hist.data_ptr(), layout,
                 st), "dsr_preprocess_cut")
         else:
+            if STATEFUL_EXACT_BINNING:  # the scatter below repeats the same test
+                layout |= LAYOUT_EXACT_BINNING
             _lib.check(_timed("k_preprocess", lib.dsr_preprocess_fwd,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                 cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), layout, st),
@@ -510,8 +522,9 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             seg_sorted = None
         else:
             scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev) if maxc > lds_cap else None
+            # (counted by dsr_preprocess_cut when the cut was planned: 3-sigma rects, no exact bit)
             _lib.check(_timed("k_scatter", lib.dsr_bin_scatter, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
-                              keys.data_ptr(), st), "dsr_bin_scatter")
+                              keys.data_ptr(), layout & LAYOUT_EXACT_BINNING, st), "dsr_bin_scatter")
             ws = _sort_workspace(lib, V, H, W, maxc, dev)
             stride = 0
             seg_sorted = _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, maxc, ws, st,
@@ -535,6 +548,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             # in the pruned lists (a subsequence of the reference's), not in the 3-sigma lists
             state.seg_count = snap
             state.pruned_lists = not (layout & LAYOUT_RECT_BINNING)
+        else:
+            state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING)
         _last["counts"] = None if fast else state.counts
         return color, state
     overflow = None
@@ -559,6 +574,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                       *outs), "dsr_render_fwd(overflow)")
     state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, seg_sorted, overflow,
                         tile_count if stride == SEG_ENDS else None, cams=cams)
+    state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING) and stride != SEG_ENDS
     _last["counts"] = state.counts
     return color, state
 

@@ -1,10 +1,11 @@
 """Parity of the rasterizer at the BASELINE configurations' full sizes (HIP vs oracle).
 
 * config B (2-view 256x256 context -> G = 131,072; 3 target views): the stateful path
-  (reference 3-sigma binning; what training uses) and the inference fast path that
-  bench.py times (cameras built in float inside the binning kernel, exact tile binning).
-  Stateful: geometry and every per-tile sorted list bit-exact, images within the
-  north_star bars. Fast path: the oracle is fed the camera block the kernel built (so
+  (what training uses) with the reference's 3-sigma binning and with exact binning (the
+  product default), and the inference fast path that bench.py times (cameras built in float
+  inside the binning kernel, exact tile binning). Stateful, reference binning: geometry and
+  every per-tile sorted list bit-exact, images within the north_star bars; exact binning:
+  lists are subsequences as below, last contributors equal the oracle's. Fast path: the oracle is fed the camera block the kernel built (so
   geometry and keys are comparable bit for bit); every per-tile list is an order-preserving
   subsequence of the oracle's 3-sigma list, every pair it drops fails alpha >= 1/255 at
   every pixel of its tile, and its images equal those of the same kernel with the
@@ -118,37 +119,67 @@ def _gpu_scene(sc, gpu):
     return [t.to(gpu) for t in (g.means, g.covariances, g.harmonics, g.opacities)]
 
 
-def test_config_b_stateful_path_vs_oracle(gpu):
-    """Config B at full size through the stateful (reference-binning) path, all 3 views."""
+@pytest.mark.parametrize("exact", [False, True])
+def test_config_b_stateful_path_vs_oracle(gpu, exact, monkeypatch):
+    """Config B at full size through the stateful (training) path, all 3 views. exact=False:
+    the reference's 3-sigma binning, every per-tile list bit-exact. exact=True (the product
+    default, DSR_LAYOUT_EXACT_BINNING): every list is an order-preserving subsequence of the
+    oracle's, every dropped pair fails the alpha test at every pixel of its tile, and each
+    pixel's last contributor (n_contrib, a position in the shorter list) is the oracle's."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setattr(raster, "STATEFUL_EXACT_BINNING", exact)
     sc = scene_inputs(h=256, w=256, n_ctx=2, n_tgt=3, seed=1000)
     st = settings_for(sc)
-    from my_depthsplat_amd import raster
     means, shs, opac, cov6 = flat_inputs(sc)
     cams = packed_cams(st, [0, 0, 0]).to(gpu)
     color, state = raster.forward_raw(means.to(gpu), shs.to(gpu), True, 2, opac.to(gpu), cov6.to(gpu), cams, 3,
                                       256, 256)
     torch.cuda.synchronize()
-    assert state.seg_stride > 0 and not state.pruned_lists
+    assert state.seg_stride > 0 and state.pruned_lists == exact
     col, geom, radii = color.cpu().numpy(), state.geom.cpu().numpy(), state.radii.cpu().numpy()
     ncon = state.n_contrib.cpu().numpy()
     begin, end, keys = _segments(state, 3, 256)
+    n_hip = n_ref = 0
     for v, o in enumerate(oracle_views(sc, st)):
-        _check_geometry(geom[v], radii[v], o.geom())
+        og = o.geom()
+        _check_geometry(geom[v], radii[v], og)
         okeys, ovals, ranges = o.binning()
-        assert int(state.counts[v * 256:(v + 1) * 256].sum()) == o.num_rendered
+        oc, ot, on = o.image()
+        last_agree = 0
         for t in range(256):
             hk = keys[begin[v * 256 + t]:end[v * 256 + t]]
+            ids = (hk & np.uint64(0xFFFFFFFF)).astype(np.uint32)
             ob, oe = ranges[t]
-            np.testing.assert_array_equal((hk & np.uint64(0xFFFFFFFF)).astype(np.uint32), ovals[ob:oe])
-            np.testing.assert_array_equal((hk >> np.uint64(32)).astype(np.uint32),
-                                          (okeys[ob:oe] & np.uint64(0xFFFFFFFF)).astype(np.uint32))
-        oc, ot, on = o.image()
+            oids = ovals[ob:oe]
+            n_hip += len(ids)
+            n_ref += len(oids)
+            if not exact:
+                np.testing.assert_array_equal(ids, oids)
+                np.testing.assert_array_equal((hk >> np.uint64(32)).astype(np.uint32),
+                                              (okeys[ob:oe] & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+                continue
+            keep = np.isin(oids, ids)
+            np.testing.assert_array_equal(oids[keep], ids)  # subsequence, order kept
+            dropped = oids[~keep]
+            if len(dropped):
+                assert not _alpha_reaches_tile(og, dropped.astype(np.int64), t % 16, t // 16, 256, 256).any()
+            ty, tx = divmod(t, 16)
+            nh = ncon[v, ty * 16:ty * 16 + 16, tx * 16:tx * 16 + 16].reshape(-1).astype(np.int64)
+            no = on[ty * 16:ty * 16 + 16, tx * 16:tx * 16 + 16].reshape(-1).astype(np.int64)
+            lh = np.where(nh > 0, ids[np.maximum(nh - 1, 0)] if len(ids) else 0, -1)
+            lo = np.where(no > 0, oids[np.maximum(no - 1, 0)] if len(oids) else 0, -1)
+            last_agree += int((lh == lo).sum())
+        if not exact:
+            assert int(state.counts[v * 256:(v + 1) * 256].sum()) == o.num_rendered
         l1, mx, dp = _image_bars(col[v], oc, f"stateful view {v}")
-        agree = float((ncon[v] == on).mean())
+        agree = float((ncon[v] == on).mean()) if not exact else last_agree / (256 * 256)
         assert agree > 0.999, agree
-        _report(test="config_b_stateful", view=v, l1=l1, max_abs=mx, dpsnr=dp, n_contrib_agree=agree,
-                num_rendered=int(o.num_rendered))
+        _report(test=f"config_b_stateful{'_exact' if exact else ''}", view=v, l1=l1, max_abs=mx, dpsnr=dp,
+                n_contrib_agree=agree, num_rendered=int(o.num_rendered))
         o.close()
+    if exact:
+        assert n_hip < n_ref
+        _report(test="config_b_stateful_exact_entries", exact=n_hip, reference=n_ref)
 
 
 def _fast_forward(g, sc, gpu, exact: bool, monkeypatch):

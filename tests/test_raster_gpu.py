@@ -18,6 +18,16 @@ from raster_cases import flat_inputs, oracle_views, packed_cams, scene_inputs, s
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def reference_lists(monkeypatch):
+    """Most tests here compare the per-tile lists with the oracle's 3-sigma lists: run the
+    stateful path with the reference's binning (raster.STATEFUL_EXACT_BINNING off). The
+    product default (exact binning) is covered by test_stateful_exact_binning below and by the
+    drop-in module / full-size parity tests."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setattr(raster, "STATEFUL_EXACT_BINNING", False)
+
+
 def hip_forward(sc, st, gpu, use_sh=True, bg=(0.0, 0.0, 0.0)):
     from my_depthsplat_amd import raster
     means, shs, opac, cov6 = flat_inputs(sc)
@@ -736,3 +746,74 @@ def test_inference_exact_tile_binning(gpu, case):
     torch.cuda.synchronize()
     assert float((img - ref).abs().mean()) < 1e-5, case
     assert float((img - ref).abs().max()) < 2e-2, case
+
+
+@pytest.mark.parametrize("layout", ["fixed", "two_phase"])
+@pytest.mark.parametrize("case", ["default", "large", "anisotropic", "low_opacity"])
+def test_stateful_exact_binning(gpu, layout, case, monkeypatch):
+    """The stateful (training) path with exact tile binning (DSR_LAYOUT_EXACT_BINNING: the
+    product default) against the same forward + backward on the reference's 3-sigma lists:
+    every exact list is an order-preserving subsequence of the reference list, the images and
+    final T are bit-identical (dropped pairs fail the alpha >= 1/255 test at every pixel of
+    their tile), and the gradients agree to float-atomic reordering. Both key layouts: the
+    fixed-capacity dsr_project_bin and the two-phase preprocess / scan / scatter."""
+    from my_depthsplat_amd import raster
+    sc = scene_inputs(h=64, w=96, seed=31, n_tgt=2)
+    g = sc.gaussians
+    if case == "large":
+        g.covariances = g.covariances * 30.0
+    elif case == "anisotropic":
+        sv = torch.tensor([6.0, 0.15, 1.0])
+        g.covariances = g.covariances * 20.0 * sv[:, None] * sv[None, :]
+    elif case == "low_opacity":
+        u = torch.rand(g.opacities.shape, generator=torch.Generator().manual_seed(5))
+        g.opacities = torch.where(u < 0.3, torch.full_like(u, 0.5 / 255.0),
+                                  torch.where(u < 0.6, torch.full_like(u, 1.5 / 255.0), g.opacities))
+        g.covariances = g.covariances * 10.0
+    st = settings_for(sc)
+    if layout == "two_phase":
+        monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+        monkeypatch.setattr(raster, "CUT_PREFIX", 0)
+    means, shs, opac, cov6 = flat_inputs(sc)
+    B, v = sc.target_extrinsics.shape[:2]
+    h, w = sc.image_shape
+    gx, gy = raster.tiles(h, w)
+    T = gx * gy
+    dpix = torch.randn(B * v, 3, h, w, generator=torch.Generator().manual_seed(9)).to(gpu)
+    runs = {}
+    for exact in (False, True):
+        monkeypatch.setattr(raster, "STATEFUL_EXACT_BINNING", exact)
+        color, state, cams = hip_forward(sc, st, gpu)
+        assert state.pruned_lists == exact
+        assert (state.seg_stride > 0) == (layout == "fixed")
+        grads = raster.backward_raw(means.to(gpu), shs.to(gpu), True, 2, opac.to(gpu), cov6.to(gpu), cams,
+                                    [i // v for i in range(B * v)], state, dpix, want_mean2d=True)
+        torch.cuda.synchronize()
+        runs[exact] = (color, state, grads)
+    (c0, s0, g0), (c1, s1, g1) = runs[False], runs[True]
+    assert torch.equal(c1, c0) and torch.equal(s1.final_T, s0.final_T)
+    b0, e0, k0 = _segments(s0, B * v, T)
+    b1, e1, k1 = _segments(s1, B * v, T)
+    n0, n1 = int((e0 - b0).sum()), int((e1 - b1).sum())
+    assert n1 <= n0
+    if case != "default":
+        assert n1 < n0  # something was dropped
+    # long two-phase segments are prefix-sorted (seg_sorted: the nearest >= 1024 entries in
+    # order, the tail unordered): compare as sets, and the sorted parts for order
+    p0 = None if s0.seg_sorted is None else s0.seg_sorted.cpu().numpy()
+    p1 = None if s1.seg_sorted is None else s1.seg_sorted.cpu().numpy()
+    for sg in range(B * v * T):
+        ref = k0[b0[sg]:e0[sg]]
+        sub = k1[b1[sg]:e1[sg]]
+        assert np.isin(sub, ref).all(), sg
+        n_sorted = len(sub) if p1 is None else int(p1[sg])
+        assert np.all(sub[1:n_sorted] > sub[:n_sorted - 1]), sg  # keys are distinct
+        if p0 is None and p1 is None:  # both fully sorted: sub keeps ref's order
+            keep = np.isin(ref, sub)
+            assert np.array_equal(ref[keep], sub), sg
+    for a, b_, name in zip(g1, g0, ("means", "shs", "opacity", "cov6", "mean2d")):
+        if a is None:
+            continue
+        scale = float(b_.abs().max()) + 1e-12
+        err = float((a - b_).abs().max()) / scale
+        assert err < 1e-4, (case, layout, name, err)

@@ -136,7 +136,7 @@ def main():
 
             def launch():
                 cur.copy_(state.seg_start)
-                return lib.dsr_bin_scatter(G, V, H, W, state.geom.data_ptr(), cur.data_ptr(), keys3.data_ptr(), st)
+                return lib.dsr_bin_scatter(G, V, H, W, state.geom.data_ptr(), cur.data_ptr(), keys3.data_ptr(), 0, st)
         elif a.kernel == "sort_sorted":  # re-sort the (already sorted) keys in place: pass cost only
             tot3 = torch.empty(4, dtype=torch.int32, device=dev)
             scr = torch.empty_like(state.keys)
