@@ -2563,21 +2563,18 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
   float Tr = Tfin;
   float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
   float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f, last_alpha = 0.f;
-  for (int hi = (int)nproc; hi > 0; hi -= BCH) {
-    const int lo = max(0, hi - BCH);
-    const uint32_t e = start + (uint32_t)(lo + lane);
-    bool mine = false;
-    float4 q = make_float4(0.f, 0.f, 0.f, 0.f), r = q;
-    float bl = 0.f;
-    uint32_t id = 0;
-    if (lo + lane < hi) {
-      id = (uint32_t)keys[e];
-      const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
-      q = rec[0];
-      r = rec[1];
-      bl = rec[2].x;
-      mine = subtile_hit(q, r, fx0, fy0);
-    }
+  // chunk c covers list positions [hi_c - BCH, hi_c), hi_c = nproc - c * BCH (back to front).
+  // Entry ids and records of the first PD chunks are gathered in one batch up front, later
+  // chunks one ahead (a wave walks ~3 chunks: one memory round trip instead of one per chunk).
+  const int nch = (int)((nproc + BCH - 1) / BCH);
+  auto id_at = [&](int c) -> uint32_t {  // unconditional key read (clamped), id 0 past the range
+    const int pos = (int)nproc - (c + 1) * BCH + lane;
+    const uint32_t k = (uint32_t)keys[start + (uint32_t)min(max(pos, 0), max((int)nproc - 1, 0))];
+    return (pos >= 0 && c < nch) ? k : 0u;
+  };
+  auto chunk = [&](int ch, uint32_t id, float4 q, float4 r, float bl) {
+    const int p = (int)nproc - (ch + 1) * BCH + lane;  // this lane's list position (< 0: none)
+    const bool mine = p >= 0 && subtile_hit(q, r, fx0, fy0);
     const uint64_t bal = __ballot(mine);
     if (mine) {
       BwdRec& d = list[__popcll(bal & lt)];
@@ -2586,7 +2583,7 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
       d.r = make_float4(sq.w, r.y, r.z, r.w);
       d.s = make_float4(bl, q.z, q.w, r.x);
       d.id = id;
-      d.pos = (uint32_t)(lo + lane);
+      d.pos = (uint32_t)p;
     }
     const int cnt = __popcll(bal);
     __builtin_amdgcn_wave_barrier();
@@ -2671,6 +2668,30 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
         atomicAdd(&dgv[(size_t)list[k].id * GS + (i - k * 9)], a);
     }
     __builtin_amdgcn_wave_barrier();
+  };
+  uint32_t ids[PD];
+  float4 q[PD], r[PD];
+  float bl[PD];
+#pragma unroll
+  for (int c = 0; c < PD; ++c) ids[c] = id_at(c);
+#pragma unroll
+  for (int c = 0; c < PD; ++c) {
+    const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)ids[c] * GS);
+    q[c] = rec[0];
+    r[c] = rec[1];
+    bl[c] = rec[2].x;
+  }
+  uint32_t nid = id_at(PD);
+#pragma unroll
+  for (int c = 0; c < PD; ++c)
+    if (c < nch) chunk(c, ids[c], q[c], r[c], bl[c]);
+  for (int c = PD; c < nch; ++c) {
+    const uint32_t id = nid;
+    const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
+    const float4 cq = rec[0], cr = rec[1];
+    const float cb = rec[2].x;
+    nid = id_at(c + 1);
+    chunk(c, id, cq, cr, cb);
   }
 }
 

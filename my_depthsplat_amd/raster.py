@@ -177,10 +177,26 @@ class RasterState:
 # Key-buffer sizing. N (the number of (view, tile, Gaussian) entries) is only known on the
 # device after the scan. Instead of reading it back mid-pipeline (the reference's per-view
 # D2H + .item() syncs), the key buffers are sized by the exact worst case V*G*tiles when
-# that fits KEY_BUDGET_BYTES (1.6 GB at 2x256^2 x 3 views: cheap on a 288 GB part, and
-# untouched pages cost no bandwidth); the whole forward then runs with NO host sync.
+# that fits KEY_BUDGET_BYTES (1.6 GB at 2x256^2 x 3 views; 34 GB for config C's 64 training
+# views: cheap on a 288 GB part, and untouched pages cost no bandwidth); the whole forward
+# then runs with NO host sync and the projection emits keys directly (no scan / scatter).
 # Larger problems fall back to one 8-byte read of (N, max tile count) after the scan.
-KEY_BUDGET_BYTES = int(float(os.environ.get("DSPLAT_KEY_BUDGET_GB", "8")) * (1 << 30))
+# None = automatic: 48 GiB, at most 40 % of the device's memory (env DSPLAT_KEY_BUDGET_GB
+# overrides; tests set 0 to force the two-phase layout).
+_kb_env = os.environ.get("DSPLAT_KEY_BUDGET_GB")
+KEY_BUDGET_BYTES = None if _kb_env is None else int(float(_kb_env) * (1 << 30))
+_auto_budget: dict = {}
+
+
+def key_budget(device) -> int:
+    if KEY_BUDGET_BYTES is not None:
+        return KEY_BUDGET_BYTES
+    idx = torch.device(device).index or 0
+    b = _auto_budget.get(idx)
+    if b is None:
+        total = torch.cuda.get_device_properties(idx).total_memory
+        b = _auto_budget[idx] = int(min(48 * (1 << 30), 0.4 * total))
+    return b
 # Segments larger than this many entries (only when some exceed the LDS sort) get only their
 # nearest SORT_PREFIX entries put in order (dsr_bin_sort prefix mode): at 6x448x768 the
 # compositor uses at most ~1.2K of 30-40K entries per tile. 0 sorts everything.
@@ -242,14 +258,15 @@ def _note_counts(counts: torch.Tensor) -> None:
 _ws_cache: dict = {}
 
 
-def workspace(G: int, H: int, W: int, V: int) -> _lib.Workspace:
+def workspace(G: int, H: int, W: int, V: int, device=None) -> _lib.Workspace:
     """dsr_workspace_size: the bytes of every buffer of one call sequence and whether the
-    sync-free fixed-capacity layout fits KEY_BUDGET_BYTES (the C ABI's own sizing rule)."""
-    key = (G, H, W, V, KEY_BUDGET_BYTES)
+    sync-free fixed-capacity layout fits the key budget (the C ABI's own sizing rule)."""
+    budget = key_budget(device if device is not None else torch.cuda.current_device())
+    key = (G, H, W, V, budget)
     ws = _ws_cache.get(key)
     if ws is None:
         ws = _lib.Workspace()
-        _lib.check(_lib.load().dsr_workspace_size(G, H, W, V, KEY_BUDGET_BYTES, _lib.ctypes.byref(ws)),
+        _lib.check(_lib.load().dsr_workspace_size(G, H, W, V, budget, _lib.ctypes.byref(ws)),
                    "dsr_workspace_size")
         if len(_ws_cache) > 256:
             _ws_cache.clear()
@@ -419,7 +436,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
     radii = torch.empty((V, G), dtype=torch.int32, device=dev)
     lds_cap = lib.dsr_sort_lds_capacity()
-    fixed = bool(workspace(G, H, W, V).fixed_capacity)
+    fixed = bool(workspace(G, H, W, V, dev).fixed_capacity)
     maxc_hint = _spec["max_count"] or lds_cap
     fused = fixed and FUSED_SORT_RENDER and maxc_hint <= FUSED_MAX
     # eager inference fast path: cameras set up inside the binning kernel, counters taken zeroed
@@ -496,7 +513,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         _lib.check(_timed("k_scan", lib.dsr_bin_scan, V, H, W, seg_count.data_ptr(), seg_start.data_ptr(),
                           cursor.data_ptr(), totals.data_ptr(), st), "dsr_bin_scan")
         if torch.cuda.is_current_stream_capturing():
-            raise _lib.DsplatError(f"V*G*tiles = {V * G * T} key slots exceed KEY_BUDGET_BYTES: this size needs a "
+            raise _lib.DsplatError(f"V*G*tiles = {V * G * T} key slots exceed the key budget: this size needs a "
                                    "host read-back and cannot be captured into a graph")
         tot = totals[:3].cpu()  # one small read-back: N sizes the key buffer
         N, maxc = int(tot[0]), int(tot[1])
