@@ -63,7 +63,8 @@ def main():
         objs = []
         for s in sorted(d.glob("*.hip")):
             o = d / (s.stem + ".o")
-            r = subprocess.run([_build.HIPCC, *_build.CFLAGS, "-c", str(s), "-o", str(o)], capture_output=True, text=True)
+            r = subprocess.run([_build.HIPCC, *_build.CFLAGS, *_build.FILE_FLAGS.get(s.name, []), "-c", str(s), "-o", str(o)],
+                               capture_output=True, text=True)
             if r.returncode:
                 raise SystemExit(r.stderr)
             objs.append(str(o))

@@ -21,7 +21,7 @@ def build(name, flags):
     objs = []
     for s in _build._sources():
         o = d / (s.stem + ".o")
-        r = subprocess.run([_build.HIPCC, *_build.CFLAGS, *flags, "-c", str(s), "-o", str(o)], capture_output=True,
+        r = subprocess.run([_build.HIPCC, *_build.CFLAGS, *_build.FILE_FLAGS.get(s.name, []), *flags, "-c", str(s), "-o", str(o)], capture_output=True,
                            text=True)
         if r.returncode:
             raise RuntimeError(f"{name}: {s.name}\n{r.stderr}")
