@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)  # ~30 ms timed at ~60 us per scene
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--batch", type=int, default=1, help="scenes per step per GPU (reference test loop: 1)")
+    p.add_argument("--batch", type=int, default=0,
+                   help="scenes per step per GPU (reference test loop: 1); 0 = calibrate over 1, 2, 4")
     p.add_argument("--views", type=int, default=3, help="target views per scene (RE10K eval: 3)")
     p.add_argument("--size", type=int, default=256)
     p.add_argument("--context", type=int, default=2)
@@ -55,7 +56,8 @@ def parse():
                    help="skip the 3-sigma-binning timed region (profiling passes: one kernel variant per name)")
     p.add_argument("--eager", action="store_true", help="time eager launches only (no hipGraph capture)")
     p.add_argument("--launch", choices=["auto", "hipgraph", "eager"] + [f"hipgraph{n}" for n in range(2, 9)], default="auto",
-                   help="launch mode of the timed region (auto: the fastest in a short calibration of all)")
+                   help="launch mode of the timed region (auto: the fastest per scene in a short calibration of "
+                        "all modes and batch sizes; a fixed mode takes --batch, default 1)")
     p.add_argument("--extra", default="train,dl3dv,recon12,costvol,train_d",
                    help="secondary measurements: train (config C step), dl3dv (6-view 448x768 render), "
                         "recon12 (12-view 512x960 reconstruction, 100 views in chunks of 10), costvol (plane-sweep "
@@ -86,10 +88,7 @@ def main():
     _lib.load()
     H = W = args.size
     max_lanes = 1 if args.eager else int(os.environ.get("DSPLAT_BENCH_MAX_LANES", "4"))
-    # one resident scene per in-flight lane (distinct Gaussians: the lanes do not share inputs)
-    scenes = [make_scene(batch=args.batch, n_context=args.context, n_targets=args.views, height=H, width=W,
-                         seed=1000 + 16 * rank + lane, device=dev) for lane in range(max_lanes)]
-    sc = scenes[0]
+    batches = [args.batch] if args.batch else ([1, 2, 4] if args.launch == "auto" and not args.eager else [1])
     dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
 
     def step_of(s):
@@ -98,20 +97,12 @@ def main():
                 return dec(s.gaussians, s.target_extrinsics, s.target_intrinsics, s.near, s.far, (H, W))
         return step
 
-    steps = [step_of(s) for s in scenes]
-    step = steps[0]
-    for _ in range(args.warmup):
-        out = step()
-    torch.cuda.synchronize()
-    n_rendered = raster.last_stats()["num_rendered"]  # also primes the LDS-sort size hint
-    # short eager pass timing every launch -> the dominant kernel
-    probe = raster.KernelTimer()
-    raster.set_timer(probe)
-    for _ in range(max(3, args.warmup)):
-        out = step()
-    raster.set_timer(None)
-    dominant = max(probe.summary().items(), key=lambda kv: kv[1][0] * kv[1][1])[0]
-    all_kernels = probe.summary()
+    # per batch size B (scenes per step): one resident batch of B distinct scenes per in-flight
+    # lane (the lanes do not share inputs: seed = 1000 + 64 rank + 16 lane + B)
+    scenes = {B: [make_scene(batch=B, n_context=args.context, n_targets=args.views, height=H, width=W,
+                             seed=1000 + 64 * rank + 16 * lane + B, device=dev) for lane in range(max_lanes)]
+              for B in batches}
+    steps = {B: [step_of(sc_) for sc_ in scenes[B]] for B in batches}
 
     def timed(fn, nsteps):
         if world > 1:
@@ -132,13 +123,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return tuple(float(x) for x in t.tolist())
 
-    # launch mode: the whole decoder call replayed as ONE hipGraph per step, or launched
-    # eagerly; "hipgraphN" (N = 2..4): N captures, one per lane (own scene, own buffers),
-    # replayed in turn on N HIP streams so consecutive scenes overlap — one scene's compositing
-    # tail shares the chip with the next scene's binning. Every step renders a whole scene.
-    def build_modes():
+    # launch mode: the whole decoder call of a B-scene batch replayed as ONE hipGraph per step,
+    # or launched eagerly; "hipgraphN" (N = 2..4): N captures, one per lane (own scenes, own
+    # buffers), replayed in turn on N HIP streams so consecutive batches overlap — one batch's
+    # compositing tail shares the chip with the next one's binning. B scenes per launch pair
+    # fill the chip's workgroup slots several times over, so tiles of different scenes balance
+    # each other inside one launch (no reliance on cross-stream overlap). Every step renders B
+    # whole scenes; the calibration picks (B, mode) by time per scene.
+    def build_modes(B):
         from my_depthsplat_amd.graphs import GraphedCall
-        graphs = [GraphedCall(fn, warmup=2) for fn in steps]
+        graphs = [GraphedCall(fn, warmup=2) for fn in steps[B]]
         lanes = [torch.cuda.Stream(device=dev) for _ in graphs]
         turn = [0]
 
@@ -149,28 +143,58 @@ def main():
                 with torch.cuda.stream(lanes[i]):
                     return graphs[i]()
             return run
-        modes = {"hipgraph": graphs[0], **{f"hipgraph{n}": multi_stream(n) for n in range(2, len(graphs) + 1)},
-                 "eager": step}
+        modes = {"hipgraph": graphs[0], **{f"hipgraph{n}": multi_stream(n) for n in range(2, len(graphs) + 1)}}
         return modes, graphs
 
-    runner, mode, cal, graphs = step, "eager", None, []
-    if not args.eager:
-        modes, graphs = build_modes()
-        if args.launch == "auto":
-            ncal = max(10, min(50, args.steps))
-            names = list(modes)
-            cal = dict(zip(names, max_over_ranks(*[timed(modes[m], ncal) for m in names])))
-            mode = min(cal, key=cal.get)  # every rank takes the same decision
-            cal = {m: round(1e3 * t / ncal, 4) for m, t in cal.items()}
-        else:
-            mode = args.launch
+    for B in batches:
+        for _ in range(args.warmup):
+            steps[B][0]()
+    torch.cuda.synchronize()
+    B, runner, mode, cal, graphs = batches[0], steps[batches[0]][0], "eager", None, []
+    if args.eager:
+        cal = None
+    elif args.launch == "auto":
+        ncal = max(10, min(50, args.steps))
+        cal, best = {}, None
+        for b_ in batches:
+            modes_b, graphs_b = build_modes(b_)
+            modes_b["eager"] = steps[b_][0]
+            names = list(modes_b)
+            ts = max_over_ranks(*[timed(modes_b[m], ncal) for m in names])
+            for m, t in zip(names, ts):
+                per_scene = t / ncal / b_
+                cal[f"b{b_}:{m}"] = round(1e3 * per_scene, 4)
+                if best is None or per_scene < best[0]:  # every rank takes the same decision
+                    best = (per_scene, b_, m)
+            del modes_b, graphs_b
+        _, B, mode = best
+        torch.cuda.empty_cache()
+    else:
+        mode = args.launch
+    step = steps[B][0]
+    sc = scenes[B][0]
+    if mode != "eager":
+        modes, graphs = build_modes(B)
         runner = modes[mode]
+    else:
+        runner = step
+    out = step()
+    torch.cuda.synchronize()
+    n_rendered = raster.last_stats()["num_rendered"]  # one step (B scenes); also primes the sort hint
+    # short eager pass timing every launch -> the dominant kernel
+    probe = raster.KernelTimer()
+    raster.set_timer(probe)
+    for _ in range(max(3, args.warmup)):
+        out = step()
+    raster.set_timer(None)
+    dominant = max(probe.summary().items(), key=lambda kv: kv[1][0] * kv[1][1])[0]
+    all_kernels = probe.summary()
     lanes_used = int(mode[len("hipgraph"):] or 1) if mode.startswith("hipgraph") else 1
     # timed region 1 (value): exactly K steps in the chosen mode
     elapsed = timed(runner, args.steps)
-    # every capture in use rendered its own scene exactly as an eager call does
+    # every capture in use rendered its own scenes exactly as an eager call does
     for i in range(lanes_used if graphs else 0):
-        assert torch.equal(graphs[i].out.color, steps[i]().color), f"lane {i} of {mode} differs from eager"
+        assert torch.equal(graphs[i].out.color, steps[B][i]().color), f"lane {i} of {mode} differs from eager"
     # timed region 2: the same K steps in the same mode with the reference's 3-sigma tile
     # binning (DSR_LAYOUT_RECT_BINNING) instead of the exact alpha test — the throughput the
     # reference's lists give on the same kernels
@@ -180,8 +204,8 @@ def main():
     try:
         if args.no_reference_binning:
             pass
-        elif not args.eager:
-            modes_ref, graphs_ref = build_modes()
+        elif mode != "eager":
+            modes_ref, graphs_ref = build_modes(B)
             runner_ref = modes_ref[mode]
         if not args.no_reference_binning:
             elapsed_ref = timed(runner_ref, args.steps)
@@ -201,12 +225,12 @@ def main():
     raster.set_timer(None)
     ktimes = ev.summary()  # name -> (launches, avg_ms)
     elapsed, elapsed_eager, elapsed_ref = max_over_ranks(elapsed, elapsed_eager, elapsed_ref)
-    views_per_step = args.batch * args.views
+    views_per_step = B * args.views
     total_views = views_per_step * args.steps * world
     value = total_views / elapsed
 
     roof = psnr = cpu = None
-    workload_tag = f"{args.context}v{H}x{W}x{args.views}b{args.batch}"
+    workload_tag = f"{args.context}v{H}x{W}x{args.views}b{B}"
     if rank == 0:
         G = sc.gaussians.means.shape[1]
         V = views_per_step
@@ -254,10 +278,10 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.context}-view {H}x{W} RE10K feed-forward render, 1 Gaussian/pixel "
                                    f"(G={sc.gaussians.means.shape[1]}), {args.views} target views/scene, fp32",
-                       "global_batch": args.batch * world, "views_per_scene": args.views,
+                       "global_batch": B * world, "scenes_per_step_per_gpu": B, "views_per_scene": args.views,
                        "gaussians": sc.gaussians.means.shape[1], "num_rendered_per_step": n_rendered,
                        "parallelism": f"dp{world} (per-scene, no collective)",
-                       "scenes_in_flight_per_gpu": lanes_used, "distinct_scenes_per_gpu": lanes_used},
+                       "scenes_in_flight_per_gpu": B * lanes_used, "distinct_scenes_per_gpu": B * lanes_used},
             "parity_vs_oracle": psnr,
             "roofline": roof, "cpu_baseline": cpu,
             **extra,
@@ -267,20 +291,26 @@ def main():
         dist.destroy_process_group()
 
 
-def _pmc_file():
-    f = ROOT / "profiles" / "pmc_traffic.json"
-    return json.loads(f.read_text()) if f.exists() else None
+def _pmc_file(workload):
+    """The committed PMC summary of `workload` (profiles/pmc_traffic_<workload>.json, else
+    profiles/pmc_traffic.json when its workload tag matches)."""
+    for f in (ROOT / "profiles" / f"pmc_traffic_{workload}.json", ROOT / "profiles" / "pmc_traffic.json"):
+        if f.exists():
+            d = json.loads(f.read_text())
+            if d.get("workload") == workload:
+                return d
+    return None
 
 
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same
     workload (profiles/pmc_traffic.json, written by tools/pmc_summary.py --json: FETCH_SIZE
     x2 per the gfx950 correction + WRITE_SIZE, separate --pmc passes). None if absent."""
-    d = _pmc_file()
+    d = _pmc_file(workload)
     rec = None if d is None else _pmc_record(d, kernel)
-    if d is None or d.get("workload") != workload or rec is None:
+    if d is None or rec is None:
         return None, None
-    return int(rec["hbm_bytes"]), f"profiles/pmc_traffic.json ({d.get('source', '')})"
+    return int(rec["hbm_bytes"]), f"profiles/pmc_traffic[_{workload}].json ({d.get('source', '')})"
 
 
 def _pmc_record(d, kernel):
@@ -296,14 +326,14 @@ def pmc_valu(kernel, workload, avg_ms):
     the committed PMC summary of the same workload) over its live average duration, against
     the chip's wave64 issue peak (VALU_PEAK_GWI: 256 CUs x 4 SIMD-32, one wave instruction per
     2 cycles at 2.4 GHz = 1,229 G wave-instructions/s)."""
-    d = _pmc_file()
+    d = _pmc_file(workload)
     rec = None if d is None else _pmc_record(d, kernel)
-    if d is None or d.get("workload") != workload or rec is None or "SQ_INSTS_VALU" not in rec:
+    if d is None or rec is None or "SQ_INSTS_VALU" not in rec:
         return None
     ach = rec["SQ_INSTS_VALU"] / (avg_ms * 1e-3) / 1e9
     return {"achieved": round(ach, 1), "peak": VALU_PEAK_GWI, "unit": "G wave-instr/s",
             "frac": round(ach / VALU_PEAK_GWI, 4), "valu_instr_per_launch": int(rec["SQ_INSTS_VALU"]),
-            "source": "profiles/pmc_traffic.json"}
+            "source": f"profiles/pmc_traffic[_{workload}].json"}
 
 
 def train_leg(args, dev, rank, world, timed, max_over_ranks):
