@@ -1,7 +1,9 @@
 #!/bin/bash
-# Round-2 profile on the GPU box (repo root): GPU tests, kernel-trace stats of the bench,
-# separate PMC passes per counter group for the headline (exact binning only), the config C
-# training step, the config E reconstruction and the cost volume, then JSON summaries.
+# Round-2 profile on the GPU box (repo root): GPU tests, kernel-trace stats of the bench (the
+# calibrated headline configuration: 4 scenes per step on 4 streams, and one scene per step on
+# one graph), separate PMC passes per counter group for the headline (exact binning only, one
+# and four scenes per launch), the config C training step, the config E reconstruction and
+# the cost volume, then JSON summaries.
 # usage: bash tools/profile_r02.sh TAG
 set -u
 tag=${1:?tag}
@@ -16,31 +18,38 @@ run() {  # run NAME TIMEOUT CMD...: stop the whole script on a timeout / signal 
   if [ $rc -ge 124 ]; then echo "stopping after $name"; exit $rc; fi
 }
 B="python3 bench.py --no-cpu-baseline --no-reference-binning"
-run gputest 300 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 240 --timeout-method thread
+export DSPLAT_PARITY_REPORT=$out/parity.jsonl
+run gputest 400 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 240 --timeout-method thread
 tail -3 $out/gputest.log
-run stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats -o run -- \
-  $B --steps 50 --warmup 5 --extra "" --launch hipgraph
-run stats_default 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_default -o run -- \
-  $B --steps 50 --warmup 5 --extra ""
-for pass in FETCH_SIZE WRITE_SIZE \
-  "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT"; do
-  n=$(echo $pass | cut -d' ' -f1 | tr 'A-Z' 'a-z')
-  run pmc_$n 240 rocprofv3 --kernel-trace --pmc $pass --output-format csv -d $out/pmc_$n -o run -- \
-    $B --steps 10 --warmup 3 --eager --extra ""
+unset DSPLAT_PARITY_REPORT
+run stats_b4 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b4 -o run -- \
+  $B --steps 50 --warmup 5 --extra "" --batch 4 --launch hipgraph4
+run stats_b1 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b1 -o run -- \
+  $B --steps 50 --warmup 5 --extra "" --batch 1 --launch hipgraph
+for b in 1 4; do
+  for pass in FETCH_SIZE WRITE_SIZE \
+    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT"; do
+    n=$(echo $pass | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+    run pmc_b${b}_$n 240 rocprofv3 --kernel-trace --pmc $pass --output-format csv -d $out/pmc_b${b}_$n -o run -- \
+      $B --steps 10 --warmup 3 --eager --batch $b --extra ""
+  done
+  python3 tools/pmc_summary.py --json $out/pmc_traffic_2v256x256x3b$b.json 2v256x256x3b$b \
+    "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ, $tag" $out/pmc_b${b}_fetch_size $out/pmc_b${b}_write_size \
+    $out/pmc_b${b}_sq_waves
 done
-python3 tools/pmc_summary.py --json $out/pmc_traffic.json 2v256x256x3b1 "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ, $tag" \
-  $out/pmc_fetch_size $out/pmc_write_size $out/pmc_sq_waves
 # config C training step and config E reconstruction (the headline runs too, 3 steps)
 for leg in train recon12; do
   for pass in FETCH_SIZE WRITE_SIZE \
-    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY"; do
+    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT"; do
     n=$(echo $pass | cut -d' ' -f1 | tr 'A-Z' 'a-z')
     run ${leg}_$n 300 rocprofv3 --kernel-trace --pmc $pass --output-format csv -d $out/${leg}_$n -o run -- \
-      $B --steps 3 --warmup 2 --eager --extra $leg --extra-steps 3
+      $B --steps 3 --warmup 2 --eager --batch 1 --extra $leg --extra-steps 3
   done
   python3 tools/pmc_summary.py --json $out/pmc_$leg.json $leg "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ, $tag" \
     $out/${leg}_fetch_size $out/${leg}_write_size $out/${leg}_sq_waves
 done
+run stats_train 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_train -o run -- \
+  $B --steps 5 --warmup 2 --batch 1 --launch hipgraph --extra train --extra-steps 10
 # cost volume, per shape (config A and config B scale 0, the bench's costvol leg)
 for shp in a b0; do
   run cv_stats_$shp 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out/cv_stats_$shp -o run -- \
@@ -52,4 +61,6 @@ for shp in a b0; do
     python3 tools/cv_bench.py $shp
   python3 tools/pmc_summary.py $out/cv_sq_$shp $out/cv_fetch_$shp > $out/pmc_costvol_$shp.json
 done
+run bench 400 python3 -u bench.py
+tail -c 1500 $out/bench.log
 echo done
