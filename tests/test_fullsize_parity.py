@@ -11,8 +11,9 @@
   every pixel of its tile, and its images equal those of the same kernel with the
   reference's binning (DSR_LAYOUT_RECT_BINNING) bit for bit.
 * config C shape (256x256, 2 scenes x 4 target views): forward + backward vs the oracle.
-* config D shape (6-view 448x768 context -> G = 2,064,384; 2 target views): the product
-  path at that size (two-phase binning with the depth cut) vs the oracle.
+* config D shape (6-view 448x768 context -> G = 2,064,384; 2 target views) and config E shape
+  (12-view 512x960 context -> G = 5,898,240; 1 target view): the product path at those sizes
+  (two-phase binning with the depth cut) vs the oracle.
 
 Bars (BASELINE.json north_star): mean L1 < 1e-4, PSNR delta < 0.01 dB, sort indices
 bit-exact; gradients within 2e-3 of the largest magnitude (float atomics reorder sums).
@@ -337,3 +338,35 @@ def test_config_d_shape_render_vs_oracle(gpu, monkeypatch):
         _report(test="config_d_view", view=v, l1=l1, max_abs=mx, dpsnr=dp, num_rendered=int(o.num_rendered))
         o.close()
     _report(test="config_d_written", written=written, total=int(state.counts.sum()), layout=int(state.seg_stride))
+
+
+def test_config_e_shape_render_vs_oracle(gpu, monkeypatch):
+    """Config E's shape: 12-view 512x960 context (G = 5,898,240), one target view through the
+    product path at this size (two-phase binning with the depth cut) vs the oracle's full
+    render; the written heads equal the heads of the oracle's sorted lists."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setitem(raster._spec, "two_phase_max", None)  # no short-list hint from earlier tests
+    sc = scene_inputs(h=512, w=960, n_ctx=12, n_tgt=1, seed=3000)
+    assert sc.gaussians.means.shape[1] == 12 * 512 * 960
+    st = settings_for(sc)
+    means, shs, opac, cov6 = flat_inputs(sc)
+    cams = packed_cams(st, [0]).to(gpu)
+    color, state = raster.forward_raw(means.to(gpu), shs.to(gpu), True, 2, opac.to(gpu), cov6.to(gpu), cams, 1,
+                                      512, 960)
+    torch.cuda.synchronize()
+    assert state.seg_stride == raster.SEG_ENDS  # the depth-cut layout ran
+    T = 32 * 60
+    begin, end, keys = _segments(state, 1, T)
+    written = int((end - begin).sum())
+    (o,) = oracle_views(sc, st)
+    okeys, ovals, ranges = o.binning()
+    for t in range(T):
+        hk = (keys[begin[t]:end[t]] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        ob, oe = ranges[t]
+        assert len(hk) <= oe - ob
+        np.testing.assert_array_equal(hk, ovals[ob:ob + len(hk)])
+    oc, _, _ = o.image()
+    l1, mx, dp = _image_bars(color[0].cpu().numpy(), oc, "config E view 0")
+    _report(test="config_e_view", view=0, l1=l1, max_abs=mx, dpsnr=dp, num_rendered=int(o.num_rendered),
+            written=written)
+    o.close()
