@@ -171,12 +171,16 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
 /* Super-block edge in tiles for a W x H image (0: the image is too large for this path). */
 int dsr_cut_superblock(int H, int W);
 /* depth_hist [V, nsb, DSR_CUT_BUCKETS] uint32 (zeroed by this call), nsb = ceil(tiles_x/sb)
- * * ceil(tiles_y/sb); other arguments and outputs as dsr_preprocess_fwd. */
+ * * ceil(tiles_y/sb); other arguments and outputs as dsr_preprocess_fwd.
+ * cut_rec (optional, [V, G, 2] uint32): per (view, Gaussian) the super-block rect of its tile
+ * rect (x0 | x1 << 8 | y0 << 16 | y1 << 24, 0 when culled) and its depth bits: 8 bytes the
+ * scatter's whole-Gaussian pre-test reads instead of the 48-byte geometry record (requires
+ * ceil(tiles/sb) <= 255 per axis; NULL skips it). */
 int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,
                        float* geom, int32_t* radii, uint32_t* seg_count, uint32_t* depth_hist,
-                       int layout, void* stream);
+                       uint32_t* cut_rec, int layout, void* stream);
 /* cut [V, nsb] uint32: per super-block, the largest depth (float bits) emitted: inside the
  * bucket where the count reaches `prefix` per tile, interpolated by the fraction still
  * needed (0xffffffff = all). */
@@ -189,7 +193,8 @@ int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t pre
  * written. */
 int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor,
                         uint64_t* keys, const uint32_t* cut, int tail, const uint32_t* seg_overflow,
-                        void* stream);
+                        const uint32_t* cut_rec, void* stream);
+/* cut_rec: dsr_preprocess_cut's compact records (or NULL: the pre-test reads geom). */
 
 /* Sort every segment by (depth, id) ascending — identical to upstream's stable radix
  * sort of (tile << 32 | depth) with emission-order ties (K4/K5). max_count sizes the LDS

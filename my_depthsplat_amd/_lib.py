@@ -27,9 +27,9 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_bin_scatter": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P]),
     "dsr_project_bin": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dsr_cut_superblock": (_I, [_I, _I]),
-    "dsr_preprocess_cut": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "dsr_preprocess_cut": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dsr_bin_cutoff": (_I, [_I, _I, _I, _P, c_uint32, _P, _P]),
-    "dsr_bin_scatter_cut": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "dsr_bin_scatter_cut": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
     "dsr_bin_sort": (_I, [_I, _I, _I, _I, _P, _P, c_uint32, _P, _P, c_uint32, _P, c_uint32, _P, _P, _P]),
     "dsr_bin_sort_workspace_size": (ctypes.c_size_t, [_I, _I, _I, c_uint32]),
     "dsr_workspace_size": (_I, [_I, _I, _I, _I, ctypes.c_uint64, _P]),

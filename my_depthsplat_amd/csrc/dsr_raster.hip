@@ -984,7 +984,8 @@ template <int NTH>
 __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int gy, const float* __restrict__ geom,
                                                      uint32_t* __restrict__ cursor, uint64_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ cut, int tail,
-                                                     const uint32_t* __restrict__ seg_overflow, int per_view) {
+                                                     const uint32_t* __restrict__ seg_overflow,
+                                                     const uint2* __restrict__ cut_rec, int per_view) {
   constexpr int NW = NTH / 64;
   __shared__ uint32_t s_cut[kCutMaxSB];
   __shared__ WaveRects s_wr[NW];
@@ -1011,22 +1012,43 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
     int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     uint64_t key = 0;
     if (g < G) {
+      // whole-Gaussian pre-test over the super-blocks its rect touches: from the 8-byte compact
+      // record when given (most Gaussians fail it: only ~4-9 % of the entries are kept), the
+      // 48-byte geometry record is read only by the survivors
+      int sx0 = 0, sx1 = 0, sy0 = 0, sy1 = 0;
+      uint32_t zb = 0u;
       const float* rec = gv + (size_t)g * GS;
-      r = __float_as_int(rec[10]);
-      if (r > 0) {
-        tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
-        key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
-        const int sx0 = x0 >> sbl, sx1 = ((x1 - 1) >> sbl) + 1, sy0 = y0 >> sbl, sy1 = ((y1 - 1) >> sbl) + 1;
-        if ((sx1 - sx0) * (sy1 - sy0) <= 16) {
-          const uint32_t zb = (uint32_t)(key >> 32);
-          bool any = false;
-          for (int sy = sy0; sy < sy1; ++sy)
-            for (int sx = sx0; sx < sx1; ++sx) {
-              const bool nearer = zb <= s_cut[sy * nsx + sx];
-              any |= tail ? (!nearer && sbov[sy * nsx + sx] != 0u) : nearer;
-            }
-          if (!any) r = 0;
+      if (cut_rec) {
+        const uint2 cr = cut_rec[(size_t)v * G + g];
+        sx0 = (int)(cr.x & 0xFFu);
+        sx1 = (int)((cr.x >> 8) & 0xFFu);
+        sy0 = (int)((cr.x >> 16) & 0xFFu);
+        sy1 = (int)(cr.x >> 24);
+        zb = cr.y;
+        r = cr.x != 0u ? 1 : 0;
+      } else {
+        r = __float_as_int(rec[10]);
+        if (r > 0) {
+          tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
+          sx0 = x0 >> sbl, sx1 = ((x1 - 1) >> sbl) + 1, sy0 = y0 >> sbl, sy1 = ((y1 - 1) >> sbl) + 1;
+          zb = __float_as_uint(rec[9]);
         }
+      }
+      if (r > 0 && (sx1 - sx0) * (sy1 - sy0) <= 16) {
+        bool any = false;
+        for (int sy = sy0; sy < sy1; ++sy)
+          for (int sx = sx0; sx < sx1; ++sx) {
+            const bool nearer = zb <= s_cut[sy * nsx + sx];
+            any |= tail ? (!nearer && sbov[sy * nsx + sx] != 0u) : nearer;
+          }
+        if (!any) r = 0;
+      }
+      if (r > 0) {
+        if (cut_rec) {
+          r = __float_as_int(rec[10]);
+          tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
+        }
+        key = ((uint64_t)zb << 32) | (uint32_t)g;
       }
     }
     s_key[tid] = key;
@@ -1058,8 +1080,8 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
                                                         const dsr_camera* __restrict__ cams,
                                                         float* __restrict__ geom, int32_t* __restrict__ radii,
                                                         uint32_t* __restrict__ seg_count,
-                                                        uint32_t* __restrict__ depth_hist, int per_view,
-                                                        int layout) {
+                                                        uint32_t* __restrict__ depth_hist,
+                                                        uint2* __restrict__ cut_rec, int per_view, int layout) {
   constexpr int NW = NTH / 64;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_mem[];
   __shared__ WaveRects s_wr[NW];
@@ -1103,6 +1125,10 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
     s_bk[w][lane] = (uint32_t)depth_bucket(zb);
     const int sx0 = x0 >> sbl, sy0 = y0 >> sbl;
     const int sx1 = r > 0 ? ((x1 - 1) >> sbl) + 1 : sx0, sy1 = r > 0 ? ((y1 - 1) >> sbl) + 1 : sy0;
+    if (cut_rec && g < G)
+      cut_rec[(size_t)v * G + g] =
+          make_uint2(r > 0 ? (uint32_t)sx0 | ((uint32_t)sx1 << 8) | ((uint32_t)sy0 << 16) | ((uint32_t)sy1 << 24) : 0u,
+                     zb);
     for_each_rect_tile(wr, lane, sx0, sy0, sx1, sy1, r > 0, nsx, [&](int s, int o, int sx, int sy) {
       const uint32_t rx = s_rx[w][o], ry = s_ry[w][o];
       const int ox = min((int)(rx >> 16), sx * sb + sb) - max((int)(rx & 0xFFFFu), sx * sb);
@@ -3125,7 +3151,7 @@ int dsr_cut_superblock(int H, int W) {
 int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                        const float* shs, const float* colors, const float* opacities, const float* cov6,
                        const dsr_camera* cams, float* geom, int32_t* radii, uint32_t* seg_count,
-                       uint32_t* depth_hist, int layout, void* stream) {
+                       uint32_t* depth_hist, uint32_t* cut_rec, int layout, void* stream) {
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_preprocess_cut: bad sizes S=%d G=%d V=%d H=%d W=%d", S, G, V, H, W);
   DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "dsr_preprocess_cut: exactly one of shs/colors must be given");
   DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
@@ -3136,6 +3162,8 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, 
   const int sb = cut_superblock(gx, gy);
   DSPLAT_REQUIRE(sb > 0, "dsr_preprocess_cut: %dx%d tiles exceed the LDS histograms", gx, gy);
   const int nsb = ((gx + sb - 1) / sb) * ((gy + sb - 1) / sb);
+  DSPLAT_REQUIRE(cut_rec == nullptr || ((gx + sb - 1) / sb <= 255 && (gy + sb - 1) / sb <= 255),
+                 "dsr_preprocess_cut: cut_rec needs at most 255 super-blocks per axis");
   hipStream_t st = (hipStream_t)stream;
   if (!(layout & kLayoutCountsZeroed))
     if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
@@ -3160,7 +3188,7 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, 
     }                                                                                                        \
     k_preprocess_cut<D, kNTH><<<xcd_grid(per_view, V), kNTH, lds, st>>>(                                     \
         G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, geom, radii, seg_count, depth_hist, \
-        per_view, layout);                                                                                   \
+        reinterpret_cast<uint2*>(cut_rec), per_view, layout);                                                \
   } while (0)
   switch (deg) {
     case -1: DSR_PC(-1); break;
@@ -3185,7 +3213,8 @@ int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t pre
 }
 
 int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor, uint64_t* keys,
-                        const uint32_t* cut, int tail, const uint32_t* seg_overflow, void* stream) {
+                        const uint32_t* cut, int tail, const uint32_t* seg_overflow, const uint32_t* cut_rec,
+                        void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_scatter_cut: bad sizes");
   DSPLAT_REQUIRE(geom && seg_cursor && keys && cut && (!tail || seg_overflow), "dsr_bin_scatter_cut: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
@@ -3194,6 +3223,7 @@ int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t*
   const int per_view = max(1, min((G + kNTH - 1) / kNTH, (256 * 8) / V));
   k_scatter_cut<kNTH><<<(unsigned)(V * per_view), kNTH, 0, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor,
                                                                                   keys, cut, tail, seg_overflow,
+                                                                                  reinterpret_cast<const uint2*>(cut_rec),
                                                                                   per_view);
   return dsplat::check_launch("k_scatter_cut");
 }

@@ -496,10 +496,13 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         if sb > 0:
             nsb = -(-gx // sb) * -(-gy // sb)
             hist = torch.empty(V * nsb * 128, dtype=torch.int32, device=dev)
+            # 8 bytes per (view, Gaussian) for the scatter's pre-test instead of the 48-byte record
+            cut_rec = torch.empty(V * G * 2, dtype=torch.int32, device=dev) \
+                if -(-gx // sb) <= 255 and -(-gy // sb) <= 255 else None
             _lib.check(_timed("k_preprocess_cut", lib.dsr_preprocess_cut,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), hist.data_ptr(), layout,
-                st), "dsr_preprocess_cut")
+                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), hist.data_ptr(),
+                _ptr(cut_rec), layout, st), "dsr_preprocess_cut")
         else:
             if STATEFUL_EXACT_BINNING:  # the scatter below repeats the same test
                 layout |= LAYOUT_EXACT_BINNING
@@ -531,7 +534,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             _lib.check(_timed("k_bin_cutoff", lib.dsr_bin_cutoff, V, H, W, hist.data_ptr(), CUT_PREFIX,
                               cut.data_ptr(), st), "dsr_bin_cutoff")
             _lib.check(_timed("k_scatter", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
-                              keys.data_ptr(), cut.data_ptr(), 0, None, st), "dsr_bin_scatter_cut")
+                              keys.data_ptr(), cut.data_ptr(), 0, None, _ptr(cut_rec), st), "dsr_bin_scatter_cut")
             tile_count, seg_count, stride = seg_count, cursor, SEG_ENDS
             _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), seg_count.data_ptr(),
                               stride, keys.data_ptr(), scratch.data_ptr(), CUT_SORT_HINT, None, 0, None, None, st),
@@ -582,7 +585,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         # in full, render them again (every launch returns at once for unflagged tiles; no sync)
         if stride == SEG_ENDS:
             _lib.check(lib.dsr_bin_scatter_cut(G, V, H, W, geom.data_ptr(), seg_count.data_ptr(), keys.data_ptr(),
-                                               cut.data_ptr(), 1, overflow.data_ptr(), st), "dsr_bin_scatter_cut(tail)")
+                                               cut.data_ptr(), 1, overflow.data_ptr(), _ptr(cut_rec), st),
+                       "dsr_bin_scatter_cut(tail)")
         _lib.check(lib.dsr_bin_sort(G, V, H, W, _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(),
                                     scratch.data_ptr(), 0, None, 0, _ptr(seg_sorted), overflow.data_ptr(), st),
                    "dsr_bin_sort(overflow)")
