@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--steps", type=int, default=500)  # ~30 ms timed at ~60 us per scene
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=0,
-                   help="scenes per step per GPU (reference test loop: 1); 0 = calibrate over 1, 2, 4")
+                   help="scenes per step per GPU (reference test loop: 1); 0 = calibrate over 1, 2, 4, 8")
     p.add_argument("--views", type=int, default=3, help="target views per scene (RE10K eval: 3)")
     p.add_argument("--size", type=int, default=256)
     p.add_argument("--context", type=int, default=2)
@@ -88,7 +88,7 @@ def main():
     _lib.load()
     H = W = args.size
     max_lanes = 1 if args.eager else int(os.environ.get("DSPLAT_BENCH_MAX_LANES", "4"))
-    batches = [args.batch] if args.batch else ([1, 2, 4] if args.launch == "auto" and not args.eager else [1])
+    batches = [args.batch] if args.batch else ([1, 2, 4, 8] if args.launch == "auto" and not args.eager else [1])
     dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
 
     def step_of(s):

@@ -1,6 +1,6 @@
 """Config B throughput with scenes batched into one decoder call (B scenes x 3 views per
 launch pair) vs one scene per call, each replayed as hipGraphs on 1..4 streams (GPU box).
-usage: python tools/batch_exp.py [steps]"""
+usage: python tools/batch_exp.py [steps] [B,B,...]"""
 import sys
 import time
 from pathlib import Path
@@ -43,7 +43,7 @@ def bench(fns, n, nstreams):
     return (time.perf_counter() - t0) / n
 
 
-for B in (1, 2, 4):
+for B in [int(x) for x in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "2", "4"])]:
     scs = [make_scene(batch=B, n_context=2, n_targets=3, height=256, width=256, seed=1000 + 16 * i, device=dev)
            for i in range(4)]
     for ns in (1, 2, 4):
