@@ -2600,7 +2600,14 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
   };
   auto chunk = [&](int ch, uint32_t id, float4 q, float4 r, float bl) {
     const int p = (int)nproc - (ch + 1) * BCH + lane;  // this lane's list position (< 0: none)
-    const bool mine = p >= 0 && subtile_hit(q, r, fx0, fy0);
+    // pixels that can take a gradient from this chunk: last contributor past its lowest
+    // position (walking back to front, few pixels are active in the first chunks); entries
+    // whose alpha >= 1/255 region misses their box are skipped for the whole wave
+    const uint32_t plo = (uint32_t)max((int)nproc - (ch + 1) * BCH, 0);
+    const uint64_t act_px = __ballot(inside && lastc > plo);
+    float lx0 = fx0, ly0 = fy0, lx1 = fx0 + (SUB - 1), ly1 = fy0 + (SUB - 1);
+    if (act_px) live_rect(act_px, fx0, fy0, lx0, ly0, lx1, ly1);
+    const bool mine = p >= 0 && act_px != 0ull && rect_hit(q, r, lx0, ly0, lx1, ly1);
     const uint64_t bal = __ballot(mine);
     if (mine) {
       BwdRec& d = list[__popcll(bal & lt)];
