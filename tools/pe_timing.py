@@ -63,3 +63,18 @@ print(f"reserve      {q(us(t[:, 3] - t[:, 2]))}")
 print(f"emit         {q(us(t[:, 4] - t[:, 3]))}")
 print(f"end          {q(us(t[:, 4] - base))}")
 print(f"pairs/wg     {q(t[:, 5].astype(float))}")
+# residency: workgroups live at once on each CU (HW_ID: CU_ID [11:8], SH_ID [12], SE_ID [15:13];
+# XCC_ID [3:0])
+hwid, xcc = t[:, 6], t[:, 7]
+cu = (xcc & 0xF) * 1000 + ((hwid >> 13) & 7) * 100 + ((hwid >> 12) & 1) * 16 + ((hwid >> 8) & 0xF)
+peak = []
+for c in np.unique(cu):
+    ev = sorted([(s, 1) for s in t[cu == c, 0]] + [(e, -1) for e in t[cu == c, 4]], key=lambda p: (p[0], p[1]))
+    live = best = 0
+    for _, dlt in ev:
+        live += dlt
+        best = max(best, live)
+    peak.append(best)
+peak = np.array(peak)
+print(f"CUs used {len(peak)}; workgroups per CU {q(np.bincount(np.searchsorted(np.unique(cu), cu)).astype(float))}")
+print(f"max live workgroups per CU {q(peak.astype(float))}")
