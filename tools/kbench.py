@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--two-phase", action="store_true", help="force the two-phase binning layout")
     ap.add_argument("--exact", action="store_true", help="replay the inference path's exact-binning lists")
     ap.add_argument("--no-ncontrib", action="store_true", help="sort_render without n_contrib (inference)")
+    ap.add_argument("--counters", action="store_true",
+                    help="render_bwd: print the 4 uint32 counters an instrumented variant parks in the padding "
+                         "words of dgeom's last two rows")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -58,6 +61,7 @@ def main():
         color, state = raster.forward_raw(g.means, g.harmonics, True, 2, g.opacities, g.covariances, cams, V, H, W,
                                           layout)
     G = g.means.shape[1]
+    GS_ = raster.GEOM_STRIDE
     torch.cuda.synchronize()
     print(f"G={G} V={V} {H}x{W} N={state.num_rendered}", flush=True)
     st = _lib.stream_of(dev)
@@ -155,6 +159,11 @@ def main():
                                           state.n_contrib.data_ptr(), dpix.data_ptr(), out[0].data_ptr(), st)
         assert launch() == 0, lib.dsplat_last_error()
         torch.cuda.synchronize()
+        if a.counters and a.kernel == "render_bwd":
+            flat = out[0].view(-1).view(torch.int32)
+            c = [int(flat[-3]), int(flat[-2]), int(flat[-1]), int(flat[-GS_ - 1])]
+            print(f"{name:>12s}  counters: entries {c[0]}, entries with an active lane {c[1]}, "
+                  f"groups reduced {c[2]} of {c[3]}", flush=True)
         if ref is None:
             ref = [o.clone() for o in out]
         diff = max(float((o.float() - r.float()).abs().max()) for o, r in zip(out, ref))

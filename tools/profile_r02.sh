@@ -24,6 +24,10 @@ tail -3 $out/gputest.log
 unset DSPLAT_PARITY_REPORT
 run stats_b4 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b4 -o run -- \
   $B --steps 50 --warmup 5 --extra "" --batch 4 --launch hipgraph4
+# the bench's roofline leg: the same 4-scene step launched eagerly on one stream (HIP events
+# around the dominant kernel; the rocprof average of that kernel here must agree with it)
+run stats_b4_eager 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b4_eager -o run -- \
+  $B --steps 50 --warmup 5 --extra "" --batch 4 --launch eager
 run stats_b1 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b1 -o run -- \
   $B --steps 50 --warmup 5 --extra "" --batch 1 --launch hipgraph
 for b in 1 4; do
