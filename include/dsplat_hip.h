@@ -243,15 +243,19 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
                    void* stream);
 
 /* dsr_bin_sort + dsr_render_fwd in one launch (no prefix / cut modes): each workgroup sorts its
- * tile's keys in LDS and composites from that copy; segments above 4096 entries are sorted
- * through `scratch` (same size as keys) by the same workgroup. The sorted keys are written
- * back to `keys` only when write_keys != 0 (dsr_render_bwd needs them). Outputs as
+ * tile's keys in LDS and composites from that copy; segments above the LDS class (below) are
+ * sorted through `scratch` (same size as keys) by the same workgroup. The sorted keys are
+ * written back to `keys` only when write_keys != 0 (dsr_render_bwd needs them). Outputs as
  * dsr_render_fwd; n_contrib may be NULL (an inference call with no backward: the compositor
- * then does not track the last blended position). */
+ * then does not track the last blended position).
+ * max_count_hint: the caller's estimate of the largest segment (e.g. the max of an earlier
+ * call's counts; 0 = unknown). It picks the LDS class — 2048, 3072 or 4096 keys per tile
+ * (smaller classes keep 4 workgroups per CU resident instead of 3) — and affects speed only:
+ * results are identical for any hint. */
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                     const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
-                    uint64_t* scratch, int write_keys, int clear_counts, float* out_color, float* final_T,
-                    uint32_t* n_contrib, void* stream);
+                    uint64_t* scratch, int write_keys, int clear_counts, uint32_t max_count_hint,
+                    float* out_color, float* final_T, uint32_t* n_contrib, void* stream);
 /* clear_counts != 0 (fixed-capacity layout only): seg_count is zeroed as it is consumed, so
  * the buffer can serve the next dsr_project_bin_cameras call as already-zeroed counters. */
 

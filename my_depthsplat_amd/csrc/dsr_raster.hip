@@ -31,9 +31,9 @@ constexpr int kSortNBinLog2 = 13;  // counting-sort depth bins (8192)
 constexpr int kSortWPE = 3;        // waves per EU of the sort kernels: all config-B segments resident
 // LDS words of the sort's counter area: the LSD passes' u16 counters (16 per thread) or the
 // counting sort's u16 bins, whichever is larger
-template <int NTH>
+template <int NTH, int NBL = kSortNBinLog2>
 constexpr int sort_cnt_words() {
-  return NTH * 8 > (1 << kSortNBinLog2) / 2 ? NTH * 8 : (1 << kSortNBinLog2) / 2;
+  return NTH * 8 > (1 << NBL) / 2 ? NTH * 8 : (1 << NBL) / 2;
 }
 constexpr int kHistLdsMax = 32768;            // tiles per view histogrammed in LDS
 
@@ -1576,13 +1576,13 @@ __device__ __forceinline__ uint32_t bin_word(uint32_t w) {
   return w ^ ((((w >> RL) >> 2) & (uint32_t)(R / 4 - 1)) << 2);
 }
 
-template <int KMAX, int NTH = NT>
+template <int KMAX, int NTH = NT, int NBL = kSortNBinLog2>
 __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A, int id_bits, uint16_t* cnt,
                            uint32_t* wsum, uint32_t* flag) {
-  constexpr int NBIN = 1 << kSortNBinLog2, BPT = NBIN / NTH;  // bins per thread in the scan
+  constexpr int NBIN = 1 << NBL, BPT = NBIN / NTH;  // bins per thread in the scan
   constexpr int R = BPT / 2;                                    // scan row: bin-pair words per thread
   constexpr uint32_t kBinMax = 16;  // larger bins (clustered / equal depths): LSD passes instead
-  static_assert(BPT % 8 == 0 && NTH * KMAX < 65536 && NBIN / 2 <= sort_cnt_words<NTH>(), "u16 bin pairs in cnt");
+  static_assert(BPT % 8 == 0 && NTH * KMAX < 65536 && NBIN / 2 <= sort_cnt_words<NTH, NBL>(), "u16 bin pairs in cnt");
   uint32_t* hw = reinterpret_cast<uint32_t*>(cnt);  // NBIN / 2 words (cnt holds NTH * 16 u16), 16-B aligned
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t mn = 0xffffffffu, mx = 0u;
@@ -1599,7 +1599,7 @@ __device__ void count_sort(const uint64_t (&tmp)[KMAX], uint32_t n, uint64_t* A,
   }
   block_minmax<NTH>(mn, mx, flag);
   const uint32_t range = mx - mn;
-  const int shift = max(0, (range ? 31 - __clz(range) : 0) - (kSortNBinLog2 - 1));
+  const int shift = max(0, (range ? 31 - __clz(range) : 0) - (NBL - 1));
   // count pass: the atomic's return value is the key's rank among the keys of its bin that
   // got there first, so the scatter needs no second atomic pass (u16 halves never carry:
   // n < 65536)
@@ -2011,14 +2011,11 @@ __device__ __forceinline__ float gauss_weight(float power) { return __expf(power
 
 // The compositing loops evaluate the Gaussian falloff in base 2 with the conic pre-scaled
 // once per staged entry: p2 = log2(e) * power = A dx^2 + C dy^2 + B dx dy with
-// A = -0.5 log2(e) a, C = -0.5 log2(e) c, B = -log2(e) b, and G = 2^p2 (one v_exp_f32).
-// Forward and backward use this exact sequence, so their skip decisions agree.
+// A = -0.5 log2(e) a, C = -0.5 log2(e) c, B = -log2(e) b, and G = 2^p2 (one v_exp_f32),
+// p2 itself as a polynomial in the pixel's sub-tile offset (fall_poly / fall_p2 below).
 constexpr float kLog2e = 1.4426950408889634f;
 __device__ __forceinline__ float4 scaled_conic_q(float4 q) {  // (x, y, a, b) -> (x, y, A, B)
   return make_float4(q.x, q.y, -0.5f * kLog2e * q.z, -kLog2e * q.w);
-}
-__device__ __forceinline__ float falloff_p2(float A, float B, float C, float dx, float dy) {
-  return fmaf(A * dx, dx, fmaf(C * dy, dy, B * dx * dy));
 }
 
 __device__ __forceinline__ uint32_t subtile_mask(float4 q, float4 r, int tx0, int ty0) {
@@ -2102,39 +2099,103 @@ constexpr int CH = 64;  // list entries per chunk (one per lane)
 // wave walks ~160 entries (p99 ~280, 3-5 chunks) of its tile at config B, so with only the
 // next chunk prefetched the walk was a chain of one memory round trip per chunk.
 constexpr int PD = 4;
-// Two consecutive list entries with their fields interleaved, so the falloff of both runs
-// as packed FP32 (v_pk_fma/mul/add) with no operand shuffling; per-element results are the
-// same IEEE operations as falloff_p2 (the backward's decisions still agree).
 typedef float f2v __attribute__((ext_vector_type(2)));
-struct __align__(16) PairRec {
-  f2v x, y, A, C, B, o;  // falloff fields of entries 0 and 1, interleaved (packed math)
-  f2v rg[2];             // (r, g) of entry j: one packed FMA into the pixel's (R, G)
-  f2v b;
-  uint32_t pos[2];
+// The falloff as a polynomial in the pixel's offset (u, v) from its 8x8 sub-tile's centre
+// (cx, cy) = (x0 + 3.5, y0 + 3.5): with X = x - cx, Y = y - cy (the Gaussian's centre),
+//   p2 = A dx^2 + C dy^2 + B dx dy  (dx = X - u, dy = Y - v)
+//      = F + D u + E v + A u^2 + C v^2 + B u v,
+//   F = A X^2 + C Y^2 + B X Y,  D = -2 A X - B Y,  E = -2 C Y - B X.
+// A wave stages (F, D, E) once per entry; per pixel the falloff is then 5 FMAs on per-lane
+// constants (u, v, u^2, v^2, u v are exact: halves in [-3.5, 3.5]) instead of 8 operations.
+// The forward, the backward and the tail check all evaluate exactly this sequence, so their
+// skip decisions agree; the culling tests (rect_hit, tile_reach) keep margins far above its
+// rounding (|terms| of a reachable entry are O(10), so errors are ~1e-6 in p2).
+struct PixUV {
+  float u, v, uu, vv, uv;
 };
-__device__ __forceinline__ void pair_put(PairRec* l, int k, float x, float y, float A, float C, float B, float o,
-                                         float r, float g, float b, uint32_t pos) {
-  PairRec& d = l[k >> 1];
+__device__ __forceinline__ PixUV pix_uv(int px, int py, float fx0, float fy0) {
+  PixUV p;
+  p.u = (float)px - (fx0 + 3.5f);
+  p.v = (float)py - (fy0 + 3.5f);
+  p.uu = p.u * p.u;
+  p.vv = p.v * p.v;
+  p.uv = p.u * p.v;
+  return p;
+}
+struct FallPoly {
+  float F, D, E;
+};
+__device__ __forceinline__ FallPoly fall_poly(float x, float y, float A, float B, float C, float fx0, float fy0) {
+  const float X = x - (fx0 + 3.5f), Y = y - (fy0 + 3.5f);
+  FallPoly f;
+  f.F = fmaf(A * X, X, fmaf(C * Y, Y, B * X * Y));
+  f.D = fmaf(-2.0f * A, X, -(B * Y));
+  f.E = fmaf(-2.0f * C, Y, -(B * X));
+  return f;
+}
+// The reference skips a pixel when power > 0, which for a positive-definite conic happens only
+// through its own rounding; the polynomial's absolute rounding near the centre is up to
+// ~2e-5 (terms of magnitude <= ~100), so "power <= 0" is tested as p2 <= kP2Max: every
+// positive-definite Gaussian still blends at its centre pixel (G = 2^p2 <= 1.00007 there).
+constexpr float kP2Max = 1e-4f;
+__device__ __forceinline__ float fall_p2(const PixUV& p, float F, float D, float E, float A, float B, float C) {
+  return fmaf(A, p.uu, fmaf(C, p.vv, fmaf(B, p.uv, fmaf(D, p.u, fmaf(E, p.v, F)))));
+}
+// Two consecutive list entries with their fields interleaved, so the falloff of both runs
+// as packed FP32 (v_pk_fma/mul) with no operand shuffling; per-element results are the same
+// IEEE operations as fall_p2 (the backward's decisions agree).
+struct __align__(16) PairRec {
+  f2v F, D, E, A, C, B, o;  // falloff fields of entries 0 and 1, interleaved (packed math)
+  f2v b;
+  f2v rg[2];                // (r, g) of entry j: one packed FMA into the pixel's (R, G)
+};
+// A wave's staged chunk: up to CH kept entries + 8 pads as field-interleaved pairs (80 B: a
+// 20-word stride, so the 32 lanes' stores of one field hit 2-way at most), and beside them
+// each entry's list position (read once per chunk by a backward-bound forward: n_contrib).
+struct __align__(16) WaveList {
+  PairRec rec[(CH + 8) / 2];
+  uint32_t pos[CH + 8];
+};
+// the pixel terms stay scalars; the packed FMAs broadcast them (op_sel), no duplicated registers
+typedef PixUV PixUV2;
+__device__ __forceinline__ PixUV2 pix_uv2(const PixUV& p) { return p; }
+__device__ __forceinline__ f2v fall_p2x2(const PixUV2& p, const PairRec& P) {
+  const f2v t0 = __builtin_elementwise_fma(P.E, f2v{p.v, p.v}, P.F);
+  const f2v t1 = __builtin_elementwise_fma(P.D, f2v{p.u, p.u}, t0);
+  const f2v t2 = __builtin_elementwise_fma(P.B, f2v{p.uv, p.uv}, t1);
+  const f2v t3 = __builtin_elementwise_fma(P.C, f2v{p.vv, p.vv}, t2);
+  return __builtin_elementwise_fma(P.A, f2v{p.uu, p.uu}, t3);
+}
+// stage one entry (centre x, y; scaled conic A, B, C) as element k of the wave's pair list
+__device__ __forceinline__ void pair_put(WaveList* wl, int k, float x, float y, float A, float C, float B, float o,
+                                         float r, float g, float b, uint32_t pos, float fx0, float fy0) {
+  PairRec& d = wl->rec[k >> 1];
   const int j = k & 1;
-  d.x[j] = x; d.y[j] = y; d.A[j] = A; d.C[j] = C; d.B[j] = B; d.o[j] = o;
-  d.rg[j] = f2v{r, g}; d.b[j] = b; d.pos[j] = pos;
+  const FallPoly f = fall_poly(x, y, A, B, C, fx0, fy0);
+  d.F[j] = f.F; d.D[j] = f.D; d.E[j] = f.E; d.A[j] = A; d.C[j] = C; d.B[j] = B; d.o[j] = o;
+  d.rg[j] = f2v{r, g}; d.b[j] = b;
+  wl->pos[k] = pos;
+}
+__device__ __forceinline__ void pair_pad(WaveList* wl, int k) {  // opacity 0: alpha 0, never blends
+  PairRec& d = wl->rec[k >> 1];
+  const int j = k & 1;
+  d.F[j] = 0.f; d.D[j] = 0.f; d.E[j] = 0.f; d.A[j] = 0.f; d.C[j] = 0.f; d.B[j] = 0.f; d.o[j] = 0.f;
+  d.rg[j] = f2v{0.f, 0.f}; d.b[j] = 0.f;
 }
 // Front-to-back step over two entries. A pixel's state is its transmittance with the sign
 // as the stop flag (Tr < 0: stopped or outside the image, |Tr| the final T), so the chain
 // T -> test T -> stop -> T is vector compares and selects (VCC) only: no per-pixel lane mask
-// round-trips through SALU ops at every entry. Per entry, exactly as the reference: skip
-// unless power <= 0 and alpha = min(.99, o G) >= 1/255; test T = T (1 - alpha); stop
+// round-trips through SALU ops at every entry. Per entry, as the reference: skip
+// unless power <= 0 (p2 <= kP2Max) and alpha = min(.99, o G) >= 1/255; test T = T (1 - alpha); stop
 // (without blending) when test T < 1e-4; else colour += rgb alpha T, T = test T, last =
 // position. A skipped entry gets alpha 0, which leaves T bit-identical (T * 1) and adds +0
 // colour; a stopped pixel fails the stop test at every later entry (T (1 - alpha) <= 0).
-// LAST: track the last blended position (n_contrib, which only a backward reads).
+// LAST: track the chunk index of the last blended entry (its list position, n_contrib, which
+// only a backward reads, is looked up once per chunk).
 template <bool LAST>
-__device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v pfy2, float& Tr, f2v& C01, float& C2,
-                                               uint32_t& last) {
-  const f2v dx = P.x - pfx2, dy = P.y - pfy2;
-  const f2v Adx = P.A * dx, Cdy = P.C * dy, Bdx = P.B * dx;
-  const f2v Bdxdy = Bdx * dy;
-  const f2v p2 = __builtin_elementwise_fma(Adx, dx, __builtin_elementwise_fma(Cdy, dy, Bdxdy));
+__device__ __forceinline__ void composite_pair(const PairRec& P, const PixUV2& pp, float& Tr, f2v& C01, float& C2,
+                                               int& lastk, int k0) {
+  const f2v p2 = fall_p2x2(pp, P);
   f2v G;
   G.x = __builtin_amdgcn_exp2f(p2.x);
   G.y = __builtin_amdgcn_exp2f(p2.y);
@@ -2142,9 +2203,9 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v p
   f2v alpha;
   alpha.x = fminf(0.99f, oG.x);
   alpha.y = fminf(0.99f, oG.y);
-  // ok <=> min(0 - p2, alpha - 1/255) >= 0 (0 - p2 turns p2 = -0 into +0; each difference
-  // has the exact sign of its comparison)
-  const f2v np2 = f2v{0.f, 0.f} - p2;
+  // ok <=> min(kP2Max - p2, alpha - 1/255) >= 0 (each difference has the exact sign of its
+  // comparison)
+  const f2v np2 = f2v{kP2Max, kP2Max} - p2;
   const f2v over = alpha - f2v{1.0f / 255.0f, 1.0f / 255.0f};
   f2v a;
   a.x = fminf(np2.x, over.x) >= 0.f ? alpha.x : 0.f;
@@ -2162,7 +2223,7 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v p
     C01 = __builtin_elementwise_fma(rg, w2, C01);
     C2 = fmaf(P.b[j], wgt, C2);
     Tr = stop ? -fabsf(Tr) : testT;
-    if (LAST) last = wgt > 0.f ? P.pos[j] : last;  // blended <=> wgt > 0 (alpha >= 1/255, T >= 1e-4)
+    if (LAST) lastk = wgt > 0.f ? k0 + j : lastk;  // blended <=> wgt > 0 (alpha >= 1/255, T >= 1e-4)
   }
 }
 
@@ -2172,7 +2233,7 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, f2v pfx2, f2v p
 // when none does the prefix alone gives the exact result. Returns (wave-uniform) whether
 // one does.
 __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* __restrict__ keys, uint32_t b,
-                                  uint32_t e, float fx0, float fy0, f2v pfx2, f2v pfy2, bool alive, PairRec* plist,
+                                  uint32_t e, float fx0, float fy0, const PixUV2& pp, bool alive, WaveList* plist,
                                   uint64_t lt, int lane) {
   uint32_t nid = b + lane < e ? (uint32_t)keys[b + lane] : 0xffffffffu;
   for (uint32_t base = b; base < e; base += 64) {
@@ -2192,20 +2253,20 @@ __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* 
     const uint64_t bal = __ballot(mine);
     if (mine) {
       const float4 sq = scaled_conic_q(q);
-      pair_put(plist, __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * r.x, sq.w, r.y, 0.f, 0.f, 0.f, 0u);
+      pair_put(plist, __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * r.x, sq.w, r.y, 0.f, 0.f, 0.f, 0u, fx0,
+               fy0);
     }
     const int cnt = __popcll(bal);
-    if (lane < 2) pair_put(plist, cnt + lane, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u);
+    if (lane < 2) pair_pad(plist, cnt + lane);
     __builtin_amdgcn_wave_barrier();
     bool hit = false;
     for (int k = 0; k < cnt; k += 2) {
-      const PairRec& P = plist[k >> 1];
-      const f2v dx = P.x - pfx2, dy = P.y - pfy2;
-      const f2v p2 = __builtin_elementwise_fma(P.A * dx, dx, __builtin_elementwise_fma(P.C * dy, dy, P.B * dx * dy));
+      const PairRec& P = plist->rec[k >> 1];
+      const f2v p2 = fall_p2x2(pp, P);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const float alpha = fminf(0.99f, P.o[j] * __builtin_amdgcn_exp2f(p2[j]));
-        hit |= p2[j] <= 0.0f && alpha >= 1.0f / 255.0f;
+        hit |= p2[j] <= kP2Max && alpha >= 1.0f / 255.0f;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -2221,32 +2282,33 @@ __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* 
 // four read ahead.
 template <bool LAST>
 __device__ __forceinline__ void composite_chunk(uint32_t base, uint32_t start, uint32_t end, float4 q, float4 r,
-                                                float b, float lx0, float ly0, float lx1, float ly1, f2v pfx2,
-                                                f2v pfy2, int lane, uint64_t lt, PairRec* plist, float& Tr, f2v& C01,
-                                                float& C2, uint32_t& last) {
+                                                float b, float lx0, float ly0, float lx1, float ly1, float fx0,
+                                                float fy0, const PixUV2& pp, int lane, uint64_t lt, WaveList* plist,
+                                                float& Tr, f2v& C01, float& C2, uint32_t& last) {
   const uint32_t e = base + lane;
   const bool mine = e < end && rect_hit(q, r, lx0, ly0, lx1, ly1);
   const uint64_t bal = __ballot(mine);
   if (mine) {
     const float4 sq = scaled_conic_q(q);  // (x, y, A, B)
     pair_put(plist, __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * r.x, sq.w, r.y, r.z, r.w, b,
-             e - start + 1u);
+             e - start + 1u, fx0, fy0);
   }
   const int cnt = __popcll(bal);
-  if (lane < 8)  // pad up to 8 entries: opacity 0 -> alpha 0 -> never blends
-    pair_put(plist, cnt + lane, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u);
+  if (lane < 8) pair_pad(plist, cnt + lane);  // pad up to 8 entries (never blend)
   __builtin_amdgcn_wave_barrier();
-  const PairRec* pp = plist;
-  PairRec a0 = pp[0], a1 = pp[1];
+  const PairRec* pl = plist->rec;
+  PairRec a0 = pl[0], a1 = pl[1];
+  int lastk = -1;  // LAST: index of the chunk's last blended entry
   for (int k = 0; k < cnt; k += 4) {
-    pp += 2;
-    const PairRec b0 = pp[0], b1 = pp[1];  // in bounds: pair k/2 + 3 <= (CH + 8) / 2 - 1
-    composite_pair<LAST>(a0, pfx2, pfy2, Tr, C01, C2, last);
-    composite_pair<LAST>(a1, pfx2, pfy2, Tr, C01, C2, last);
+    pl += 2;
+    const PairRec b0 = pl[0], b1 = pl[1];  // in bounds: pair k/2 + 3 <= (CH + 8) / 2 - 1
+    composite_pair<LAST>(a0, pp, Tr, C01, C2, lastk, k);
+    composite_pair<LAST>(a1, pp, Tr, C01, C2, lastk, k + 2);
     if (!__any(Tr > 0.f)) break;
     a0 = b0;
     a1 = b1;
   }
+  if (LAST && lastk >= 0) last = plist->pos[lastk];
   __builtin_amdgcn_wave_barrier();  // list reads of this chunk before the next chunk's writes
 }
 
@@ -2259,8 +2321,8 @@ __device__ __forceinline__ void composite_chunk(uint32_t base, uint32_t start, u
 // in flight.
 template <bool LAST, typename KeyAt>
 __device__ __forceinline__ void composite_walk(KeyAt key_at, uint32_t start, uint32_t end, const float* __restrict__ gv,
-                                               float fx0, float fy0, f2v pfx2, f2v pfy2, int lane, uint64_t lt,
-                                               PairRec* plist, float& Tr, f2v& C01, float& C2, uint32_t& last) {
+                                               float fx0, float fy0, const PixUV2& pp, int lane, uint64_t lt,
+                                               WaveList* plist, float& Tr, f2v& C01, float& C2, uint32_t& last) {
   if (start >= end) return;
   // unconditional key reads (clamped index), so HBM key loads need no wait each; entries past
   // the end read record 0 (a valid address) and are masked by the chunk's e < end test
@@ -2289,8 +2351,8 @@ __device__ __forceinline__ void composite_walk(KeyAt key_at, uint32_t start, uin
     if (!live) return;
     float lx0, ly0, lx1, ly1;
     live_rect(live, fx0, fy0, lx0, ly0, lx1, ly1);
-    composite_chunk<LAST>(base, start, end, q[s], r[s], b[s], lx0, ly0, lx1, ly1, pfx2, pfy2, lane, lt, plist, Tr, C01, C2,
-                    last);
+    composite_chunk<LAST>(base, start, end, q[s], r[s], b[s], lx0, ly0, lx1, ly1, fx0, fy0, pp, lane, lt, plist, Tr,
+                          C01, C2, last);
   }
   float4 cq = make_float4(0.f, 0.f, 0.f, 0.f), cr = cq;
   float cb = 0.f;
@@ -2310,7 +2372,8 @@ __device__ __forceinline__ void composite_walk(KeyAt key_at, uint32_t start, uin
     const float4 nq = rec[0], nr = rec[1];
     const float nb = rec[2].x;
     nid = id_of(base + 2 * CH + lane);
-    composite_chunk<LAST>(base, start, end, cq, cr, cb, lx0, ly0, lx1, ly1, pfx2, pfy2, lane, lt, plist, Tr, C01, C2, last);
+    composite_chunk<LAST>(base, start, end, cq, cr, cb, lx0, ly0, lx1, ly1, fx0, fy0, pp, lane, lt, plist, Tr, C01, C2,
+                          last);
     cq = nq;
     cr = nr;
     cb = nb;
@@ -2321,11 +2384,11 @@ __device__ __forceinline__ void composite_walk(KeyAt key_at, uint32_t start, uin
 // stopped) and T = the pixel's transmittance (the final T once stopped).
 template <bool LAST, typename KeyAt>
 __device__ __forceinline__ void composite_tile(KeyAt key_at, uint32_t start, uint32_t end, const float* __restrict__ gv,
-                                               float fx0, float fy0, f2v pfx2, f2v pfy2, int lane, uint64_t lt,
-                                               PairRec* plist, float& Tr, f2v& C01, float& C2, uint32_t& last,
+                                               float fx0, float fy0, const PixUV2& pp, int lane, uint64_t lt,
+                                               WaveList* plist, float& Tr, f2v& C01, float& C2, uint32_t& last,
                                                bool& alive) {
   Tr = alive ? Tr : -Tr;
-  composite_walk<LAST>(key_at, start, end, gv, fx0, fy0, pfx2, pfy2, lane, lt, plist, Tr, C01, C2, last);
+  composite_walk<LAST>(key_at, start, end, gv, fx0, fy0, pp, lane, lt, plist, Tr, C01, C2, last);
   alive = Tr > 0.f;
   Tr = fabsf(Tr);
 }
@@ -2369,7 +2432,7 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
                                                    const uint32_t* __restrict__ seg_filter,
                                                    float* __restrict__ out, float* __restrict__ finalT,
                                                    uint32_t* __restrict__ ncontrib) {
-  __shared__ PairRec l_pair[4][(CH + 8) / 2];
+  __shared__ WaveList l_pair[4];
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   int tx, ty;
@@ -2389,19 +2452,19 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   const float fx0 = (float)sx0, fy0 = (float)sy0;
   const float* gv = geom + (size_t)v * G * GS;
   const uint64_t lt = dsplat::lanemask_lt(lane);
-  PairRec* plist = l_pair[w];
-  const f2v pfx2 = {(float)px, (float)px}, pfy2 = {(float)py, (float)py};
+  WaveList* plist = &l_pair[w];
+  const PixUV2 pp = pix_uv2(pix_uv(px, py, fx0, fy0));
   f2v C01 = {0.f, 0.f};
   float Tr = 1.0f, C2 = 0.f;
   bool alive = inside;
   uint32_t last = 0;
-  composite_tile<true>([&](uint32_t e) { return (uint32_t)keys[e]; }, start, end, gv, fx0, fy0, pfx2, pfy2, lane, lt,
-                 plist, Tr, C01, C2, last, alive);
+  composite_tile<true>([&](uint32_t e) { return (uint32_t)keys[e]; }, start, end, gv, fx0, fy0, pp, lane, lt, plist,
+                       Tr, C01, C2, last, alive);
   bool void_tile = false;  // wave-uniform
   if (absent_tail)
     void_tile = __any(alive);  // a pixel still live at the end of the written part: the rest may blend
   else if (end < tail_end)
-    void_tile = tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pfx2, pfy2, alive, plist, lt, lane);
+    void_tile = tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pp, alive, plist, lt, lane);
   if (void_tile && lane == 0) {  // the tile's output is void: completed, sorted and re-rendered by the caller
     seg_overflow[seg] = 1u;
     seg_overflow[(size_t)gridDim.z * T] = 1u;  // any-flag
@@ -2420,8 +2483,21 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
 // (write_keys), the render never re-reads keys from HBM, and the sort and compositing phases
 // of different tiles overlap inside one launch. A segment above the LDS capacity is sorted
 // through HBM (scratch) by the same workgroup and composited from there.
-template <int KMAX, bool LAST>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kSortWPE))) void k_sort_render(
+// LDS of k_sort_render<KMAX, ·, NBL>: the padded key array, then one area shared by the
+// sort's counters (u16 bins / LSD counters / HBM-path histogram) and, after the sort, the 4
+// waves' pair lists, then the wave sums and flag.
+template <int NBL>
+constexpr int sort_render_aux_words() {
+  constexpr int pl = (int)(sizeof(WaveList) * 4 / 4);
+  return sort_cnt_words<NT, NBL>() > pl ? sort_cnt_words<NT, NBL>() : pl;
+}
+template <int KMAX, int NBL>
+constexpr size_t sort_render_lds_bytes() {
+  return (size_t)(NT * KMAX + NT) * 8 + (size_t)sort_render_aux_words<NBL>() * 4 + 64 * 4;
+}
+
+template <int KMAX, bool LAST, int NBL, int WPE>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_sort_render(
     int G, int H, int W, int gx, int T, const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
     const uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_count, uint32_t stride,
     uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits, int write_keys, int clear_counts,
@@ -2432,9 +2508,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kSortWPE))) 
   uint64_t* A = s_keys;
   uint32_t* aux = reinterpret_cast<uint32_t*>(A + padded);
   uint16_t* cnt = reinterpret_cast<uint16_t*>(aux);
-  uint32_t* wsum = aux + sort_cnt_words<NT>();
+  uint32_t* wsum = aux + sort_render_aux_words<NBL>();
   uint32_t* flag = wsum + 16;
-  static_assert(sizeof(PairRec) * 4 * ((CH + 8) / 2) <= (size_t)sort_cnt_words<NT>() * 4, "pair lists fit the counters");
+  static_assert(NT * 4 <= sort_render_aux_words<NBL>(), "HBM-path radix histogram fits the aux area");
   const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   int tx, ty;
@@ -2452,7 +2528,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kSortWPE))) 
       tmp[i] = idx < n ? keys[b + idx] : 0ull;
     }
     if (n > 1) {
-      count_sort<KMAX, NT>(tmp, n, A, id_bits, cnt, wsum, flag);
+      count_sort<KMAX, NT, NBL>(tmp, n, A, id_bits, cnt, wsum, flag);
     } else {
       if (tid == 0 && n == 1) A[0] = tmp[0];
       __syncthreads();
@@ -2469,18 +2545,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kSortWPE))) 
   const bool inside = px < W && py < H;
   const float* gv = geom + (size_t)v * G * GS;
   const uint64_t lt = dsplat::lanemask_lt(lane);
-  PairRec* plist = reinterpret_cast<PairRec*>(aux) + w * ((CH + 8) / 2);
-  const f2v pfx2 = {(float)px, (float)px}, pfy2 = {(float)py, (float)py};
+  WaveList* plist = reinterpret_cast<WaveList*>(aux) + w;
+  const PixUV2 pp = pix_uv2(pix_uv(px, py, (float)sx0, (float)sy0));
   f2v C01 = {0.f, 0.f};
   float Tr = 1.0f, C2 = 0.f;
   bool alive = inside;
   uint32_t last = 0;
   if (in_lds)
-    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)A[padi<KMAX>(i)]; }, 0u, n, gv, (float)sx0, (float)sy0, pfx2,
-                   pfy2, lane, lt, plist, Tr, C01, C2, last, alive);
+    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)A[padi<KMAX>(i)]; }, 0u, n, gv, (float)sx0, (float)sy0, pp,
+                         lane, lt, plist, Tr, C01, C2, last, alive);
   else
-    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)keys[i]; }, b, e, gv, (float)sx0, (float)sy0, pfx2, pfy2,
-                   lane, lt, plist, Tr, C01, C2, last, alive);
+    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)keys[i]; }, b, e, gv, (float)sx0, (float)sy0, pp, lane, lt,
+                         plist, Tr, C01, C2, last, alive);
   if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
   // counts handed back zeroed for the next call's binning (every thread read it before the
   // sort's first barrier)
@@ -2528,7 +2604,8 @@ struct __align__(16) BwdRec {
   float4 q;   // x, y, A, C (scaled conic, as in the forward)
   float4 r;   // B, opacity, red, green
   float4 s;   // blue, conic a, b, c
-  uint32_t id, pos, pad0, pad1;
+  float F, D, E;  // the forward's falloff polynomial of this wave's sub-tile (fall_poly)
+  uint32_t id, pos, pad[3];
 };
 
 // K7: back-to-front gradient of the compositing (upstream renderCUDA backward semantics).
@@ -2566,6 +2643,7 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
   const size_t pix = (size_t)py * W + px;
   const float pfx = (float)px, pfy = (float)py;
   const float fx0 = (float)sx0, fy0 = (float)sy0;
+  const PixUV puv = pix_uv(px, py, fx0, fy0);
   const float* gv = geom + (size_t)v * G * GS;
   float* dgv = dgeom + (size_t)v * G * GS;
   const float* bg = cams[v].bg;
@@ -2615,6 +2693,10 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
       d.q = make_float4(sq.x, sq.y, sq.z, -0.5f * kLog2e * r.x);
       d.r = make_float4(sq.w, r.y, r.z, r.w);
       d.s = make_float4(bl, q.z, q.w, r.x);
+      const FallPoly f = fall_poly(sq.x, sq.y, sq.z, sq.w, d.q.w, fx0, fy0);
+      d.F = f.F;
+      d.D = f.D;
+      d.E = f.E;
       d.id = id;
       d.pos = (uint32_t)p;
     }
@@ -2633,10 +2715,10 @@ __global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, 
         for (int c = 0; c < 9; ++c) g[j][c] = 0.f;
         const float dx = cur.q.x - pfx, dy = cur.q.y - pfy;
         // same falloff sequence as k_render_fwd (decisions must agree with the forward)
-        const float p2 = falloff_p2(cur.q.z, cur.r.x, cur.q.w, dx, dy);
+        const float p2 = fall_p2(puv, cur.F, cur.D, cur.E, cur.q.z, cur.r.x, cur.q.w);
         const float Gs = __builtin_amdgcn_exp2f(p2);
         const float alpha = fminf(0.99f, cur.r.y * Gs);
-        const bool act = kk >= 0 && cur.pos < lastc && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+        const bool act = kk >= 0 && cur.pos < lastc && p2 <= kP2Max && alpha >= 1.0f / 255.0f;
         any = any || act;
         if (act) {
           const float inv1ma = __builtin_amdgcn_rcpf(1.f - alpha);  // 1 ulp; the grads' tolerance is 2e-3
@@ -3393,30 +3475,61 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
 
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                     const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
-                    uint64_t* scratch, int write_keys, int clear_counts, float* out_color, float* final_T,
-                    uint32_t* n_contrib, void* stream) {
+                    uint64_t* scratch, int write_keys, int clear_counts, uint32_t max_count_hint,
+                    float* out_color, float* final_T, uint32_t* n_contrib, void* stream) {
   DSPLAT_REQUIRE(!clear_counts || seg_stride > 0, "dsr_sort_render: clear_counts needs the fixed-capacity layout");
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_sort_render: bad sizes");
   DSPLAT_REQUIRE(cams && geom && keys && scratch && seg_ptrs_ok(seg_start, seg_count, seg_stride) && out_color &&
                      final_T,
                  "dsr_sort_render: null pointer");
+  // LDS size class from the caller's hint of the largest segment (earlier calls' counts):
+  // smaller key arrays leave room for more resident workgroups (16: 3 per CU, 12 and 8: 4 per
+  // CU at <= 128 VGPRs). A segment above the chosen class is still sorted exactly, through
+  // `scratch` (slower), so the hint only affects speed.
+  struct Cls {
+    uint32_t cap;
+    const void* k[2];  // LAST = false, true
+    size_t lds;
+  };
+  static const Cls cls[3] = {
+      {NT * 8u, {(const void*)k_sort_render<8, false, 12, 4>, (const void*)k_sort_render<8, true, 12, 4>},
+       sort_render_lds_bytes<8, 12>()},
+      {NT * 12u, {(const void*)k_sort_render<12, false, 12, 4>, (const void*)k_sort_render<12, true, 12, 4>},
+       sort_render_lds_bytes<12, 12>()},
+      {NT * 16u, {(const void*)k_sort_render<16, false, 13, 3>, (const void*)k_sort_render<16, true, 13, 3>},
+       sort_render_lds_bytes<16, 13>()}};
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)k_sort_render<16, true>, (const void*)k_sort_render<16, false>})
-      if (int e = dsplat::check_hip(
-              hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sort_lds_bytes<16>()),
-              "hipFuncSetAttribute(k_sort_render)"))
-        return e;
+    for (const Cls& c : cls)
+      for (const void* f : c.k)
+        if (int e = dsplat::check_hip(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds),
+                                      "hipFuncSetAttribute(k_sort_render)"))
+          return e;
     attr = true;
   }
+  int ci = 0;
+  while (ci < 2 && (max_count_hint == 0 || max_count_hint > cls[ci].cap)) ++ci;
   int id_bits = 0;
   while (id_bits < 32 && ((uint64_t)1 << id_bits) < (uint64_t)G) ++id_bits;
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
-  auto kern = n_contrib ? k_sort_render<16, true> : k_sort_render<16, false>;  // n_contrib is optional
-  kern<<<grid, NT, sort_lds_bytes<16>(), (hipStream_t)stream>>>(
-      G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count, seg_stride, keys, scratch, id_bits, write_keys,
-      clear_counts, out_color, final_T, n_contrib);
+  const int T = gx * gy;
+  const size_t lds = cls[ci].lds;
+  hipStream_t st = (hipStream_t)stream;
+#define DSR_SR_LAUNCH(K, L, NB, WP)                                                                          \
+  k_sort_render<K, L, NB, WP><<<grid, NT, lds, st>>>(G, H, W, gx, T, cams, geom, seg_start, seg_count, seg_stride, \
+                                                     keys, scratch, id_bits, write_keys, clear_counts, out_color,  \
+                                                     final_T, n_contrib)
+  // n_contrib is optional (inference: LAST = false)
+  switch (ci * 2 + (n_contrib ? 1 : 0)) {
+    case 0: DSR_SR_LAUNCH(8, false, 12, 4); break;
+    case 1: DSR_SR_LAUNCH(8, true, 12, 4); break;
+    case 2: DSR_SR_LAUNCH(12, false, 12, 4); break;
+    case 3: DSR_SR_LAUNCH(12, true, 12, 4); break;
+    case 4: DSR_SR_LAUNCH(16, false, 13, 3); break;
+    default: DSR_SR_LAUNCH(16, true, 13, 3); break;
+  }
+#undef DSR_SR_LAUNCH
   return dsplat::check_launch("k_sort_render");
 }
 

@@ -211,6 +211,9 @@ CUT_SORT_HINT = 4096  # LDS sort size for the written parts (larger ones sort th
 # dsr_render_fwd (MSD split, prefix sort). Either is exact for any list length.
 FUSED_SORT_RENDER = os.environ.get("DSPLAT_FUSED_SORT_RENDER", "1") != "0"
 FUSED_MAX = 4096
+# dsr_sort_render's LDS class comes from the largest count of earlier calls (_spec); a nonzero
+# override pins it (tests: every class on the same lists)
+SORT_RENDER_HINT = 0
 # inference fast path (cameras inside the binning kernel, self-zeroing counters); env
 # DSPLAT_INKERNEL_CAMERAS=0 keeps the separate camera launch (experiments)
 INKERNEL_CAMERAS = os.environ.get("DSPLAT_INKERNEL_CAMERAS", "1") != "0"
@@ -560,7 +563,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         snap = seg_count.clone() if (fast and DEBUG_KEEP_FAST_LISTS) else None
         _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(), None,
                           seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(),
-                          int(bool(need_state) or snap is not None), int(fast), *outs), "dsr_sort_render")
+                          int(bool(need_state) or snap is not None), int(fast), SORT_RENDER_HINT or _spec["max_count"],
+                          *outs), "dsr_sort_render")
         state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, cams=cams)
         if fast:  # the counters are zero again once the launch above has run
             _give_back_clean_counts(seg_count, dev, st)

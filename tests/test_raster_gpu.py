@@ -247,6 +247,40 @@ def test_large_tiles_sort_paths(gpu, binning, hint, prefix, monkeypatch):
         o.close()
 
 
+@pytest.mark.parametrize("n_keep", [1900, 2600, 3500, 5000])
+def test_sort_render_lds_classes(gpu, n_keep, monkeypatch):
+    """dsr_sort_render's LDS classes (2048 / 3072 / 4096 keys per tile, picked by
+    max_count_hint) on tiles of ~n_keep entries: below, inside and above each class (above:
+    the in-kernel HBM sort). Every class writes the oracle's sorted lists and the same image,
+    n_contrib and final T bit for bit."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setitem(raster._spec, "max_count", 4096)  # fused sort + render
+    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
+    sc = _large_tile_scene(opacity_scale=0.02)
+    g = sc.gaussians
+    g.means, g.covariances = g.means[:, :n_keep].contiguous(), g.covariances[:, :n_keep].contiguous()
+    g.harmonics, g.opacities = g.harmonics[:, :n_keep].contiguous(), g.opacities[:, :n_keep].contiguous()
+    st = settings_for(sc)
+    outs = {}
+    for hint in (4096, 3072, 2048):
+        monkeypatch.setattr(raster, "SORT_RENDER_HINT", hint)
+        color, state, _ = hip_forward(sc, st, gpu)
+        assert state.seg_stride > 0 and state.seg_sorted is None  # the fused launch ran
+        outs[hint] = (color, state.n_contrib.clone(), state.final_T.clone(), _segments(state, 2, 4))
+    assert max(int(c) for c in outs[4096][3][1] - outs[4096][3][0]) > 0.8 * n_keep
+    for hint in (3072, 2048):
+        for a, b in zip(outs[hint][:3], outs[4096][:3]):
+            assert torch.equal(a, b), f"class {hint} differs from class 4096"
+    b0, e0, k0 = outs[4096][3]
+    for hint in (3072, 2048):
+        b1, e1, k1 = outs[hint][3]
+        for s in range(len(b0)):
+            np.testing.assert_array_equal(k1[b1[s]:e1[s]], k0[b0[s]:e0[s]])
+    monkeypatch.setattr(raster, "SORT_RENDER_HINT", 2048)
+    color, state, _ = hip_forward(sc, st, gpu)
+    _check_segments_vs_oracle(state, oracle_views(sc, st), 2, 4)
+
+
 @pytest.mark.parametrize("binning", ["fused", "two_phase"])
 def test_prefix_sort_overflow_fixup(gpu, binning, monkeypatch):
     """Faint Gaussians (alpha just above 1/255): no pixel saturates, so the unsorted tail of
@@ -315,8 +349,11 @@ def test_prefix_sort_matches_full_sort(gpu, monkeypatch):
     fa, fb = out[4096][1], out[0][1]
     for a, b in zip(fa[:3], fb[:3]):  # forward: bit-identical
         assert torch.equal(a, b)
-    for a, b in zip(fa[3:], fb[3:]):  # gradients: same terms, float atomics add them in any order
-        assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max())
+    # gradients: same terms, float atomics add them in any order. On this scene the per-pixel
+    # terms cancel heavily (dL/dopacity reaches ~350 for sums ~0.1): two runs of the SAME
+    # layout already differ by up to ~1e-4 of the max (tools/grad_determinism.py on the GPU box)
+    for a, b in zip(fa[3:], fb[3:]):
+        assert float((a - b).abs().max()) <= 5e-4 * float(b.abs().max())
 
 
 def _forward_backward(sc, st, gpu):
@@ -371,8 +408,11 @@ def test_depth_cut_matches_full_scatter(gpu, opacity, monkeypatch):
     fa, fb = out[1024][1], out[0][1]
     for a, b in zip(fa[:3], fb[:3]):  # forward: bit-identical
         assert torch.equal(a, b)
-    for a, b in zip(fa[3:], fb[3:]):  # gradients: same terms, float atomics add them in any order
-        assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max())
+    # gradients: same terms, float atomics add them in any order. On this scene the per-pixel
+    # terms cancel heavily (dL/dopacity reaches ~350 for sums ~0.1): two runs of the SAME
+    # layout already differ by up to ~1e-4 of the max (tools/grad_determinism.py on the GPU box)
+    for a, b in zip(fa[3:], fb[3:]):
+        assert float((a - b).abs().max()) <= 5e-4 * float(b.abs().max())
     orcs = oracle_views(sc, st)
     _check_segments_vs_oracle(stc, orcs, 2, 4)
     for v, o in enumerate(orcs):

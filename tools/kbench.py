@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--two-phase", action="store_true", help="force the two-phase binning layout")
     ap.add_argument("--exact", action="store_true", help="replay the inference path's exact-binning lists")
     ap.add_argument("--no-ncontrib", action="store_true", help="sort_render without n_contrib (inference)")
+    ap.add_argument("--hint", type=int, default=0, help="sort_render max_count_hint (LDS class; 0 = largest)")
     ap.add_argument("--counters", action="store_true",
                     help="render_bwd: print the 4 uint32 counters an instrumented variant parks in the padding "
                          "words of dgeom's last two rows")
@@ -130,7 +131,7 @@ def main():
 
             def launch():
                 return lib.dsr_sort_render(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), None, sc_p, stride,
-                                           state.keys.data_ptr(), scr4.data_ptr(), 0, 0, out[0].data_ptr(),
+                                           state.keys.data_ptr(), scr4.data_ptr(), 0, 0, a.hint, out[0].data_ptr(),
                                            out[1].data_ptr(), out[2].data_ptr() if len(out) > 2 else None, st)
         elif a.kernel == "scatter":  # two-phase key scatter from the scan's segment starts
             assert stride == 0, "two-phase layout expected (--two-phase)"

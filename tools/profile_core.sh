@@ -1,0 +1,48 @@
+#!/bin/bash
+# Round-2 profile on the GPU box (repo root): GPU tests, kernel-trace stats of the bench (the
+# calibrated headline configuration: 4 scenes per step on 4 streams, and one scene per step on
+# one graph), separate PMC passes per counter group for the headline (exact binning only, one
+# and four scenes per launch), the config C training step, the config E reconstruction and
+# the cost volume, then JSON summaries.
+# usage: bash tools/profile_core.sh TAG  (the legs: tools/profile_legs2.sh TAG)
+set -u
+tag=${1:?tag}
+export TMPDIR=/tmp
+out=gpurun_out/prof_$tag
+mkdir -p $out
+run() {  # run NAME TIMEOUT CMD...: stop the whole script on a timeout / signal / crash
+  local name=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $out/$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  if [ $rc -ge 124 ]; then echo "stopping after $name"; exit $rc; fi
+}
+B="python3 bench.py --no-cpu-baseline --no-reference-binning"
+export DSPLAT_PARITY_REPORT=$out/parity.jsonl
+run gputest 400 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 240 --timeout-method thread
+tail -3 $out/gputest.log
+unset DSPLAT_PARITY_REPORT
+run stats_b4 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b4 -o run -- \
+  $B --steps 50 --warmup 5 --extra "" --batch 4 --launch hipgraph4
+# the bench's roofline leg: the same 4-scene step launched eagerly on one stream (HIP events
+# around the dominant kernel; the rocprof average of that kernel here must agree with it)
+run stats_b4_eager 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b4_eager -o run -- \
+  $B --steps 50 --warmup 5 --extra "" --batch 4 --launch eager
+run stats_b8_eager 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b8_eager -o run -- \
+  $B --steps 50 --warmup 5 --extra "" --batch 8 --launch eager
+run stats_b1 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b1 -o run -- \
+  $B --steps 50 --warmup 5 --extra "" --batch 1 --launch hipgraph
+for b in 1 2 4 8; do
+  for pass in FETCH_SIZE WRITE_SIZE \
+    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT"; do
+    n=$(echo $pass | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+    run pmc_b${b}_$n 240 rocprofv3 --kernel-trace --pmc $pass --output-format csv -d $out/pmc_b${b}_$n -o run -- \
+      $B --steps 10 --warmup 3 --eager --batch $b --extra ""
+  done
+  python3 tools/pmc_summary.py --json $out/pmc_traffic_2v256x256x3b$b.json 2v256x256x3b$b \
+    "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ, $tag" $out/pmc_b${b}_fetch_size $out/pmc_b${b}_write_size \
+    $out/pmc_b${b}_sq_waves
+done
+run bench 400 python3 -u bench.py
+tail -c 1500 $out/bench.log
+echo done

@@ -37,7 +37,7 @@ scr = torch.zeros_like(st.keys)
 s = _lib.stream_of(dev)
 for _ in range(20):
     assert lib.dsr_sort_render(G, V, H, W, st.cams.data_ptr(), st.geom.data_ptr(), None, st.seg_count.data_ptr(),
-                               st.seg_stride, st.keys.data_ptr(), scr.data_ptr(), 0, 0, out[0].data_ptr(),
+                               st.seg_stride, st.keys.data_ptr(), scr.data_ptr(), 0, 0, 0, out[0].data_ptr(),
                                out[1].data_ptr(), out[2].data_ptr(), s) == 0
 torch.cuda.synchronize()
 nt = st.seg_count.numel()
