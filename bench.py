@@ -74,12 +74,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL ("nccl"). DSPLAT_DIST_BACKEND=gloo with more ranks than GPUs
+    # rehearses the multi-rank path on a one-GPU box (ranks share device local % count; RCCL
+    # refuses two ranks on one device)
+    backend = os.environ.get("DSPLAT_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % ndev if backend != "nccl" and ndev else local)
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from my_depthsplat_amd import _lib, raster
     from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
@@ -119,7 +126,7 @@ def main():
     def max_over_ranks(*vals):
         if world == 1:
             return vals
-        t = torch.tensor(vals, device=dev, dtype=torch.float64)
+        t = torch.tensor(vals, device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return tuple(float(x) for x in t.tolist())
 

@@ -56,7 +56,12 @@ def allreduce_gradients(params, world: int | None = None) -> int:
     grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
     flat = torch.cat([g.reshape(-1).float() for g in grads])
     if world > 1:
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        if flat.is_cuda and dist.get_backend() == "gloo":  # gloo rehearsal of the GPU path
+            host = flat.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM)
+            flat.copy_(host)
+        else:
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM)
         flat /= world
     off = 0
     for p, g in zip(params, grads):
