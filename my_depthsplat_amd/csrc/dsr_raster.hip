@@ -606,8 +606,8 @@ __device__ __forceinline__ TileEll tile_ell(const float* rec, int r) {
   e.c = rec[4];
   const float op = rec[5];
   e.t2 = (r > 0 && op >= 1.0f / 255.0f) ? 2.0f * __logf(255.0f * op) * 1.002f + 0.02f : -1.0f;
-  e.ia = 1.0f / e.a;
-  e.ic = 1.0f / e.c;
+  e.ia = __builtin_amdgcn_rcpf(e.a);  // edge minimiser only (see rect_hit)
+  e.ic = __builtin_amdgcn_rcpf(e.c);
   return e;
 }
 __device__ __forceinline__ TileEll tile_ell_of(const TileEll& e, int o) {
@@ -2021,27 +2021,6 @@ __device__ __forceinline__ float4 scaled_conic_q(float4 q) {  // (x, y, a, b) ->
   return make_float4(q.x, q.y, -0.5f * kLog2e * q.z, -kLog2e * q.w);
 }
 
-__device__ __forceinline__ uint32_t subtile_mask(float4 q, float4 r, int tx0, int ty0) {
-  // q = (x, y, conic a, conic b), r = (conic c, opacity, ...); tile origin (tx0, ty0)
-  const float op = r.y;
-  if (!(op >= 1.0f / 255.0f)) return 0u;  // alpha = min(.99, o G) <= o < 1/255 everywhere
-  const float t2 = 2.0f * __logf(255.0f * op);
-  const float det = q.z * r.x - q.w * q.w;
-  // half extents of the ellipse's bounding box, padded against rounding
-  const float hx = sqrtf(fmaxf(t2 * r.x / det, 0.f)) * 1.002f + 0.05f;
-  const float hy = sqrtf(fmaxf(t2 * q.z / det, 0.f)) * 1.002f + 0.05f;
-  uint32_t m = 0;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const float x0 = (float)(tx0 + (w & 1) * SUB), y0 = (float)(ty0 + (w >> 1) * SUB);
-    const bool out = (q.x + hx < x0) || (q.x - hx > x0 + (SUB - 1)) || (q.y + hy < y0) || (q.y - hy > y0 + (SUB - 1));
-    m |= (out ? 0u : 1u) << w;
-  }
-  // NaN / degenerate conic: keep (never cull what cannot be proven irrelevant)
-  if (!(det > 0.f) || !(hx == hx) || !(hy == hy)) m = 0xFu;
-  return m;
-}
-
 // Can the alpha >= 1/255 region of a Gaussian reach any pixel centre of the 8x8 sub-tile
 // [x0, x0 + 7] x [y0, y0 + 7]? Exact for the continuous box (conservative for the pixel
 // centres in it): with Q(d) = a dx^2 + 2b dx dy + c dy^2 (the conic; power = -Q/2) and
@@ -2059,7 +2038,9 @@ __device__ __forceinline__ bool rect_hit(float4 q, float4 r, float x0, float y0,
   const float ly = y0 - q.y, hy = y1 - q.y;
   if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;
   if (lx <= 0.f && hx >= 0.f && ly <= 0.f && hy >= 0.f) return true;
-  const float ia = 1.0f / a, ic = 1.0f / c;
+  // the clamped 1-D minimiser only has to be a point of the edge: with the hardware
+  // reciprocal (1 ulp) it moves by ~1e-7 relative, which changes Q there to second order
+  const float ia = __builtin_amdgcn_rcpf(a), ic = __builtin_amdgcn_rcpf(c);
   float m = 3.4e38f;
   // edges x = const
 #pragma unroll
@@ -2076,9 +2057,6 @@ __device__ __forceinline__ bool rect_hit(float4 q, float4 r, float x0, float y0,
     m = fminf(m, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
   }
   return !(m > t2);
-}
-__device__ __forceinline__ bool subtile_hit(float4 q, float4 r, float x0, float y0) {
-  return rect_hit(q, r, x0, y0, x0 + (SUB - 1), y0 + (SUB - 1));
 }
 
 // Bounding box (pixel centres) of the wave's still-live pixels (lane = 8 * row + col of the
@@ -3501,6 +3479,11 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
        sort_render_lds_bytes<12, 12>()},
       {NT * 16u, {(const void*)k_sort_render<16, false, 13, 3>, (const void*)k_sort_render<16, true, 13, 3>},
        sort_render_lds_bytes<16, 13>()}};
+  // 2048-key class without n_contrib at 5 waves per EU (31 KB: 5 WGs per CU at <= 96 VGPRs,
+  // some spills): wins once the grid fills the chip several times over (kbench at 12 / 24
+  // views: -2 / -3 %), loses on one scene's 768 tiles (+5 %)
+  constexpr int kWide = 2048;  // (view, tile) segments from which the 5-wave kernel is used
+  const void* k8w5 = (const void*)k_sort_render<8, false, 12, 5>;
   static bool attr = false;
   if (!attr) {
     for (const Cls& c : cls)
@@ -3508,6 +3491,10 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
         if (int e = dsplat::check_hip(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds),
                                       "hipFuncSetAttribute(k_sort_render)"))
           return e;
+    if (int e = dsplat::check_hip(
+            hipFuncSetAttribute(k8w5, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cls[0].lds),
+            "hipFuncSetAttribute(k_sort_render)"))
+      return e;
     attr = true;
   }
   int ci = 0;
@@ -3524,8 +3511,14 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
                                                      keys, scratch, id_bits, write_keys, clear_counts, out_color,  \
                                                      final_T, n_contrib)
   // n_contrib is optional (inference: LAST = false)
+  const bool wide = (int64_t)V * T >= kWide;
   switch (ci * 2 + (n_contrib ? 1 : 0)) {
-    case 0: DSR_SR_LAUNCH(8, false, 12, 4); break;
+    case 0:
+      if (wide)
+        DSR_SR_LAUNCH(8, false, 12, 5);
+      else
+        DSR_SR_LAUNCH(8, false, 12, 4);
+      break;
     case 1: DSR_SR_LAUNCH(8, true, 12, 4); break;
     case 2: DSR_SR_LAUNCH(12, false, 12, 4); break;
     case 3: DSR_SR_LAUNCH(12, true, 12, 4); break;

@@ -521,6 +521,35 @@ def test_decoder_batched_views(gpu):
         assert torch.equal(out.color[b], want)
 
 
+def test_sort_render_wide_grid_kernel(gpu, monkeypatch):
+    """Inference (no n_contrib) on >= 2048 (view, tile) segments takes the 2048-key class at
+    5 waves per EU; its images equal the 3072-key class's bit for bit, and view 0 matches the
+    oracle (config B scenes, 4 per call: 12 views x 256 tiles)."""
+    from my_depthsplat_amd import raster
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.synthetic import make_scene
+    sc = make_scene(batch=4, n_context=2, n_targets=3, height=256, width=256, seed=21, device=gpu)
+    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(gpu)
+    outs = {}
+    for hint in (2048, 3072, 2048):
+        monkeypatch.setattr(raster, "SORT_RENDER_HINT", hint)
+        with torch.no_grad():
+            outs.setdefault(hint, []).append(
+                dec(sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near, sc.far, (256, 256)).color)
+    assert torch.equal(outs[2048][0], outs[3072][0]) and torch.equal(outs[2048][1], outs[3072][0])
+    from my_depthsplat_amd.cuda_splatting import _cov6, camera_settings
+    from oracle import raster as orc
+    g = sc.gaussians
+    shs = g.harmonics[0].transpose(-1, -2).contiguous().cpu()
+    st = {k: t.cpu().numpy() for k, t in
+          camera_settings(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0]).items()}
+    o = orc.render_settings(g.means[0].cpu().numpy(), shs.numpy(), None, g.opacities[0].cpu().numpy(),
+                            _cov6(g.covariances[0]).cpu().numpy(), st, 0, np.zeros(3, np.float32), 256, 256, 2)
+    ref, _, _ = o.image()
+    o.close()
+    assert float(np.abs(outs[2048][0][0, 0].cpu().numpy() - ref).mean()) < 1e-4
+
+
 @pytest.mark.parametrize("n_ties", [6, 100000, -1])
 def test_equal_depth_ties_sorted_by_id(gpu, n_ties):
     """Equal view-space depths: a few tie pairs (insertion fix-up) and a fronto-parallel
