@@ -1,7 +1,7 @@
 """Phase timing of k_project_emit (inference binning, in-kernel cameras) from an instrumented
 variant (GPU box): per workgroup, s_memrealtime (100 MHz) at start, after projection, after the
 count pass, after the global range reservation and at the end of the emission, written into
-the tail of the key buffer. usage: python tools/pe_timing.py VARIANT [batch]"""
+the tail of the key buffer. usage: python tools/pe_timing_build.py (builds VARIANT "pet"); python tools/pe_timing.py pet [batch]"""
 import ctypes
 import sys
 from pathlib import Path
