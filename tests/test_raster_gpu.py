@@ -350,10 +350,12 @@ def test_prefix_sort_matches_full_sort(gpu, monkeypatch):
     for a, b in zip(fa[:3], fb[:3]):  # forward: bit-identical
         assert torch.equal(a, b)
     # gradients: same terms, float atomics add them in any order. On this scene the per-pixel
-    # terms cancel heavily (dL/dopacity reaches ~350 for sums ~0.1): two runs of the SAME
-    # layout already differ by up to ~1e-4 of the max (tools/grad_determinism.py on the GPU box)
+    # terms cancel heavily (dL/dopacity reaches ~350 for sums ~0.1; dmeans goes through the
+    # conic's Jacobian): two runs of the SAME layout differ by up to ~7e-4 of the max of dmeans
+    # (tools/grad_determinism.py on the GPU box), so the bar is the gradient parity bar of
+    # DESIGN.md §3 (2e-3 of the max)
     for a, b in zip(fa[3:], fb[3:]):
-        assert float((a - b).abs().max()) <= 5e-4 * float(b.abs().max())
+        assert float((a - b).abs().max()) <= 2e-3 * float(b.abs().max())
 
 
 def _forward_backward(sc, st, gpu):
@@ -409,10 +411,12 @@ def test_depth_cut_matches_full_scatter(gpu, opacity, monkeypatch):
     for a, b in zip(fa[:3], fb[:3]):  # forward: bit-identical
         assert torch.equal(a, b)
     # gradients: same terms, float atomics add them in any order. On this scene the per-pixel
-    # terms cancel heavily (dL/dopacity reaches ~350 for sums ~0.1): two runs of the SAME
-    # layout already differ by up to ~1e-4 of the max (tools/grad_determinism.py on the GPU box)
+    # terms cancel heavily (dL/dopacity reaches ~350 for sums ~0.1; dmeans goes through the
+    # conic's Jacobian): two runs of the SAME layout differ by up to ~7e-4 of the max of dmeans
+    # (tools/grad_determinism.py on the GPU box), so the bar is the gradient parity bar of
+    # DESIGN.md §3 (2e-3 of the max)
     for a, b in zip(fa[3:], fb[3:]):
-        assert float((a - b).abs().max()) <= 5e-4 * float(b.abs().max())
+        assert float((a - b).abs().max()) <= 2e-3 * float(b.abs().max())
     orcs = oracle_views(sc, st)
     _check_segments_vs_oracle(stc, orcs, 2, 4)
     for v, o in enumerate(orcs):
