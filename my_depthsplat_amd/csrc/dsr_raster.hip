@@ -3479,11 +3479,11 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
        sort_render_lds_bytes<12, 12>()},
       {NT * 16u, {(const void*)k_sort_render<16, false, 13, 3>, (const void*)k_sort_render<16, true, 13, 3>},
        sort_render_lds_bytes<16, 13>()}};
-  // 2048-key class without n_contrib at 5 waves per EU (31 KB: 5 WGs per CU at <= 96 VGPRs,
-  // some spills): wins once the grid fills the chip several times over (kbench at 12 / 24
-  // views: -2 / -3 %), loses on one scene's 768 tiles (+5 %)
-  constexpr int kWide = 2048;  // (view, tile) segments from which the 5-wave kernel is used
-  const void* k8w5 = (const void*)k_sort_render<8, false, 12, 5>;
+  // 2048-key class at 5 waves per EU (31 KB: 5 WGs per CU at <= 96 VGPRs, some spills): wins
+  // once the grid fills the chip several times over (kbench, inference at 12 / 24 views: -2 /
+  // -3 %; with n_contrib at 16 / 64 views: -5 / -6 %), loses on one scene's 768 tiles (+5 %)
+  constexpr int kWide = 2048;  // (view, tile) segments from which the 5-wave kernels are used
+  const void* k8w5[2] = {(const void*)k_sort_render<8, false, 12, 5>, (const void*)k_sort_render<8, true, 12, 5>};
   static bool attr = false;
   if (!attr) {
     for (const Cls& c : cls)
@@ -3491,10 +3491,10 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
         if (int e = dsplat::check_hip(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds),
                                       "hipFuncSetAttribute(k_sort_render)"))
           return e;
-    if (int e = dsplat::check_hip(
-            hipFuncSetAttribute(k8w5, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cls[0].lds),
-            "hipFuncSetAttribute(k_sort_render)"))
-      return e;
+    for (const void* f : k8w5)
+      if (int e = dsplat::check_hip(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cls[0].lds),
+                                    "hipFuncSetAttribute(k_sort_render)"))
+        return e;
     attr = true;
   }
   int ci = 0;
@@ -3519,7 +3519,12 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
       else
         DSR_SR_LAUNCH(8, false, 12, 4);
       break;
-    case 1: DSR_SR_LAUNCH(8, true, 12, 4); break;
+    case 1:
+      if (wide)
+        DSR_SR_LAUNCH(8, true, 12, 5);
+      else
+        DSR_SR_LAUNCH(8, true, 12, 4);
+      break;
     case 2: DSR_SR_LAUNCH(12, false, 12, 4); break;
     case 3: DSR_SR_LAUNCH(12, true, 12, 4); break;
     case 4: DSR_SR_LAUNCH(16, false, 13, 3); break;

@@ -552,6 +552,19 @@ def test_sort_render_wide_grid_kernel(gpu, monkeypatch):
     ref, _, _ = o.image()
     o.close()
     assert float(np.abs(outs[2048][0][0, 0].cpu().numpy() - ref).mean()) < 1e-4
+    # with a backward (n_contrib tracked: the LAST kernels): same image, gradients at the
+    # float-atomic-order bar
+    res = {}
+    for hint in (2048, 3072):
+        monkeypatch.setattr(raster, "SORT_RENDER_HINT", hint)
+        means = sc.gaussians.means.clone().requires_grad_(True)
+        gs = type(sc.gaussians)(means, sc.gaussians.covariances, sc.gaussians.harmonics, sc.gaussians.opacities)
+        col = dec(gs, sc.target_extrinsics, sc.target_intrinsics, sc.near, sc.far, (256, 256)).color
+        (col * torch.linspace(-1, 1, col.numel(), device=gpu).view_as(col)).sum().backward()
+        res[hint] = (col.detach(), means.grad)
+    assert torch.equal(res[2048][0], res[3072][0]) and torch.equal(res[2048][0], outs[3072][0])
+    d, m = (res[2048][1] - res[3072][1]).abs().max(), res[3072][1].abs().max()
+    assert float(d) <= 2e-3 * float(m)
 
 
 @pytest.mark.parametrize("n_ties", [6, 100000, -1])
