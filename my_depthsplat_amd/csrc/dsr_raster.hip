@@ -2597,7 +2597,10 @@ struct __align__(16) BwdRec {
 // lane 63 parks the sums in LDS; at the end of the chunk the wave adds them to dgeom with
 // one global atomic per non-zero (entry, component).
 constexpr int BCH = 64;
-__global__ __launch_bounds__(NT) void k_render_bwd(int G, int H, int W, int gx, int T,
+// WPE = 5 (96 VGPRs, small spills) pays only on wide grids (kbench at 64 views: -3 %; 16:
+// level; 3: +12 %), so dsr_render_bwd picks it from the number of tiles.
+template <int WPE>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_render_bwd(int G, int H, int W, int gx, int T,
                                                    const dsr_camera* __restrict__ cams,
                                                    const float* __restrict__ geom,
                                                    const uint32_t* __restrict__ seg_start,
@@ -3544,8 +3547,10 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
                  "dsr_render_bwd: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
-  k_render_bwd<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count,
-                                                     seg_stride, keys, final_T, n_contrib, dL_dpix, dgeom);
+  constexpr int64_t kWideBwd = 8192;  // (view, tile) segments from which WPE = 5 pays
+  auto kern = (int64_t)V * gx * gy >= kWideBwd ? k_render_bwd<5> : k_render_bwd<1>;
+  kern<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count, seg_stride, keys,
+                                             final_T, n_contrib, dL_dpix, dgeom);
   return dsplat::check_launch("k_render_bwd");
 }
 

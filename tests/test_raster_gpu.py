@@ -567,6 +567,40 @@ def test_sort_render_wide_grid_kernel(gpu, monkeypatch):
     assert float(d) <= 2e-3 * float(m)
 
 
+def test_render_bwd_wide_grid_kernel(gpu):
+    """dsr_render_bwd on >= 8192 (view, tile) segments runs the 5-waves-per-EU instance: its
+    per-view gradients equal those of the narrow instance (the same call on the first 3 views
+    only) up to float-atomic order."""
+    from my_depthsplat_amd import _lib, raster
+    from my_depthsplat_amd.synthetic import make_scene
+    V, H, W = 32, 256, 256
+    sc = make_scene(batch=1, n_context=2, n_targets=V, height=H, width=W, seed=33, device=gpu)
+    g = sc.gaussians
+    cams = raster.build_cameras(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0],
+                                torch.zeros(V, 3, device=gpu), [0] * V, True)
+    layout = raster.input_layout(g.harmonics, g.covariances, True, True)
+    color, st = raster.forward_raw(g.means, g.harmonics, True, 2, g.opacities, g.covariances, cams, V, H, W, layout)
+    G = g.means.shape[1]
+    gx, gy = raster.tiles(H, W)
+    assert V * gx * gy >= 8192
+    dpix = torch.randn(color.shape, generator=torch.Generator(device=gpu).manual_seed(3), device=gpu)
+    lib, stream = _lib.load(), _lib.stream_of(gpu)
+    sp = None if st.seg_start is None else st.seg_start.data_ptr()
+    out = {}
+    for n in (V, 3):
+        dgeom = torch.zeros((n, G, raster.GEOM_STRIDE), device=gpu)
+        _lib.check(lib.dsr_render_bwd(G, n, H, W, cams.data_ptr(), st.geom.data_ptr(), sp, st.seg_count.data_ptr(),
+                                      st.seg_stride, st.keys.data_ptr(), st.final_T.data_ptr(),
+                                      st.n_contrib.data_ptr(), dpix.data_ptr(), dgeom.data_ptr(), stream),
+                   "dsr_render_bwd")
+        out[n] = dgeom
+    torch.cuda.synchronize()
+    a, b = out[V][:3], out[3]
+    for c in range(9):  # the 9 gradient fields of each record
+        m = float(b[..., c].abs().max())
+        assert m > 0 and float((a[..., c] - b[..., c]).abs().max()) <= 2e-3 * m, c
+
+
 @pytest.mark.parametrize("n_ties", [6, 100000, -1])
 def test_equal_depth_ties_sorted_by_id(gpu, n_ties):
     """Equal view-space depths: a few tie pairs (insertion fix-up) and a fronto-parallel
