@@ -1,5 +1,5 @@
-"""Phase timing of k_sort_render from the instrumented variant of tools/timing_variant.py
-(GPU box).
+"""Phase timing of k_sort_render from the instrumented variant built by
+tools/sr_timing_build.py (GPU box); the inference launch (2048-key class, no n_contrib).
 usage: python tools/sr_timing.py VARIANT [H W V]"""
 import ctypes
 import sys
@@ -37,8 +37,8 @@ scr = torch.zeros_like(st.keys)
 s = _lib.stream_of(dev)
 for _ in range(20):
     assert lib.dsr_sort_render(G, V, H, W, st.cams.data_ptr(), st.geom.data_ptr(), None, st.seg_count.data_ptr(),
-                               st.seg_stride, st.keys.data_ptr(), scr.data_ptr(), 0, 0, 0, out[0].data_ptr(),
-                               out[1].data_ptr(), out[2].data_ptr(), s) == 0
+                               st.seg_stride, st.keys.data_ptr(), scr.data_ptr(), 0, 0, 2048, out[0].data_ptr(),
+                               out[1].data_ptr(), None, s) == 0
 torch.cuda.synchronize()
 nt = st.seg_count.numel()
 t = scr[: nt * 32].view(nt, 4, 8).cpu().numpy().astype(np.int64)
