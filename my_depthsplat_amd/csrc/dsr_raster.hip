@@ -2436,10 +2436,9 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
                                                    float* __restrict__ out, float* __restrict__ finalT,
                                                    uint32_t* __restrict__ ncontrib) {
   __shared__ WaveList l_pair[4];
-  const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   int tx, ty;
-  tile_of(gx, T / gx, tx, ty);
+  const int v = tile_xcd(gx, T / gx, tx, ty);  // kbench: 3 views -4..-6 %, 64 views level
   const int sx0 = tx * BX + (w & 1) * SUB, sy0 = ty * BY + (w >> 1) * SUB;
   const int px = sx0 + (lane & (SUB - 1));
   const int py = sy0 + (lane >> 3);
@@ -2633,10 +2632,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                                                    float* __restrict__ dgeom) {
   __shared__ BwdRec l_rec[4][BCH + 1];
   __shared__ float l_acc[4][BCH * 9];
-  const int v = blockIdx.z;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   int tx, ty;
-  tile_of(gx, T / gx, tx, ty);
+  const int v = tile_xcd(gx, T / gx, tx, ty);  // kbench: 3 views -4..-6 %, 64 views level
   const int sx0 = tx * BX + (w & 1) * SUB, sy0 = ty * BY + (w >> 1) * SUB;
   const int px = sx0 + (lane & (SUB - 1));
   const int py = sy0 + (lane >> 3);
