@@ -727,10 +727,8 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
 // Gaussian come from HBM once and from that XCD's L2 for the other views (one workgroup per
 // scene looping over its views would hold 3x fewer waves in flight to hide the load and
 // atomic latencies).
-#ifndef DSR_PROJECT_WPE
-#define DSR_PROJECT_WPE 1
-#endif
-constexpr int kProjectWPE = DSR_PROJECT_WPE;
+// (70 VGPRs: 7 waves per SIMD; forcing 8 spills 860 B per lane and runs 6-8x slower)
+constexpr int kProjectWPE = 1;
 // pair cache of the count pass (kPairCapW (tile, rank, owner) words per wave in LDS)
 constexpr int kPairCapW = 768;
 // EXACT: a pair is kept only when tile_reach says the alpha >= 1/255 ellipse reaches the tile
