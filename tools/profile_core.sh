@@ -30,9 +30,11 @@ run stats_b4_eager 300 rocprofv3 --kernel-trace --stats --output-format csv -d $
   $B --steps 50 --warmup 5 --extra "" --batch 4 --launch eager
 run stats_b8_eager 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b8_eager -o run -- \
   $B --steps 50 --warmup 5 --extra "" --batch 8 --launch eager
+run stats_b16_eager 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b16_eager -o run -- \
+  $B --steps 50 --warmup 5 --extra "" --batch 16 --launch eager
 run stats_b1 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats_b1 -o run -- \
   $B --steps 50 --warmup 5 --extra "" --batch 1 --launch hipgraph
-for b in 1 2 4 8; do
+for b in 1 2 4 8 16; do
   for pass in FETCH_SIZE WRITE_SIZE \
     "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT"; do
     n=$(echo $pass | cut -d' ' -f1 | tr 'A-Z' 'a-z')
