@@ -63,30 +63,156 @@ def parse():
                         "recon12 (12-view 512x960 reconstruction, 100 views in chunks of 10), costvol (plane-sweep "
                         "cost volume, configs A / B shapes), train_d (config D data-parallel training step); '' = none")
     p.add_argument("--extra-steps", type=int, default=10)
+    p.add_argument("--selftest", action="store_true",
+                   help="launcher self-test on the CPU: gloo ranks, a stub step instead of the renderer (no GPU)")
     return p.parse_args()
 
 
-def main():
-    args = parse()
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N ranks, one process per
+    GPU, with torch.distributed.run as a CHILD process and return its exit code. This process
+    has touched no GPU (nothing above imports torch.cuda state), so there is no exec after a
+    GPU init; each child pins cuda:LOCAL_RANK and initialises RCCL itself."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def init_dist(args):
+    """One rank per GPU over RCCL ("nccl"), world from the launcher's env. Returns
+    (world, rank, device, backend, n_devices). DSPLAT_DIST_BACKEND=gloo with more ranks than
+    GPUs rehearses the multi-rank path on a one-GPU box (ranks share device local % count;
+    RCCL refuses two ranks on one device): n_devices then counts the distinct devices, not
+    the ranks. --selftest: gloo on the CPU."""
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one rank per GPU over RCCL ("nccl"). DSPLAT_DIST_BACKEND=gloo with more ranks than GPUs
-    # rehearses the multi-rank path on a one-GPU box (ranks share device local % count; RCCL
-    # refuses two ranks on one device)
-    backend = os.environ.get("DSPLAT_DIST_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
-    dev = torch.device("cuda", local % ndev if backend != "nccl" and ndev else local)
-    torch.cuda.set_device(dev)
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.selftest:
+        backend, dev, ndev_used = "gloo", torch.device("cpu"), 0
+    else:
+        backend = os.environ.get("DSPLAT_DIST_BACKEND", "nccl")
+        ndev = torch.cuda.device_count()
+        dev = torch.device("cuda", local % ndev if backend != "nccl" and ndev else local)
+        torch.cuda.set_device(dev)
+        ndev_used = world if backend == "nccl" else min(world, ndev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        seen = dist.get_world_size()
+        if seen != world:
+            raise SystemExit(f"process group has {seen} ranks, WORLD_SIZE says {world}")
+    return world, rank, dev, backend, ndev_used
+
+
+def dist_info(world, backend, ndev_used, selftest=False) -> dict:
+    """Launch facts for the headline line: ranks the process group saw, backend, distinct
+    devices; `rehearsal` when ranks share a device or the data moved through gloo."""
+    import torch.distributed as dist
+    seen = dist.get_world_size() if dist.is_initialized() else 1
+    info = {"world_size_seen": seen, "backend": (dist.get_backend() if dist.is_initialized() else None),
+            "devices_distinct": ndev_used}
+    if world > 1 and (backend != "nccl" or ndev_used < world):
+        info["rehearsal"] = True
+    if selftest:
+        info["selftest"] = True
+    return info
+
+
+def make_timing(world, dev, backend):
+    """timed(fn, n): exactly n calls between barrier + device sync on both sides (wall clock);
+    max_over_ranks(*vals): the max of each value over all ranks (one all-reduce)."""
+    import torch
+    import torch.distributed as dist
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+
+    def timed(fn, nsteps):
+        if world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(nsteps):
+            fn()
+        sync()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    def max_over_ranks(*vals):
+        if world == 1:
+            return vals
+        t = torch.tensor(vals, device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return tuple(float(x) for x in t.tolist())
+    return timed, max_over_ranks
+
+
+METRIC = "rendered views/sec + PSNR, 2-view 256x256 RE10K, 1/2/4/8 MI355X"
+
+
+def selftest_main(args):
+    """The launcher, timing and reporting path of the bench with a stub step (a small dense
+    torch op per 'view' on the CPU): tests/test_bench_launch.py runs `--gpus 2 --selftest`
+    and checks that 2 ranks ran and one JSON line came out."""
+    import torch
+    import torch.distributed as dist
+    world, rank, dev, backend, ndev_used = init_dist(args)
+    timed, max_over_ranks = make_timing(world, dev, backend)
+    x = torch.randn(64, 64, generator=torch.Generator().manual_seed(rank))
+    views = 3
+
+    def step():
+        return [x @ x for _ in range(views)]
+
+    for _ in range(args.warmup):
+        step()
+    (el,) = max_over_ranks(timed(step, args.steps))
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, rank)
+    else:
+        ranks = [0]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(views * args.steps * world / el, 2), "unit": "views/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(1e3 * el / args.steps, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                          "ranks_reporting": sorted(ranks), **dist_info(world, backend, ndev_used, True),
+                          "config": {"workload": "launcher self-test (stub step on the CPU)",
+                                     "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    if args.selftest:
+        return selftest_main(args)
+    import torch
+    import torch.distributed as dist
+
+    world, rank, dev, backend, ndev_used = init_dist(args)
 
     from my_depthsplat_amd import _lib, raster
     from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
@@ -112,24 +238,7 @@ def main():
               for B in batches}
     steps = {B: [step_of(sc_) for sc_ in scenes[B]] for B in batches}
 
-    def timed(fn, nsteps):
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(nsteps):
-            fn()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        return time.perf_counter() - t0
-
-    def max_over_ranks(*vals):
-        if world == 1:
-            return vals
-        t = torch.tensor(vals, device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return tuple(float(x) for x in t.tolist())
+    timed, max_over_ranks = make_timing(world, dev, backend)
 
     # launch mode: the whole decoder call of a B-scene batch replayed as ONE hipGraph per step,
     # or launched eagerly; "hipgraphN" (N = 2..4): N captures, one per lane (own scenes, own
@@ -294,8 +403,9 @@ def main():
         extra["train_config_d_dp"] = train_d_leg(args, dev, rank, world, timed, max_over_ranks)
     if rank == 0:
         line = {
-            "metric": "rendered views/sec + PSNR, 2-view 256x256 RE10K, 1/2/4/8 MI355X",
-            "value": round(value, 2), "unit": "views/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC,
+            "value": round(value, 2), "unit": "views/s", "n_gpus": ndev_used, "steps": args.steps,
+            **dist_info(world, backend, ndev_used),
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
             "launch_mode": mode, "launch_calibration_ms_per_step": cal,
             "ms_per_step_eager": round(1e3 * elapsed_eager / args.steps, 4),
@@ -310,7 +420,7 @@ def main():
                                    f"(G={sc.gaussians.means.shape[1]}), {args.views} target views/scene, fp32",
                        "global_batch": B * world, "scenes_per_step_per_gpu": B, "views_per_scene": args.views,
                        "gaussians": sc.gaussians.means.shape[1], "num_rendered_per_step": n_rendered,
-                       "parallelism": f"dp{world} (per-scene, no collective)",
+                       "parallelism": f"dp{world} (per-scene, no collective)", "ranks": world,
                        "scenes_in_flight_per_gpu": B * lanes_used, "distinct_scenes_per_gpu": B * lanes_used},
             "parity_vs_oracle": psnr,
             "roofline": roof, "cpu_baseline": cpu,
@@ -446,7 +556,7 @@ def recon12_leg(args, dev, rank, world, timed, max_over_ranks):
     network, which is out of scope here, so no ratio is reported. Per GPU; weak scaling."""
     import torch
 
-    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg, render_chunked
     from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg, gaussians_from_head
     from my_depthsplat_amd.synthetic import context_cameras, target_cameras
 
@@ -463,14 +573,11 @@ def recon12_leg(args, dev, rank, world, timed, max_over_ranks):
     near = torch.full((1, v), 0.5, device=dev)
     far = torch.full((1, v), 100.0, device=dev)
     dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
-    out = torch.empty(1, v, 3, H, W, device=dev)
 
     def step():
         with torch.no_grad():
             gs = gaussians_from_head(head, depths, images, ctx, ctx_k, adapter)
-            for c in range(0, v, chunk):
-                sl = slice(c, min(v, c + chunk))
-                out[:, sl] = dec(gs, tgt[:, sl], tgt_k[:, sl], near[:, sl], far[:, sl], (H, W)).color
+            return render_chunked(dec, gs, tgt, tgt_k, near, far, (H, W), chunk)  # model_wrapper.py:455-484
 
     step()
     steps = max(2, args.extra_steps // 2)
@@ -622,7 +729,7 @@ def train_d_leg(args, dev, rank, world, timed, max_over_ranks):
     head = GaussianHead(3 + adapter.d_in).to(dev)
     dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
     step = TrainStep(head, adapter, lambda gs, e, k, n, f, hw: dec(gs, e, k, n, f, hw).color,
-                     lambda p, t: l1_mse_loss(p, t, 1.0, 1.0), lr=1e-4, world=world)
+                     lambda p, t: l1_mse_loss(p, t, 1.0, 1.0), world=world)
     for _ in range(2):
         step(batch)
     n_steps = max(3, args.extra_steps // 2)
@@ -635,9 +742,12 @@ def train_d_leg(args, dev, rank, world, timed, max_over_ranks):
     for p in head.parameters():
         p.grad = None
     nparam = sum(p.numel() for p in head.parameters())
+    bk = dist.get_backend() if dist.is_initialized() else None
+    coll = {"nccl": "RCCL all-reduce", None: "all-reduce (world 1: no collective)"}.get(
+        bk, f"{bk} all-reduce through host copies (rehearsal)")
     return {"workload": f"config D shape: {V}-view {H}x{W} context (G={V * H * W}/scene), {per_rank} scenes x {v} "
-                        "target views per GPU, head -> fused adapter -> raster fwd+bwd -> L1+MSE -> one-bucket "
-                        "RCCL all-reduce -> clip -> AdamW (dense encoder out of scope)",
+                        f"target views per GPU, head -> fused adapter -> raster fwd+bwd -> L1+MSE -> one-bucket "
+                        f"{coll} -> clip -> AdamW + OneCycleLR (dense encoder out of scope)",
             "ms_per_step": round(ms, 3), "views_per_s": round(n_global * v / (ms * 1e-3), 1),
             "scenes_per_s": round(n_global / (ms * 1e-3), 2), "global_batch": n_global, "steps": n_steps,
             "n_gpus": world, "world_size_seen": dist.get_world_size() if dist.is_initialized() else 1,

@@ -172,14 +172,17 @@ class _RefAdapter(torch.autograd.Function):
 
 
 def _per_view(t: torch.Tensor, b: int, v: int, tail: tuple, name: str) -> torch.Tensor:
-    """[b, v, 1, ..., 1, *tail] (the reference's "b v i j -> b v () () () i j") -> [b*v, *tail]."""
-    if t.dim() < 2 + len(tail) or tuple(t.shape[-len(tail):]) != tail:
+    """[b, v, 1, ..., 1, *tail] (the reference's "b v i j -> b v () () () i j") -> [b*v, *tail].
+    Leading dims of 1 broadcast as in the reference (one camera for every batch entry or
+    view); a camera that varies per pixel is not representable by the fused kernel."""
+    if t.dim() < len(tail) or tuple(t.shape[-len(tail):]) != tail:
         raise ValueError(f"{name} must end in {tail}; got {tuple(t.shape)}")
-    lead = t.shape[:-len(tail)]
-    if lead[:2] != (b, v) or any(d != 1 for d in lead[2:]):
+    lead = tuple(t.shape[:-len(tail)])
+    lead = (1,) * max(0, 2 - len(lead)) + lead
+    if lead[0] not in (1, b) or lead[1] not in (1, v) or any(d != 1 for d in lead[2:]):
         raise ValueError(f"{name} {tuple(t.shape)}: the fused adapter takes one camera per (batch, view), "
-                         f"shaped [{b}, {v}, 1, ..., 1, {', '.join(map(str, tail))}]")
-    return t.reshape(b * v, *tail)
+                         f"broadcastable to [{b}, {v}, 1, ..., 1, {', '.join(map(str, tail))}]")
+    return t.reshape(lead[0], lead[1], *tail).expand(b, v, *tail).reshape(b * v, *tail)
 
 
 def adapter_forward_hip(adapter, extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians, image_shape,

@@ -100,6 +100,35 @@ class DecoderSplattingCUDA(Decoder[DecoderSplattingCUDACfg]):
         return out.reshape(b, v, *image_shape)
 
 
+def render_chunked(decoder: Decoder, gaussians: Gaussians, extrinsics: torch.Tensor, intrinsics: torch.Tensor,
+                   near: torch.Tensor, far: torch.Tensor, image_shape: tuple[int, int],
+                   chunk_size: int | None, depth_mode: DepthRenderingMode | None = None) -> DecoderOutput:
+    """The test loop's chunked render over target views (model_wrapper.py:455-484): views
+    [i*chunk_size, (i+1)*chunk_size) per decoder call, colours concatenated along the view
+    axis; the depth (if any) is the first chunk's, as in the reference ("ignore depth").
+    chunk_size None renders all views in one call (model_wrapper.py:486-494).
+
+    The colours land in one preallocated [b, v, 3, h, w] buffer (no growing torch.cat), and
+    every chunk is one batched decoder call, so a chunk of 10 views of a 5.9 M-Gaussian scene
+    is one launch sequence with its key buffers sized for 10 views, not 100."""
+    if chunk_size is None:
+        return decoder(gaussians, extrinsics, intrinsics, near, far, image_shape, depth_mode=depth_mode)
+    if chunk_size <= 0:
+        raise ValueError("render_chunk_size must be positive")
+    b, v = extrinsics.shape[:2]
+    h, w = image_shape
+    first, color = None, None
+    for start in range(0, v, chunk_size):
+        sl = slice(start, min(v, start + chunk_size))
+        out = decoder(gaussians, extrinsics[:, sl], intrinsics[:, sl], near[:, sl], far[:, sl], image_shape,
+                      depth_mode=depth_mode if first is None else None)
+        if first is None:
+            first = out
+            color = out.color.new_empty((b, v, 3, h, w))
+        color[:, sl] = out.color
+    return DecoderOutput(color, first.depth)
+
+
 DECODERS = {"splatting_cuda": DecoderSplattingCUDA}
 DecoderCfg = DecoderSplattingCUDACfg
 

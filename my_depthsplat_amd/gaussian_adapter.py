@@ -87,7 +87,12 @@ class GaussianAdapter(nn.Module):
 
     def forward(self, extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians, image_shape,
                 eps: float = 1e-8, point_cloud=None, input_images=None) -> AdapterGaussians:
-        if raw_gaussians.is_cuda:  # the fused HIP kernel (no torch fallback on the device)
+        # The fused HIP kernel differentiates w.r.t. raw_gaussians, coordinates and depths; the
+        # reference's autograd also reaches extrinsics, intrinsics and input_images. A caller
+        # that optimises those (pose refinement) gets the torch composition on the device, so
+        # its gradients are never silently dropped.
+        cam_grad = any(t is not None and t.requires_grad for t in (extrinsics, intrinsics, input_images))
+        if raw_gaussians.is_cuda and not (cam_grad and torch.is_grad_enabled()):
             from .adapter_hip import adapter_forward_hip
             return adapter_forward_hip(self, extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians,
                                        image_shape, eps, input_images)

@@ -129,8 +129,16 @@ def plane_sweep_cost_volume(ref: torch.Tensor, tgt: torch.Tensor, intrinsics: to
 def batch_features_camera_parameters(features, intrinsics, extrinsics, nn_matrix=None, no_batch=False):
     """Reference view + its source views for every view (mv_transformer.py:653-747).
     features/intrinsics/extrinsics: lists over views of [B,C,H,W] / [B,3,3] / [B,4,4].
-    Returns ref [BV,C,H,W], ref K, ref c2w, tgt [BV,V-1,C,H,W], tgt K, tgt c2w."""
+    Returns ref [BV,C,H,W], ref K, ref c2w, tgt [BV,V-1,C,H,W], tgt K, tgt c2w.
+
+    Token features [B,HW,C] per view (the reference's `features_tensor.dim() == 4` branch,
+    mv_transformer.py:706-708: the nn_matrix gather over "b v -> b v hw c") are accepted too.
+    The reference reaches that branch only with its entry assert disabled and then only
+    returns lists (no_batch; its batched return unpacks C, H, W); here the batched return
+    stacks them as ref [BV,HW,C] and tgt [BV,n,HW,C]."""
     V = len(features)
+    if features[0].dim() not in (3, 4) or intrinsics[0].dim() != 3 or extrinsics[0].dim() != 3:
+        raise ValueError("features must be [B,C,H,W] (or [B,HW,C] tokens), intrinsics [B,3,3], extrinsics [B,4,4]")
     if nn_matrix is not None:
         F_ = torch.stack(features, 1)
         K_ = torch.stack(intrinsics, 1)
@@ -145,8 +153,13 @@ def batch_features_camera_parameters(features, intrinsics, extrinsics, nn_matrix
         qe.append(extrinsics[i])
         if nn_matrix is not None:
             sel = nn_matrix[:, i, 1:]
-            c, h, w = F_.shape[-3:]
-            kv.append(torch.gather(F_, 1, repeat(sel, "b v -> b v c h w", c=c, h=h, w=w)))
+            if F_.dim() == 5:
+                c, h, w = F_.shape[-3:]
+                idx = repeat(sel, "b v -> b v c h w", c=c, h=h, w=w)
+            else:
+                hw, c = F_.shape[-2:]
+                idx = repeat(sel, "b v -> b v hw c", hw=hw, c=c)
+            kv.append(torch.gather(F_, 1, idx))
             kvk.append(torch.gather(K_, 1, repeat(sel, "b v -> b v i j", i=3, j=3)))
             kve.append(torch.gather(E_, 1, repeat(sel, "b v -> b v i j", i=4, j=4)))
         else:
@@ -156,9 +169,9 @@ def batch_features_camera_parameters(features, intrinsics, extrinsics, nn_matrix
             kve.append(torch.stack([extrinsics[j] for j in others], 1))
     if no_batch:
         return q, qk, qe, kv, kvk, kve
-    c, h, w = q[0].shape[1:]
-    return (torch.stack(q, 1).reshape(-1, c, h, w), torch.stack(qk, 1).reshape(-1, 3, 3),
-            torch.stack(qe, 1).reshape(-1, 4, 4), torch.stack(kv, 1).reshape(-1, n_sel, c, h, w),
+    fs = tuple(q[0].shape[1:])
+    return (torch.stack(q, 1).reshape(-1, *fs), torch.stack(qk, 1).reshape(-1, 3, 3),
+            torch.stack(qe, 1).reshape(-1, 4, 4), torch.stack(kv, 1).reshape(-1, n_sel, *fs),
             torch.stack(kvk, 1).reshape(-1, n_sel, 3, 3), torch.stack(kve, 1).reshape(-1, n_sel, 4, 4))
 
 

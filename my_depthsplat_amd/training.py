@@ -113,13 +113,21 @@ def torch_l1_mse(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
 
 class TrainStep:
     """One optimisation step on this rank's scenes. render(gaussians, extrinsics, intrinsics,
-    near, far, image_shape) -> colour [B, v, 3, H, W]; loss(pred, target) -> 0-d tensor."""
+    near, far, image_shape) -> colour [B, v, 3, H, W]; loss(pred, target) -> 0-d tensor.
 
-    def __init__(self, head: GaussianHead, adapter, render: Callable, loss: Callable, lr: float = 1e-4,
-                 clip: float = 0.5, world: int = 1):
+    Optimiser as the reference's (model_wrapper.py:1104-1158 without the monodepth group,
+    whose parameters are frozen in this fork): AdamW with lr 2e-4 and weight decay 0.01
+    (config/main.yaml:37-41), OneCycleLR over max_steps + 10 steps with pct_start 0.01, cosine
+    annealing and no momentum cycling, stepped once per optimisation step; gradient clipping
+    0.5 (config/main.yaml:92). max_steps defaults to 150,000 (scripts/re10k_depthsplat_train.sh:9)."""
+
+    def __init__(self, head: GaussianHead, adapter, render: Callable, loss: Callable, lr: float = 2e-4,
+                 clip: float = 0.5, world: int = 1, weight_decay: float = 0.01, max_steps: int = 150_000):
         self.head, self.adapter, self.render, self.loss = head, adapter, render, loss
         self.clip, self.world = clip, world
-        self.opt = torch.optim.AdamW(head.parameters(), lr=lr, weight_decay=0.05)
+        self.opt = torch.optim.AdamW(head.parameters(), lr=lr, weight_decay=weight_decay)
+        self.sched = torch.optim.lr_scheduler.OneCycleLR(self.opt, lr, max_steps + 10, pct_start=0.01,
+                                                         cycle_momentum=False, anneal_strategy="cos")
         self.bucket_bytes = 0
 
     def forward_backward(self, batch: TrainBatch) -> torch.Tensor:
@@ -138,6 +146,7 @@ class TrainStep:
         if self.clip:
             torch.nn.utils.clip_grad_norm_(self.head.parameters(), self.clip)
         self.opt.step()
+        self.sched.step()
         self.opt.zero_grad(set_to_none=True)
         return loss
 

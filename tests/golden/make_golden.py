@@ -296,6 +296,30 @@ def gen_matching():
     np.savez_compressed(OUT / "matching.npz", **{k: t2n(v) for k, v in out.items()})
 
 
+def gen_matching_tokens():
+    """The token-feature branch of batch_features_camera_parameters (mv_transformer.py:706-708:
+    features [B, HW, C] per view, nn_matrix gather over "b v -> b v hw c") ->
+    matching_tokens.npz. The reference's entry assert (features[0].dim() == 4, :665) rejects
+    such features, so this runs under `python -O` (asserts stripped), with no_batch=True (the
+    batched return unpacks C, H, W from a 4-D feature)."""
+    if not sys.flags.optimize:
+        raise SystemExit("matching_tokens: run as `python -O tests/golden/make_golden.py matching_tokens`")
+    mvt = importlib.import_module("src.model.encoder.unimatch.mv_transformer")
+    g = torch.Generator().manual_seed(4)
+    B, V, HW, C = 2, 4, 6, 5
+    feats = [torch.randn(B, HW, C, generator=g) for _ in range(V)]
+    intr = [torch.rand(B, 3, 3, generator=g) for _ in range(V)]
+    extr = [torch.randn(B, 4, 4, generator=g) for _ in range(V)]
+    nn = torch.stack([torch.stack([torch.tensor([i] + [(i + k) % V for k in (1, 2)]) for i in range(V)]),
+                      torch.stack([torch.tensor([i] + [(i + k) % V for k in (3, 1)]) for i in range(V)])])
+    q, qk, qe, kv, kvk, kve = mvt.batch_features_camera_parameters(feats, intr, extr, nn_matrix=nn, no_batch=True)
+    out = {"feats": torch.stack(feats, 1), "intr": torch.stack(intr, 1), "extr": torch.stack(extr, 1),
+           "nn_matrix": nn}
+    for k, lst in zip(("ref", "ref_k", "ref_e", "tgt", "tgt_k", "tgt_e"), (q, qk, qe, kv, kvk, kve)):
+        out[k] = torch.stack(lst, 1)  # [B, V, ...] (one entry per reference view)
+    np.savez_compressed(OUT / "matching_tokens.npz", **{k: t2n(v) for k, v in out.items()})
+
+
 if __name__ == "__main__":
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     setup_imports()
@@ -305,5 +329,7 @@ if __name__ == "__main__":
                      ("adapter", gen_adapter), ("matching", gen_matching)):
         if not only or name in only:
             fn()
+    if "matching_tokens" in only:  # separate: needs `python -O` (see gen_matching_tokens)
+        gen_matching_tokens()
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)

@@ -164,3 +164,32 @@ def test_reference_signature_matches_torch_fwd_bwd(gpu, sh_degree, srf):
         grads.append((r_.grad, c_.grad, d_.grad))
     for a, b, name in zip(grads[0], grads[1], ("raw", "coordinates", "depths")):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()), msg=name)
+
+
+def test_reference_signature_camera_grads_and_broadcast(gpu):
+    """Cameras that require grad (pose refinement) get gradients as in the reference: the
+    module routes them to the torch composition on the device instead of silently detaching
+    them. Cameras broadcast over the batch ([1, v, ...]) are expanded for the fused kernel."""
+    from my_depthsplat_amd.projection import sample_image_grid
+    head, depths, images, ext, K, adapter = _inputs(2, B=2, V=2, H=8, W=12, seed=77)
+    B, V, HW = head.shape[:3]
+    g = torch.Generator(device=gpu).manual_seed(3)
+    raw = torch.randn(B, V, HW, 1, 1, adapter.d_in, generator=g, device=gpu)
+    xy, _ = sample_image_grid((8, 12), gpu)
+    coords = xy.reshape(1, 1, HW, 1, 1, 2).expand(B, V, HW, 1, 1, 2)
+    dep = torch.rand(B, V, HW, 1, 1, generator=g, device=gpu) * 9 + 1
+    opac = torch.rand(B, V, HW, 1, 1, generator=g, device=gpu)
+    e = ext[:, :, None, None, None].clone().requires_grad_(True)
+    k = K[:, :, None, None, None]
+    out = adapter(e, k, coords, dep, opac, raw, (8, 12), input_images=images)
+    out.means.sum().backward()
+    assert e.grad is not None and float(e.grad.abs().max()) > 0
+    e2 = ext[:, :, None, None, None].detach().clone().requires_grad_(True)
+    adapter.forward_torch(e2, k, coords, dep, opac, raw, (8, 12), input_images=images).means.sum().backward()
+    torch.testing.assert_close(e.grad, e2.grad)
+    # one camera block per view shared by the batch: broadcast like the reference
+    e1 = ext[:1, :, None, None, None]
+    a = adapter(e1, k, coords, dep, opac, raw, (8, 12), input_images=images)
+    b = adapter.forward_torch(e1, k, coords, dep, opac, raw, (8, 12), input_images=images)
+    torch.testing.assert_close(a.means, b.means, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(a.harmonics, b.harmonics, rtol=2e-5, atol=2e-5)

@@ -76,3 +76,25 @@ def test_depth_candidates_scale0_match_cost_volume_fixture():
     cand = depth_candidates(inv_min, inv_max, D, 0)
     np.testing.assert_allclose((1.0 / cand).expand(BV, D, *CV["s0_depth"].shape[2:]).numpy(), CV["s0_depth"],
                                rtol=1e-6)
+
+
+def test_batch_features_token_branch_vs_reference():
+    """Token features [B, HW, C] per view with an nn_matrix: the reference's
+    `features_tensor.dim() == 4` gather (mv_transformer.py:706-708), recorded by running the
+    reference with its entry assert stripped (tests/golden/make_golden.py matching_tokens, no_batch).
+    The list outputs equal the reference's; the batched return stacks them per view."""
+    TK = np.load(GOLD / "matching_tokens.npz")
+    feats = list(torch.from_numpy(TK["feats"]).unbind(1))
+    intr = list(torch.from_numpy(TK["intr"]).unbind(1))
+    extr = list(torch.from_numpy(TK["extr"]).unbind(1))
+    nn = torch.from_numpy(TK["nn_matrix"])
+    lists = batch_features_camera_parameters(feats, intr, extr, nn_matrix=nn, no_batch=True)
+    for k, lst in zip(("ref", "ref_k", "ref_e", "tgt", "tgt_k", "tgt_e"), lists):
+        np.testing.assert_array_equal(torch.stack(lst, 1).numpy(), TK[k], err_msg=k)
+    B, V, HW, C = TK["feats"].shape
+    ref, ref_k, ref_e, tgt, tgt_k, tgt_e = batch_features_camera_parameters(feats, intr, extr, nn_matrix=nn)
+    n = nn.shape[-1] - 1
+    assert ref.shape == (B * V, HW, C) and tgt.shape == (B * V, n, HW, C)
+    np.testing.assert_array_equal(ref.numpy(), TK["ref"].reshape(B * V, HW, C))
+    np.testing.assert_array_equal(tgt.numpy(), TK["tgt"].reshape(B * V, n, HW, C))
+    np.testing.assert_array_equal(tgt_e.numpy(), TK["tgt_e"].reshape(B * V, n, 4, 4))
