@@ -260,15 +260,35 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
  * the buffer can serve the next dsr_project_bin_cameras call as already-zeroed counters. */
 
 /* ---- rasterizer backward -----------------------------------------------------------
- * Back-to-front per tile (K7). dL_dpix [V,3,H,W]. Accumulates into dgeom [V,G,12]
- * (caller zeroes): [0..1] dL/dxy (ndc scale, as upstream dL_dmean2D), [2..4] dL/dconic,
- * [5] dL/dopacity, [6..8] dL/drgb. */
+ * Deterministic: every per-Gaussian gradient is a sum over (tile, sub-tile wave) partials,
+ * accumulated as 64-bit FIXED-POINT integers (integer addition is associative, so the
+ * result does not depend on the order the partials arrive in: bit-identical run to run).
+ * The fixed-point unit follows the size of the incoming gradient so that a mean loss's tiny
+ * dL/dpix keeps full precision: with m = max |dL_dpix| rounded up to 2^k, one unit is
+ * 2^(k-32) (DSR_GRAD_FRAC_BITS), i.e. partials are stored as round(x * 2^(32-k)).
+ *
+ * dsr_grad_scale: per-block maxima of |dL_dpix [V,3,H,W]| into
+ * grad_scale [DSR_GRAD_SCALE_BLOCKS] floats (both kernels below derive m from them). */
+#define DSR_GRAD_SCALE_BLOCKS 512
+#define DSR_GRAD_FRAC_BITS 32
+#define DSR_DGEOM_WORDS 9    /* int64 words per (view, gaussian) gradient row          */
+int dsr_grad_scale(int V, int H, int W, const float* dL_dpix, float* grad_scale, void* stream);
+
+/* Back-to-front per tile (K7). dL_dpix [V,3,H,W]. Accumulates into dgeom_fx
+ * [V,G,DSR_DGEOM_WORDS] int64 fixed point (caller zeroes): [0..1] dL/dxy (ndc scale, as
+ * upstream dL_dmean2D), [2..4] dL/dconic, [5] dL/dopacity, [6..8] dL/drgb. */
 int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride,
                    const uint64_t* keys, const float* final_T, const uint32_t* n_contrib,
-                   const float* dL_dpix, float* dgeom, void* stream);
+                   const float* dL_dpix, const float* grad_scale, int64_t* dgeom_fx, void* stream);
+
+/* dgeom_fx -> float dgeom [V,G,DSR_GEOM_STRIDE] (words 9..11 zero): the values the
+ * preprocess backward consumes, for callers that want them (tests, diagnostics). */
+int dsr_dgeom_to_float(int G, int V, const int64_t* dgeom_fx, const float* grad_scale, float* dgeom,
+                       void* stream);
 
 /* Preprocess backward (K8 + K9), reduced over all views of each scene without atomics.
+ * dgeom_fx / grad_scale: as written by dsr_render_bwd / dsr_grad_scale.
  * scene_view_start [S+1], scene_views [V] list the views of each scene.
  * out (overwritten): dmeans [S,G,3], dshs [S,G,M,3] or NULL, dcolors [S,G,3] or NULL,
  * dopac [S,G], dcov6 [S,G,6]; dmean2D [V,G,3] optional (NULL to skip). `layout` as in
@@ -276,8 +296,8 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
  * zeros below, as the reference's triu-gather backward produces). */
 int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* cov6,
-                       const dsr_camera* cams, const float* geom, const float* dgeom,
-                       const int32_t* scene_view_start, const int32_t* scene_views,
+                       const dsr_camera* cams, const float* geom, const int64_t* dgeom_fx,
+                       const float* grad_scale, const int32_t* scene_view_start, const int32_t* scene_views,
                        float* dmeans, float* dshs, float* dcolors, float* dopac, float* dcov6,
                        float* dmean2D, int layout, void* stream);
 
@@ -392,11 +412,11 @@ int dls_l1_mse_psnr(int n_images, int64_t n_per_image, const float* pred, const 
  * W x H pixels and G gaussians per scene (T = ceil(W/16) * ceil(H/16) tiles per view), so a
  * host that is not the Python layer can allocate them (the library never allocates).
  * key_budget: largest key buffer the caller accepts for the sync-free fixed-capacity layout
- * (the Python layer uses 8 GiB). fixed_capacity = 1: dsr_project_bin(_cameras) applies and
+ * (the Python layer: min(48 GiB, 40 % of the device, free memory minus a reserve)). fixed_capacity = 1: dsr_project_bin(_cameras) applies and
  * keys / scratch are sized V*T*G; 0: the two-phase layout (dsr_preprocess_fwd / _cut, scan,
  * scatter), whose keys / scratch hold N = totals[0] of dsr_bin_scan entries (known only
  * after the scan: keys_bytes is then 0 here). Forward outputs: color [V,3,H,W], final_T
- * [V,H,W], n_contrib [V,H,W]; backward: dgeom [V,G,12]. */
+ * [V,H,W], n_contrib [V,H,W]; backward: dgeom_fx [V,G,DSR_DGEOM_WORDS] int64. */
 typedef struct dsr_workspace {
     uint64_t cams_bytes;        /* dsr_camera [V]                                   */
     uint64_t geom_bytes;        /* [V,G,12] f32                                     */

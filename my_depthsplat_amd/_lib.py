@@ -38,8 +38,10 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_sort_render": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _I, _I, c_uint32, _P, _P, _P, _P]),
     "dsr_project_bin_cameras": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P,
                                      _P, _P, _P, _P, _I, _P]),
-    "dsr_render_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P, _P, _P]),
-    "dsr_preprocess_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
+    "dsr_grad_scale": (_I, [_I, _I, _I, _P, _P, _P]),
+    "dsr_render_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P, _P, _P, _P]),
+    "dsr_dgeom_to_float": (_I, [_I, _I, _P, _P, _P, _P]),
+    "dsr_preprocess_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                 _P, _P, _P, _P, _P, _P, _I, _P]),
     "dcv_cost_volume_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P, _P]),
     "dcv_cost_volume_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P,

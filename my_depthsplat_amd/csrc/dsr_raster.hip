@@ -9,9 +9,10 @@
 //   * binning is a per-(view, tile) bucket pass (LDS histogram + one global atomic per
 //     bucket per workgroup) followed by a per-tile LSD radix sort of (depth, id) keys in
 //     LDS (wave64 ballot ranking) — no device-wide sort passes over HBM;
-//   * the backward reduces each Gaussian's per-pixel gradients across the wave and the
-//     16x16 tile in registers/LDS first and issues one global atomic per (tile, Gaussian,
-//     component) instead of one per pixel.
+//   * the backward reduces each Gaussian's per-pixel gradients across the wave in
+//     registers first and issues one 64-bit fixed-point atomic per (sub-tile wave, Gaussian,
+//     component) instead of one float atomic per pixel: integer sums are order-independent,
+//     so the gradients are bit-identical run to run.
 // All floating-point expressions feeding the bit-exact outputs (depth, radius, xy, tile
 // rect, sort keys) keep the evaluation order of oracle/dsr_oracle.cpp (-ffp-contract=off).
 
@@ -2598,6 +2599,57 @@ __device__ __forceinline__ void reduce36(const float (&g)[4][9], float (&R)[9]) 
   asm volatile("s_nop 1" ::: "memory");
 }
 
+// ------------------------------------------------------------------------------------
+// Deterministic gradient sums (include/dsplat_hip.h, DSR_GRAD_FRAC_BITS): partials are
+// accumulated as int64 fixed point with a unit derived from m = max |dL_dpix|.
+constexpr int kGradBlocks = DSR_GRAD_SCALE_BLOCKS;
+static_assert(kGradBlocks % 64 == 0, "grad-scale blocks: whole waves");
+
+// per-block maxima of |d| (non-finite values: +inf, so the unit derivation sees them)
+__global__ __launch_bounds__(256) void k_grad_scale(size_t n, const float* __restrict__ d, float* __restrict__ out) {
+  float m = 0.f;
+  bool bad = false;
+  const size_t n4 = n / 4, stride = (size_t)256 * gridDim.x;
+  const float4* d4 = reinterpret_cast<const float4*>(d);
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+    const float4 x = d4[i];
+    const float a = fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
+    bad = bad || !(fabsf(x.x) + fabsf(x.y) + fabsf(x.z) + fabsf(x.w) <= 3.0e38f);
+    m = fmaxf(m, a);
+  }
+  for (size_t i = 4 * n4 + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const float a = fabsf(d[i]);
+    bad = bad || !(a <= 3.0e38f);
+    m = fmaxf(m, a);
+  }
+  if (bad) m = __builtin_inff();
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+}
+
+// k with m <= 2^k from the per-block maxima (one wave; every wave of every kernel reading
+// the same maxima gets the same k). Returns false when m is not finite.
+__device__ __forceinline__ bool grad_fx_exp(const float* __restrict__ bm, int lane, int& k) {
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < kGradBlocks / 64; ++i) m = fmaxf(m, bm[i * 64 + lane]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if (!(m <= 3.0e38f)) return false;
+  int e = 0;
+  frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1); m == 0 -> e = 0
+  k = max(e, -60);  // keeps 2^(32 - k) a normal float
+  return true;
+}
+// partial -> fixed point (saturating far inside the int64 range)
+__device__ __forceinline__ long long to_fx(float a, float unit_inv) {
+  return (long long)rintf(fminf(fmaxf(a * unit_inv, -4.0e18f), 4.0e18f));
+}
+
 // one compacted backward list entry
 struct __align__(16) BwdRec {
   float4 q;   // x, y, A, C (scaled conic, as in the forward)
@@ -2613,7 +2665,7 @@ struct __align__(16) BwdRec {
 // time: entries that can reach its sub-tile (same exact test as the forward) go to a
 // wave-private LDS list; per entry the 64 pixel gradients (9 values) are summed with DPP and
 // lane 63 parks the sums in LDS; at the end of the chunk the wave adds them to dgeom with
-// one global atomic per non-zero (entry, component).
+// one 64-bit fixed-point atomic per non-zero (entry, component): order-independent sums.
 constexpr int BCH = 64;
 // WPE = 5 (96 VGPRs, small spills) pays only on wide grids (kbench at 64 views: -3 %; 16:
 // level; 3: +12 %), so dsr_render_bwd picks it from the number of tiles.
@@ -2627,7 +2679,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                                                    const float* __restrict__ finalT,
                                                    const uint32_t* __restrict__ ncontrib,
                                                    const float* __restrict__ dpix,
-                                                   float* __restrict__ dgeom) {
+                                                   const float* __restrict__ gscale,
+                                                   long long* __restrict__ dgeom) {
   __shared__ BwdRec l_rec[4][BCH + 1];
   __shared__ float l_acc[4][BCH * 9];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -2646,7 +2699,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const float fx0 = (float)sx0, fy0 = (float)sy0;
   const PixUV puv = pix_uv(px, py, fx0, fy0);
   const float* gv = geom + (size_t)v * G * GS;
-  float* dgv = dgeom + (size_t)v * G * GS;
+  long long* dgv = dgeom + (size_t)v * G * DSR_DGEOM_WORDS;
+  int fx_k = 0;
+  const bool fx_ok = grad_fx_exp(gscale, lane, fx_k);
+  const float fx_unit_inv = fx_ok ? ldexpf(1.f, DSR_GRAD_FRAC_BITS - fx_k) : 0.f;  // exact power of 2
   const float* bg = cams[v].bg;
   const uint64_t lt = dsplat::lanemask_lt(lane);
   BwdRec* list = l_rec[w];
@@ -2781,7 +2837,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const float a = acc[i];
       const int k = i / 9;
       if (a != 0.f)
-        atomicAdd(&dgv[(size_t)list[k].id * GS + (i - k * 9)], a);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&dgv[(size_t)list[k].id * DSR_DGEOM_WORDS + (i - k * 9)]),
+                  (unsigned long long)to_fx(a, fx_unit_inv));
     }
     __builtin_amdgcn_wave_barrier();
   };
@@ -2817,11 +2874,14 @@ template <int DEG>
 __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     int G, int H, int W, int M, const float* __restrict__ means, const float* __restrict__ shs,
     const float* __restrict__ cov6, const dsr_camera* __restrict__ cams,
-    const float* __restrict__ geom, const float* __restrict__ dgeom,
+    const float* __restrict__ geom, const long long* __restrict__ dgeom, const float* __restrict__ gscale,
     const int32_t* __restrict__ scene_view_start, const int32_t* __restrict__ scene_views,
     float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
     float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D, int layout) {
   constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
+  int fx_k = 0;  // fixed-point unit of dgeom (k_render_bwd); non-finite dL_dpix -> NaN gradients
+  const float fx_unit = grad_fx_exp(gscale, threadIdx.x & 63, fx_k) ? ldexpf(1.f, fx_k - DSR_GRAD_FRAC_BITS)
+                                                                     : __builtin_nanf("");
   extern __shared__ __attribute__((aligned(16))) float lds[];  // NT * max(3 M, 9) floats: row staging
   const int s = blockIdx.y;
   const int tid = threadIdx.x;
@@ -2888,9 +2948,10 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
       }
       continue;
     }
-    const float4* dg4 = reinterpret_cast<const float4*>(dgeom + vg * GS);
-    const float4 dgA = dg4[0], dgB = dg4[1], dgC = dg4[2];
-    const float dg[9] = {dgA.x, dgA.y, dgA.z, dgA.w, dgB.x, dgB.y, dgB.z, dgB.w, dgC.x};
+    const long long* dq = dgeom + vg * DSR_DGEOM_WORDS;
+    float dg[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) dg[c] = (float)dq[c] * fx_unit;
     const dsr_camera* cam = cams + v;
     // scale-invariant rescale of this view: forward used m*s and cov*s^2
     const float gsc = cam->scale, gsc2 = gsc * gsc;
@@ -3086,6 +3147,17 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     __syncthreads();
     dsplat::stage_out<NT>(dshs + (size_t)rw * sg0, (size_t)rw * nrows, lds);
   }
+}
+
+// dgeom_fx -> float [rows, GS] (diagnostics / tests): the values k_preprocess_bwd consumes
+__global__ __launch_bounds__(NT) void k_dgeom_to_float(size_t rows, const long long* __restrict__ dq,
+                                                       const float* __restrict__ gscale, float* __restrict__ out) {
+  int k = 0;
+  const float unit = grad_fx_exp(gscale, threadIdx.x & 63, k) ? ldexpf(1.f, k - DSR_GRAD_FRAC_BITS) : __builtin_nanf("");
+  const size_t r = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (r >= rows) return;
+#pragma unroll
+  for (int c = 0; c < GS; ++c) out[r * GS + c] = c < 9 ? (float)dq[r * DSR_DGEOM_WORDS + c] * unit : 0.f;
 }
 
 // pointers a segment layout needs (seg_bounds): ENDS both, fixed capacity the counts, prefix the starts
@@ -3345,7 +3417,7 @@ int dsr_workspace_size(int G, int H, int W, int n_views, uint64_t key_budget, ds
   ws.color_bytes = V * 3 * HW * 4;
   ws.final_T_bytes = V * HW * 4;
   ws.n_contrib_bytes = V * HW * 4;
-  ws.dgeom_bytes = ws.geom_bytes;
+  ws.dgeom_bytes = (uint64_t)V * G * DSR_DGEOM_WORDS * 8;  // int64 fixed point
   ws.total_bytes = ws.cams_bytes + ws.geom_bytes + ws.radii_bytes + ws.seg_count_bytes + ws.seg_start_bytes +
                    ws.keys_bytes + ws.scratch_bytes + ws.sort_ws_bytes + ws.color_bytes + ws.final_T_bytes +
                    ws.n_contrib_bytes + ws.dgeom_bytes;
@@ -3554,26 +3626,45 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
   return dsplat::check_launch("k_sort_render");
 }
 
+int dsr_grad_scale(int V, int H, int W, const float* dL_dpix, float* grad_scale, void* stream) {
+  DSPLAT_REQUIRE(V > 0 && H > 0 && W > 0, "dsr_grad_scale: bad sizes");
+  DSPLAT_REQUIRE(dL_dpix && grad_scale, "dsr_grad_scale: null pointer");
+  DSPLAT_REQUIRE(((uintptr_t)dL_dpix & 15) == 0, "dsr_grad_scale: dL_dpix must be 16-byte aligned");
+  k_grad_scale<<<kGradBlocks, 256, 0, (hipStream_t)stream>>>((size_t)V * 3 * H * W, dL_dpix, grad_scale);
+  return dsplat::check_launch("k_grad_scale");
+}
+
 int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride, const uint64_t* keys,
-                   const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, float* dgeom,
-                   void* stream) {
+                   const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, const float* grad_scale,
+                   int64_t* dgeom_fx, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_render_bwd: bad sizes");
   DSPLAT_REQUIRE(cams && geom && seg_ptrs_ok(seg_start, seg_count, seg_stride) && final_T && n_contrib &&
-                     dL_dpix && dgeom,
+                     dL_dpix && grad_scale && dgeom_fx,
                  "dsr_render_bwd: null pointer");
+  long long* dgeom = reinterpret_cast<long long*>(dgeom_fx);
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
   constexpr int64_t kWideBwd = 8192;  // (view, tile) segments from which WPE = 5 pays
   auto kern = (int64_t)V * gx * gy >= kWideBwd ? k_render_bwd<5> : k_render_bwd<1>;
   kern<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count, seg_stride, keys,
-                                             final_T, n_contrib, dL_dpix, dgeom);
+                                             final_T, n_contrib, dL_dpix, grad_scale, dgeom);
   return dsplat::check_launch("k_render_bwd");
+}
+
+int dsr_dgeom_to_float(int G, int V, const int64_t* dgeom_fx, const float* grad_scale, float* dgeom, void* stream) {
+  DSPLAT_REQUIRE(G > 0 && V > 0, "dsr_dgeom_to_float: bad sizes");
+  DSPLAT_REQUIRE(dgeom_fx && grad_scale && dgeom, "dsr_dgeom_to_float: null pointer");
+  const size_t rows = (size_t)G * V;
+  k_dgeom_to_float<<<(unsigned)((rows + NT - 1) / NT), NT, 0, (hipStream_t)stream>>>(
+      rows, reinterpret_cast<const long long*>(dgeom_fx), grad_scale, dgeom);
+  return dsplat::check_launch("k_dgeom_to_float");
 }
 
 int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                        const float* shs, const float* cov6, const dsr_camera* cams, const float* geom,
-                       const float* dgeom, const int32_t* scene_view_start, const int32_t* scene_views,
+                       const int64_t* dgeom_fx, const float* grad_scale, const int32_t* scene_view_start,
+                       const int32_t* scene_views,
                        float* dmeans, float* dshs, float* dcolors, float* dopac, float* dcov6, float* dmean2D,
                        int layout, void* stream) {
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_preprocess_bwd: bad sizes");
@@ -3581,15 +3672,18 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   DSPLAT_REQUIRE(shs != nullptr || dcolors != nullptr, "dsr_preprocess_bwd: colors path needs dcolors");
   DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
                  "dsr_preprocess_bwd: sh_degree=%d M=%d unsupported", sh_degree, M);
-  DSPLAT_REQUIRE(means && cov6 && cams && geom && dgeom && scene_view_start && scene_views && dmeans && dopac && dcov6,
+  DSPLAT_REQUIRE(means && cov6 && cams && geom && dgeom_fx && grad_scale && scene_view_start && scene_views && dmeans &&
+                     dopac && dcov6,
                  "dsr_preprocess_bwd: null pointer");
+  const long long* dgeom = reinterpret_cast<const long long*>(dgeom_fx);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((G + NT - 1) / NT, S);
   const int deg = shs ? sh_degree : -1;
   const size_t lds = (size_t)NT * (size_t)max(shs ? 3 * M : 0, 9) * sizeof(float);
   DSPLAT_REQUIRE(lds <= 64 * 1024, "dsr_preprocess_bwd: M=%d SH coefficients exceed the LDS row staging", M);
 #define DSR_PREB(D)                                                                                              \
-  k_preprocess_bwd<D><<<grid, NT, lds, st>>>(G, H, W, M, means, shs, cov6, cams, geom, dgeom, scene_view_start, \
+  k_preprocess_bwd<D><<<grid, NT, lds, st>>>(G, H, W, M, means, shs, cov6, cams, geom, dgeom, grad_scale,          \
+                                           scene_view_start,                                                     \
                                            scene_views, dmeans, dshs, dcolors, dopac, dcov6, dmean2D, layout)
   switch (deg) {
     case -1: DSR_PREB(-1); break;

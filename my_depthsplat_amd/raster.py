@@ -153,6 +153,8 @@ class RasterState:
     # inference fast path with exact binning: the lists hold only entries whose alpha >= 1/255
     # ellipse reaches the tile, and n_contrib counts positions in those shorter lists
     pruned_lists: bool = False
+    # (zeroed int64 gradient accumulator, event) prepared during the forward for the backward
+    dgeom: tuple | None = None
 
     @property
     def counts(self) -> torch.Tensor:
@@ -623,8 +625,39 @@ def _sort_workspace(lib, V, H, W, max_count, dev):
     return torch.empty(n, dtype=torch.uint8, device=dev) if n else None
 
 
+DGEOM_WORDS = 9           # DSR_DGEOM_WORDS: int64 fixed-point gradient words per (view, Gaussian)
+GRAD_SCALE_BLOCKS = 512   # DSR_GRAD_SCALE_BLOCKS
+
+
+def zeroed_dgeom(V: int, G: int, dev) -> tuple[torch.Tensor, object]:
+    """The backward's fixed-point accumulator [V, G, DGEOM_WORDS] int64, zero-filled on a
+    side stream so that the fill (HBM-bound: 604 MB at config C's 64 views) runs under the
+    forward's VALU-bound kernels instead of in front of the backward. Returns (buffer,
+    event the consumer waits on). Inside a graph capture: filled on the current stream."""
+    if torch.cuda.is_current_stream_capturing():
+        return torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev), None
+    cur = torch.cuda.current_stream(dev)
+    side = _side_streams.get(str(dev))
+    if side is None:
+        side = _side_streams[str(dev)] = torch.cuda.Stream(device=dev)
+    side.wait_stream(cur)  # the memory block may have been freed by work still queued on cur
+    with torch.cuda.stream(side):
+        buf = torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    buf.record_stream(cur)  # consumed (and freed) in the current stream's order
+    return buf, ev
+
+
+_side_streams: dict = {}
+
+
 def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, state: RasterState,
-                 dcolor, want_mean2d: bool, layout=0):
+                 dcolor, want_mean2d: bool, layout=0, want_dgeom: bool = False):
+    """Rasterizer backward (K7 -> K8 + K9). Deterministic: the per-Gaussian sums are 64-bit
+    fixed-point atomics (dsr_grad_scale + dsr_render_bwd), bit-identical run to run.
+    Returns dmeans, dfeat, dopac, dcov6, dmean2d (or None), dgeom [V,G,12] float (only with
+    want_dgeom; the values K8 + K9 consumed, else None)."""
     lib = _lib.load()
     S, G = means.shape[0], means.shape[1]
     V, _, H, W = dcolor.shape
@@ -632,11 +665,24 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     dev = means.device
     st = _lib.stream_of(dev)
     dcolor = dcolor.contiguous().float()
-    dgeom = torch.zeros((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
+    if state.dgeom is not None:  # zero-filled during the forward (zeroed_dgeom)
+        dgeom_fx, ev = state.dgeom
+        state.dgeom = None
+        if ev is not None:
+            torch.cuda.current_stream(dev).wait_event(ev)
+    else:
+        dgeom_fx = torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev)
+    gscale = torch.empty(GRAD_SCALE_BLOCKS, dtype=torch.float32, device=dev)
+    _lib.check(lib.dsr_grad_scale(V, H, W, dcolor.data_ptr(), gscale.data_ptr(), st), "dsr_grad_scale")
     _lib.check(lib.dsr_render_bwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), _ptr(state.seg_start),
                                   state.seg_count.data_ptr(), state.seg_stride, state.keys.data_ptr(),
                                   state.final_T.data_ptr(), state.n_contrib.data_ptr(), dcolor.data_ptr(),
-                                  dgeom.data_ptr(), st), "dsr_render_bwd")
+                                  gscale.data_ptr(), dgeom_fx.data_ptr(), st), "dsr_render_bwd")
+    dgeom = None
+    if want_dgeom:
+        dgeom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
+        _lib.check(lib.dsr_dgeom_to_float(G, V, dgeom_fx.data_ptr(), gscale.data_ptr(), dgeom.data_ptr(), st),
+                   "dsr_dgeom_to_float")
     # views of each scene, in view order (fixed summation order -> deterministic reduce)
     order = sorted(range(V), key=lambda v: (view_scene[v], v))
     starts = [0] * (S + 1)
@@ -652,7 +698,8 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     dmean2d = torch.empty((V, G, 3), dtype=torch.float32, device=dev) if want_mean2d else None
     _lib.check(lib.dsr_preprocess_bwd(
         S, G, V, H, W, sh_degree if use_sh else -1, M, means.data_ptr(), feats.data_ptr() if use_sh else None,
-        cov6.data_ptr(), cams.data_ptr(), state.geom.data_ptr(), dgeom.data_ptr(), idx.data_ptr(),
+        cov6.data_ptr(), cams.data_ptr(), state.geom.data_ptr(), dgeom_fx.data_ptr(), gscale.data_ptr(),
+        idx.data_ptr(),
         idx[S + 1:].data_ptr(), dmeans.data_ptr(), dfeat.data_ptr() if use_sh else None,
         None if use_sh else dfeat.data_ptr(), dopac.data_ptr(), dcov6.data_ptr(),
         None if dmean2d is None else dmean2d.data_ptr(), layout, st), "dsr_preprocess_bwd")
@@ -664,8 +711,11 @@ class _RasterizeViews(torch.autograd.Function):
     def forward(ctx, means, feats, opacities, cov6, means2d, cams, view_scene, use_sh, sh_degree, H, W, layout,
                 zeroed_counts):
         V = len(view_scene)
+        need = any(ctx.needs_input_grad[:5])
+        dgeom = zeroed_dgeom(V, means.shape[1], means.device) if need else None  # fill overlaps the forward
         color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout,
-                                   zeroed_counts, need_state=any(ctx.needs_input_grad[:5]))
+                                   zeroed_counts, need_state=need)
+        state.dgeom = dgeom
         ctx.save_for_backward(means, feats, opacities, cov6, state.cams)
         ctx.state = state
         ctx.meta = (view_scene, use_sh, sh_degree, None if means2d is None else means2d.shape, layout)

@@ -51,12 +51,15 @@ constexpr float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457
                             0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
                             -0.5900435899266435f};
 
-struct V3 { float x, y, z; };
+template <typename R>
+struct V3T { R x, y, z; };
+using V3 = V3T<float>;
 
 // Column-major 4x4 (the layout of GaussianRasterizationSettings.viewmatrix/projmatrix,
 // i.e. the row-major storage of the transposed torch matrices, cuda_splatting.py:83-86).
-inline V3 xform43(const float* m, V3 p) {
-  V3 r;
+template <typename R>
+inline V3T<R> xform43(const float* m, V3T<R> p) {
+  V3T<R> r;
   r.x = m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12];
   r.y = m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13];
   r.z = m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14];
@@ -66,36 +69,40 @@ inline float xform44w(const float* m, V3 p) { return m[3] * p.x + m[7] * p.y + m
 
 inline float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5); }
 
-struct Cov2DWork {
+template <typename R>
+struct Cov2DWorkT {
   // T = J*W (2 x 3, the only non-zero rows), cov2D (a, b, c) after the +0.3 filter
-  float T[2][3];
-  float a, b, c;
-  float tx, ty, tz;
-  float xmul, ymul;
+  R T[2][3];
+  R a, b, c;
+  R tx, ty, tz;
+  R xmul, ymul;
 };
+using Cov2DWork = Cov2DWorkT<float>;
 
 // EWA splatting: cov2D = J W Sigma W^T J^T.
-inline void cov2d(V3 mean, float fx, float fy, float tanx, float tany, const float* c6,
-                  const float* view, Cov2DWork& w) {
-  V3 t = xform43(view, mean);
-  const float limx = 1.3f * tanx;
-  const float limy = 1.3f * tany;
-  const float txtz = t.x / t.z;
-  const float tytz = t.y / t.z;
-  w.xmul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
-  w.ymul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+// R = float: the forward's (and the float backward's) arithmetic; R = double: the
+// high-precision gradient reference (orc_backward_f64) of the same function.
+template <typename R>
+inline void cov2d(V3T<R> mean, R fx, R fy, R tanx, R tany, const float* c6, const float* view, Cov2DWorkT<R>& w) {
+  V3T<R> t = xform43(view, mean);
+  const R limx = R(1.3f) * tanx;
+  const R limy = R(1.3f) * tany;
+  const R txtz = t.x / t.z;
+  const R tytz = t.y / t.z;
+  w.xmul = (txtz < -limx || txtz > limx) ? R(0) : R(1);
+  w.ymul = (tytz < -limy || tytz > limy) ? R(0) : R(1);
   t.x = std::min(limx, std::max(-limx, txtz)) * t.z;
   t.y = std::min(limy, std::max(-limy, tytz)) * t.z;
   w.tx = t.x; w.ty = t.y; w.tz = t.z;
   // Jacobian rows: J0 = (fx/z, 0, -fx x/z^2), J1 = (0, fy/z, -fy y/z^2)
-  const float j00 = fx / t.z;
-  const float j02 = -(fx * t.x) / (t.z * t.z);
-  const float j11 = fy / t.z;
-  const float j12 = -(fy * t.y) / (t.z * t.z);
+  const R j00 = fx / t.z;
+  const R j02 = -(fx * t.x) / (t.z * t.z);
+  const R j11 = fy / t.z;
+  const R j12 = -(fy * t.y) / (t.z * t.z);
   // W = rotation part of world->camera: Wr[r][c] = view[c*4 + r]
-  const float W00 = view[0], W01 = view[4], W02 = view[8];
-  const float W10 = view[1], W11 = view[5], W12 = view[9];
-  const float W20 = view[2], W21 = view[6], W22 = view[10];
+  const R W00 = view[0], W01 = view[4], W02 = view[8];
+  const R W10 = view[1], W11 = view[5], W12 = view[9];
+  const R W20 = view[2], W21 = view[6], W22 = view[10];
   // T = J * Wr  (2x3)
   w.T[0][0] = j00 * W00 + j02 * W20;
   w.T[0][1] = j00 * W01 + j02 * W21;
@@ -104,17 +111,17 @@ inline void cov2d(V3 mean, float fx, float fy, float tanx, float tany, const flo
   w.T[1][1] = j11 * W11 + j12 * W21;
   w.T[1][2] = j11 * W12 + j12 * W22;
   // V = Sigma (symmetric from cov6 = xx, xy, xz, yy, yz, zz)
-  const float V[3][3] = {{c6[0], c6[1], c6[2]}, {c6[1], c6[3], c6[4]}, {c6[2], c6[4], c6[5]}};
+  const R V[3][3] = {{c6[0], c6[1], c6[2]}, {c6[1], c6[3], c6[4]}, {c6[2], c6[4], c6[5]}};
   // U = T * V (2x3), cov = U * T^T
-  float U[2][3];
+  R U[2][3];
   for (int r = 0; r < 2; ++r)
     for (int c = 0; c < 3; ++c) U[r][c] = w.T[r][0] * V[0][c] + w.T[r][1] * V[1][c] + w.T[r][2] * V[2][c];
-  const float a = U[0][0] * w.T[0][0] + U[0][1] * w.T[0][1] + U[0][2] * w.T[0][2];
-  const float b = U[0][0] * w.T[1][0] + U[0][1] * w.T[1][1] + U[0][2] * w.T[1][2];
-  const float c = U[1][0] * w.T[1][0] + U[1][1] * w.T[1][1] + U[1][2] * w.T[1][2];
-  w.a = a + 0.3f;
+  const R a = U[0][0] * w.T[0][0] + U[0][1] * w.T[0][1] + U[0][2] * w.T[0][2];
+  const R b = U[0][0] * w.T[1][0] + U[0][1] * w.T[1][1] + U[0][2] * w.T[1][2];
+  const R c = U[1][0] * w.T[1][0] + U[1][1] * w.T[1][1] + U[1][2] * w.T[1][2];
+  w.a = a + R(0.3f);
   w.b = b;
-  w.c = c + 0.3f;
+  w.c = c + R(0.3f);
 }
 
 inline V3 sh_to_rgb(int deg, const float* sh /*[M][3]*/, V3 pos, const float* campos, uint8_t* clamped) {
@@ -291,6 +298,230 @@ void render(State& s) {
   }
 }
 
+template <typename R>
+void backward_t(State& s, const float* dL_dpix, float* dmean2D, float* dconic, float* dopac, float* dcolor,
+                float* dmean3D, float* dcov6, float* dsh) {
+  const int P = s.P, HW = s.H * s.W, T = s.gx * s.gy;
+  std::memset(dmean2D, 0, 3 * (size_t)P * 4); std::memset(dconic, 0, 3 * (size_t)P * 4);
+  std::memset(dopac, 0, (size_t)P * 4); std::memset(dcolor, 0, 3 * (size_t)P * 4);
+  std::memset(dmean3D, 0, 3 * (size_t)P * 4); std::memset(dcov6, 0, 6 * (size_t)P * 4);
+  if (dsh) std::memset(dsh, 0, (size_t)P * s.M * 3 * 4);
+  const R ddelx_dx = 0.5f * s.W, ddely_dy = 0.5f * s.H;
+  std::vector<double> acc_m2(2 * (size_t)P, 0), acc_con(3 * (size_t)P, 0), acc_op(P, 0), acc_col(3 * (size_t)P, 0);
+  // --- render backward (serial; double accumulators make the checker order-insensitive) ---
+  for (int t = 0; t < T; ++t) {
+    const int tx = t % s.gx, ty = t / s.gx;
+    const uint32_t b = s.ranges[2 * t], e = s.ranges[2 * t + 1];
+    for (int ly = 0; ly < BY; ++ly)
+      for (int lx = 0; lx < BX; ++lx) {
+        const int x = tx * BX + lx, y = ty * BY + ly;
+        if (x >= s.W || y >= s.H) continue;
+        const int pix = y * s.W + x;
+        const R pfx = (float)x, pfy = (float)y;
+        const R Tfin = s.finalT[pix];
+        R Tr = Tfin;
+        const uint32_t last_contrib = s.ncontrib[pix];
+        R dpix[3], accum[3] = {0, 0, 0}, last_color[3] = {0, 0, 0}, last_alpha = 0.f;
+        for (int ch = 0; ch < 3; ++ch) dpix[ch] = dL_dpix[(size_t)ch * HW + pix];
+        R bg_dot = 0.f;
+        for (int ch = 0; ch < 3; ++ch) bg_dot += s.bg[ch] * dpix[ch];
+        // positions >= last_contrib never blended: start the back-to-front walk below them
+        for (uint32_t k = b + std::min(e - b, last_contrib); k > b; --k) {
+          const uint32_t id = s.vals[k - 1];
+          const float* co = &s.conic_o[4 * id];
+          // which entries blend: decided in float, exactly as the forward decided it
+          {
+            const float fdx = s.xy[2 * id] - (float)x, fdy = s.xy[2 * id + 1] - (float)y;
+            const float fpower = -0.5f * (co[0] * fdx * fdx + co[2] * fdy * fdy) - co[1] * fdx * fdy;
+            if (fpower > 0.0f) continue;
+            if (std::min(0.99f, co[3] * std::exp(fpower)) < 1.0f / 255.0f) continue;
+          }
+          const R dx = R(s.xy[2 * id]) - pfx, dy = R(s.xy[2 * id + 1]) - pfy;
+          const R power = R(-0.5f) * (R(co[0]) * dx * dx + R(co[2]) * dy * dy) - R(co[1]) * dx * dy;
+          const R G = std::exp(power);
+          const R alpha = std::min(R(0.99f), R(co[3]) * G);
+          Tr = Tr / (1.f - alpha);
+          const R dchannel_dcolor = alpha * Tr;
+          R dL_dalpha = 0.f;
+          for (int ch = 0; ch < 3; ++ch) {
+            const R c = s.rgb[3 * id + ch];
+            accum[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum[ch];
+            last_color[ch] = c;
+            dL_dalpha += (c - accum[ch]) * dpix[ch];
+            acc_col[3 * id + ch] += dchannel_dcolor * dpix[ch];
+          }
+          dL_dalpha *= Tr;
+          last_alpha = alpha;
+          dL_dalpha += (-Tfin / (1.f - alpha)) * bg_dot;
+          const R dL_dG = co[3] * dL_dalpha;
+          const R gdx = G * dx, gdy = G * dy;
+          const R dG_ddelx = -gdx * co[0] - gdy * co[1];
+          const R dG_ddely = -gdy * co[2] - gdx * co[1];
+          acc_m2[2 * id] += dL_dG * dG_ddelx * ddelx_dx;
+          acc_m2[2 * id + 1] += dL_dG * dG_ddely * ddely_dy;
+          acc_con[3 * id] += -0.5f * gdx * dx * dL_dG;
+          acc_con[3 * id + 1] += -0.5f * gdx * dy * dL_dG;
+          acc_con[3 * id + 2] += -0.5f * gdy * dy * dL_dG;
+          acc_op[id] += G * dL_dalpha;
+        }
+      }
+  }
+  for (int i = 0; i < P; ++i) {
+    dmean2D[3 * i] = (float)acc_m2[2 * i]; dmean2D[3 * i + 1] = (float)acc_m2[2 * i + 1];
+    for (int c = 0; c < 3; ++c) { dconic[3 * i + c] = (float)acc_con[3 * i + c]; dcolor[3 * i + c] = (float)acc_col[3 * i + c]; }
+    dopac[i] = (float)acc_op[i];
+  }
+  // --- preprocess backward ---
+  const R fx = R(s.W) / (R(2.0f) * R(s.tanx));
+  const R fy = R(s.H) / (R(2.0f) * R(s.tany));
+  const float* proj = s.proj.data();
+  for (int i = 0; i < P; ++i) {
+    if (!(s.radii[i] > 0)) continue;
+    const V3T<R> m = {s.means[3 * i], s.means[3 * i + 1], s.means[3 * i + 2]};
+    const float* c6 = &s.cov6[6 * i];
+    // the forward's 2D covariance, Jacobian and clamps, in float exactly as the forward
+    // computed them (the conic the compositing used is the inverse of THIS cov2D): the
+    // derivative is evaluated at the forward's own point. For needle-shaped Gaussians
+    // (det(cov2D) << a c) the inverse is ill-conditioned, and a cov2D recomputed in double
+    // would be a measurably different point.
+    Cov2DWork wf;
+    cov2d(V3{s.means[3 * i], s.means[3 * i + 1], s.means[3 * i + 2]}, (float)s.W / (2.0f * s.tanx),
+          (float)s.H / (2.0f * s.tany), s.tanx, s.tany, c6, s.view.data(), wf);
+    Cov2DWorkT<R> w;
+    for (int r = 0; r < 2; ++r)
+      for (int c = 0; c < 3; ++c) w.T[r][c] = wf.T[r][c];
+    w.a = wf.a; w.b = wf.b; w.c = wf.c; w.tx = wf.tx; w.ty = wf.ty; w.tz = wf.tz; w.xmul = wf.xmul; w.ymul = wf.ymul;
+    // conic = inverse(cov2D); gradient of the symmetric-matrix inverse. The render bwd
+    // accumulates dconic.y as HALF the derivative w.r.t. the off-diagonal entry (it appears
+    // twice in the quadratic form), so the off-diagonal weight below is 2.
+    const R a = w.a, b = w.b, c = w.c;
+    const R ga = R(acc_con[3 * i]), gb = R(acc_con[3 * i + 1]), gc = R(acc_con[3 * i + 2]);
+    const R denom = a * c - b * b;
+    const R denom2inv = R(1) / ((denom * denom) + R(0.0000001f));
+    R dL_da = 0, dL_db = 0, dL_dc = 0;
+    if (denom2inv != 0) {
+      dL_da = denom2inv * (-c * c * ga + 2 * b * c * gb + (denom - a * c) * gc);
+      dL_dc = denom2inv * (-a * a * gc + 2 * a * b * gb + (denom - a * c) * ga);
+      dL_db = denom2inv * 2 * (b * c * ga - (denom + 2 * b * b) * gb + a * b * gc);
+    }
+    // cov2D = T V T^T  (a = T0 V T0^T, b = T0 V T1^T, c = T1 V T1^T)
+    const R (*T)[3] = w.T;
+    // dL/dV (symmetric, cov6 order xx, xy, xz, yy, yz, zz; off-diagonals carry both halves)
+    float* dc = &dcov6[6 * i];
+    dc[0] = T[0][0] * T[0][0] * dL_da + T[0][0] * T[1][0] * dL_db + T[1][0] * T[1][0] * dL_dc;
+    dc[3] = T[0][1] * T[0][1] * dL_da + T[0][1] * T[1][1] * dL_db + T[1][1] * T[1][1] * dL_dc;
+    dc[5] = T[0][2] * T[0][2] * dL_da + T[0][2] * T[1][2] * dL_db + T[1][2] * T[1][2] * dL_dc;
+    dc[1] = 2 * T[0][0] * T[0][1] * dL_da + (T[0][0] * T[1][1] + T[0][1] * T[1][0]) * dL_db + 2 * T[1][0] * T[1][1] * dL_dc;
+    dc[2] = 2 * T[0][0] * T[0][2] * dL_da + (T[0][0] * T[1][2] + T[0][2] * T[1][0]) * dL_db + 2 * T[1][0] * T[1][2] * dL_dc;
+    dc[4] = 2 * T[0][2] * T[0][1] * dL_da + (T[0][1] * T[1][2] + T[0][2] * T[1][1]) * dL_db + 2 * T[1][1] * T[1][2] * dL_dc;
+    // dL/dT (2x3): dA/dT0 = 2 V T0, dB/dT0 = V T1, dB/dT1 = V T0, dC/dT1 = 2 V T1
+    const R V[3][3] = {{c6[0], c6[1], c6[2]}, {c6[1], c6[3], c6[4]}, {c6[2], c6[4], c6[5]}};
+    R VT0[3], VT1[3];
+    for (int r = 0; r < 3; ++r) {
+      VT0[r] = V[r][0] * T[0][0] + V[r][1] * T[0][1] + V[r][2] * T[0][2];
+      VT1[r] = V[r][0] * T[1][0] + V[r][1] * T[1][1] + V[r][2] * T[1][2];
+    }
+    R dT0[3], dT1[3];
+    for (int r = 0; r < 3; ++r) {
+      dT0[r] = 2 * VT0[r] * dL_da + VT1[r] * dL_db;
+      dT1[r] = 2 * VT1[r] * dL_dc + VT0[r] * dL_db;
+    }
+    // T = J Wr -> dL/dJ = dL/dT Wr^T ; only J00, J02, J11, J12 are live
+    const float* vw = s.view.data();
+    const R W00 = vw[0], W01 = vw[4], W02 = vw[8];
+    const R W10 = vw[1], W11 = vw[5], W12 = vw[9];
+    const R W20 = vw[2], W21 = vw[6], W22 = vw[10];
+    const R dJ00 = dT0[0] * W00 + dT0[1] * W01 + dT0[2] * W02;
+    const R dJ02 = dT0[0] * W20 + dT0[1] * W21 + dT0[2] * W22;
+    const R dJ11 = dT1[0] * W10 + dT1[1] * W11 + dT1[2] * W12;
+    const R dJ12 = dT1[0] * W20 + dT1[1] * W21 + dT1[2] * W22;
+    const R tz = 1.f / w.tz, tz2 = tz * tz, tz3 = tz2 * tz;
+    const R dtx = w.xmul * -fx * tz2 * dJ02;
+    const R dty = w.ymul * -fy * tz2 * dJ12;
+    const R dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * w.tx) * tz3 * dJ02 + (2 * fy * w.ty) * tz3 * dJ12;
+    // camera -> world: dL/dmean = Wr^T dL/dt
+    R dm[3];
+    dm[0] = W00 * dtx + W10 * dty + W20 * dtz;
+    dm[1] = W01 * dtx + W11 * dty + W21 * dtz;
+    dm[2] = W02 * dtx + W12 * dty + W22 * dtz;
+    // projection: ndc = (P p).xy / (P p).w
+    const R mhx = proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12];
+    const R mhy = proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13];
+    const R mw = R(1) / (proj[3] * m.x + proj[7] * m.y + proj[11] * m.z + proj[15] + R(0.0000001f));
+    const R mul1 = mhx * mw * mw, mul2 = mhy * mw * mw;
+    const R g2x = R(acc_m2[2 * i]), g2y = R(acc_m2[2 * i + 1]);
+    dm[0] += (proj[0] * mw - proj[3] * mul1) * g2x + (proj[1] * mw - proj[3] * mul2) * g2y;
+    dm[1] += (proj[4] * mw - proj[7] * mul1) * g2x + (proj[5] * mw - proj[7] * mul2) * g2y;
+    dm[2] += (proj[8] * mw - proj[11] * mul1) * g2x + (proj[9] * mw - proj[11] * mul2) * g2y;
+    // SH backward (view-dependent colour): dL/dsh and dL/dmean through the view direction
+    if (!s.precomp) {
+      const float* sh = &s.shs[(size_t)i * s.M * 3];
+      float* dshi = &dsh[(size_t)i * s.M * 3];
+      const R dirx0 = m.x - s.campos[0], diry0 = m.y - s.campos[1], dirz0 = m.z - s.campos[2];
+      const R len = std::sqrt(dirx0 * dirx0 + diry0 * diry0 + dirz0 * dirz0);
+      const R x = dirx0 / len, y = diry0 / len, z = dirz0 / len;
+      R dRGB[3];
+      for (int ch = 0; ch < 3; ++ch) dRGB[ch] = s.clamped[3 * i + ch] ? R(0) : R(acc_col[3 * i + ch]);
+      R ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};  // dRGB/ddir per channel
+      for (int ch = 0; ch < 3; ++ch) {
+        auto sv = [&](int k) { return sh[k * 3 + ch]; };
+        const R g = dRGB[ch];
+        dshi[0 * 3 + ch] = SH_C0 * g;
+        if (s.D > 0) {
+          dshi[1 * 3 + ch] = -SH_C1 * y * g;
+          dshi[2 * 3 + ch] = SH_C1 * z * g;
+          dshi[3 * 3 + ch] = -SH_C1 * x * g;
+          ddx[ch] = -SH_C1 * sv(3);
+          ddy[ch] = -SH_C1 * sv(1);
+          ddz[ch] = SH_C1 * sv(2);
+          if (s.D > 1) {
+            const R xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            dshi[4 * 3 + ch] = SH_C2[0] * xy * g;
+            dshi[5 * 3 + ch] = SH_C2[1] * yz * g;
+            dshi[6 * 3 + ch] = SH_C2[2] * (2.f * zz - xx - yy) * g;
+            dshi[7 * 3 + ch] = SH_C2[3] * xz * g;
+            dshi[8 * 3 + ch] = SH_C2[4] * (xx - yy) * g;
+            ddx[ch] += SH_C2[0] * y * sv(4) + SH_C2[2] * 2.f * -x * sv(6) + SH_C2[3] * z * sv(7) + SH_C2[4] * 2.f * x * sv(8);
+            ddy[ch] += SH_C2[0] * x * sv(4) + SH_C2[1] * z * sv(5) + SH_C2[2] * 2.f * -y * sv(6) + SH_C2[4] * 2.f * -y * sv(8);
+            ddz[ch] += SH_C2[1] * y * sv(5) + SH_C2[2] * 2.f * 2.f * z * sv(6) + SH_C2[3] * x * sv(7);
+            if (s.D > 2) {
+              dshi[9 * 3 + ch] = SH_C3[0] * y * (3.f * xx - yy) * g;
+              dshi[10 * 3 + ch] = SH_C3[1] * xy * z * g;
+              dshi[11 * 3 + ch] = SH_C3[2] * y * (4.f * zz - xx - yy) * g;
+              dshi[12 * 3 + ch] = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy) * g;
+              dshi[13 * 3 + ch] = SH_C3[4] * x * (4.f * zz - xx - yy) * g;
+              dshi[14 * 3 + ch] = SH_C3[5] * z * (xx - yy) * g;
+              dshi[15 * 3 + ch] = SH_C3[6] * x * (xx - 3.f * yy) * g;
+              ddx[ch] += SH_C3[0] * sv(9) * 3.f * 2.f * xy + SH_C3[1] * sv(10) * yz +
+                         SH_C3[2] * sv(11) * -2.f * xy + SH_C3[3] * sv(12) * -3.f * 2.f * xz +
+                         SH_C3[4] * sv(13) * (-3.f * xx + 4.f * zz - yy) + SH_C3[5] * sv(14) * 2.f * xz +
+                         SH_C3[6] * sv(15) * 3.f * (xx - yy);
+              ddy[ch] += SH_C3[0] * sv(9) * 3.f * (xx - yy) + SH_C3[1] * sv(10) * xz +
+                         SH_C3[2] * sv(11) * (-3.f * yy + 4.f * zz - xx) + SH_C3[3] * sv(12) * -3.f * 2.f * yz +
+                         SH_C3[4] * sv(13) * -2.f * xy + SH_C3[5] * sv(14) * -2.f * yz +
+                         SH_C3[6] * sv(15) * -3.f * 2.f * xy;
+              ddz[ch] += SH_C3[1] * sv(10) * xy + SH_C3[2] * sv(11) * 4.f * 2.f * yz +
+                         SH_C3[3] * sv(12) * 3.f * (2.f * zz - xx - yy) + SH_C3[4] * sv(13) * 4.f * 2.f * xz +
+                         SH_C3[5] * sv(14) * (xx - yy);
+            }
+          }
+        }
+      }
+      // dL/ddir (normalised), then through the normalisation
+      const R gdx = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
+      const R gdy = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
+      const R gdz = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
+      const R sum2 = dirx0 * dirx0 + diry0 * diry0 + dirz0 * dirz0;
+      const R invsum32 = 1.0f / std::sqrt(sum2 * sum2 * sum2);
+      dm[0] += ((sum2 - dirx0 * dirx0) * gdx - diry0 * dirx0 * gdy - dirz0 * dirx0 * gdz) * invsum32;
+      dm[1] += (-dirx0 * diry0 * gdx + (sum2 - diry0 * diry0) * gdy - dirz0 * diry0 * gdz) * invsum32;
+      dm[2] += (-dirx0 * dirz0 * gdx - diry0 * dirz0 * gdy + (sum2 - dirz0 * dirz0) * gdz) * invsum32;
+    }
+    dmean3D[3 * i] = dm[0]; dmean3D[3 * i + 1] = dm[1]; dmean3D[3 * i + 2] = dm[2];
+  }
+}
+
+
 }  // namespace
 
 extern "C" {
@@ -355,211 +586,17 @@ void orc_get_binning(void* h, uint64_t* keys, uint32_t* vals, uint32_t* ranges) 
 // dopac [P], dcolor [P][3], dmean3D [P][3], dcov6 [P][6], dsh [P][M][3] (or NULL when precomp).
 void orc_backward(void* h, const float* dL_dpix, float* dmean2D, float* dconic, float* dopac,
                   float* dcolor, float* dmean3D, float* dcov6, float* dsh) {
-  State& s = *static_cast<State*>(h);
-  const int P = s.P, HW = s.H * s.W, T = s.gx * s.gy;
-  std::memset(dmean2D, 0, 3 * (size_t)P * 4); std::memset(dconic, 0, 3 * (size_t)P * 4);
-  std::memset(dopac, 0, (size_t)P * 4); std::memset(dcolor, 0, 3 * (size_t)P * 4);
-  std::memset(dmean3D, 0, 3 * (size_t)P * 4); std::memset(dcov6, 0, 6 * (size_t)P * 4);
-  if (dsh) std::memset(dsh, 0, (size_t)P * s.M * 3 * 4);
-  const float ddelx_dx = 0.5f * s.W, ddely_dy = 0.5f * s.H;
-  std::vector<double> acc_m2(2 * (size_t)P, 0), acc_con(3 * (size_t)P, 0), acc_op(P, 0), acc_col(3 * (size_t)P, 0);
-  // --- render backward (serial; double accumulators make the checker order-insensitive) ---
-  for (int t = 0; t < T; ++t) {
-    const int tx = t % s.gx, ty = t / s.gx;
-    const uint32_t b = s.ranges[2 * t], e = s.ranges[2 * t + 1];
-    for (int ly = 0; ly < BY; ++ly)
-      for (int lx = 0; lx < BX; ++lx) {
-        const int x = tx * BX + lx, y = ty * BY + ly;
-        if (x >= s.W || y >= s.H) continue;
-        const int pix = y * s.W + x;
-        const float pfx = (float)x, pfy = (float)y;
-        const float Tfin = s.finalT[pix];
-        float Tr = Tfin;
-        const uint32_t last_contrib = s.ncontrib[pix];
-        float dpix[3], accum[3] = {0, 0, 0}, last_color[3] = {0, 0, 0}, last_alpha = 0.f;
-        for (int ch = 0; ch < 3; ++ch) dpix[ch] = dL_dpix[(size_t)ch * HW + pix];
-        float bg_dot = 0.f;
-        for (int ch = 0; ch < 3; ++ch) bg_dot += s.bg[ch] * dpix[ch];
-        for (uint32_t k = e; k > b; --k) {
-          const uint32_t contributor = k - 1 - b;  // 0-based position in the tile list
-          if (contributor >= last_contrib) continue;
-          const uint32_t id = s.vals[k - 1];
-          const float* co = &s.conic_o[4 * id];
-          const float dx = s.xy[2 * id] - pfx, dy = s.xy[2 * id + 1] - pfy;
-          const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-          if (power > 0.0f) continue;
-          const float G = std::exp(power);
-          const float alpha = std::min(0.99f, co[3] * G);
-          if (alpha < 1.0f / 255.0f) continue;
-          Tr = Tr / (1.f - alpha);
-          const float dchannel_dcolor = alpha * Tr;
-          float dL_dalpha = 0.f;
-          for (int ch = 0; ch < 3; ++ch) {
-            const float c = s.rgb[3 * id + ch];
-            accum[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum[ch];
-            last_color[ch] = c;
-            dL_dalpha += (c - accum[ch]) * dpix[ch];
-            acc_col[3 * id + ch] += dchannel_dcolor * dpix[ch];
-          }
-          dL_dalpha *= Tr;
-          last_alpha = alpha;
-          dL_dalpha += (-Tfin / (1.f - alpha)) * bg_dot;
-          const float dL_dG = co[3] * dL_dalpha;
-          const float gdx = G * dx, gdy = G * dy;
-          const float dG_ddelx = -gdx * co[0] - gdy * co[1];
-          const float dG_ddely = -gdy * co[2] - gdx * co[1];
-          acc_m2[2 * id] += dL_dG * dG_ddelx * ddelx_dx;
-          acc_m2[2 * id + 1] += dL_dG * dG_ddely * ddely_dy;
-          acc_con[3 * id] += -0.5f * gdx * dx * dL_dG;
-          acc_con[3 * id + 1] += -0.5f * gdx * dy * dL_dG;
-          acc_con[3 * id + 2] += -0.5f * gdy * dy * dL_dG;
-          acc_op[id] += G * dL_dalpha;
-        }
-      }
-  }
-  for (int i = 0; i < P; ++i) {
-    dmean2D[3 * i] = (float)acc_m2[2 * i]; dmean2D[3 * i + 1] = (float)acc_m2[2 * i + 1];
-    for (int c = 0; c < 3; ++c) { dconic[3 * i + c] = (float)acc_con[3 * i + c]; dcolor[3 * i + c] = (float)acc_col[3 * i + c]; }
-    dopac[i] = (float)acc_op[i];
-  }
-  // --- preprocess backward ---
-  const float fx = s.W / (2.0f * s.tanx);
-  const float fy = s.H / (2.0f * s.tany);
-  const float* proj = s.proj.data();
-  for (int i = 0; i < P; ++i) {
-    if (!(s.radii[i] > 0)) continue;
-    const V3 m = {s.means[3 * i], s.means[3 * i + 1], s.means[3 * i + 2]};
-    const float* c6 = &s.cov6[6 * i];
-    Cov2DWork w;
-    cov2d(m, fx, fy, s.tanx, s.tany, c6, s.view.data(), w);
-    // conic = inverse(cov2D); gradient of the symmetric-matrix inverse. The render bwd
-    // accumulates dconic.y as HALF the derivative w.r.t. the off-diagonal entry (it appears
-    // twice in the quadratic form), so the off-diagonal weight below is 2.
-    const float a = w.a, b = w.b, c = w.c;
-    const float ga = dconic[3 * i], gb = dconic[3 * i + 1], gc = dconic[3 * i + 2];
-    const float denom = a * c - b * b;
-    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-    float dL_da = 0, dL_db = 0, dL_dc = 0;
-    if (denom2inv != 0) {
-      dL_da = denom2inv * (-c * c * ga + 2 * b * c * gb + (denom - a * c) * gc);
-      dL_dc = denom2inv * (-a * a * gc + 2 * a * b * gb + (denom - a * c) * ga);
-      dL_db = denom2inv * 2 * (b * c * ga - (denom + 2 * b * b) * gb + a * b * gc);
-    }
-    // cov2D = T V T^T  (a = T0 V T0^T, b = T0 V T1^T, c = T1 V T1^T)
-    const float (*T)[3] = w.T;
-    // dL/dV (symmetric, cov6 order xx, xy, xz, yy, yz, zz; off-diagonals carry both halves)
-    float* dc = &dcov6[6 * i];
-    dc[0] = T[0][0] * T[0][0] * dL_da + T[0][0] * T[1][0] * dL_db + T[1][0] * T[1][0] * dL_dc;
-    dc[3] = T[0][1] * T[0][1] * dL_da + T[0][1] * T[1][1] * dL_db + T[1][1] * T[1][1] * dL_dc;
-    dc[5] = T[0][2] * T[0][2] * dL_da + T[0][2] * T[1][2] * dL_db + T[1][2] * T[1][2] * dL_dc;
-    dc[1] = 2 * T[0][0] * T[0][1] * dL_da + (T[0][0] * T[1][1] + T[0][1] * T[1][0]) * dL_db + 2 * T[1][0] * T[1][1] * dL_dc;
-    dc[2] = 2 * T[0][0] * T[0][2] * dL_da + (T[0][0] * T[1][2] + T[0][2] * T[1][0]) * dL_db + 2 * T[1][0] * T[1][2] * dL_dc;
-    dc[4] = 2 * T[0][2] * T[0][1] * dL_da + (T[0][1] * T[1][2] + T[0][2] * T[1][1]) * dL_db + 2 * T[1][1] * T[1][2] * dL_dc;
-    // dL/dT (2x3): dA/dT0 = 2 V T0, dB/dT0 = V T1, dB/dT1 = V T0, dC/dT1 = 2 V T1
-    const float V[3][3] = {{c6[0], c6[1], c6[2]}, {c6[1], c6[3], c6[4]}, {c6[2], c6[4], c6[5]}};
-    float VT0[3], VT1[3];
-    for (int r = 0; r < 3; ++r) {
-      VT0[r] = V[r][0] * T[0][0] + V[r][1] * T[0][1] + V[r][2] * T[0][2];
-      VT1[r] = V[r][0] * T[1][0] + V[r][1] * T[1][1] + V[r][2] * T[1][2];
-    }
-    float dT0[3], dT1[3];
-    for (int r = 0; r < 3; ++r) {
-      dT0[r] = 2 * VT0[r] * dL_da + VT1[r] * dL_db;
-      dT1[r] = 2 * VT1[r] * dL_dc + VT0[r] * dL_db;
-    }
-    // T = J Wr -> dL/dJ = dL/dT Wr^T ; only J00, J02, J11, J12 are live
-    const float* vw = s.view.data();
-    const float W00 = vw[0], W01 = vw[4], W02 = vw[8];
-    const float W10 = vw[1], W11 = vw[5], W12 = vw[9];
-    const float W20 = vw[2], W21 = vw[6], W22 = vw[10];
-    const float dJ00 = dT0[0] * W00 + dT0[1] * W01 + dT0[2] * W02;
-    const float dJ02 = dT0[0] * W20 + dT0[1] * W21 + dT0[2] * W22;
-    const float dJ11 = dT1[0] * W10 + dT1[1] * W11 + dT1[2] * W12;
-    const float dJ12 = dT1[0] * W20 + dT1[1] * W21 + dT1[2] * W22;
-    const float tz = 1.f / w.tz, tz2 = tz * tz, tz3 = tz2 * tz;
-    const float dtx = w.xmul * -fx * tz2 * dJ02;
-    const float dty = w.ymul * -fy * tz2 * dJ12;
-    const float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * w.tx) * tz3 * dJ02 + (2 * fy * w.ty) * tz3 * dJ12;
-    // camera -> world: dL/dmean = Wr^T dL/dt
-    float dm[3];
-    dm[0] = W00 * dtx + W10 * dty + W20 * dtz;
-    dm[1] = W01 * dtx + W11 * dty + W21 * dtz;
-    dm[2] = W02 * dtx + W12 * dty + W22 * dtz;
-    // projection: ndc = (P p).xy / (P p).w
-    const float mhx = proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12];
-    const float mhy = proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13];
-    const float mw = 1.0f / (proj[3] * m.x + proj[7] * m.y + proj[11] * m.z + proj[15] + 0.0000001f);
-    const float mul1 = mhx * mw * mw, mul2 = mhy * mw * mw;
-    const float g2x = dmean2D[3 * i], g2y = dmean2D[3 * i + 1];
-    dm[0] += (proj[0] * mw - proj[3] * mul1) * g2x + (proj[1] * mw - proj[3] * mul2) * g2y;
-    dm[1] += (proj[4] * mw - proj[7] * mul1) * g2x + (proj[5] * mw - proj[7] * mul2) * g2y;
-    dm[2] += (proj[8] * mw - proj[11] * mul1) * g2x + (proj[9] * mw - proj[11] * mul2) * g2y;
-    // SH backward (view-dependent colour): dL/dsh and dL/dmean through the view direction
-    if (!s.precomp) {
-      const float* sh = &s.shs[(size_t)i * s.M * 3];
-      float* dshi = &dsh[(size_t)i * s.M * 3];
-      const float dirx0 = m.x - s.campos[0], diry0 = m.y - s.campos[1], dirz0 = m.z - s.campos[2];
-      const float len = std::sqrt(dirx0 * dirx0 + diry0 * diry0 + dirz0 * dirz0);
-      const float x = dirx0 / len, y = diry0 / len, z = dirz0 / len;
-      float dRGB[3];
-      for (int ch = 0; ch < 3; ++ch) dRGB[ch] = s.clamped[3 * i + ch] ? 0.f : dcolor[3 * i + ch];
-      float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};  // dRGB/ddir per channel
-      for (int ch = 0; ch < 3; ++ch) {
-        auto sv = [&](int k) { return sh[k * 3 + ch]; };
-        const float g = dRGB[ch];
-        dshi[0 * 3 + ch] = SH_C0 * g;
-        if (s.D > 0) {
-          dshi[1 * 3 + ch] = -SH_C1 * y * g;
-          dshi[2 * 3 + ch] = SH_C1 * z * g;
-          dshi[3 * 3 + ch] = -SH_C1 * x * g;
-          ddx[ch] = -SH_C1 * sv(3);
-          ddy[ch] = -SH_C1 * sv(1);
-          ddz[ch] = SH_C1 * sv(2);
-          if (s.D > 1) {
-            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-            dshi[4 * 3 + ch] = SH_C2[0] * xy * g;
-            dshi[5 * 3 + ch] = SH_C2[1] * yz * g;
-            dshi[6 * 3 + ch] = SH_C2[2] * (2.f * zz - xx - yy) * g;
-            dshi[7 * 3 + ch] = SH_C2[3] * xz * g;
-            dshi[8 * 3 + ch] = SH_C2[4] * (xx - yy) * g;
-            ddx[ch] += SH_C2[0] * y * sv(4) + SH_C2[2] * 2.f * -x * sv(6) + SH_C2[3] * z * sv(7) + SH_C2[4] * 2.f * x * sv(8);
-            ddy[ch] += SH_C2[0] * x * sv(4) + SH_C2[1] * z * sv(5) + SH_C2[2] * 2.f * -y * sv(6) + SH_C2[4] * 2.f * -y * sv(8);
-            ddz[ch] += SH_C2[1] * y * sv(5) + SH_C2[2] * 2.f * 2.f * z * sv(6) + SH_C2[3] * x * sv(7);
-            if (s.D > 2) {
-              dshi[9 * 3 + ch] = SH_C3[0] * y * (3.f * xx - yy) * g;
-              dshi[10 * 3 + ch] = SH_C3[1] * xy * z * g;
-              dshi[11 * 3 + ch] = SH_C3[2] * y * (4.f * zz - xx - yy) * g;
-              dshi[12 * 3 + ch] = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy) * g;
-              dshi[13 * 3 + ch] = SH_C3[4] * x * (4.f * zz - xx - yy) * g;
-              dshi[14 * 3 + ch] = SH_C3[5] * z * (xx - yy) * g;
-              dshi[15 * 3 + ch] = SH_C3[6] * x * (xx - 3.f * yy) * g;
-              ddx[ch] += SH_C3[0] * sv(9) * 3.f * 2.f * xy + SH_C3[1] * sv(10) * yz +
-                         SH_C3[2] * sv(11) * -2.f * xy + SH_C3[3] * sv(12) * -3.f * 2.f * xz +
-                         SH_C3[4] * sv(13) * (-3.f * xx + 4.f * zz - yy) + SH_C3[5] * sv(14) * 2.f * xz +
-                         SH_C3[6] * sv(15) * 3.f * (xx - yy);
-              ddy[ch] += SH_C3[0] * sv(9) * 3.f * (xx - yy) + SH_C3[1] * sv(10) * xz +
-                         SH_C3[2] * sv(11) * (-3.f * yy + 4.f * zz - xx) + SH_C3[3] * sv(12) * -3.f * 2.f * yz +
-                         SH_C3[4] * sv(13) * -2.f * xy + SH_C3[5] * sv(14) * -2.f * yz +
-                         SH_C3[6] * sv(15) * -3.f * 2.f * xy;
-              ddz[ch] += SH_C3[1] * sv(10) * xy + SH_C3[2] * sv(11) * 4.f * 2.f * yz +
-                         SH_C3[3] * sv(12) * 3.f * (2.f * zz - xx - yy) + SH_C3[4] * sv(13) * 4.f * 2.f * xz +
-                         SH_C3[5] * sv(14) * (xx - yy);
-            }
-          }
-        }
-      }
-      // dL/ddir (normalised), then through the normalisation
-      const float gdx = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
-      const float gdy = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
-      const float gdz = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
-      const float sum2 = dirx0 * dirx0 + diry0 * diry0 + dirz0 * dirz0;
-      const float invsum32 = 1.0f / std::sqrt(sum2 * sum2 * sum2);
-      dm[0] += ((sum2 - dirx0 * dirx0) * gdx - diry0 * dirx0 * gdy - dirz0 * dirx0 * gdz) * invsum32;
-      dm[1] += (-dirx0 * diry0 * gdx + (sum2 - diry0 * diry0) * gdy - dirz0 * diry0 * gdz) * invsum32;
-      dm[2] += (-dirx0 * dirz0 * gdx - diry0 * dirz0 * gdy + (sum2 - dirz0 * dirz0) * gdz) * invsum32;
-    }
-    dmean3D[3 * i] = dm[0]; dmean3D[3 * i + 1] = dm[1]; dmean3D[3 * i + 2] = dm[2];
-  }
+  backward_t<float>(*static_cast<State*>(h), dL_dpix, dmean2D, dconic, dopac, dcolor, dmean3D, dcov6, dsh);
+}
+
+// The same backward evaluated in double (per-pixel chain, transmittance recovery, Jacobians;
+// which entries blend is still decided in float, as the forward decided it): the gradient of
+// the very function the float forward computed, to ~1e-15. Tests use it as the reference
+// for device gradients whose per-pixel terms cancel heavily (a float implementation's error
+// relative to the largest gradient is then limited by its float terms, not by the checker).
+void orc_backward_f64(void* h, const float* dL_dpix, float* dmean2D, float* dconic, float* dopac,
+                      float* dcolor, float* dmean3D, float* dcov6, float* dsh) {
+  backward_t<double>(*static_cast<State*>(h), dL_dpix, dmean2D, dconic, dopac, dcolor, dmean3D, dcov6, dsh);
 }
 
 }  // extern "C"

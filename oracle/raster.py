@@ -32,6 +32,7 @@ def load():
         lib.orc_get_geom.argtypes = [c_void_p] * 8
         lib.orc_get_binning.argtypes = [c_void_p] * 4
         lib.orc_backward.argtypes = [c_void_p] * 9
+        lib.orc_backward_f64.argtypes = [c_void_p] * 9
         _lib = lib
     return _lib
 
@@ -87,14 +88,17 @@ class View:
         load().orc_get_binning(self.h, _p(keys), _p(vals), _p(ranges))
         return keys[:N], vals[:N], ranges
 
-    def backward(self, dL_dpix):
+    def backward(self, dL_dpix, f64: bool = False):
+        """Gradients of this view. f64: the same backward evaluated in double (which entries
+        blend still decided in float, as the forward did): the high-precision reference."""
         P, M = self.P, self.M
         d = np.ascontiguousarray(dL_dpix, dtype=np.float32).reshape(3, self.H, self.W)
         out = dict(dmean2D=np.empty((P, 3), np.float32), dconic=np.empty((P, 3), np.float32),
                    dopacity=np.empty(P, np.float32), dcolor=np.empty((P, 3), np.float32),
                    dmean3D=np.empty((P, 3), np.float32), dcov6=np.empty((P, 6), np.float32),
                    dsh=np.empty((P, max(M, 1), 3), np.float32) if self.shs is not None else None)
-        load().orc_backward(self.h, _p(d), _p(out["dmean2D"]), _p(out["dconic"]), _p(out["dopacity"]),
+        fn = load().orc_backward_f64 if f64 else load().orc_backward
+        fn(self.h, _p(d), _p(out["dmean2D"]), _p(out["dconic"]), _p(out["dopacity"]),
                             _p(out["dcolor"]), _p(out["dmean3D"]), _p(out["dcov6"]), _p(out["dsh"]))
         return out
 

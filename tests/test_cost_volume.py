@@ -141,3 +141,30 @@ def test_hip_cost_volume_rotated_views_vs_oracle(gpu, spread):
     (ocv.cost_volume(r2, t2, K, pose, depth) * dcost).sum().backward()
     rel_close(rg.grad.cpu(), r2.grad, 1e-4)
     rel_close(tg_.grad.cpu(), t2.grad, 1e-4)
+
+
+@pytest.mark.gpu
+def test_hip_cost_volume_config_a_shape_vs_oracle(gpu):
+    """BASELINE configs[0]'s cost-volume shape (2 views, C = D = 128, 32x32 features, the
+    reference's linspace inverse-depth candidates, mv_unimatch.py:416-435): forward and both
+    feature gradients vs the oracle (oracle/cost_volume.py, the reference's grid_sample
+    formulation) within 1e-4."""
+    g = torch.Generator().manual_seed(12)
+    B, J, C, H, W, D = 2, 1, 128, 32, 32, 128
+    ref = torch.randn(B, C, H, W, generator=g)
+    tgt = torch.randn(B, J, C, H, W, generator=g)
+    K = torch.tensor([[W * 1.0, 0, W / 2], [0, H * 1.0, H / 2], [0, 0, 1]]).expand(B, J, 3, 3).contiguous()
+    pose = torch.eye(4).expand(B, J, 4, 4).clone()
+    pose[0, :, 0, 3], pose[1, :, 0, 3] = 0.1, -0.1  # each view is the other's source
+    depth = 1.0 / torch.linspace(1 / 0.5, 1 / 100.0, D).expand(B, D).contiguous()
+    from my_depthsplat_amd.matching import plane_sweep_cost_volume
+    rg, tg_ = ref.to(gpu).requires_grad_(True), tgt.to(gpu).requires_grad_(True)
+    cost = plane_sweep_cost_volume(rg, tg_, K.to(gpu), pose.to(gpu), depth.to(gpu))
+    want = ocv.cost_volume(ref, tgt, K, pose, depth)
+    rel_close(cost.detach().cpu(), want, 1e-4)
+    dcost = torch.randn(want.shape, generator=g)
+    (cost * dcost.to(gpu)).sum().backward()
+    r2, t2 = ref.clone().requires_grad_(True), tgt.clone().requires_grad_(True)
+    (ocv.cost_volume(r2, t2, K, pose, depth) * dcost).sum().backward()
+    rel_close(rg.grad.cpu(), r2.grad, 1e-4)
+    rel_close(tg_.grad.cpu(), t2.grad, 1e-4)

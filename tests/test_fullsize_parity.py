@@ -16,7 +16,8 @@
   (two-phase binning with the depth cut) vs the oracle.
 
 Bars (BASELINE.json north_star): mean L1 < 1e-4, PSNR delta < 0.01 dB, sort indices
-bit-exact; gradients within 2e-3 of the largest magnitude (float atomics reorder sums).
+bit-exact; gradients within 5e-4 of the largest magnitude (the oracle accumulates in
+double; the device sums per-wave float partials as 64-bit fixed point).
 The oracle (oracle/dsr_oracle.cpp) restates the upstream algorithm; it is "parity
 unpinned" against the absent CUDA library. Max-abs errors are written to
 $DSPLAT_PARITY_REPORT (JSON lines) when that is set.
@@ -289,21 +290,21 @@ def test_config_c_shape_forward_backward_vs_oracle(gpu):
         b = vs[i]
         oc, _, _ = o.image()
         l1, mx, dp = _image_bars(col[i], oc, f"config C view {i}")
-        gr = o.backward(dpix[i].numpy())
+        gr = o.backward(dpix[i].numpy(), f64=True)
         s = float(st["scale"][i])
         acc[b]["dmean3D"] = acc[b]["dmean3D"] + gr["dmean3D"] * s
         acc[b]["dcov6"] = acc[b]["dcov6"] + gr["dcov6"] * (s * s)
         acc[b]["dsh"] = acc[b]["dsh"] + gr["dsh"]
         acc[b]["dopacity"] = acc[b]["dopacity"] + gr["dopacity"]
         e2 = np.abs(dm2[i].cpu().numpy() - gr["dmean2D"]).max() / (np.abs(gr["dmean2D"]).max() + 1e-12)
-        assert e2 < 2e-3, ("dmean2D", i, e2)
+        assert e2 < 5e-4, ("dmean2D", i, e2)
         _report(test="config_c_view", view=i, l1=l1, max_abs=mx, dpsnr=dp, dmean2d_rel=float(e2))
         o.close()
     for b in range(B):
         for hip, key in ((dm[b], "dmean3D"), (dc6[b], "dcov6"), (dsh[b], "dsh"), (dop[b], "dopacity")):
             ref = acc[b][key]
             err = float(np.abs(hip.cpu().numpy().reshape(ref.shape) - ref).max() / (np.abs(ref).max() + 1e-12))
-            assert err < 2e-3, (b, key, err)
+            assert err < 5e-4, (b, key, err)
             _report(test="config_c_grad", scene=b, grad=key, rel_max_err=err)
 
 

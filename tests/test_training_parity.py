@@ -1,0 +1,241 @@
+"""Parity of the TRAINING path at the BASELINE training configurations' stated sizes (GPU).
+
+* config C (BASELINE configs[2]: 2-view 256x256 context -> G = 131,072 per scene, batch 16
+  x 4 target views = 64 views in one batch; model_wrapper.py:165-270): the product training
+  entry (render_views under autograd: device camera set-up, exact tile binning, fused sort +
+  composite, deterministic fixed-point backward) — every one of the 64 images vs the oracle,
+  and every gradient of two scenes vs the oracle's backward.
+* config D training shape (BASELINE configs[3]: 6-view 448x768 context -> G = 2,064,384,
+  scripts/dl3dv_depthsplat_train.sh:28-29): the two-phase layout with the depth cut that the
+  config-D training leg runs, forward + backward of 2 target views, gradients vs the oracle.
+* config B through the product inference entry (cameras built in float inside the binning
+  kernel) vs the reference wrapper's camera settings: how many (view, tile) list entries
+  differ (DESIGN.md §3 states the bound).
+
+The oracle is fed the camera blocks the device built (state.cams / build_cameras), so the
+comparison isolates the rasterizer. The gradient reference is the oracle's backward evaluated in
+double (orc_backward_f64): on these scenes the per-pixel terms cancel heavily, and the float
+oracle itself sits ~1e-3 of the largest dL/dmean3D away from the exact gradient at config D.
+Bars (north_star): mean L1 < 1e-4 and PSNR delta < 0.01 dB per image; gradients within
+1e-3 of each tensor's largest magnitude (GRAD_BAR below).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from raster_cases import flat_inputs, oracle_views, scene_inputs, settings_for
+from test_fullsize_parity import _image_bars, _report, _segments
+
+pytestmark = pytest.mark.gpu
+
+# Gradient bar at these sizes: 1e-3 of each tensor's largest magnitude. The scenes hold huge,
+# needle-shaped Gaussians (radius ~375 px, det(cov2D) ~1e-3 of a*c) whose dL/dmean3D is a sum
+# of ~1e5 cancelling per-pixel terms through an ill-conditioned conic inverse: any float32
+# evaluation carries ~5e-4 there (device: 4.4e-4 at config C, 4.7e-4 at config D; the float
+# oracle itself is 1.03e-3 from the double reference at config D). Other gradients stay below
+# 2.3e-4; the smaller scenes' tests keep 5e-4. A wrong term moves a gradient by O(1).
+GRAD_BAR = 1e-3
+
+
+def _oracle_view(means, shs, opac, cov6, cams, i, H, W):
+    """Oracle render of view i with the camera block the device built (cams [V, 44] numpy)."""
+    from oracle import raster as orc
+    c = cams[i]
+    st = {"viewmatrix": c[None, 0:16].reshape(1, 4, 4), "projmatrix": c[None, 16:32].reshape(1, 4, 4),
+          "campos": c[None, 32:35], "tanfovx": c[None, 35], "tanfovy": c[None, 36], "scale": c[None, 41]}
+    deg = math.isqrt(shs.shape[1]) - 1
+    return orc.render_settings(means, shs, None, opac, cov6, st, 0, c[37:40].copy(), H, W, deg)
+
+
+def _rel(hip, ref):
+    return float(np.abs(hip - ref).max() / (np.abs(ref).max() + 1e-12))
+
+
+def _check_grads(tag, scene, got, acc):
+    """got: the device gradients of one scene in the oracle's layouts; acc: oracle sums."""
+    for key in ("dmean3D", "dcov6", "dsh", "dopacity"):
+        err = _rel(got[key], acc[key])
+        _report(test=f"{tag}_grad", scene=scene, grad=key, rel_max_err=err)
+        assert err < GRAD_BAR, (tag, scene, key, err)
+
+
+def _accumulate(acc, gr, s):
+    """The views of one scene: the rescaled camera's gradients back to the scene's units."""
+    for key, f in (("dmean3D", s), ("dcov6", s * s), ("dsh", 1.0), ("dopacity", 1.0)):
+        acc[key] = acc.get(key, 0) + gr[key].astype(np.float64) * f
+
+
+def test_config_c_batch16_training_vs_oracle(gpu):
+    from my_depthsplat_amd import raster
+    from my_depthsplat_amd.cuda_splatting import render_views
+    B, v, H, W = 16, 4, 256, 256
+    sc = scene_inputs(h=H, w=W, n_ctx=2, n_tgt=v, seed=4100, batch=B)
+    g = sc.gaussians
+    leaves = [t.to(gpu).requires_grad_(True) for t in (g.means, g.covariances, g.harmonics, g.opacities)]
+    ext = sc.target_extrinsics.reshape(B * v, 4, 4).to(gpu)
+    K = sc.target_intrinsics.reshape(B * v, 3, 3).to(gpu)
+    near, far = sc.near.reshape(B * v).to(gpu), sc.far.reshape(B * v).to(gpu)
+    bg = torch.zeros(B * v, 3, device=gpu)
+    vs = [i // v for i in range(B * v)]
+    color = render_views(ext, K, near, far, (H, W), bg, *leaves, view_scene=vs)
+    dpix = torch.randn(B * v, 3, H, W, generator=torch.Generator().manual_seed(5)) * 1e-3
+    (color * dpix.to(gpu)).sum().backward()
+    cams = raster.build_cameras(ext, K, near, far, bg, vs, True).cpu().numpy()
+    torch.cuda.synchronize()
+    col = color.detach().cpu().numpy()
+    means, shs, opac, cov6 = (t.numpy() for t in flat_inputs(sc))
+    check = (0, B - 1)
+    accs = {b: {} for b in check}
+    worst = 0.0
+    for i in range(B * v):
+        b = vs[i]
+        o = _oracle_view(means[b], shs[b], opac[b], cov6[b], cams, i, H, W)
+        oc, _, _ = o.image()
+        l1, mx, dp = _image_bars(col[i], oc, f"config C view {i}")
+        worst = max(worst, l1)
+        if b in check:
+            _accumulate(accs[b], o.backward(dpix[i].numpy(), f64=True), float(cams[i, 41]))
+        o.close()
+    _report(test="config_c_b16_images", views=B * v, max_l1=worst)
+    tri = (torch.tensor([0, 0, 0, 1, 1, 2]), torch.tensor([0, 1, 2, 1, 2, 2]))
+    for b in check:
+        got = {"dmean3D": leaves[0].grad[b].cpu().numpy(),
+               "dcov6": leaves[1].grad[b][:, tri[0], tri[1]].cpu().numpy(),
+               "dsh": leaves[2].grad[b].transpose(-1, -2).cpu().numpy(),
+               "dopacity": leaves[3].grad[b].cpu().numpy()}
+        # the triu gather puts the whole off-diagonal gradient on the upper element
+        assert float(leaves[1].grad[b][:, 1, 0].abs().max()) == 0.0
+        _check_grads("config_c_b16", b, got, accs[b])
+
+
+def test_config_c_backward_is_deterministic(gpu):
+    """Two backward passes of the same batch give bit-identical gradients (fixed-point sums:
+    no float-atomic order noise), and so does a second forward + backward."""
+    from my_depthsplat_amd.cuda_splatting import render_views
+    B, v, H, W = 4, 4, 256, 256
+    sc = scene_inputs(h=H, w=W, n_ctx=2, n_tgt=v, seed=4200, batch=B)
+    g = sc.gaussians
+    ext = sc.target_extrinsics.reshape(B * v, 4, 4).to(gpu)
+    K = sc.target_intrinsics.reshape(B * v, 3, 3).to(gpu)
+    near, far = sc.near.reshape(B * v).to(gpu), sc.far.reshape(B * v).to(gpu)
+    dpix = torch.randn(B * v, 3, H, W, generator=torch.Generator().manual_seed(6)).to(gpu)
+    grads = []
+    for _ in range(2):
+        leaves = [t.to(gpu).requires_grad_(True) for t in (g.means, g.covariances, g.harmonics, g.opacities)]
+        color = render_views(ext, K, near, far, (H, W), torch.zeros(B * v, 3, device=gpu), *leaves,
+                             view_scene=[i // v for i in range(B * v)])
+        (color * dpix).sum().backward()
+        grads.append([t.grad.clone() for t in leaves])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
+def test_config_d_training_backward_vs_oracle(gpu, monkeypatch):
+    """6-view 448x768 context (G = 2,064,384), 2 target views, forward + backward through the
+    two-phase layout with the depth cut (the layout the config-D training leg uses: its V*T*G
+    key slots exceed the key budget): images and every gradient vs the oracle."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+    monkeypatch.setitem(raster._spec, "two_phase_max", None)
+    H, W, v = 448, 768, 2
+    sc = scene_inputs(h=H, w=W, n_ctx=6, n_tgt=v, seed=2100)
+    g = sc.gaussians
+    dev = [t.to(gpu) for t in (g.means, g.harmonics, g.opacities, g.covariances)]
+    ci = raster.camera_inputs(sc.target_extrinsics[0].to(gpu), sc.target_intrinsics[0].to(gpu), sc.near[0].to(gpu),
+                              sc.far[0].to(gpu), torch.zeros(v, 3, device=gpu), [0] * v, True)
+    layout = raster.input_layout(dev[1], dev[3], True, True)
+    color, state = raster.forward_raw(dev[0], dev[1], True, 2, dev[2], dev[3], ci, v, H, W, layout)
+    assert state.seg_stride == raster.SEG_ENDS  # the depth-cut layout ran
+    dpix = torch.randn(v, 3, H, W, generator=torch.Generator().manual_seed(8)) * 1e-3
+    dm, dh, dop, dcov, _, _ = raster.backward_raw(dev[0], dev[1], True, 2, dev[2], dev[3], state.cams, [0] * v,
+                                                  state, dpix.to(gpu), want_mean2d=False, layout=layout)
+    torch.cuda.synchronize()
+    cams = state.cams.cpu().numpy()
+    means, shs, opac, cov6 = (t.numpy() for t in flat_inputs(sc))
+    col = color.cpu().numpy()
+    acc = {}
+    for i in range(v):
+        o = _oracle_view(means[0], shs[0], opac[0], cov6[0], cams, i, H, W)
+        oc, _, _ = o.image()
+        l1, mx, dp = _image_bars(col[i], oc, f"config D train view {i}")
+        _report(test="config_d_train_view", view=i, l1=l1, max_abs=mx, dpsnr=dp)
+        _accumulate(acc, o.backward(dpix[i].numpy(), f64=True), float(cams[i, 41]))
+        o.close()
+    tri = (torch.tensor([0, 0, 0, 1, 1, 2]), torch.tensor([0, 1, 2, 1, 2, 2]))
+    got = {"dmean3D": dm[0].cpu().numpy(), "dcov6": dcov[0][:, tri[0], tri[1]].cpu().numpy(),
+           "dsh": dh[0].transpose(-1, -2).cpu().numpy(), "dopacity": dop[0].cpu().numpy()}
+    _check_grads("config_d_train", 0, got, acc)
+
+
+def test_product_entry_lists_vs_reference_settings(gpu, monkeypatch):
+    """Config B through the benched entry (cameras built in float inside the binning kernel)
+    with the reference's 3-sigma binning, against the oracle fed the reference wrapper's own
+    camera settings (torch: get_fov, get_projection_matrix, inverse; cuda_splatting.py:62-111).
+    Counts, over every (view, tile), the list entries that are not the same Gaussian at the
+    same position; DESIGN.md §3 states the bound asserted here. Images: north_star bars."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setitem(raster._spec, "max_count", 2048)
+    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
+    H = W = 256
+    sc = scene_inputs(h=H, w=W, n_ctx=2, n_tgt=3, seed=1000)
+    g = sc.gaussians
+    gd = [t.to(gpu) for t in (g.means, g.covariances, g.harmonics, g.opacities)]
+    ci = raster.camera_inputs(sc.target_extrinsics[0].to(gpu), sc.target_intrinsics[0].to(gpu), sc.near[0].to(gpu),
+                              sc.far[0].to(gpu), torch.zeros(3, 3, device=gpu), [0] * 3, True)
+    prev = (raster.EXACT_BINNING, raster.DEBUG_KEEP_FAST_LISTS)
+    raster.EXACT_BINNING, raster.DEBUG_KEEP_FAST_LISTS = False, True
+    try:
+        with torch.no_grad():
+            color, state = raster.forward_raw(gd[0], gd[2], True, 2, gd[3], gd[1], ci, 3, H, W,
+                                              raster.input_layout(gd[2], gd[1], True, True), need_state=False)
+        torch.cuda.synchronize()
+    finally:
+        raster.EXACT_BINNING, raster.DEBUG_KEEP_FAST_LISTS = prev
+    T = (W // 16) * (H // 16)
+    begin, end, keys = _segments(state, 3, T)
+    col = color.cpu().numpy()
+    st = settings_for(sc)
+    n_total = n_set = n_order = n_tiles_diff = 0
+    for v, o in enumerate(oracle_views(sc, st)):
+        okeys, ovals, ranges = o.binning()
+        for t in range(T):
+            s = v * T + t
+            ids = (keys[begin[s]:end[s]] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+            ob, oe = ranges[t]
+            oids = ovals[ob:oe].astype(np.int64)
+            n_total += len(oids)
+            if np.array_equal(ids, oids):
+                continue
+            n_tiles_diff += 1
+            common = np.intersect1d(ids, oids)
+            n_set += len(ids) + len(oids) - 2 * len(common)  # in one list only
+            a_ = ids[np.isin(ids, common)]
+            pos = {g_: k for k, g_ in enumerate(oids[np.isin(oids, common)])}
+            n_order += len(a_) - _lis_len([pos[g_] for g_ in a_])  # entries out of the oracle's order
+        oc, _, _ = o.image()
+        l1, mx, dp = _image_bars(col[v], oc, f"product entry view {v}")
+        _report(test="product_entry_vs_reference_settings", view=v, l1=l1, max_abs=mx, dpsnr=dp)
+        o.close()
+    _report(test="product_entry_list_diff", entries=n_total, not_in_both=n_set, out_of_order=n_order,
+            tiles_differing=n_tiles_diff, tiles=3 * T)
+    # the in-kernel float cameras differ from the wrapper's torch matrices by a few
+    # ulps, which moves a Gaussian's 3-sigma rect across a tile edge or swaps two depths that
+    # differ by an ulp only rarely; the bound asserted is 1e-4 of the entries for each kind
+    assert n_set <= 1e-4 * n_total and n_order <= 1e-4 * n_total, (n_set, n_order, n_total, n_tiles_diff)
+
+
+def _lis_len(seq):
+    """Length of the longest strictly increasing subsequence (patience sorting)."""
+    import bisect
+    tails = []
+    for x in seq:
+        k = bisect.bisect_left(tails, x)
+        if k == len(tails):
+            tails.append(x)
+        else:
+            tails[k] = x
+    return len(tails)
