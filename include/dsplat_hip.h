@@ -90,8 +90,13 @@ int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, c
 int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,
-                       float* geom, int32_t* radii, uint32_t* seg_count, int layout,
-                       void* stream);
+                       float* geom, int32_t* radii, int64_t* dgeom_zero, uint32_t* seg_count,
+                       int layout, void* stream);
+/* dgeom_zero (every forward entry point that writes geom; optional, NULL = none): the
+ * backward's fixed-point gradient accumulator [V, G, DSR_DGEOM_WORDS] int64. The row of every
+ * rendered (view, gaussian) (radius > 0) is zeroed in the same pass that writes its geometry
+ * record, so a forward with a backward coming needs no separate fill of the accumulator
+ * (dsr_render_bwd / dsr_preprocess_bwd never touch the rows of culled gaussians). */
 
 /* Fused alternative to dsr_preprocess_fwd + dsr_bin_scan + dsr_bin_scatter (K1 + K3) for
  * problems whose fixed-capacity key buffer fits: the same projection, plus the keys of every
@@ -105,8 +110,8 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
 int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M,
                     const float* means, const float* shs, const float* colors,
                     const float* opacities, const float* cov6, const dsr_camera* cams,
-                    float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout,
-                    void* stream);
+                    float* geom, int32_t* radii, int64_t* dgeom_zero, uint32_t* seg_count, uint64_t* keys,
+                    int layout, void* stream);
 
 /* dsr_build_cameras + dsr_project_bin in one launch (the inference fast path): every
  * workgroup sets up its view's camera from the render_cuda inputs (as dsr_build_cameras, in
@@ -122,8 +127,8 @@ int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, in
                             const float* opacities, const float* cov6, const float* extrinsics,
                             const float* intrinsics, const float* near, const float* far,
                             const float* bg, const int32_t* view_scene, int scale_invariant,
-                            dsr_camera* cams, float* geom, int32_t* radii, uint32_t* seg_count,
-                            uint64_t* keys, int layout, void* stream);
+                            dsr_camera* cams, float* geom, int32_t* radii, int64_t* dgeom_zero,
+                            uint32_t* seg_count, uint64_t* keys, int layout, void* stream);
 
 /* Exclusive scan of seg_count[V*T] -> seg_start[V*T+1], seg_cursor[V*T] (= seg_start),
  * totals[0] = N (num_rendered over all views), totals[1] = max entries in one tile,
@@ -179,8 +184,8 @@ int dsr_cut_superblock(int H, int W);
 int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,
-                       float* geom, int32_t* radii, uint32_t* seg_count, uint32_t* depth_hist,
-                       uint32_t* cut_rec, int layout, void* stream);
+                       float* geom, int32_t* radii, int64_t* dgeom_zero, uint32_t* seg_count,
+                       uint32_t* depth_hist, uint32_t* cut_rec, int layout, void* stream);
 /* cut [V, nsb] uint32: per super-block, the largest depth (float bits) emitted: inside the
  * bucket where the count reaches `prefix` per tile, interpolated by the fraction still
  * needed (0xffffffff = all). */
@@ -275,17 +280,19 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
 int dsr_grad_scale(int V, int H, int W, const float* dL_dpix, float* grad_scale, void* stream);
 
 /* Back-to-front per tile (K7). dL_dpix [V,3,H,W]. Accumulates into dgeom_fx
- * [V,G,DSR_DGEOM_WORDS] int64 fixed point (caller zeroes): [0..1] dL/dxy (ndc scale, as
+ * [V,G,DSR_DGEOM_WORDS] int64 fixed point (rows of rendered gaussians zeroed beforehand: by
+ * the forward's dgeom_zero or by the caller): [0..1] dL/dxy (ndc scale, as
  * upstream dL_dmean2D), [2..4] dL/dconic, [5] dL/dopacity, [6..8] dL/drgb. */
 int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride,
                    const uint64_t* keys, const float* final_T, const uint32_t* n_contrib,
                    const float* dL_dpix, const float* grad_scale, int64_t* dgeom_fx, void* stream);
 
-/* dgeom_fx -> float dgeom [V,G,DSR_GEOM_STRIDE] (words 9..11 zero): the values the
- * preprocess backward consumes, for callers that want them (tests, diagnostics). */
-int dsr_dgeom_to_float(int G, int V, const int64_t* dgeom_fx, const float* grad_scale, float* dgeom,
-                       void* stream);
+/* dgeom_fx -> float dgeom [V,G,DSR_GEOM_STRIDE] (words 9..11 zero, rows of culled Gaussians
+ * zero): the values the preprocess backward consumes, for callers that want them (tests,
+ * diagnostics). */
+int dsr_dgeom_to_float(int G, int V, const float* geom, const int64_t* dgeom_fx, const float* grad_scale,
+                       float* dgeom, void* stream);
 
 /* Preprocess backward (K8 + K9), reduced over all views of each scene without atomics.
  * dgeom_fx / grad_scale: as written by dsr_render_bwd / dsr_grad_scale.

@@ -22,12 +22,13 @@ _P = c_void_p
 _I = c_int
 SIGNATURES: dict[str, tuple] = {
     "dsr_build_cameras": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _P, _P, c_uint32, _P]),
-    "dsr_preprocess_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "dsr_preprocess_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dsr_bin_scan": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
     "dsr_bin_scatter": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P]),
-    "dsr_project_bin": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "dsr_project_bin": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dsr_cut_superblock": (_I, [_I, _I]),
-    "dsr_preprocess_cut": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "dsr_preprocess_cut": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I,
+                                _P]),
     "dsr_bin_cutoff": (_I, [_I, _I, _I, _P, c_uint32, _P, _P]),
     "dsr_bin_scatter_cut": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
     "dsr_bin_sort": (_I, [_I, _I, _I, _I, _P, _P, c_uint32, _P, _P, c_uint32, _P, c_uint32, _P, _P, _P]),
@@ -37,10 +38,10 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_render_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dsr_sort_render": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _I, _I, c_uint32, _P, _P, _P, _P]),
     "dsr_project_bin_cameras": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P,
-                                     _P, _P, _P, _P, _I, _P]),
+                                     _P, _P, _P, _P, _P, _I, _P]),
     "dsr_grad_scale": (_I, [_I, _I, _I, _P, _P, _P]),
     "dsr_render_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P, _P, _P, _P]),
-    "dsr_dgeom_to_float": (_I, [_I, _I, _P, _P, _P, _P]),
+    "dsr_dgeom_to_float": (_I, [_I, _I, _P, _P, _P, _P, _P]),
     "dsr_preprocess_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                 _P, _P, _P, _P, _P, _P, _I, _P]),
     "dcv_cost_volume_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P, _P]),

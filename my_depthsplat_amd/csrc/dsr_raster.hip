@@ -580,13 +580,21 @@ __device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_c
   return r;
 }
 
+// dzero (optional): the backward's fixed-point gradient accumulator [V, G, DSR_DGEOM_WORDS];
+// the row of every rendered (view, Gaussian) is zeroed here, in the kernel that writes its
+// record anyway (no separate HBM fill pass; culled rows are never read by the backward).
 __device__ __forceinline__ void store_geom(float* __restrict__ geom, int32_t* __restrict__ radii, size_t vg,
-                                           const float* rec, int r) {
+                                           const float* rec, int r, long long* __restrict__ dzero) {
   float4* out = reinterpret_cast<float4*>(geom + vg * GS);
   out[0] = make_float4(rec[0], rec[1], rec[2], rec[3]);
   out[1] = make_float4(rec[4], rec[5], rec[6], rec[7]);
   out[2] = make_float4(rec[8], rec[9], rec[10], rec[11]);
   radii[vg] = r;
+  if (dzero != nullptr && r > 0) {
+    long long* z = dzero + vg * DSR_DGEOM_WORDS;
+#pragma unroll
+    for (int k = 0; k < DSR_DGEOM_WORDS; ++k) z[k] = 0ll;
+  }
 }
 
 // Exact tile test of the inference binning (k_project_emit EXACT): can the alpha >= 1/255 ellipse of a
@@ -671,6 +679,7 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
                                                    const float* __restrict__ cov6,
                                                    const dsr_camera* __restrict__ cams,
                                                    float* __restrict__ geom, int32_t* __restrict__ radii,
+                                                   long long* __restrict__ dzero,
                                                    uint32_t* __restrict__ seg_count, int lds_hist, int layout) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
   int v, blk;
@@ -690,7 +699,7 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
     load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
     float rec[GS];
     r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
-    store_geom(geom, radii, (size_t)v * G + g, rec, r);
+    store_geom(geom, radii, (size_t)v * G + g, rec, r, dzero);
     if constexpr (EXACT) {  // same terms as k_scatter<true> recomputes from the stored record
       ell = tile_ell(rec, r);
       if (r > 0) tile_rect_alpha(ell, x0, y0, x1, y1);
@@ -744,6 +753,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
                                                      const float* __restrict__ cov6,
                                                      dsr_camera* __restrict__ cams,
                                                      float* __restrict__ geom, int32_t* __restrict__ radii,
+                                                     long long* __restrict__ dzero,
                                                      uint32_t* __restrict__ seg_count,
                                                      uint64_t* __restrict__ keys, int layout, CamIn ci) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
@@ -778,7 +788,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
   if (g < G) {
     float rec[GS];
     r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
-    store_geom(geom, radii, (size_t)v * G + g, rec, r);
+    store_geom(geom, radii, (size_t)v * G + g, rec, r, dzero);
     key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
     if constexpr (EXACT) {
       ell = tile_ell(rec, r);
@@ -1081,6 +1091,7 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
                                                         const float* __restrict__ cov6,
                                                         const dsr_camera* __restrict__ cams,
                                                         float* __restrict__ geom, int32_t* __restrict__ radii,
+                                                        long long* __restrict__ dzero,
                                                         uint32_t* __restrict__ seg_count,
                                                         uint32_t* __restrict__ depth_hist,
                                                         uint2* __restrict__ cut_rec, int per_view, int layout) {
@@ -1113,7 +1124,7 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
       load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
       float rec[GS];
       r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
-      store_geom(geom, radii, (size_t)v * G + g, rec, r);
+      store_geom(geom, radii, (size_t)v * G + g, rec, r, dzero);
       zb = __float_as_uint(rec[9]);
     }
     if (r > 0) {
@@ -2649,6 +2660,13 @@ __device__ __forceinline__ bool grad_fx_exp(const float* __restrict__ bm, int la
 __device__ __forceinline__ long long to_fx(float a, float unit_inv) {
   return (long long)rintf(fminf(fmaxf(a * unit_inv, -4.0e18f), 4.0e18f));
 }
+// fixed point -> float: high word (signed) and low word (unsigned) converted by the hardware
+// and recombined with one FMA (within 1 ulp; the unit is a power of 2, so scaling is exact)
+__device__ __forceinline__ float fx_to_float(long long q, float unit) {
+  const int hi = (int)(q >> 32);
+  const unsigned lo = (unsigned)(q & 0xffffffffll);
+  return fmaf((float)hi, 4294967296.0f * unit, (float)lo * unit);
+}
 
 // one compacted backward list entry
 struct __align__(16) BwdRec {
@@ -2951,7 +2969,7 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     const long long* dq = dgeom + vg * DSR_DGEOM_WORDS;
     float dg[9];
 #pragma unroll
-    for (int c = 0; c < 9; ++c) dg[c] = (float)dq[c] * fx_unit;
+    for (int c = 0; c < 9; ++c) dg[c] = fx_to_float(dq[c], fx_unit);
     const dsr_camera* cam = cams + v;
     // scale-invariant rescale of this view: forward used m*s and cov*s^2
     const float gsc = cam->scale, gsc2 = gsc * gsc;
@@ -3150,14 +3168,17 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
 }
 
 // dgeom_fx -> float [rows, GS] (diagnostics / tests): the values k_preprocess_bwd consumes
-__global__ __launch_bounds__(NT) void k_dgeom_to_float(size_t rows, const long long* __restrict__ dq,
+// (rows of culled Gaussians: zero; their accumulator rows are never written or zeroed)
+__global__ __launch_bounds__(NT) void k_dgeom_to_float(size_t rows, const float* __restrict__ geom,
+                                                       const long long* __restrict__ dq,
                                                        const float* __restrict__ gscale, float* __restrict__ out) {
   int k = 0;
   const float unit = grad_fx_exp(gscale, threadIdx.x & 63, k) ? ldexpf(1.f, k - DSR_GRAD_FRAC_BITS) : __builtin_nanf("");
   const size_t r = (size_t)blockIdx.x * NT + threadIdx.x;
   if (r >= rows) return;
+  const bool vis = __float_as_int(geom[r * GS + 10]) > 0;
 #pragma unroll
-  for (int c = 0; c < GS; ++c) out[r * GS + c] = c < 9 ? (float)dq[r * DSR_DGEOM_WORDS + c] * unit : 0.f;
+  for (int c = 0; c < GS; ++c) out[r * GS + c] = (c < 9 && vis) ? fx_to_float(dq[r * DSR_DGEOM_WORDS + c], unit) : 0.f;
 }
 
 // pointers a segment layout needs (seg_bounds): ENDS both, fixed capacity the counts, prefix the starts
@@ -3178,7 +3199,8 @@ uint32_t dsr_sort_lds_capacity(void) { return kSortCap; }
 int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                        const float* shs, const float* colors, const float* opacities,
                        const float* cov6, const dsr_camera* cams, float* geom, int32_t* radii,
-                       uint32_t* seg_count, int layout, void* stream) {
+                       int64_t* dgeom_zero, uint32_t* seg_count, int layout, void* stream) {
+  long long* dzero = reinterpret_cast<long long*>(dgeom_zero);
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_preprocess_fwd: bad sizes S=%d G=%d V=%d H=%d W=%d", S, G, V, H, W);
   DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "dsr_preprocess_fwd: exactly one of shs/colors must be given");
   DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
@@ -3195,10 +3217,10 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   do {                                                                                                         \
     if (layout & kLayoutExactBinning)                                                                          \
       k_preprocess<D, true><<<grid, NT, lds, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, \
-                                                   cams, geom, radii, seg_count, lds > 0, layout);             \
+                                                   cams, geom, radii, dzero, seg_count, lds > 0, layout);      \
     else                                                                                                       \
       k_preprocess<D, false><<<grid, NT, lds, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, opacities,      \
-                                                    cov6, cams, geom, radii, seg_count, lds > 0, layout);      \
+                                                    cov6, cams, geom, radii, dzero, seg_count, lds > 0, layout); \
   } while (0)
   switch (deg) {
     case -1: DSR_PRE(-1); break;
@@ -3215,8 +3237,8 @@ int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
 namespace {
 int project_bin_impl(const char* who, int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                      const float* shs, const float* colors, const float* opacities, const float* cov6,
-                     dsr_camera* cams, const CamIn* ci, float* geom, int32_t* radii, uint32_t* seg_count,
-                     uint64_t* keys, int layout, void* stream) {
+                     dsr_camera* cams, const CamIn* ci, float* geom, int32_t* radii, long long* dzero,
+                     uint32_t* seg_count, uint64_t* keys, int layout, void* stream) {
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "%s: bad sizes S=%d G=%d V=%d H=%d W=%d", who, S, G, V, H, W);
   DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "%s: exactly one of shs/colors must be given", who);
   DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
@@ -3234,19 +3256,19 @@ int project_bin_impl(const char* who, int S, int G, int V, int H, int W, int sh_
   do {                                                                                                         \
     if (ci && !(layout & kLayoutRectBinning))                                                                  \
       k_project_emit<D, true, true><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,         \
-                                                             opacities, cov6, cams, geom, radii, seg_count,     \
+                                                             opacities, cov6, cams, geom, radii, dzero, seg_count,     \
                                                              keys, layout, *ci);                                \
     else if (ci)                                                                                               \
       k_project_emit<D, true, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,        \
-                                                              opacities, cov6, cams, geom, radii, seg_count,    \
+                                                              opacities, cov6, cams, geom, radii, dzero, seg_count,    \
                                                               keys, layout, *ci);                               \
     else if (layout & kLayoutExactBinning)                                                                     \
       k_project_emit<D, false, true><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,        \
-                                                              opacities, cov6, cams, geom, radii, seg_count,    \
+                                                              opacities, cov6, cams, geom, radii, dzero, seg_count,    \
                                                               keys, layout, CamIn{});                           \
     else                                                                                                       \
       k_project_emit<D, false, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,       \
-                                                               opacities, cov6, cams, geom, radii, seg_count,   \
+                                                               opacities, cov6, cams, geom, radii, dzero, seg_count,   \
                                                                keys, layout, CamIn{});                          \
   } while (0)
   switch (deg) {
@@ -3264,22 +3286,25 @@ extern "C" {
 
 int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means, const float* shs,
                     const float* colors, const float* opacities, const float* cov6, const dsr_camera* cams,
-                    float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout, void* stream) {
+                    float* geom, int32_t* radii, int64_t* dgeom_zero, uint32_t* seg_count, uint64_t* keys, int layout,
+                    void* stream) {
   return project_bin_impl("dsr_project_bin", S, G, V, H, W, sh_degree, M, means, shs, colors, opacities, cov6,
-                          const_cast<dsr_camera*>(cams), nullptr, geom, radii, seg_count, keys, layout, stream);
+                          const_cast<dsr_camera*>(cams), nullptr, geom, radii,
+                          reinterpret_cast<long long*>(dgeom_zero), seg_count, keys, layout, stream);
 }
 
 int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                             const float* shs, const float* colors, const float* opacities, const float* cov6,
                             const float* extrinsics, const float* intrinsics, const float* near, const float* far,
                             const float* bg, const int32_t* view_scene, int scale_invariant, dsr_camera* cams,
-                            float* geom, int32_t* radii, uint32_t* seg_count, uint64_t* keys, int layout,
-                            void* stream) {
+                            float* geom, int32_t* radii, int64_t* dgeom_zero, uint32_t* seg_count, uint64_t* keys,
+                            int layout, void* stream) {
   DSPLAT_REQUIRE(extrinsics && intrinsics && near && far && bg && view_scene,
                  "dsr_project_bin_cameras: null camera input");
   const CamIn ci{extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant};
   return project_bin_impl("dsr_project_bin_cameras", S, G, V, H, W, sh_degree, M, means, shs, colors, opacities,
-                          cov6, cams, &ci, geom, radii, seg_count, keys, layout, stream);
+                          cov6, cams, &ci, geom, radii, reinterpret_cast<long long*>(dgeom_zero), seg_count, keys,
+                          layout, stream);
 }
 
 int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_start, uint32_t* seg_cursor,
@@ -3312,8 +3337,9 @@ int dsr_cut_superblock(int H, int W) {
 
 int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                        const float* shs, const float* colors, const float* opacities, const float* cov6,
-                       const dsr_camera* cams, float* geom, int32_t* radii, uint32_t* seg_count,
-                       uint32_t* depth_hist, uint32_t* cut_rec, int layout, void* stream) {
+                       const dsr_camera* cams, float* geom, int32_t* radii, int64_t* dgeom_zero,
+                       uint32_t* seg_count, uint32_t* depth_hist, uint32_t* cut_rec, int layout, void* stream) {
+  long long* dzero = reinterpret_cast<long long*>(dgeom_zero);
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_preprocess_cut: bad sizes S=%d G=%d V=%d H=%d W=%d", S, G, V, H, W);
   DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "dsr_preprocess_cut: exactly one of shs/colors must be given");
   DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
@@ -3349,7 +3375,8 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, 
       attr = true;                                                                                           \
     }                                                                                                        \
     k_preprocess_cut<D, kNTH><<<xcd_grid(per_view, V), kNTH, lds, st>>>(                                     \
-        G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, geom, radii, seg_count, depth_hist, \
+        G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, geom, radii, dzero, seg_count,      \
+        depth_hist,                                                                                          \
         reinterpret_cast<uint2*>(cut_rec), per_view, layout);                                                \
   } while (0)
   switch (deg) {
@@ -3652,12 +3679,13 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
   return dsplat::check_launch("k_render_bwd");
 }
 
-int dsr_dgeom_to_float(int G, int V, const int64_t* dgeom_fx, const float* grad_scale, float* dgeom, void* stream) {
+int dsr_dgeom_to_float(int G, int V, const float* geom, const int64_t* dgeom_fx, const float* grad_scale, float* dgeom,
+                       void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0, "dsr_dgeom_to_float: bad sizes");
-  DSPLAT_REQUIRE(dgeom_fx && grad_scale && dgeom, "dsr_dgeom_to_float: null pointer");
+  DSPLAT_REQUIRE(geom && dgeom_fx && grad_scale && dgeom, "dsr_dgeom_to_float: null pointer");
   const size_t rows = (size_t)G * V;
   k_dgeom_to_float<<<(unsigned)((rows + NT - 1) / NT), NT, 0, (hipStream_t)stream>>>(
-      rows, reinterpret_cast<const long long*>(dgeom_fx), grad_scale, dgeom);
+      rows, geom, reinterpret_cast<const long long*>(dgeom_fx), grad_scale, dgeom);
   return dsplat::check_launch("k_dgeom_to_float");
 }
 

@@ -153,8 +153,8 @@ class RasterState:
     # inference fast path with exact binning: the lists hold only entries whose alpha >= 1/255
     # ellipse reaches the tile, and n_contrib counts positions in those shorter lists
     pruned_lists: bool = False
-    # (zeroed int64 gradient accumulator, event) prepared during the forward for the backward
-    dgeom: tuple | None = None
+    # the backward's int64 gradient accumulator, its rendered rows zeroed by the forward
+    dgeom: torch.Tensor | None = None
 
     @property
     def counts(self) -> torch.Tensor:
@@ -417,7 +417,7 @@ def input_layout(feats, cov6, use_sh, channel_major_sh):
 
 
 def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0, zeroed_counts=None,
-                need_state=True):
+                need_state=True, dgeom_zero: torch.Tensor | None = None):
     """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh; [S,G,3,M] with
     LAYOUT_SH_CHANNEL_MAJOR) or [S,G,3]; opacities [S,G]; cov6 [S,G,6] (or [S,G,3,3] with
     LAYOUT_COV_FULL); cams [V,44]. Returns (color [V,3,H,W], RasterState).
@@ -425,7 +425,9 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     Two binning layouts (include/dsplat_hip.h): when the fixed-capacity key buffer
     (V*T*G slots) fits KEY_BUDGET_BYTES, dsr_project_bin projects and emits keys in one
     kernel (no scan, no second pass over the geometry, no host sync); otherwise the
-    two-phase path counts, scans (one 8-byte read-back of N), scatters."""
+    two-phase path counts, scans (one 8-byte read-back of N), scatters.
+    dgeom_zero: the backward's [V, G, DGEOM_WORDS] int64 accumulator, whose rendered rows
+    the projection kernel zeroes as it writes their records (no separate fill pass)."""
     lib = _lib.load()
     cam_in = cams if isinstance(cams, CameraInputs) else None
     _lib.require_gpu(means, feats, opacities, cov6, None if cam_in is not None else cams)
@@ -476,15 +478,16 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                 ci.extrinsics.data_ptr(), ci.intrinsics.data_ptr(), ci.near.data_ptr(), ci.far.data_ptr(),
                 ci.bg.data_ptr(), ci.view_scene.data_ptr(), int(ci.scale_invariant), cams.data_ptr(),
-                geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout, st),
+                geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(), keys.data_ptr(), layout,
+                st),
                 "dsr_project_bin_cameras")
         else:
             if STATEFUL_EXACT_BINNING:
                 layout |= LAYOUT_EXACT_BINNING
             _lib.check(_timed("k_project_emit", lib.dsr_project_bin,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), keys.data_ptr(), layout,
-                st), "dsr_project_bin")
+                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(),
+                keys.data_ptr(), layout, st), "dsr_project_bin")
         seg_start, stride = None, G
         seg_sorted = None
         if not fused:
@@ -506,15 +509,15 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                 if -(-gx // sb) <= 255 and -(-gy // sb) <= 255 else None
             _lib.check(_timed("k_preprocess_cut", lib.dsr_preprocess_cut,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), hist.data_ptr(),
-                _ptr(cut_rec), layout, st), "dsr_preprocess_cut")
+                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(),
+                hist.data_ptr(), _ptr(cut_rec), layout, st), "dsr_preprocess_cut")
         else:
             if STATEFUL_EXACT_BINNING:  # the scatter below repeats the same test
                 layout |= LAYOUT_EXACT_BINNING
             _lib.check(_timed("k_preprocess", lib.dsr_preprocess_fwd,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), seg_count.data_ptr(), layout, st),
-                "dsr_preprocess_fwd")
+                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(), layout,
+                st), "dsr_preprocess_fwd")
         seg_start = torch.empty(V * T + 1, dtype=torch.int32, device=dev)
         cursor = torch.empty(V * T, dtype=torch.int32, device=dev)
         totals = torch.empty(4, dtype=torch.int32, device=dev)
@@ -629,27 +632,6 @@ DGEOM_WORDS = 9           # DSR_DGEOM_WORDS: int64 fixed-point gradient words pe
 GRAD_SCALE_BLOCKS = 512   # DSR_GRAD_SCALE_BLOCKS
 
 
-def zeroed_dgeom(V: int, G: int, dev) -> tuple[torch.Tensor, object]:
-    """The backward's fixed-point accumulator [V, G, DGEOM_WORDS] int64, zero-filled on a
-    side stream so that the fill (HBM-bound: 604 MB at config C's 64 views) runs under the
-    forward's VALU-bound kernels instead of in front of the backward. Returns (buffer,
-    event the consumer waits on). Inside a graph capture: filled on the current stream."""
-    if torch.cuda.is_current_stream_capturing():
-        return torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev), None
-    cur = torch.cuda.current_stream(dev)
-    side = _side_streams.get(str(dev))
-    if side is None:
-        side = _side_streams[str(dev)] = torch.cuda.Stream(device=dev)
-    side.wait_stream(cur)  # the memory block may have been freed by work still queued on cur
-    with torch.cuda.stream(side):
-        buf = torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev)
-        ev = torch.cuda.Event()
-        ev.record(side)
-    buf.record_stream(cur)  # consumed (and freed) in the current stream's order
-    return buf, ev
-
-
-_side_streams: dict = {}
 
 
 def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, state: RasterState,
@@ -665,11 +647,8 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     dev = means.device
     st = _lib.stream_of(dev)
     dcolor = dcolor.contiguous().float()
-    if state.dgeom is not None:  # zero-filled during the forward (zeroed_dgeom)
-        dgeom_fx, ev = state.dgeom
-        state.dgeom = None
-        if ev is not None:
-            torch.cuda.current_stream(dev).wait_event(ev)
+    if state.dgeom is not None:  # rendered rows zeroed by the forward's projection kernel
+        dgeom_fx, state.dgeom = state.dgeom, None
     else:
         dgeom_fx = torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev)
     gscale = torch.empty(GRAD_SCALE_BLOCKS, dtype=torch.float32, device=dev)
@@ -681,8 +660,8 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     dgeom = None
     if want_dgeom:
         dgeom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
-        _lib.check(lib.dsr_dgeom_to_float(G, V, dgeom_fx.data_ptr(), gscale.data_ptr(), dgeom.data_ptr(), st),
-                   "dsr_dgeom_to_float")
+        _lib.check(lib.dsr_dgeom_to_float(G, V, state.geom.data_ptr(), dgeom_fx.data_ptr(), gscale.data_ptr(),
+                                          dgeom.data_ptr(), st), "dsr_dgeom_to_float")
     # views of each scene, in view order (fixed summation order -> deterministic reduce)
     order = sorted(range(V), key=lambda v: (view_scene[v], v))
     starts = [0] * (S + 1)
@@ -712,9 +691,11 @@ class _RasterizeViews(torch.autograd.Function):
                 zeroed_counts):
         V = len(view_scene)
         need = any(ctx.needs_input_grad[:5])
-        dgeom = zeroed_dgeom(V, means.shape[1], means.device) if need else None  # fill overlaps the forward
+        # the backward's accumulator: its rendered rows are zeroed by the projection kernel
+        dgeom = torch.empty((V, means.shape[1], DGEOM_WORDS), dtype=torch.int64, device=means.device) \
+            if need else None
         color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout,
-                                   zeroed_counts, need_state=need)
+                                   zeroed_counts, need_state=need, dgeom_zero=dgeom)
         state.dgeom = dgeom
         ctx.save_for_backward(means, feats, opacities, cov6, state.cams)
         ctx.state = state
