@@ -297,7 +297,7 @@ def main():
         runner = step
     out = step()
     torch.cuda.synchronize()
-    n_rendered = raster.last_stats()["num_rendered"]  # one step (B scenes); also primes the sort hint
+    n_rendered = dec.raster_ctx.last_stats()["num_rendered"]  # one step (B scenes); also primes the sort hint
     # short eager pass timing every launch -> the dominant kernel (after a few untimed steps:
     # the first eager launches after the graph captures run cold and would decide the pick)
     for _ in range(3):
@@ -331,7 +331,7 @@ def main():
     # timed region 2: the same K steps in the same mode with the reference's 3-sigma tile
     # binning (DSR_LAYOUT_RECT_BINNING) instead of the exact alpha test — the throughput the
     # reference's lists give on the same kernels
-    raster.EXACT_BINNING = False
+    dec.raster_ctx.set(exact_binning=False)  # this decoder's context only
     runner_ref, graphs_ref = step, []
     elapsed_ref, n_rendered_ref = float("nan"), None
     try:
@@ -350,11 +350,11 @@ def main():
             elapsed_ref = timed(runner_ref, args.steps)
             step()
             torch.cuda.synchronize()
-            n_rendered_ref = raster.last_stats()["num_rendered"]
+            n_rendered_ref = dec.raster_ctx.last_stats()["num_rendered"]
         if graphs_ref:
             assert torch.equal(graphs_ref[0].out.color, color_lane0), "binning modes disagree"
     finally:
-        raster.EXACT_BINNING = True
+        dec.raster_ctx.set(exact_binning=True)
     del runner_ref, graphs_ref
     # timed region 3: the same K steps launched eagerly, with HIP events recorded around the
     # dominant kernel on its launch stream (its average duration feeds the roofline)
@@ -589,52 +589,105 @@ def recon12_leg(args, dev, rank, world, timed, max_over_ranks):
             "n_gpus": world, "reference": "0.6 s per scene end to end on an A100 incl. the encoder (README.md:105)"}
 
 
+def _costvol_case(tag, dev, rank):
+    """Inputs of one cost-volume shape. config A / config B scale 0: 2 views of a +-0.1
+    baseline, per-image inverse-depth candidates (mv_unimatch.py:416-435). config D (BASELINE
+    configs[3], scripts/dl3dv_depthsplat_train.sh:13-15,28-36: num_scales 2, upsample 4,
+    lowest resolution 8): B = 4 scenes x 6 views of the synthetic circle rig, each view against
+    its 2 nearest views (the nn_matrix of mv_transformer.py:653-747); scale 0 at 1/8
+    resolution (56x96, C = 128, D = 128 per image), scale 1 at 1/4 (112x192, C = 128 // 2 = 64,
+    D = 128 // 4 = 32 per-pixel candidates around an upsampled depth, mv_unimatch.py:436-461)."""
+    import torch
+
+    from my_depthsplat_amd.matching import depth_candidates
+    from my_depthsplat_amd.synthetic import context_cameras
+    g = torch.Generator(device=dev).manual_seed(5 + rank)
+    if tag in ("config_a_32x32", "config_b_scale0_64x64"):
+        BV, J, C, Hc, Wc, D = {"config_a_32x32": (2, 1, 128, 32, 32, 128),
+                               "config_b_scale0_64x64": (2, 1, 128, 64, 64, 128)}[tag]
+        K = torch.tensor([[Wc * 1.0, 0, Wc / 2], [0, Hc * 1.0, Hc / 2], [0, 0, 1]], device=dev).expand(BV, J, 3, 3)
+        pose = torch.eye(4, device=dev).repeat(BV, J, 1, 1)
+        pose[:, :, 0, 3] = 0.1
+        depth = (1.0 / torch.linspace(1 / 0.5, 1 / 100.0, D, device=dev)).expand(BV, D).contiguous()
+    else:
+        B, V, J = 4, 6, 2
+        scale1 = tag == "config_d_scale1_112x192"
+        C, Hc, Wc, D = (64, 112, 192, 32) if scale1 else (128, 56, 96, 128)
+        BV = B * V
+        c2w = context_cameras(V).to(dev)
+        centres = c2w[:, :3, 3]
+        dist = (centres[:, None] - centres[None]).norm(dim=-1) + torch.eye(V, device=dev) * 1e9
+        nn = dist.argsort(dim=1)[:, :J]                        # 2 nearest views of each view
+        rel = torch.linalg.inv(c2w[nn]) @ c2w[:, None]        # tgt_c2w^-1 ref_c2w (mv_unimatch.py:405-407)
+        pose = rel[None].expand(B, V, J, 4, 4).reshape(BV, J, 4, 4).contiguous()
+        K = torch.tensor([[Wc * 1.0, 0, Wc / 2], [0, Hc * 1.0, Hc / 2], [0, 0, 1]], device=dev).expand(BV, J, 3, 3)
+        inv_min = torch.full((BV,), 1 / 100.0, device=dev)
+        inv_max = torch.full((BV,), 1 / 0.5, device=dev)
+        if scale1:  # per-pixel window around the previous scale's (upsampled) inverse depth
+            prior = inv_min.view(-1, 1, 1, 1) + torch.rand(BV, 1, Hc, Wc, generator=g, device=dev) * 0.5
+            depth = 1.0 / depth_candidates(inv_min, inv_max, 128, 1, prior)
+        else:
+            depth = (1.0 / torch.linspace(1 / 0.5, 1 / 100.0, D, device=dev)).expand(BV, D)
+        depth = depth.contiguous()
+    ref = torch.randn(BV, C, Hc, Wc, generator=g, device=dev)
+    tgt = torch.randn(BV, J, C, Hc, Wc, generator=g, device=dev)
+    return ref, tgt, K.contiguous(), pose, depth, (BV, J, C, Hc, Wc, D)
+
+
 def costvol_leg(args, dev, rank, world, max_over_ranks):
     """Fused plane-sweep warp + correlation (matching.py:24-90 + mv_unimatch.py:494-505) at
-    BASELINE configs[0]'s shape (2 views, C = 128, D = 128, 32x32) and config B's scale 0
-    (2 views, C = 128, D = 128, 64x64): HIP time per call from HIP events on the launch stream,
-    FLOP rate against the FP32 matrix-core peak (the correlation runs on
-    v_mfma_f32_16x16x4_f32), algorithmic HBM bytes, and the same call on the host CPU through
-    the torch restatement (oracle/cost_volume.py, rank 0). FLOPs = 2 BV J C D H W."""
+    BASELINE configs[0]'s shape (2 views, C = 128, D = 128, 32x32), config B's scale 0
+    (2 views, C = 128, D = 128, 64x64) and config D's two scales (4 scenes x 6 views x 2
+    neighbours: 56x96 C = 128 D = 128 per image; 112x192 C = 64 D = 32 per pixel): HIP time
+    per call from HIP events on the launch stream, forward and forward + backward, FLOP rate
+    against the FP32 matrix-core peak (the correlations run on v_mfma_f32_16x16x4_f32),
+    algorithmic HBM bytes, and the configs A / B forward on the host CPU through the torch
+    restatement (oracle/cost_volume.py, rank 0). FLOPs = 2 BV J C D H W (forward; the
+    backward computes both feature gradients: 2x that)."""
     import torch
 
     from my_depthsplat_amd.matching import plane_sweep_cost_volume
 
     res = {}
-    for tag, (BV, J, C, Hc, Wc, D) in {"config_a_32x32": (2, 1, 128, 32, 32, 128),
-                                       "config_b_scale0_64x64": (2, 1, 128, 64, 64, 128)}.items():
-        g = torch.Generator(device=dev).manual_seed(5 + rank)
-        ref = torch.randn(BV, C, Hc, Wc, generator=g, device=dev)
-        tgt = torch.randn(BV, J, C, Hc, Wc, generator=g, device=dev)
-        K = torch.tensor([[Wc * 1.0, 0, Wc / 2], [0, Hc * 1.0, Hc / 2], [0, 0, 1]], device=dev).expand(BV, J, 3, 3)
-        pose = torch.eye(4, device=dev).repeat(BV, J, 1, 1)
-        pose[:, :, 0, 3] = 0.1
-        depth = (1.0 / torch.linspace(1 / 0.5, 1 / 100.0, D, device=dev)).expand(BV, D).contiguous()
-        K = K.contiguous()
+    for tag in ("config_a_32x32", "config_b_scale0_64x64", "config_d_scale0_56x96", "config_d_scale1_112x192"):
+        ref, tgt, K, pose, depth, (BV, J, C, Hc, Wc, D) = _costvol_case(tag, dev, rank)
 
         def call():
             return plane_sweep_cost_volume(ref, tgt, K, pose, depth)
 
-        for _ in range(3):
-            call()
-        n = 50
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(n):
-            call()
-        e1.record()
-        torch.cuda.synchronize()
-        (ms,) = max_over_ranks(e0.elapsed_time(e1) / n)
+        def timed_ms(fn, n):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(n):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / n
+
+        (ms,) = max_over_ranks(timed_ms(call, 50))
+        rg, tg_ = ref.clone().requires_grad_(True), tgt.clone().requires_grad_(True)
+        dcost = torch.randn(BV, D, Hc, Wc, generator=torch.Generator(device=dev).manual_seed(9), device=dev)
+
+        def fwd_bwd():
+            rg.grad = tg_.grad = None
+            (plane_sweep_cost_volume(rg, tg_, K, pose, depth) * dcost).sum().backward()
+
+        (ms_fb,) = max_over_ranks(timed_ms(fwd_bwd, 20))
         flops = 2.0 * BV * J * C * D * Hc * Wc
-        nbytes = 4.0 * (BV * C * Hc * Wc * (1 + J) + BV * D * Hc * Wc)
+        nbytes = 4.0 * (BV * C * Hc * Wc * (1 + J) + BV * D * Hc * Wc * (2 if depth.dim() == 4 else 1))
         tf = flops / (ms * 1e-3) / 1e12
-        ent = {"shape": {"BV": BV, "J": J, "C": C, "H": Hc, "W": Wc, "D": D}, "ms_per_call": round(ms, 5),
-               "tflops": round(tf, 3), "peak_tflops": FP32_MATRIX_PEAK_TFLOPS,
+        tf_fb = 3 * flops / (ms_fb * 1e-3) / 1e12
+        ent = {"shape": {"BV": BV, "J": J, "C": C, "H": Hc, "W": Wc, "D": D,
+                         "candidates": "per_pixel" if depth.dim() == 4 else "per_image"},
+               "ms_per_call": round(ms, 5), "tflops": round(tf, 3), "peak_tflops": FP32_MATRIX_PEAK_TFLOPS,
                "frac": round(tf / FP32_MATRIX_PEAK_TFLOPS, 4), "gbps": round(nbytes / (ms * 1e-3) / 1e9, 1),
                "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-               "mfma_busy": pmc_mfma(tag)}
-        if rank == 0 and not args.no_cpu_baseline:
+               "ms_fwd_bwd": round(ms_fb, 5), "tflops_fwd_bwd": round(tf_fb, 3),
+               "frac_fwd_bwd": round(tf_fb / FP32_MATRIX_PEAK_TFLOPS, 4), "mfma_busy": pmc_mfma(tag)}
+        if rank == 0 and not args.no_cpu_baseline and tag.startswith(("config_a", "config_b")):
             ent["cpu"] = costvol_cpu(ref, tgt, K, pose, depth)
         res[tag] = ent
     res["note"] = ("fp32 in / fp32 accumulate on the matrix cores (exact f32); FLOP rate vs the dense FP32-matrix "

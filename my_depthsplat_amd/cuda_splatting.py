@@ -86,11 +86,12 @@ def render_views(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch
                  image_shape: tuple[int, int], background_color: torch.Tensor, gaussian_means: torch.Tensor,
                  gaussian_covariances: torch.Tensor, gaussian_sh_coefficients: torch.Tensor,
                  gaussian_opacities: torch.Tensor, view_scene: list[int], scale_invariant: bool = True,
-                 use_sh: bool = True, return_radii: bool = False):
+                 use_sh: bool = True, return_radii: bool = False, ctx: "raster.RasterContext | None" = None):
     """Render V views of S scenes in one batch. extrinsics/intrinsics [V,4,4]/[V,3,3],
     near/far [V], background [V,3]; Gaussians per SCENE: means [S,G,3], covariances
     [S,G,3,3], harmonics [S,G,3,d_sh], opacities [S,G]; view_scene[v] in [0, S).
-    Equivalent to render_cuda on the per-view repeated Gaussians. -> [V,3,H,W]."""
+    Equivalent to render_cuda on the per-view repeated Gaussians. -> [V,3,H,W].
+    ctx: the caller's raster.RasterContext (a decoder passes its own)."""
     if not (use_sh or gaussian_sh_coefficients.shape[-1] == 1):
         raise ValueError("use_sh=False needs harmonics with d_sh == 1 (cuda_splatting.py:60)")
     V = extrinsics.shape[0]
@@ -100,7 +101,7 @@ def render_views(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch
     try:
         return _render_views(extrinsics, intrinsics, near, far, image_shape, background_color, gaussian_means,
                              gaussian_covariances, gaussian_sh_coefficients, gaussian_opacities, view_scene,
-                             scale_invariant, use_sh, return_radii, degree)
+                             scale_invariant, use_sh, return_radii, degree, ctx)
     except raster.EntryOverflow:
         if V == 1:
             raise
@@ -109,7 +110,7 @@ def render_views(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch
     parts = [render_views(extrinsics[sl], intrinsics[sl], near[sl], far[sl], image_shape, background_color[sl]
                           if background_color.dim() > 1 else background_color, gaussian_means, gaussian_covariances,
                           gaussian_sh_coefficients, gaussian_opacities, list(view_scene[sl]),
-                          scale_invariant=scale_invariant, use_sh=use_sh, return_radii=return_radii)
+                          scale_invariant=scale_invariant, use_sh=use_sh, return_radii=return_radii, ctx=ctx)
              for sl in (slice(0, k), slice(k, V))]
     if return_radii:
         return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
@@ -118,7 +119,7 @@ def render_views(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch
 
 def _render_views(extrinsics, intrinsics, near, far, image_shape, background_color, gaussian_means,
                   gaussian_covariances, gaussian_sh_coefficients, gaussian_opacities, view_scene, scale_invariant,
-                  use_sh, return_radii, degree):
+                  use_sh, return_radii, degree, ctx=None):
     V = extrinsics.shape[0]
     h, w = image_shape
     # the camera_settings() math runs on the device (no torch op chain, no host sync): in one
@@ -132,7 +133,7 @@ def _render_views(extrinsics, intrinsics, near, far, image_shape, background_col
     feats = gaussian_sh_coefficients if use_sh else gaussian_sh_coefficients[..., 0]
     color, radii = raster.rasterize_views(
         gaussian_means, feats, gaussian_opacities, gaussian_covariances, cams, view_scene,
-        use_sh=use_sh, sh_degree=degree, image_height=h, image_width=w, channel_major_sh=True)
+        use_sh=use_sh, sh_degree=degree, image_height=h, image_width=w, channel_major_sh=True, ctx=ctx)
     return (color, radii) if return_radii else color
 
 
@@ -140,12 +141,13 @@ def render_cuda(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch.
                 image_shape: tuple[int, int], background_color: torch.Tensor, gaussian_means: torch.Tensor,
                 gaussian_covariances: torch.Tensor, gaussian_sh_coefficients: torch.Tensor,
                 gaussian_opacities: torch.Tensor, scale_invariant: bool = True,
-                use_sh: bool = True) -> torch.Tensor:
-    """cuda_splatting.py:46-126: view i renders Gaussian set i. -> [b,3,H,W]."""
+                use_sh: bool = True, ctx: "raster.RasterContext | None" = None) -> torch.Tensor:
+    """cuda_splatting.py:46-126: view i renders Gaussian set i. -> [b,3,H,W].
+    (ctx, optional and last: the caller's raster.RasterContext.)"""
     b = extrinsics.shape[0]
     return render_views(extrinsics, intrinsics, near, far, image_shape, background_color, gaussian_means,
                         gaussian_covariances, gaussian_sh_coefficients, gaussian_opacities, list(range(b)),
-                        scale_invariant=scale_invariant, use_sh=use_sh)
+                        scale_invariant=scale_invariant, use_sh=use_sh, ctx=ctx)
 
 
 def orthographic_settings(extrinsics: torch.Tensor, width: torch.Tensor, height: torch.Tensor, near: torch.Tensor,
@@ -213,12 +215,13 @@ def depth_colors(extrinsics: torch.Tensor, gaussian_means: torch.Tensor, near: t
 def render_depth_cuda(extrinsics: torch.Tensor, intrinsics: torch.Tensor, near: torch.Tensor, far: torch.Tensor,
                       image_shape: tuple[int, int], gaussian_means: torch.Tensor,
                       gaussian_covariances: torch.Tensor, gaussian_opacities: torch.Tensor,
-                      scale_invariant: bool = True, mode: DepthRenderingMode = "depth") -> torch.Tensor:
+                      scale_invariant: bool = True, mode: DepthRenderingMode = "depth",
+                      ctx: "raster.RasterContext | None" = None) -> torch.Tensor:
     """Depth / disparity / log-depth as colour (cuda_splatting.py:225-264). -> [b,H,W]."""
     fake = depth_colors(extrinsics, gaussian_means, near, far, mode)
     b = fake.shape[0]
     out = render_cuda(extrinsics, intrinsics, near, far, image_shape,
                       torch.zeros((b, 3), dtype=fake.dtype, device=fake.device), gaussian_means,
                       gaussian_covariances, fake[..., None, None].expand(-1, -1, 3, 1), gaussian_opacities,
-                      scale_invariant=scale_invariant, use_sh=False)
+                      scale_invariant=scale_invariant, use_sh=False, ctx=ctx)
     return out.mean(dim=1)

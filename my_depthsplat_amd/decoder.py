@@ -16,6 +16,7 @@ from typing import Generic, Literal, TypeVar
 import torch
 from torch import nn
 
+from . import raster
 from .cuda_splatting import DepthRenderingMode, render_depth_cuda, render_views
 
 
@@ -65,12 +66,15 @@ def _background(dataset_cfg) -> list[float]:
 
 
 class DecoderSplattingCUDA(Decoder[DecoderSplattingCUDACfg]):
-    """decoder_splatting_cuda.py:19-91 on libdsplat_hip.so."""
+    """decoder_splatting_cuda.py:19-91 on libdsplat_hip.so. Each decoder owns its rasterizer
+    context (`raster_ctx`: binning options and the hints its own calls learn), so decoders of
+    different workloads never steer each other's kernels."""
 
-    def __init__(self, cfg: DecoderSplattingCUDACfg, dataset_cfg) -> None:
+    def __init__(self, cfg: DecoderSplattingCUDACfg, dataset_cfg, **raster_options) -> None:
         super().__init__(cfg, dataset_cfg)
         self.register_buffer("background_color", torch.tensor(_background(dataset_cfg), dtype=torch.float32),
                              persistent=False)
+        self.raster_ctx = raster.RasterContext(**raster_options)
 
     def forward(self, gaussians: Gaussians, extrinsics: torch.Tensor, intrinsics: torch.Tensor,
                 near: torch.Tensor, far: torch.Tensor, image_shape: tuple[int, int],
@@ -81,7 +85,7 @@ class DecoderSplattingCUDA(Decoder[DecoderSplattingCUDACfg]):
             extrinsics.reshape(b * v, 4, 4), intrinsics.reshape(b * v, 3, 3), near.reshape(b * v),
             far.reshape(b * v), image_shape, self.background_color.expand(b * v, 3), gaussians.means,
             gaussians.covariances, gaussians.harmonics, gaussians.opacities,
-            view_scene=[i // v for i in range(b * v)])
+            view_scene=[i // v for i in range(b * v)], ctx=self.raster_ctx)
         color = color.reshape(b, v, 3, h, w)
         depth = None if depth_mode is None else self.render_depth(
             gaussians, extrinsics, intrinsics, near, far, image_shape, depth_mode)
@@ -96,7 +100,7 @@ class DecoderSplattingCUDA(Decoder[DecoderSplattingCUDACfg]):
         rep = lambda t: t[:, None].expand(b, v, *t.shape[1:]).reshape(b * v, *t.shape[1:])  # noqa: E731
         out = render_depth_cuda(extrinsics.reshape(b * v, 4, 4), intrinsics.reshape(b * v, 3, 3),
                                 near.reshape(b * v), far.reshape(b * v), image_shape, rep(gaussians.means),
-                                rep(gaussians.covariances), rep(gaussians.opacities), mode=mode)
+                                rep(gaussians.covariances), rep(gaussians.opacities), mode=mode, ctx=self.raster_ctx)
         return out.reshape(b, v, *image_shape)
 
 

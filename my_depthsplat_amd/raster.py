@@ -79,8 +79,9 @@ class KernelTimer:
         return {k: (len(v), sum(a.elapsed_time(b) for a, b in v) / len(v)) for k, v in self.events.items()}
 
 
+# bench / profiling instrumentation only (HIP events around named launches); never set on
+# the product path
 _timer: KernelTimer | None = None
-_last: dict = {"counts": None}
 
 
 def set_timer(t: KernelTimer | None) -> None:
@@ -88,18 +89,10 @@ def set_timer(t: KernelTimer | None) -> None:
     _timer = t
 
 
-def last_stats() -> dict:
-    """(num_rendered, max tile count) of the last forward (reads the device: syncs)."""
-    c = _last["counts"]
-    if c is None:  # consumed on the device (inference fast path): the newest pinned copy
-        hc = _last.get("host_counts")
-        if hc is None:
-            return {"num_rendered": 0, "max_count": 0}
-        hc[1].synchronize()
-        c = hc[0]
-    n, m = int(c.sum()), int(c.max())
-    _spec["max_count"] = m
-    return {"num_rendered": n, "max_count": m}
+def last_stats(ctx: "RasterContext | None" = None) -> dict:
+    """(num_rendered, max tile count) of the last forward through `ctx` (default: the current
+    device's default context). Reads the device: syncs."""
+    return (ctx or default_context(torch.cuda.current_device())).last_stats()
 
 
 def _timed(name, fn, *args):
@@ -183,22 +176,17 @@ class RasterState:
 # views: cheap on a 288 GB part, and untouched pages cost no bandwidth); the whole forward
 # then runs with NO host sync and the projection emits keys directly (no scan / scatter).
 # Larger problems fall back to one 8-byte read of (N, max tile count) after the scan.
-# None = automatic: 48 GiB, at most 40 % of the device's memory (env DSPLAT_KEY_BUDGET_GB
-# overrides; tests set 0 to force the two-phase layout).
+# None = automatic per RasterContext: 48 GiB, at most 40 % of the device's memory and half of
+# what is free when the context first asks (env DSPLAT_KEY_BUDGET_GB overrides; tests set 0 to
+# force the two-phase layout).
+#
+# The upper-case settings below are the DEFAULTS of every RasterContext option of the same
+# name (read at call time where a context leaves the option unset); the product path never
+# assigns them: a decoder changes its own context (RasterContext.set).
 _kb_env = os.environ.get("DSPLAT_KEY_BUDGET_GB")
 KEY_BUDGET_BYTES = None if _kb_env is None else int(float(_kb_env) * (1 << 30))
-_auto_budget: dict = {}
 
 
-def key_budget(device) -> int:
-    if KEY_BUDGET_BYTES is not None:
-        return KEY_BUDGET_BYTES
-    idx = torch.device(device).index or 0
-    b = _auto_budget.get(idx)
-    if b is None:
-        total = torch.cuda.get_device_properties(idx).total_memory
-        b = _auto_budget[idx] = int(min(48 * (1 << 30), 0.4 * total))
-    return b
 # Segments larger than this many entries (only when some exceed the LDS sort) get only their
 # nearest SORT_PREFIX entries put in order (dsr_bin_sort prefix mode): at 6x448x768 the
 # compositor uses at most ~1.2K of 30-40K entries per tile. 0 sorts everything.
@@ -213,7 +201,8 @@ CUT_SORT_HINT = 4096  # LDS sort size for the written parts (larger ones sort th
 # dsr_render_fwd (MSD split, prefix sort). Either is exact for any list length.
 FUSED_SORT_RENDER = os.environ.get("DSPLAT_FUSED_SORT_RENDER", "1") != "0"
 FUSED_MAX = 4096
-# dsr_sort_render's LDS class comes from the largest count of earlier calls (_spec); a nonzero
+# dsr_sort_render's LDS class comes from the largest count of earlier calls (the context's
+# hints); a nonzero
 # override pins it (tests: every class on the same lists)
 SORT_RENDER_HINT = 0
 # inference fast path (cameras inside the binning kernel, self-zeroing counters); env
@@ -237,36 +226,156 @@ LAYOUT_EXACT_BINNING = 16
 # copy and the key stores; the product never sets it.
 DEBUG_KEEP_FAST_LISTS = False
 SEG_ENDS = 0xFFFFFFFF  # DSR_SEG_ENDS
-_spec = {"max_count": 0}
-_inflight: list = []  # (pinned int32 counts, event) read-backs, consumed without blocking
 
 
-def _note_counts(counts: torch.Tensor) -> None:
-    """Queue a non-blocking copy of the per-segment counts to pinned memory; completed
-    copies from earlier calls update the LDS-sort size hint (their max). Never waits on the
-    device, never adds a kernel (a device-side max would need same-address atomics from
-    every workgroup, which serialise)."""
-    if torch.cuda.is_current_stream_capturing():
-        return  # inside a hipGraph capture: no host-side bookkeeping (hint stays fixed)
-    while _inflight and _inflight[0][1].query():
-        host, _ = _inflight.pop(0)
-        _spec["max_count"] = int(host.max())
-    if len(_inflight) < 4:
-        host = torch.empty(counts.shape, dtype=torch.int32, pin_memory=True)
-        host.copy_(counts, non_blocking=True)
+class RasterContext:
+    """Per-(device, caller) rasterizer state: the options of one decoder and the adaptive
+    hints its earlier calls produced. SURVEY §8(b): nothing that one caller's calls learn or
+    set leaks into another's (two decoders of different workloads, on different streams or
+    devices, each keep their own LDS sort class, depth-cut plan, zeroed-counter pool and
+    binning options; a hipGraph captured through a context keeps the hint it had then).
+
+    Options (None: the module default of the same upper-case name, read at call time):
+      exact_binning (inference path), stateful_exact_binning (training path),
+      fused_sort_render, sort_render_hint, inkernel_cameras, sort_prefix, cut_prefix,
+      debug_keep_fast_lists, key_budget_bytes (None and no module override: automatic,
+      min(48 GiB, 40 % of the device, half of its memory free when first asked)).
+    hints: max_count (largest tile list seen: picks the fused sort's LDS class),
+      two_phase_max (largest list of the last two-phase call: plans the depth cut).
+    adapt_hints False freezes the hints (tests pin a class)."""
+
+    _OPTS = {"exact_binning": "EXACT_BINNING", "stateful_exact_binning": "STATEFUL_EXACT_BINNING",
+             "fused_sort_render": "FUSED_SORT_RENDER", "sort_render_hint": "SORT_RENDER_HINT",
+             "inkernel_cameras": "INKERNEL_CAMERAS", "sort_prefix": "SORT_PREFIX", "cut_prefix": "CUT_PREFIX",
+             "debug_keep_fast_lists": "DEBUG_KEEP_FAST_LISTS", "key_budget_bytes": "KEY_BUDGET_BYTES"}
+
+    def __init__(self, **options):
+        unknown = set(options) - set(self._OPTS)
+        if unknown:
+            raise TypeError(f"unknown rasterizer options {sorted(unknown)}")
+        self.options = dict(options)
+        self.hints = {"max_count": 0, "two_phase_max": None}
+        self.adapt_hints = True
+        self._inflight: list = []      # (pinned int32 counts, event) read-backs, consumed without blocking
+        self._last: dict = {"counts": None, "host_counts": None}
+        self._auto_budget: dict = {}   # device index -> bytes
+        self._clean_counts: dict = {}  # (device, n) -> (zeroed counters, last stream, event)
+        self._graph_owned: list = []
+
+    def opt(self, name: str):
+        v = self.options.get(name)
+        return globals()[self._OPTS[name]] if v is None else v
+
+    def set(self, **options) -> "RasterContext":
+        unknown = set(options) - set(self._OPTS)
+        if unknown:
+            raise TypeError(f"unknown rasterizer options {sorted(unknown)}")
+        self.options.update(options)
+        return self
+
+    def key_budget(self, device) -> int:
+        b = self.opt("key_budget_bytes")
+        if b is not None:
+            return int(b)
+        idx = torch.device(device).index or 0
+        b = self._auto_budget.get(idx)
+        if b is None:
+            total = torch.cuda.get_device_properties(idx).total_memory
+            free, _ = torch.cuda.mem_get_info(idx)
+            b = self._auto_budget[idx] = int(min(48 * (1 << 30), 0.4 * total, 0.5 * free))
+        return b
+
+    def note_counts(self, counts: torch.Tensor) -> None:
+        """Queue a non-blocking copy of the per-segment counts to pinned memory; completed
+        copies from earlier calls update the LDS-sort size hint (their max). Never waits on
+        the device, never adds a kernel (a device-side max would need same-address atomics
+        from every workgroup, which serialise)."""
+        if torch.cuda.is_current_stream_capturing():
+            return  # inside a hipGraph capture: no host-side bookkeeping (hint stays fixed)
+        while self._inflight and self._inflight[0][1].query():
+            host, _ = self._inflight.pop(0)
+            if self.adapt_hints:
+                self.hints["max_count"] = int(host.max())
+        if len(self._inflight) < 4:
+            host = torch.empty(counts.shape, dtype=torch.int32, pin_memory=True)
+            host.copy_(counts, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._inflight.append((host, ev))
+            self._last["host_counts"] = (host, ev)
+
+    def last_stats(self) -> dict:
+        """(num_rendered, max tile count) of this context's last forward (syncs)."""
+        c = self._last["counts"]
+        if c is None:  # consumed on the device (inference fast path): the newest pinned copy
+            hc = self._last.get("host_counts")
+            if hc is None:
+                return {"num_rendered": 0, "max_count": 0}
+            hc[1].synchronize()
+            c = hc[0]
+        n, m = int(c.sum()), int(c.max())
+        if self.adapt_hints:
+            self.hints["max_count"] = m
+        return {"num_rendered": n, "max_count": m}
+
+    # Counter buffers that are zero once the work of their last user is done:
+    # dsr_sort_render(clear_counts=1) zeroes each counter as it consumes it, so the next
+    # inference forward needs no zeroing launch (dsr_project_bin_cameras takes them as
+    # zeroed). A buffer is reused on the stream that last used it (stream order), or on another
+    # stream once an event recorded after its last use has completed. A buffer taken while a
+    # stream is captured into a graph belongs to that graph from then on (each replay leaves
+    # it zeroed again).
+    def take_clean_counts(self, n: int, dev, stream) -> torch.Tensor | None:
+        key = (str(dev), n)
+        ent = self._clean_counts.get(key)
+        capturing = torch.cuda.is_current_stream_capturing()
+        if ent is not None:
+            t, last_stream, ev = ent
+            # (events cannot be queried during capture: graphs.GraphedCall synchronizes the device
+            # before capturing, so the buffer's last user has finished by then)
+            if capturing or last_stream == int(stream) or ev.query():
+                del self._clean_counts[key]
+                return t
+        if capturing:
+            return None  # a zeroing node inside the graph would cost what the fast path saves
+        return torch.zeros(n, dtype=torch.int32, device=dev)
+
+    def give_back_clean_counts(self, t: torch.Tensor, dev, stream) -> None:
+        if torch.cuda.is_current_stream_capturing():
+            self._graph_owned.append(t)  # the captured graph keeps using (and re-zeroing) it
+            return
         ev = torch.cuda.Event()
         ev.record()
-        _inflight.append((host, ev))
-        _last["host_counts"] = (host, ev)
+        if len(self._clean_counts) > 64:
+            self._clean_counts.clear()
+        self._clean_counts[(str(dev), t.numel())] = (t, int(stream), ev)
+
+
+_default_contexts: dict = {}
+
+
+def default_context(device=None) -> RasterContext:
+    """The context of callers that bring none (the functional API: render_cuda & co.), one
+    per device."""
+    idx = torch.device(device).index if device is not None else torch.cuda.current_device()
+    idx = idx or 0
+    ctx = _default_contexts.get(idx)
+    if ctx is None:
+        ctx = _default_contexts[idx] = RasterContext()
+    return ctx
+
+
+def key_budget(device, ctx: RasterContext | None = None) -> int:
+    return (ctx or default_context(device)).key_budget(device)
 
 
 _ws_cache: dict = {}
 
 
-def workspace(G: int, H: int, W: int, V: int, device=None) -> _lib.Workspace:
+def workspace(G: int, H: int, W: int, V: int, device=None, ctx: RasterContext | None = None) -> _lib.Workspace:
     """dsr_workspace_size: the bytes of every buffer of one call sequence and whether the
     sync-free fixed-capacity layout fits the key budget (the C ABI's own sizing rule)."""
-    budget = key_budget(device if device is not None else torch.cuda.current_device())
+    budget = key_budget(device if device is not None else torch.cuda.current_device(), ctx)
     key = (G, H, W, V, budget)
     ws = _ws_cache.get(key)
     if ws is None:
@@ -346,43 +455,6 @@ def camera_inputs(extrinsics, intrinsics, near, far, bg, view_scene, scale_invar
     return CameraInputs(f(extrinsics), f(intrinsics), f(near), f(far), _dense_bg(bg), vs, bool(scale_invariant))
 
 
-# Per-(device, size) counter buffers that are zero once the work of their last user is done:
-# dsr_sort_render(clear_counts=1) zeroes each counter as it consumes it, so the next inference
-# forward needs no zeroing launch (dsr_project_bin_cameras takes them as zeroed). A buffer is
-# reused on the stream that last used it (stream order), or on another stream once an event
-# recorded after its last use has completed. A buffer taken while a stream is captured into
-# a graph belongs to that graph from then on (each replay leaves it zeroed again).
-_clean_counts: dict = {}
-_graph_owned: list = []
-
-
-def _take_clean_counts(n: int, dev, stream) -> torch.Tensor | None:
-    key = (str(dev), n)
-    ent = _clean_counts.get(key)
-    capturing = torch.cuda.is_current_stream_capturing()
-    if ent is not None:
-        t, last_stream, ev = ent
-        # (events cannot be queried during capture: graphs.GraphedCall synchronizes the device
-        # before capturing, so the buffer's last user has finished by then)
-        if capturing or last_stream == int(stream) or ev.query():
-            del _clean_counts[key]
-            return t
-    if capturing:
-        return None  # a zeroing node inside the graph would cost what the fast path saves
-    return torch.zeros(n, dtype=torch.int32, device=dev)
-
-
-def _give_back_clean_counts(t: torch.Tensor, dev, stream) -> None:
-    if torch.cuda.is_current_stream_capturing():
-        _graph_owned.append(t)  # the captured graph keeps using (and re-zeroing) it
-        return
-    ev = torch.cuda.Event()
-    ev.record()
-    if len(_clean_counts) > 64:
-        _clean_counts.clear()
-    _clean_counts[(str(dev), t.numel())] = (t, int(stream), ev)
-
-
 def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True,
                   zero_counts: torch.Tensor | None = None) -> torch.Tensor:
     """Device-side camera set-up (dsr_build_cameras) -> [V, 44] float32 dsr_camera array.
@@ -417,7 +489,7 @@ def input_layout(feats, cov6, use_sh, channel_major_sh):
 
 
 def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0, zeroed_counts=None,
-                need_state=True, dgeom_zero: torch.Tensor | None = None):
+                need_state=True, dgeom_zero: torch.Tensor | None = None, ctx: RasterContext | None = None):
     """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh; [S,G,3,M] with
     LAYOUT_SH_CHANNEL_MAJOR) or [S,G,3]; opacities [S,G]; cov6 [S,G,6] (or [S,G,3,3] with
     LAYOUT_COV_FULL); cams [V,44]. Returns (color [V,3,H,W], RasterState).
@@ -427,13 +499,16 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     kernel (no scan, no second pass over the geometry, no host sync); otherwise the
     two-phase path counts, scans (one 8-byte read-back of N), scatters.
     dgeom_zero: the backward's [V, G, DGEOM_WORDS] int64 accumulator, whose rendered rows
-    the projection kernel zeroes as it writes their records (no separate fill pass)."""
+    the projection kernel zeroes as it writes their records (no separate fill pass).
+    ctx: the caller's RasterContext (options + adaptive hints; default: the device's)."""
     lib = _lib.load()
     cam_in = cams if isinstance(cams, CameraInputs) else None
     _lib.require_gpu(means, feats, opacities, cov6, None if cam_in is not None else cams)
     S, G = means.shape[0], means.shape[1]
     M = (feats.shape[3] if layout & LAYOUT_SH_CHANNEL_MAJOR else feats.shape[2]) if use_sh else 0
     dev = means.device
+    ctx = ctx or default_context(dev)
+    spec = ctx.hints
     gx, gy = tiles(H, W)
     T = gx * gy
     st = _lib.stream_of(dev)
@@ -443,18 +518,18 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
     radii = torch.empty((V, G), dtype=torch.int32, device=dev)
     lds_cap = lib.dsr_sort_lds_capacity()
-    fixed = bool(workspace(G, H, W, V, dev).fixed_capacity)
-    maxc_hint = _spec["max_count"] or lds_cap
-    fused = fixed and FUSED_SORT_RENDER and maxc_hint <= FUSED_MAX
+    fixed = bool(workspace(G, H, W, V, dev, ctx).fixed_capacity)
+    maxc_hint = spec["max_count"] or lds_cap
+    fused = fixed and ctx.opt("fused_sort_render") and maxc_hint <= FUSED_MAX
     # eager inference fast path: cameras set up inside the binning kernel, counters taken zeroed
     # from the previous call's sort + composite (two launches per forward)
-    fast = fused and INKERNEL_CAMERAS and cam_in is not None and not need_state and zeroed_counts is None
-    clean = _take_clean_counts(V * T, dev, st) if fast else None
+    fast = fused and ctx.opt("inkernel_cameras") and cam_in is not None and not need_state and zeroed_counts is None
+    clean = ctx.take_clean_counts(V * T, dev, st) if fast else None
     fast = clean is not None
     if fast:
         seg_count = clean
         layout |= LAYOUT_COUNTS_ZEROED
-        if not EXACT_BINNING:
+        if not ctx.opt("exact_binning"):
             layout |= LAYOUT_RECT_BINNING
         cams = torch.empty((V, CAM_FLOATS), dtype=torch.float32, device=dev)
     elif zeroed_counts is not None:  # zeroed by dsr_build_cameras (one launch fewer)
@@ -482,7 +557,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                 st),
                 "dsr_project_bin_cameras")
         else:
-            if STATEFUL_EXACT_BINNING:
+            if ctx.opt("stateful_exact_binning"):
                 layout |= LAYOUT_EXACT_BINNING
             _lib.check(_timed("k_project_emit", lib.dsr_project_bin,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
@@ -493,13 +568,14 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         if not fused:
             ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
             seg_sorted = _prefix_sort(lib, G, V, H, W, None, seg_count, stride, keys, scratch, maxc_hint, ws, st,
-                                      lds_cap)
-        _note_counts(seg_count)
+                                      lds_cap, ctx.opt("sort_prefix"))
+        ctx.note_counts(seg_count)
     else:
         # the depth cut pays when tile lists are long; the previous two-phase call's largest
         # list (None on the first call) decides whether this one builds the depth histogram
-        prev = _spec.get("two_phase_max")
-        want_cut = CUT_PREFIX > 0 and (prev is None or prev > 4 * CUT_PREFIX)
+        cut_prefix = ctx.opt("cut_prefix")
+        prev = spec.get("two_phase_max")
+        want_cut = cut_prefix > 0 and (prev is None or prev > 4 * cut_prefix)
         sb = lib.dsr_cut_superblock(H, W) if want_cut else 0
         if sb > 0:
             nsb = -(-gx // sb) * -(-gy // sb)
@@ -512,7 +588,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                 cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(),
                 hist.data_ptr(), _ptr(cut_rec), layout, st), "dsr_preprocess_cut")
         else:
-            if STATEFUL_EXACT_BINNING:  # the scatter below repeats the same test
+            if ctx.opt("stateful_exact_binning"):  # the scatter below repeats the same test
                 layout |= LAYOUT_EXACT_BINNING
             _lib.check(_timed("k_preprocess", lib.dsr_preprocess_fwd,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
@@ -528,18 +604,19 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                    "host read-back and cannot be captured into a graph")
         tot = totals[:3].cpu()  # one small read-back: N sizes the key buffer
         N, maxc = int(tot[0]), int(tot[1])
-        _spec["two_phase_max"] = maxc
+        if ctx.adapt_hints:
+            spec["two_phase_max"] = maxc
         if int(tot[2]):
             raise EntryOverflow(f"{V} views x {G} Gaussians produce >= 2^31 (view, tile, Gaussian) entries: "
                                 "render fewer views per call")
         keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
-        if sb > 0 and maxc <= 2 * CUT_PREFIX:  # short lists after all: write everything
+        if sb > 0 and maxc <= 2 * cut_prefix:  # short lists after all: write everything
             sb = 0
         if sb > 0:
             # depth cut: write only each tile's nearest entries (cursor ends at their end)
             scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev)  # only big segments touch it
             cut = torch.empty(V * nsb, dtype=torch.int32, device=dev)
-            _lib.check(_timed("k_bin_cutoff", lib.dsr_bin_cutoff, V, H, W, hist.data_ptr(), CUT_PREFIX,
+            _lib.check(_timed("k_bin_cutoff", lib.dsr_bin_cutoff, V, H, W, hist.data_ptr(), cut_prefix,
                               cut.data_ptr(), st), "dsr_bin_cutoff")
             _lib.check(_timed("k_scatter", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
                               keys.data_ptr(), cut.data_ptr(), 0, None, _ptr(cut_rec), st), "dsr_bin_scatter_cut")
@@ -556,30 +633,31 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             ws = _sort_workspace(lib, V, H, W, maxc, dev)
             stride = 0
             seg_sorted = _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, maxc, ws, st,
-                                      lds_cap)
+                                      lds_cap, ctx.opt("sort_prefix"))
     color = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
     # n_contrib (the last blended position, read only by the backward) is skipped on the
     # inference fast path: not tracking it takes ~4 VALU instructions off every (pixel, entry)
-    keep_nc = not fast or need_state or DEBUG_KEEP_FAST_LISTS
+    debug_lists = ctx.opt("debug_keep_fast_lists")
+    keep_nc = not fast or need_state or debug_lists
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev) if keep_nc else None
     outs = (color.data_ptr(), final_T.data_ptr(), _ptr(n_contrib), st)
     if fused:  # sort + composite in one launch; sorted keys kept only when a backward needs them
-        snap = seg_count.clone() if (fast and DEBUG_KEEP_FAST_LISTS) else None
+        snap = seg_count.clone() if (fast and debug_lists) else None
         _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(), None,
                           seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(),
-                          int(bool(need_state) or snap is not None), int(fast), SORT_RENDER_HINT or _spec["max_count"],
-                          *outs), "dsr_sort_render")
+                          int(bool(need_state) or snap is not None), int(fast),
+                          ctx.opt("sort_render_hint") or spec["max_count"], *outs), "dsr_sort_render")
         state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, cams=cams)
         if fast:  # the counters are zero again once the launch above has run
-            _give_back_clean_counts(seg_count, dev, st)
+            ctx.give_back_clean_counts(seg_count, dev, st)
             # consumed (no backward in this mode); with exact binning n_contrib counts positions
             # in the pruned lists (a subsequence of the reference's), not in the 3-sigma lists
             state.seg_count = snap
             state.pruned_lists = not (layout & LAYOUT_RECT_BINNING)
         else:
             state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING)
-        _last["counts"] = None if fast else state.counts
+        ctx._last["counts"] = None if fast else state.counts
         return color, state
     overflow = None
     if seg_sorted is not None:
@@ -605,13 +683,14 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, seg_sorted, overflow,
                         tile_count if stride == SEG_ENDS else None, cams=cams)
     state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING) and stride != SEG_ENDS
-    _last["counts"] = state.counts
+    ctx._last["counts"] = state.counts
     return color, state
 
 
-def _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, max_count, ws, st, lds_cap):
+def _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, max_count, ws, st, lds_cap,
+                 sort_prefix):
     """dsr_bin_sort; prefix mode (returns seg_sorted) when segments exceed the LDS sort."""
-    prefix = SORT_PREFIX if (scratch is not None and max_count > lds_cap and SORT_PREFIX > 0) else 0
+    prefix = sort_prefix if (scratch is not None and max_count > lds_cap and sort_prefix > 0) else 0
     seg_sorted = torch.empty(seg_count.numel(), dtype=torch.int32, device=keys.device) if prefix else None
     _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, _ptr(seg_start), seg_count.data_ptr(), stride,
                       keys.data_ptr(), _ptr(scratch), max_count, _ptr(ws), prefix, _ptr(seg_sorted), None, st),
@@ -688,14 +767,14 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means, feats, opacities, cov6, means2d, cams, view_scene, use_sh, sh_degree, H, W, layout,
-                zeroed_counts):
+                zeroed_counts, rctx):
         V = len(view_scene)
         need = any(ctx.needs_input_grad[:5])
         # the backward's accumulator: its rendered rows are zeroed by the projection kernel
         dgeom = torch.empty((V, means.shape[1], DGEOM_WORDS), dtype=torch.int64, device=means.device) \
             if need else None
         color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout,
-                                   zeroed_counts, need_state=need, dgeom_zero=dgeom)
+                                   zeroed_counts, need_state=need, dgeom_zero=dgeom, ctx=rctx)
         state.dgeom = dgeom
         ctx.save_for_backward(means, feats, opacities, cov6, state.cams)
         ctx.state = state
@@ -713,19 +792,21 @@ class _RasterizeViews(torch.autograd.Function):
             want_mean2d=want_m2d, layout=layout)
         if dmean2d is not None:
             dmean2d = dmean2d.view(m2d_shape)
-        return dmeans, dfeat, dopac, dcov6, dmean2d, None, None, None, None, None, None, None, None
+        return dmeans, dfeat, dopac, dcov6, dmean2d, None, None, None, None, None, None, None, None, None
 
 
 def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.Tensor, cov6: torch.Tensor,
                     cams: torch.Tensor, view_scene: list[int], *, use_sh: bool, sh_degree: int,
                     image_height: int, image_width: int, means2d: torch.Tensor | None = None,
-                    channel_major_sh: bool = False, zeroed_counts: torch.Tensor | None = None):
+                    channel_major_sh: bool = False, zeroed_counts: torch.Tensor | None = None,
+                    ctx: RasterContext | None = None):
     """Differentiable render of V views. means [S,G,3]; feats [S,G,M,3] (SH, coefficient-major
     like the rasterizer's `shs`; [S,G,3,M] = Gaussians.harmonics with channel_major_sh) or
     [S,G,3] (colors_precomp); opacities [S,G]; cov6 [S,G,6] or the full [S,G,3,3] matrices
     (read through the reference's triu gather); cams [V,44] (pack_cameras / build_cameras);
     view_scene[v] = scene index of view v. zeroed_counts: optional [V*tiles] int32 buffer already
-    zeroed (build_cameras(zero_counts=...)). Returns color [V,3,H,W] and radii [V,G] (int32)."""
+    zeroed (build_cameras(zero_counts=...)). ctx: the caller's RasterContext (a decoder's own;
+    default: the device's). Returns color [V,3,H,W] and radii [V,G] (int32)."""
     S = means.shape[0]
     n_cams = cams.V if isinstance(cams, CameraInputs) else cams.shape[0]
     if len(view_scene) != n_cams:
@@ -742,7 +823,7 @@ def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.T
     return _RasterizeViews.apply(f(means), f(feats), f(opacities), f(cov6), means2d,
                                  cams if isinstance(cams, CameraInputs) else cams.contiguous(),
                                  list(view_scene), use_sh, int(sh_degree), int(image_height), int(image_width),
-                                 layout, zeroed_counts)
+                                 layout, zeroed_counts, ctx)
 
 
 def sh_degree_of(n_coeffs: int) -> int:

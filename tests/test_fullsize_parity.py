@@ -189,8 +189,8 @@ def _fast_forward(g, sc, gpu, exact: bool, monkeypatch):
     from my_depthsplat_amd import raster
     # the fused sort + composite path is chosen from the previous call's largest tile list;
     # pin that hint (longer lists are still sorted exactly, through HBM scratch)
-    monkeypatch.setitem(raster._spec, "max_count", 2048)
-    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "max_count", 2048)
+    monkeypatch.setattr(raster.default_context(gpu), "adapt_hints", False)
     ext, K = sc.target_extrinsics[0].to(gpu), sc.target_intrinsics[0].to(gpu)
     V = ext.shape[0]
     bg = torch.zeros(V, 3, device=gpu)
@@ -313,7 +313,7 @@ def test_config_d_shape_render_vs_oracle(gpu, monkeypatch):
     (two-phase binning, depth cut: only each tile's nearest entries are written and sorted)
     vs the oracle's full render; the written heads equal the heads of the oracle's lists."""
     from my_depthsplat_amd import raster
-    monkeypatch.setitem(raster._spec, "two_phase_max", None)  # no short-list hint from earlier tests
+    monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)  # no short-list hint from earlier tests
     sc = scene_inputs(h=448, w=768, n_ctx=6, n_tgt=2, seed=2000)
     st = settings_for(sc)
     means, shs, opac, cov6 = flat_inputs(sc)
@@ -346,7 +346,7 @@ def test_config_e_shape_render_vs_oracle(gpu, monkeypatch):
     product path at this size (two-phase binning with the depth cut) vs the oracle's full
     render; the written heads equal the heads of the oracle's sorted lists."""
     from my_depthsplat_amd import raster
-    monkeypatch.setitem(raster._spec, "two_phase_max", None)  # no short-list hint from earlier tests
+    monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)  # no short-list hint from earlier tests
     sc = scene_inputs(h=512, w=960, n_ctx=12, n_tgt=1, seed=3000)
     assert sc.gaussians.means.shape[1] == 12 * 512 * 960
     st = settings_for(sc)

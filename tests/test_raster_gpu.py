@@ -230,8 +230,8 @@ def test_large_tiles_sort_paths(gpu, binning, hint, prefix, monkeypatch):
         monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
         monkeypatch.setattr(raster, "CUT_PREFIX", 0)  # full scatter (the depth cut has its own tests)
     monkeypatch.setattr(raster, "SORT_PREFIX", prefix)
-    monkeypatch.setitem(raster._spec, "max_count", {"low": 1, "exact": 12288 + 8, "between": cap + 1}[hint])
-    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)  # keep the hint fixed
+    monkeypatch.setitem(raster.default_context(gpu).hints, "max_count", {"low": 1, "exact": 12288 + 8, "between": cap + 1}[hint])
+    monkeypatch.setattr(raster.default_context(gpu), "adapt_hints", False)  # keep the hint fixed
     sc = _large_tile_scene()
     st = settings_for(sc)
     color, state, _ = hip_forward(sc, st, gpu)
@@ -254,8 +254,8 @@ def test_sort_render_lds_classes(gpu, n_keep, monkeypatch):
     the in-kernel HBM sort). Every class writes the oracle's sorted lists and the same image,
     n_contrib and final T bit for bit."""
     from my_depthsplat_amd import raster
-    monkeypatch.setitem(raster._spec, "max_count", 4096)  # fused sort + render
-    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "max_count", 4096)  # fused sort + render
+    monkeypatch.setattr(raster.default_context(gpu), "adapt_hints", False)
     sc = _large_tile_scene(opacity_scale=0.02)
     g = sc.gaussians
     g.means, g.covariances = g.means[:, :n_keep].contiguous(), g.covariances[:, :n_keep].contiguous()
@@ -290,8 +290,8 @@ def test_prefix_sort_overflow_fixup(gpu, binning, monkeypatch):
     if binning == "two_phase":
         monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
         monkeypatch.setattr(raster, "CUT_PREFIX", 0)
-    monkeypatch.setitem(raster._spec, "max_count", 12288 + 8)
-    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "max_count", 12288 + 8)
+    monkeypatch.setattr(raster.default_context(gpu), "adapt_hints", False)
     sc = _large_tile_scene(constant_opacity=0.0045)
     st = settings_for(sc)
     runs = {}
@@ -321,8 +321,8 @@ def test_prefix_sort_matches_full_sort(gpu, monkeypatch):
     """Default opacities: the sorted prefix suffices (no tile flagged) and forward outputs
     and backward gradients are bit-identical to sorting every entry."""
     from my_depthsplat_amd import raster
-    monkeypatch.setitem(raster._spec, "max_count", 12288 + 8)
-    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "max_count", 12288 + 8)
+    monkeypatch.setattr(raster.default_context(gpu), "adapt_hints", False)
     sc = _large_tile_scene(opacity_scale=1.0)
     st = settings_for(sc)
     means, shs, opac, cov6 = flat_inputs(sc)
@@ -385,7 +385,7 @@ def test_depth_cut_matches_full_scatter(gpu, opacity, monkeypatch):
     from my_depthsplat_amd import raster
     monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
     monkeypatch.setattr(raster, "SORT_PREFIX", 0)
-    monkeypatch.setitem(raster._spec, "two_phase_max", None)  # no short-list hint from earlier tests
+    monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)  # no short-list hint from earlier tests
     sc = _large_tile_scene(opacity_scale=1.0) if opacity == "default" else _large_tile_scene(constant_opacity=0.0045)
     st = settings_for(sc)
     out = {}
@@ -436,7 +436,7 @@ def test_depth_cut_multiview_scene_vs_oracle(gpu, monkeypatch):
     monkeypatch.setattr(raster, "CUT_PREFIX", 0)
     full, _, _ = hip_forward(sc, st, gpu)
     monkeypatch.setattr(raster, "CUT_PREFIX", 1024)
-    monkeypatch.setitem(raster._spec, "two_phase_max", None)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)
     color, state, _ = hip_forward(sc, st, gpu)
     assert state.seg_stride == raster.SEG_ENDS
     written, counts = state.written().cpu(), state.counts.cpu().long()

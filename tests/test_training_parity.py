@@ -140,7 +140,7 @@ def test_config_d_training_backward_vs_oracle(gpu, monkeypatch):
     key slots exceed the key budget): images and every gradient vs the oracle."""
     from my_depthsplat_amd import raster
     monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
-    monkeypatch.setitem(raster._spec, "two_phase_max", None)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)
     H, W, v = 448, 768, 2
     sc = scene_inputs(h=H, w=W, n_ctx=6, n_tgt=v, seed=2100)
     g = sc.gaussians
@@ -178,8 +178,8 @@ def test_product_entry_lists_vs_reference_settings(gpu, monkeypatch):
     Counts, over every (view, tile), the list entries that are not the same Gaussian at the
     same position; DESIGN.md §3 states the bound asserted here. Images: north_star bars."""
     from my_depthsplat_amd import raster
-    monkeypatch.setitem(raster._spec, "max_count", 2048)
-    monkeypatch.setattr(raster, "_note_counts", lambda counts: None)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "max_count", 2048)
+    monkeypatch.setattr(raster.default_context(gpu), "adapt_hints", False)
     H = W = 256
     sc = scene_inputs(h=H, w=W, n_ctx=2, n_tgt=3, seed=1000)
     g = sc.gaussians
