@@ -316,25 +316,30 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
  * projection of pixel (x,y) at depth[b,d,y,x] through K[b,j] and pose[b,j].
  *   ref [B,C,H,W]  tgt [B,J,C,H,W]  intr [B,J,3,3] (pixel units)  pose [B,J,4,4]
  *   depth [B,D,H,W] when depth_per_pixel else [B,D]   ->   cost [B,D,H,W]
- * C in {16, 32, 64, 128}: one workgroup per (16 reference pixels of a row, 64 depths)
- * correlates its pixels with the bounding box of the target pixels its samples tap as one
- * GEMM on the matrix cores (v_mfma_f32_16x16x4_f32, exact f32), reading ref and tgt in
- * their given layouts. tgt_hwc: workspace [B,J,H,W,C]; NULL allowed for those C (filled
- * with the channel-last copy of tgt when given: dcv_cost_volume_bwd reads it); required
- * for other C. */
+ * C in {16, 32, 64, 128} (matrix cores): the reference pixels are grouped by the epipolar line
+ * they lie on w.r.t. each source view (16 pixels of one line tap a thin band around ONE
+ * target line); each group's correlations with its band's distinct target pixels are one
+ * exact-f32 GEMM on v_mfma_f32_16x16x4_f32, finished by the 4-tap bilinear gather. Views are
+ * summed in launch order (deterministic). Other C: a direct channel-last kernel.
+ * workspace: dcv_cost_volume_workspace_size bytes (channel-last copies of tgt and ref with a
+ * zero padding row per image, and the epipolar groups), filled here and read by
+ * dcv_cost_volume_bwd. */
+size_t dcv_cost_volume_workspace_size(int B, int J, int C, int H, int W);
 int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel,
                         const float* ref, const float* tgt, const float* intr, const float* pose,
-                        const float* depth, float clamp_min_depth, float* tgt_hwc, float* cost,
+                        const float* depth, float clamp_min_depth, void* workspace, float* cost,
                         void* stream);
 
 /* Backward of dcv_cost_volume_fwd w.r.t. both feature maps (geometry gets no grad,
  * matching.py:46). dcost [B,D,H,W] -> dref [B,C,H,W] (overwritten), dtgt [B,J,C,H,W]
- * (overwritten). Needs the tgt_hwc workspace from the forward and dtgt_hwc [B,J,H,W,C]
- * scratch (zeroed here). */
+ * (overwritten). Needs the forward's workspace and dcv_cost_volume_bwd_workspace_size bytes
+ * of scratch (channel-last gradient accumulators). Reference gradients are summed in a fixed
+ * order; target gradients with float atomics (pixels shared between groups). */
+size_t dcv_cost_volume_bwd_workspace_size(int B, int J, int C, int H, int W);
 int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel,
-                        const float* ref, const float* tgt_hwc, const float* intr,
+                        const float* ref, const void* workspace, const float* intr,
                         const float* pose, const float* depth, float clamp_min_depth,
-                        const float* dcost, float* dref, float* dtgt, float* dtgt_hwc,
+                        const float* dcost, float* dref, float* dtgt, void* bwd_workspace,
                         void* stream);
 
 /* Materialising warp with the exact matching.py:24-90 signature semantics:

@@ -4,11 +4,12 @@
 //   warp_with_pose_depth_candidates   src/model/encoder/unimatch/matching.py:24-90
 //   cost = mean_j(sum_c ref * warped_j) / sqrt(C)   src/model/encoder/unimatch/mv_unimatch.py:494-505
 //
-// Layout: target features are first copied channel-last ([B,J,H,W,C]) so every bilinear
-// tap is one contiguous C-float row; a wave owns one reference pixel with its 64 lanes
-// over channels (coalesced 256-B tap reads), accumulates the per-depth partial dot
-// products of 64 depth hypotheses in registers and finishes them with a transpose
-// reduction (63 shuffles for 64 outputs) instead of 64 full wave reductions.
+// Channel counts that are multiples of 16 run on the matrix cores: reference pixels grouped by
+// epipolar line, each group correlated with the band of target pixels its samples tap as one
+// exact-f32 GEMM (k_epi_groups + k_cost_epi / k_cost_epi_bwd below). Other channel counts: the
+// target features are copied channel-last ([B,J,H,W,C]) so every bilinear tap is one
+// contiguous C-float row; a wave owns one reference pixel with its 64 lanes over channels
+// and finishes 64 depths' partial dot products with a transpose reduction (k_cost_fwd).
 // Geometry per (pixel, depth, view) is wave-uniform and follows the reference's
 // operation order: p_rot = R K^-1 [x, y, 1]; X = p_rot * depth + t; x = K X;
 // uv = x.xy / max(x.z, clamp); grid = 2 uv / (size - 1) - 1; grid_sample unnormalise
@@ -92,13 +93,16 @@ __device__ __forceinline__ void taps_at(const Cam& c, float prx, float pry, floa
 }
 
 // [B,J,C,H,W] -> [B,J,H,W,C] through a 64x64 LDS tile.
-__global__ __launch_bounds__(256) void k_to_hwc(int C, int HW, const float* __restrict__ src,
+// [n][C][HW] -> [n][rows][C] with rows >= HW; rows past HW (the zero padding row) are zeroed.
+__global__ __launch_bounds__(256) void k_to_hwc(int C, int HW, int rows, const float* __restrict__ src,
                                                 float* __restrict__ dst) {
   __shared__ float tile[64][65];
   const int bj = blockIdx.z;
   const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
   const float* s = src + (size_t)bj * C * HW;
-  float* d = dst + (size_t)bj * C * HW;
+  float* d = dst + (size_t)bj * rows * C;
+  if (blockIdx.x == 0 && (int)threadIdx.x < 64 && c0 + (int)threadIdx.x < C)
+    for (int p = HW; p < rows; ++p) d[(size_t)p * C + c0 + threadIdx.x] = 0.f;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int r = ty; r < 64; r += 4) {
     const int c = c0 + r, p = p0 + tx;
@@ -111,12 +115,13 @@ __global__ __launch_bounds__(256) void k_to_hwc(int C, int HW, const float* __re
   }
 }
 
-__global__ __launch_bounds__(256) void k_to_chw(int C, int HW, const float* __restrict__ src,
+// [n][rows][C] (the first HW rows) -> [n][C][HW]
+__global__ __launch_bounds__(256) void k_to_chw(int C, int HW, int rows, const float* __restrict__ src,
                                                 float* __restrict__ dst) {
   __shared__ float tile[64][65];
   const int bj = blockIdx.z;
   const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
-  const float* s = src + (size_t)bj * C * HW;
+  const float* s = src + (size_t)bj * rows * C;
   float* d = dst + (size_t)bj * C * HW;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int r = ty; r < 64; r += 4) {
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(256) void k_cost_fwd(int J, int C, int H, int W, in
       const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
       const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
       const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
-      const float* tg = tgt_hwc + ((size_t)b * J + j) * HW * C;
+      const float* tg = tgt_hwc + ((size_t)b * J + j) * (HW + 1) * C;
       for (int c0 = 0; c0 < C; c0 += 64) {
         const int c = c0 + lane;
         const bool cv = c < C;
@@ -207,649 +212,619 @@ __global__ __launch_bounds__(256) void k_cost_fwd(int J, int C, int H, int W, in
   }
 }
 
-// ---- MFMA formulation ------------------------------------------------------------------
-// The bilinear warp is linear, so cost(p, d) = sum_j sum_taps w * (ref[p] . tgt_j[q_tap]) / (sqrt C J):
-// every (pixel, depth) only needs the correlation of its pixel with the <= 4 target pixels it
-// taps. A workgroup takes TP = 16 consecutive reference pixels of a row; for each source view
-// it finds the distinct target pixels all its (pixel, depth) samples tap (an LDS bitmap over
-// the target image + a prefix of popcounts = a rank for every tapped pixel), computes the
-// correlations [16 pixels x U tapped pixels] as an exact-f32 GEMM on the matrix cores
-// (v_mfma_f32_16x16x4_f32, K = C channels, channel-last target rows as B), and finishes with
-// the 4-tap bilinear gather from LDS. Small-baseline epipolar segments of neighbouring pixels
-// overlap, so U is a few tens to a few hundred, far below 16 x D x 4 taps. Tiles whose U
-// exceeds kUMax fall back to a direct dot product per tap.
-constexpr int TP = 16;      // reference pixels per workgroup
-constexpr int DCH = 128;    // depth hypotheses per pass
-constexpr int kUMax = 512;  // tapped target pixels held in LDS per (tile, view)
-
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-struct CvLds {
-  float* aref;   // [TP][C]
-  float2* samp;  // [DCH][TP] sample position (ix, iy); ix = NaN: outside
-  uint32_t* bm;  // [NW] tapped-pixel bitmap
-  uint32_t* bmp; // [NW] exclusive popcount prefix
-  int* list;     // [kUMax] tapped pixel ids in rank order
-  float* corr;   // [TP][kUMax]
-  float* acc;    // [DCH][TP] cost accumulated over views
-  uint32_t* misc;
-};
+// ---- epipolar-group formulation on the matrix cores -------------------------------------
+// The bilinear warp is linear, so
+//   cost(p, d) = sum_j sum_taps w * <ref[:, p], tgt_j[:, q_tap]> / (sqrt(C) J):
+// every (pixel, depth) sample needs the correlations of its reference pixel with the <= 4
+// target pixels it taps. All depth samples of pixel p lie on p's epipolar line in target
+// view j, and reference pixels on ONE epipolar line of the reference image map to ONE
+// epipolar line of the target image. So the reference pixels are grouped by the epipolar
+// line they lie on (k_epi_groups: a counting sort by line, per (batch, view)); 16 pixels of
+// a group tap a thin band around a single target line, and their correlations with the
+// band's U distinct pixels are one [16 x U x C] GEMM on the matrix cores
+// (v_mfma_f32_16x16x4_f32, exact f32), finished by the 4-tap bilinear gather from LDS. With
+// row-segment groups (the round-2 band kernel) a diagonal epipolar line made U = the whole
+// bounding box of 16 parallel lines (thousands of pixels at the config-D rig); along the line
+// it is the line's length x ~3.
+constexpr int EG = 16;                       // reference pixels per group (MFMA M)
+// samples per thread SPT (kernel template): 8 (128 depth hypotheses per workgroup) or 2 (32,
+// for D <= 32: the per-pixel candidate windows of the finer scale); 16 depth lanes x SPT
+constexpr int kEUMax = 256;                  // band pixels per GEMM pass (LDS)
+constexpr int kECorr = kEUMax + 1;           // odd row stride: the gather's lanes spread over banks
+constexpr int kEpiBuckets = 8192;            // epipolar-line buckets per (batch, view)
 
-__device__ __forceinline__ int tap_rank(const CvLds& L, int q) {
-  const uint32_t w = L.bm[q >> 5];
-  return (int)(L.bmp[q >> 5] + __popc(w & ((1u << (q & 31)) - 1u)));
+// Line key of reference pixel (px, py) w.r.t. one source view (see k_epi_groups).
+struct EpiKey {
+  int mode;        // 0: by row (no baseline), 1: angle about a finite epipole, 2: offset across parallel lines
+  float ex, ey;    // epipole (mode 1)
+  float nx, ny;    // unit normal of the parallel lines (mode 2)
+  float o0, inv;   // bucket = floor((value - o0) * inv)
+  int nb;
+};
+__device__ __forceinline__ int epi_bucket(const EpiKey& k, float px, float py) {
+  float v;
+  if (k.mode == 0) return min((int)py, k.nb - 1);
+  if (k.mode == 1) {
+    v = atan2f(py - k.ey, px - k.ex);  // the line through the epipole, folded to [0, pi)
+    if (v < 0.f) v += 3.14159265358979f;
+  } else {
+    v = k.nx * px + k.ny * py;
+  }
+  return min(max((int)((v - k.o0) * k.inv), 0), k.nb - 1);
 }
 
-__global__ __launch_bounds__(256) void k_cost_mfma(int J, int C, int H, int W, int D, int depth_per_pixel,
-                                                   const float* __restrict__ ref,
-                                                   const float* __restrict__ tgt_hwc,
-                                                   const float* __restrict__ intr, const float* __restrict__ pose,
-                                                   const float* __restrict__ depth, float clampz,
-                                                   float* __restrict__ cost) {
-  extern __shared__ __attribute__((aligned(16))) float cv_lds[];
-  const int HW = H * W, NW = (HW + 31) / 32;
-  CvLds L;
+// One workgroup per (batch, source view j): groups[b, j, :] = the reference pixel ids
+// ordered by the epipolar line (w.r.t. view j) they lie on. The epipole e = K c, c = -R^T t
+// the source camera centre in reference camera coordinates (pose = [R | t] maps reference
+// to source coordinates). Finite epipole: lines are buckets of the angle about e, 1 / dmax
+// radians wide (dmax: farthest pixel from e), so neighbouring buckets are <= 1 px apart
+// anywhere in the image; epipole far outside the image (sideways baseline): parallel lines,
+// 1-px buckets of the offset across them; no baseline: rows. Order inside a bucket is the
+// arrival order of an LDS atomic (results do not depend on it: each output is computed
+// from its own correlations, whichever group holds its pixel).
+// Also writes geom[b, j] = {M = K R K^-1 (row-major), K t} (double, rounded once): the
+// projection of reference pixel p at depth d is M [px, py, 1] d + K t (see epi_ray).
+__global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, const float* __restrict__ intr,
+                                                     const float* __restrict__ pose, int* __restrict__ groups,
+                                                     float* __restrict__ geom) {
+  __shared__ uint32_t hist[kEpiBuckets];
+  __shared__ uint32_t wsum[16];
+  const int b = blockIdx.x, j = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int HW = H * W;
+  const size_t bj = (size_t)b * J + j;
+  EpiKey key;
   {
-    float* p = cv_lds;
-    L.aref = p;
-    p += TP * C;
-    L.samp = reinterpret_cast<float2*>(p);
-    p += 2 * DCH * TP;
-    L.acc = p;
-    p += DCH * TP;
-    L.corr = p;
-    p += TP * kUMax;
-    L.list = reinterpret_cast<int*>(p);
-    p += kUMax;
-    L.bm = reinterpret_cast<uint32_t*>(p);
-    p += NW;
-    L.bmp = reinterpret_cast<uint32_t*>(p);
-    p += NW;
-    L.misc = reinterpret_cast<uint32_t*>(p);
-  }
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int tpr = (W + TP - 1) / TP;
-  const int y = blockIdx.x / tpr, x0 = (blockIdx.x % tpr) * TP;
-  const int b = blockIdx.y;
-  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-  // reference tile as the A operand: aref[i][c]
-  for (int k = tid; k < TP * C; k += 256) {
-    const int i = k & (TP - 1), c = k >> 4;
-    L.aref[i * C + c] = (x0 + i < W) ? ref[((size_t)b * C + c) * HW + (size_t)y * W + x0 + i] : 0.f;
-  }
-  for (int d0 = 0; d0 < D; d0 += DCH) {
-    for (int k = tid; k < DCH * TP; k += 256) L.acc[k] = 0.f;
-    for (int j = 0; j < J; ++j) {
-      Cam cam;
-      load_cam(intr + ((size_t)b * J + j) * 9, pose + ((size_t)b * J + j) * 16, cam);
-      for (int w = tid; w < NW; w += 256) L.bm[w] = 0u;
-      __syncthreads();
-      // sample positions of every (pixel, depth) of the tile, taps marked in the bitmap
-      for (int k = tid; k < DCH * TP; k += 256) {
-        const int i = k & (TP - 1), dd = k >> 4, d = d0 + dd;
-        float2 sp = make_float2(__int_as_float(0x7fc00000), 0.f);
-        if (d < D && x0 + i < W) {
-          const float px = (float)(x0 + i), py = (float)y;
-          const float qx = cam.Kinv[0] * px + cam.Kinv[1] * py + cam.Kinv[2];
-          const float qy = cam.Kinv[3] * px + cam.Kinv[4] * py + cam.Kinv[5];
-          const float qz = cam.Kinv[6] * px + cam.Kinv[7] * py + cam.Kinv[8];
-          const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
-          const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
-          const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
-          const float dep = depth_per_pixel ? depth[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i]
-                                            : depth[(size_t)b * D + d];
-          const float X = prx * dep + cam.t[0];
-          const float Y = pry * dep + cam.t[1];
-          const float Z = prz * dep + cam.t[2];
-          const float xx = cam.K[0] * X + cam.K[1] * Y + cam.K[2] * Z;
-          const float yy = cam.K[3] * X + cam.K[4] * Y + cam.K[5] * Z;
-          const float zz = fmaxf(cam.K[6] * X + cam.K[7] * Y + cam.K[8] * Z, clampz);
-          const float u = xx / zz, v = yy / zz;
-          const float gxn = 2 * u / (W - 1) - 1;
-          const float gyn = 2 * v / (H - 1) - 1;
-          const float ix = ((gxn + 1) / 2) * (W - 1);
-          const float iy = ((gyn + 1) / 2) * (H - 1);
-          if (ix > -2.f && ix < (float)W + 1.f && iy > -2.f && iy < (float)H + 1.f) {
-            sp = make_float2(ix, iy);
-            const int tx0 = (int)floorf(ix), ty0 = (int)floorf(iy);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
-              if (tx >= 0 && tx < W && ty >= 0 && ty < H) {
-                const int q = ty * W + tx;
-                atomicOr(&L.bm[q >> 5], 1u << (q & 31));
-              }
-            }
-          }
-        }
-        L.samp[k] = sp;
-      }
-      __syncthreads();
-      // exclusive prefix of the bitmap popcounts (thread t owns a contiguous run of words)
-      {
-        const int per = (NW + 255) / 256;
-        const int w0 = tid * per, w1 = min(NW, w0 + per);
-        uint32_t tot = 0;
-        for (int w = w0; w < w1; ++w) tot += __popc(L.bm[w]);
-        const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
-        if (lane == 63) L.misc[wv] = incl;
-        __syncthreads();
-        uint32_t off = incl - tot;
-        for (int k = 0; k < wv; ++k) off += L.misc[k];
-        for (int w = w0; w < w1; ++w) {
-          L.bmp[w] = off;
-          off += __popc(L.bm[w]);
-        }
-        if (tid == 255) L.misc[4] = off;
-      }
-      __syncthreads();
-      const int U = (int)L.misc[4];
-      if (U <= kUMax) {
-        for (int w = tid; w < NW; w += 256) {
-          uint32_t bits = L.bm[w];
-          int r = (int)L.bmp[w];
-          while (bits) {
-            const int bpos = __builtin_ctz(bits);
-            bits &= bits - 1u;
-            L.list[r++] = w * 32 + bpos;
-          }
-        }
-        __syncthreads();
-        // corr[16 x U] = aref[16 x C] . tgt[U x C]^T on the matrix cores; per 16-channel step
-        // lane l feeds channels cb + 4 (l >> 4) + s in MFMA s (A and B permuted alike)
-        const float* tg = tgt_hwc + ((size_t)b * J + j) * (size_t)HW * C;
-        const int nblk = (U + 15) / 16;
-        for (int blk = wv; blk < nblk; blk += 4) {
-          const int u = blk * 16 + (lane & 15);
-          const int q = u < U ? L.list[u] : -1;
-          f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
-          const float* brow = tg + (size_t)(q < 0 ? 0 : q) * C + 4 * (lane >> 4);
-          const float* arow = L.aref + (lane & 15) * C + 4 * (lane >> 4);
-          for (int cb = 0; cb < C; cb += 16) {
-            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (q >= 0) bv = *reinterpret_cast<const float4*>(brow + cb);
-            const float4 av = *reinterpret_cast<const float4*>(arow + cb);
-            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc4, 0, 0, 0);
-            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc4, 0, 0, 0);
-            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc4, 0, 0, 0);
-            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc4, 0, 0, 0);
-          }
-          // D[row][col]: col = lane & 15 (tapped pixel), row = 4 (lane >> 4) + r (ref pixel)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) L.corr[(4 * (lane >> 4) + r) * kUMax + u] = acc4[r];
-        }
-        __syncthreads();
-        for (int k = tid; k < DCH * TP; k += 256) {
-          const float2 sp = L.samp[k];
-          if (!(sp.x == sp.x)) continue;
-          const int i = k & (TP - 1);
-          const float fx0 = floorf(sp.x), fy0 = floorf(sp.y);
-          const int tx0 = (int)fx0, ty0 = (int)fy0;
-          const float wx0 = (float)(tx0 + 1) - sp.x, wx1 = sp.x - fx0, wy0 = (float)(ty0 + 1) - sp.y,
-                      wy1 = sp.y - fy0;
-          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
-          float s = 0.f;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
-            if (tx >= 0 && tx < W && ty >= 0 && ty < H) s += wt[t] * L.corr[i * kUMax + tap_rank(L, ty * W + tx)];
-          }
-          L.acc[k] += s;
+    const float* k = intr + bj * 9;
+    const float* P = pose + bj * 16;
+    const double tx = P[3], ty = P[7], tz = P[11];
+    if (tid < 12) {
+      // Kinv by the adjugate, M = K R Kinv, bt = K t
+      const double a = k[0], bb = k[1], c = k[2], d = k[3], e = k[4], f = k[5], g = k[6], h = k[7], i = k[8];
+      const double A = e * i - f * h, Bc = -(d * i - f * g), Cc = d * h - e * g;
+      const double id = 1.0 / (a * A + bb * Bc + c * Cc);
+      const double Ki[9] = {A * id, -(bb * i - c * h) * id, (bb * f - c * e) * id,
+                            Bc * id, (a * i - c * g) * id, -(a * f - c * d) * id,
+                            Cc * id, -(a * h - bb * g) * id, (a * e - bb * d) * id};
+      const int r = tid / 3, q = tid % 3;
+      double v = 0.0;
+      if (tid < 9) {
+        for (int m = 0; m < 3; ++m) {
+          double rk = 0.0;  // (R Kinv)[m][q]
+          for (int n = 0; n < 3; ++n) rk += (double)P[m * 4 + n] * Ki[n * 3 + q];
+          v += (double)k[r * 3 + m] * rk;
         }
       } else {
-        // too many distinct taps for LDS: direct dot products (rare: very wide epipolar bands)
-        const float* tg = tgt_hwc + ((size_t)b * J + j) * (size_t)HW * C;
-        for (int k = tid; k < DCH * TP; k += 256) {
-          const float2 sp = L.samp[k];
-          if (!(sp.x == sp.x)) continue;
-          const int i = k & (TP - 1);
-          const float fx0 = floorf(sp.x), fy0 = floorf(sp.y);
-          const int tx0 = (int)fx0, ty0 = (int)fy0;
-          const float wx0 = (float)(tx0 + 1) - sp.x, wx1 = sp.x - fx0, wy0 = (float)(ty0 + 1) - sp.y,
-                      wy1 = sp.y - fy0;
-          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
-          float s = 0.f;
-          for (int t = 0; t < 4; ++t) {
-            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
-            if (!(tx >= 0 && tx < W && ty >= 0 && ty < H)) continue;
-            const float* row = tg + (size_t)(ty * W + tx) * C;
-            float dot = 0.f;
-            for (int c = 0; c < C; ++c) dot += L.aref[i * C + c] * row[c];
-            s += wt[t] * dot;
-          }
-          L.acc[k] += s;
-        }
+        const int rr = tid - 9;
+        v = k[rr * 3 + 0] * tx + k[rr * 3 + 1] * ty + k[rr * 3 + 2] * tz;
       }
-      __syncthreads();
+      geom[bj * 12 + tid] = (float)v;
     }
-    for (int k = tid; k < DCH * TP; k += 256) {
-      const int i = k & (TP - 1), d = d0 + (k >> 4);
-      if (d < D && x0 + i < W) cost[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i] = L.acc[k] * scale;
+    const double cx = -(P[0] * tx + P[4] * ty + P[8] * tz);
+    const double cy = -(P[1] * tx + P[5] * ty + P[9] * tz);
+    const double cz = -(P[2] * tx + P[6] * ty + P[10] * tz);
+    const double exh = k[0] * cx + k[1] * cy + k[2] * cz;
+    const double eyh = k[3] * cx + k[4] * cy + k[5] * cz;
+    const double ezh = k[6] * cx + k[7] * cy + k[8] * cz;
+    const double diag = sqrt((double)W * W + (double)H * H);
+    const double mx = 0.5 * (W - 1), my = 0.5 * (H - 1);
+    key.ex = key.ey = key.nx = key.ny = key.o0 = 0.f;
+    key.inv = 1.f;
+    if (fabs(exh) + fabs(eyh) + fabs(ezh) < 1e-12) {
+      key.mode = 0;
+      key.nb = H;
+    } else if (fabs(ezh) > 1e-12 && hypot(exh / ezh - mx, eyh / ezh - my) < 64.0 * diag) {
+      key.mode = 1;
+      key.ex = (float)(exh / ezh);
+      key.ey = (float)(eyh / ezh);
+      double dmax = 1.0;
+      for (int c = 0; c < 4; ++c)
+        dmax = fmax(dmax, hypot((c & 1) * (W - 1) - (double)key.ex, (c >> 1) * (H - 1) - (double)key.ey));
+      const double nb = ceil(3.14159265358979 * dmax) + 1;
+      key.nb = (int)fmin(nb, (double)kEpiBuckets);
+      key.inv = (float)(key.nb / 3.14159265358979);
+    } else {
+      key.mode = 2;
+      const double n = hypot(exh, eyh);
+      key.nx = (float)(-eyh / n);
+      key.ny = (float)(exh / n);
+      float lo = 3.4e38f, hi = -3.4e38f;
+      for (int c = 0; c < 4; ++c) {
+        const float v = key.nx * (float)((c & 1) * (W - 1)) + key.ny * (float)((c >> 1) * (H - 1));
+        lo = fminf(lo, v);
+        hi = fmaxf(hi, v);
+      }
+      key.o0 = lo;
+      key.nb = min(kEpiBuckets, (int)ceilf(hi - lo) + 1);
+      key.inv = (float)key.nb / fmaxf(hi - lo + 1.f, 1.f);
+    }
+  }
+  for (int i = tid; i < kEpiBuckets; i += 1024) hist[i] = 0u;
+  __syncthreads();
+  for (int p = tid; p < HW; p += 1024) atomicAdd(&hist[epi_bucket(key, (float)(p % W), (float)(p / W))], 1u);
+  __syncthreads();
+  // exclusive scan of the buckets (8 per thread)
+  {
+    constexpr int PT = kEpiBuckets / 1024;
+    uint32_t v[PT], tot = 0;
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      v[i] = hist[tid * PT + i];
+      tot += v[i];
+    }
+    const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t off = incl - tot;
+    for (int k = 0; k < wv; ++k) off += wsum[k];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      hist[tid * PT + i] = off;
+      off += v[i];
+    }
+  }
+  __syncthreads();
+  int* out = groups + bj * HW;
+  for (int p = tid; p < HW; p += 1024) out[atomicAdd(&hist[epi_bucket(key, (float)(p % W), (float)(p / W))], 1u)] = p;
+}
+
+// Shared set-up of the forward and backward group kernels: the workgroup's (b, group) with
+// a given view's groups on a contiguous range of one XCD (their target bands overlap: L2).
+__device__ __forceinline__ bool epi_item(int B, int ngroups, int& b, int& g) {
+  const int items = B * ngroups, per = (items + 7) >> 3;
+  const int item = (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
+  if ((int)(blockIdx.x >> 3) >= per || item >= items) return false;
+  b = item / ngroups;
+  g = item - b * ngroups;
+  return true;
+}
+
+// The band lives on an extended grid of (W + 2) x (H + 2) positions (image x, y in [-1, W]
+// x [-1, H]: every tap of a sample whose top-left tap is in [-1, W - 1] x [-1, H - 1]; other
+// samples tap nothing inside the image). A sample marks only its top-left tap (one LDS atomic
+// instead of four); the tapped set is that base bitmap OR-ed with itself shifted by one
+// column, one row and both (a word-parallel pass), so the sample's four taps have ranks
+// r(e), r(e) + 1, r(e + Wx), r(e + Wx) + 1. Band positions outside the image correlate to 0
+// (zero B operand) = grid_sample's zeros padding.
+struct EpiLds {
+  float* aref;      // [EG][C + 4]
+  uint32_t* base;   // [NWx] top-left taps
+  uint2* wb;        // [NWx] {tapped positions, exclusive popcount prefix} per word
+  int* nzw;         // [NWx] the non-zero words of bm, ascending
+  int* list;        // [kEUMax] image pixel of each band position of the current pass (-1: outside)
+  float* corr;      // [EG][kECorr] correlations (forward) / gradient weights (backward)
+  float* dacc;      // [EG][C + 4] reference gradients (backward)
+  uint32_t* misc;   // [16]
+};
+__host__ __device__ constexpr int epi_words(int H, int W) { return ((W + 2) * (H + 2) + 31) / 32 + 1; }
+__device__ __forceinline__ EpiLds epi_lds(float* p, int C, int NWx, bool bwd) {
+  EpiLds L;
+  L.aref = p;
+  p += EG * (C + 4);
+  L.corr = p;
+  p += EG * kECorr;
+  L.dacc = p;
+  p += bwd ? EG * (C + 4) : 0;
+  L.list = reinterpret_cast<int*>(p);
+  p += kEUMax;
+  L.base = reinterpret_cast<uint32_t*>(p);
+  p += NWx;
+  p += (NWx & 1);  // 8-byte alignment of wb (base and list above hold whole 4-byte words)
+  L.wb = reinterpret_cast<uint2*>(p);
+  p += 2 * NWx;
+  L.nzw = reinterpret_cast<int*>(p);
+  p += NWx;
+  L.misc = reinterpret_cast<uint32_t*>(p);
+  return L;
+}
+size_t epi_lds_bytes(int C, int H, int W, bool bwd) {
+  return sizeof(float) * ((size_t)EG * (C + 4) * (bwd ? 2 : 1) + EG * kECorr + kEUMax + 4 * epi_words(H, W) + 1 + 16);
+}
+
+// The group's reference tile [EG][C] into LDS from the channel-last copy (rows of 16-byte
+// vectors; a past-the-end pixel reads the zero row HW), loads issued together.
+template <int NK>
+__device__ __forceinline__ void epi_aref(const EpiLds& L, int HW, int b, const int* gids,
+                                         const float* __restrict__ ref_hwc) {
+  constexpr int C = 4 * NK, N4 = EG * C / 4, IT = (N4 + 255) / 256;
+  float4 v[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int k = min((int)threadIdx.x + 256 * it, N4 - 1), r = k / (C / 4), c4 = k - r * (C / 4);
+    const int pr = gids[r] >= 0 ? gids[r] : HW;
+    v[it] = *reinterpret_cast<const float4*>(ref_hwc + ((size_t)b * (HW + 1) + pr) * C + 4 * c4);
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int k = (int)threadIdx.x + 256 * it, r = k / (C / 4), c4 = k - r * (C / 4);
+    if (k < N4) *reinterpret_cast<float4*>(L.aref + r * (C + 4) + 4 * c4) = v[it];
+  }
+}
+
+// Per-pixel ray terms: the projection of depth d is (ax d + bx, ay d + by, az d + bz) with
+// a = M [px, py, 1], M = K R K^-1 and b = K t (from k_epi_groups' geom; matching.py:47-65
+// regrouped, each coefficient rounded once from double: within a few ulp of the reference's
+// K (R K^-1 p d + t); the parity bar is 1e-4).
+struct EpiRay {
+  float ax, ay, az, bx, by, bz;
+};
+__device__ __forceinline__ EpiRay epi_ray(const float* __restrict__ gm, float px, float py) {
+  EpiRay r;
+  r.ax = fmaf(gm[0], px, fmaf(gm[1], py, gm[2]));
+  r.ay = fmaf(gm[3], px, fmaf(gm[4], py, gm[5]));
+  r.az = fmaf(gm[6], px, fmaf(gm[7], py, gm[8]));
+  r.bx = gm[9];
+  r.by = gm[10];
+  r.bz = gm[11];
+  return r;
+}
+// Sample position (grid_sample's unnormalised coordinates = the projected pixel, align_corners
+// = True); the extended-grid index of its top-left tap, or -1 when no tap is inside the image.
+// 1 / z is the hardware reciprocal (1 ulp; the parity bar is 1e-4).
+__device__ __forceinline__ int epi_sample(const EpiRay& ry, float dep, float clampz, int H, int W, float& ix,
+                                          float& iy) {
+  const float xx = fmaf(ry.ax, dep, ry.bx), yy = fmaf(ry.ay, dep, ry.by);
+  const float zz = fmaxf(fmaf(ry.az, dep, ry.bz), clampz);
+  const float rz = __builtin_amdgcn_rcpf(zz);
+  ix = xx * rz;
+  iy = yy * rz;
+  if (!(ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H)) return -1;  // also NaN
+  const int tx0 = (int)floorf(ix), ty0 = (int)floorf(iy);  // in [-1, W - 1] x [-1, H - 1]
+  return ty0 * (W + 2) + tx0 + (W + 3);
+}
+
+// Front half shared by the forward and the backward: the samples' top-left taps into the
+// base bitmap, the tapped set (base | shifted copies), its exclusive popcount prefix and
+// its non-zero words; returns U (band positions). es[s]: extended index of sample s's
+// top-left tap (-1: zero sample). Global loads are issued unconditionally (clamped indices),
+// all before their first use, so their latencies overlap.
+template <int SPT>
+__device__ __forceinline__ int epi_front(const EpiLds& L, int H, int W, int HW, int D, int depth_per_pixel, int b,
+                                         int d0, int pix, const EpiRay& ry, const float* __restrict__ depth,
+                                         float clampz, float (&sx)[SPT], float (&sy)[SPT], int (&es)[SPT]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int dl = tid >> 4, Wx = W + 2, NWx = epi_words(H, W);
+  float dep[SPT];
+  {
+    const float* dp = depth + (size_t)b * D * (depth_per_pixel ? HW : 1);
+    const int dstride = depth_per_pixel ? HW : 1, pc = depth_per_pixel ? max(pix, 0) : 0;
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) dep[s] = dp[(uint32_t)(min(d0 + dl + 16 * s, D - 1) * dstride + pc)];
+  }
+  for (int w = tid; w < NWx; w += 256) L.base[w] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) {
+    const int d = d0 + dl + 16 * s;
+    es[s] = epi_sample(ry, dep[s], clampz, H, W, sx[s], sy[s]);
+    if (pix < 0 || d >= D) es[s] = -1;
+    if (es[s] >= 0) atomicOr(&L.base[es[s] >> 5], 1u << (es[s] & 31));
+  }
+  __syncthreads();
+  // tapped = base | base << 1 | base << Wx | base << (Wx + 1) (bit shifts across the words)
+  auto shl = [&](int w, int sft) -> uint32_t {
+    const int wo = sft >> 5, bo = sft & 31;
+    const uint32_t lo = w - wo >= 0 ? L.base[w - wo] : 0u;
+    if (bo == 0) return lo;
+    const uint32_t hi = w - wo - 1 >= 0 ? L.base[w - wo - 1] : 0u;
+    return (lo << bo) | (hi >> (32 - bo));
+  };
+  for (int w = tid; w < NWx; w += 256) L.wb[w].x = shl(w, 0) | shl(w, 1) | shl(w, Wx) | shl(w, Wx + 1);
+  __syncthreads();
+  {  // exclusive prefix of the popcounts and compaction of the non-zero words (thread t owns
+     // a contiguous run of words)
+    const int per = (NWx + 255) / 256;
+    const int w0 = tid * per, w1 = min(NWx, w0 + per);
+    uint32_t tot = 0, nz = 0;
+    for (int w = w0; w < w1; ++w) {
+      const uint32_t c = __popc(L.wb[w].x);
+      tot += c;
+      nz += c != 0u;
+    }
+    const uint32_t incl = dsplat::wave_incl_add_dpp(tot), inz = dsplat::wave_incl_add_dpp(nz);
+    if (lane == 63) {
+      L.misc[wv] = incl;
+      L.misc[8 + wv] = inz;
     }
     __syncthreads();
-  }
-}
-
-// Backward with the same tiling. Per (tile, view): G[i][u] = sum over the tile's (pixel i,
-// depth d) samples tapping target pixel list[u] of dcost(i, d) * w_tap / (sqrt C J) (LDS
-// float atomics), then on the matrix cores
-//   dref[i][c] += sum_u G[i][u] tgt[list[u]][c]      ([16 x U] x [U x C], K = U)
-//   dtgt[list[u]][c] += sum_i G[i][u] ref[i][c]       ([U x 16] x [16 x C], K = 16; global atomics)
-__global__ __launch_bounds__(256) void k_cost_mfma_bwd(int J, int C, int H, int W, int D, int depth_per_pixel,
-                                                       const float* __restrict__ ref,
-                                                       const float* __restrict__ tgt_hwc,
-                                                       const float* __restrict__ intr,
-                                                       const float* __restrict__ pose,
-                                                       const float* __restrict__ depth, float clampz,
-                                                       const float* __restrict__ dcost, float* __restrict__ dref,
-                                                       float* __restrict__ dtgt_hwc) {
-  extern __shared__ __attribute__((aligned(16))) float cv_lds[];
-  const int HW = H * W, NW = (HW + 31) / 32;
-  CvLds L;
-  float* dacc;  // [TP][C] dref accumulated over views and depth chunks
-  {
-    float* p = cv_lds;
-    L.aref = p;
-    p += TP * C;
-    L.samp = reinterpret_cast<float2*>(p);
-    p += 2 * DCH * TP;
-    L.acc = p;  // G: [TP][kUMax]
-    p += TP * kUMax;
-    dacc = p;
-    p += TP * C;
-    L.list = reinterpret_cast<int*>(p);
-    p += kUMax;
-    L.bm = reinterpret_cast<uint32_t*>(p);
-    p += NW;
-    L.bmp = reinterpret_cast<uint32_t*>(p);
-    p += NW;
-    L.misc = reinterpret_cast<uint32_t*>(p);
-  }
-  float* Gm = L.acc;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int tpr = (W + TP - 1) / TP;
-  const int y = blockIdx.x / tpr, x0 = (blockIdx.x % tpr) * TP;
-  const int b = blockIdx.y;
-  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-  for (int k = tid; k < TP * C; k += 256) {
-    const int i = k & (TP - 1), c = k >> 4;
-    L.aref[i * C + c] = (x0 + i < W) ? ref[((size_t)b * C + c) * HW + (size_t)y * W + x0 + i] : 0.f;
-    dacc[i * C + c] = 0.f;
-  }
-  for (int d0 = 0; d0 < D; d0 += DCH) {
-    for (int j = 0; j < J; ++j) {
-      Cam cam;
-      load_cam(intr + ((size_t)b * J + j) * 9, pose + ((size_t)b * J + j) * 16, cam);
-      for (int w = tid; w < NW; w += 256) L.bm[w] = 0u;
-      __syncthreads();
-      for (int k = tid; k < DCH * TP; k += 256) {
-        const int i = k & (TP - 1), dd = k >> 4, d = d0 + dd;
-        float2 sp = make_float2(__int_as_float(0x7fc00000), 0.f);
-        if (d < D && x0 + i < W) {
-          const float px = (float)(x0 + i), py = (float)y;
-          const float qx = cam.Kinv[0] * px + cam.Kinv[1] * py + cam.Kinv[2];
-          const float qy = cam.Kinv[3] * px + cam.Kinv[4] * py + cam.Kinv[5];
-          const float qz = cam.Kinv[6] * px + cam.Kinv[7] * py + cam.Kinv[8];
-          const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
-          const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
-          const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
-          const float dep = depth_per_pixel ? depth[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i]
-                                            : depth[(size_t)b * D + d];
-          const float X = prx * dep + cam.t[0];
-          const float Y = pry * dep + cam.t[1];
-          const float Z = prz * dep + cam.t[2];
-          const float xx = cam.K[0] * X + cam.K[1] * Y + cam.K[2] * Z;
-          const float yy = cam.K[3] * X + cam.K[4] * Y + cam.K[5] * Z;
-          const float zz = fmaxf(cam.K[6] * X + cam.K[7] * Y + cam.K[8] * Z, clampz);
-          const float u = xx / zz, v = yy / zz;
-          const float gxn = 2 * u / (W - 1) - 1;
-          const float gyn = 2 * v / (H - 1) - 1;
-          const float ix = ((gxn + 1) / 2) * (W - 1);
-          const float iy = ((gyn + 1) / 2) * (H - 1);
-          if (ix > -2.f && ix < (float)W + 1.f && iy > -2.f && iy < (float)H + 1.f) {
-            sp = make_float2(ix, iy);
-            const int tx0 = (int)floorf(ix), ty0 = (int)floorf(iy);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
-              if (tx >= 0 && tx < W && ty >= 0 && ty < H) {
-                const int q = ty * W + tx;
-                atomicOr(&L.bm[q >> 5], 1u << (q & 31));
-              }
-            }
-          }
-        }
-        L.samp[k] = sp;
-      }
-      __syncthreads();
-      {
-        const int per = (NW + 255) / 256;
-        const int w0 = tid * per, w1 = min(NW, w0 + per);
-        uint32_t tot = 0;
-        for (int w = w0; w < w1; ++w) tot += __popc(L.bm[w]);
-        const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
-        if (lane == 63) L.misc[wv] = incl;
-        __syncthreads();
-        uint32_t off = incl - tot;
-        for (int k = 0; k < wv; ++k) off += L.misc[k];
-        for (int w = w0; w < w1; ++w) {
-          L.bmp[w] = off;
-          off += __popc(L.bm[w]);
-        }
-        if (tid == 255) L.misc[4] = off;
-      }
-      __syncthreads();
-      const int U = (int)L.misc[4];
-      float* dtg = dtgt_hwc + ((size_t)b * J + j) * (size_t)HW * C;
-      const float* tg = tgt_hwc + ((size_t)b * J + j) * (size_t)HW * C;
-      if (U <= kUMax) {
-        const int Up = (U + 15) & ~15;
-        for (int w = tid; w < NW; w += 256) {
-          uint32_t bits = L.bm[w];
-          int r = (int)L.bmp[w];
-          while (bits) {
-            const int bpos = __builtin_ctz(bits);
-            bits &= bits - 1u;
-            L.list[r++] = w * 32 + bpos;
-          }
-        }
-        for (int k = tid; k < TP * Up; k += 256) Gm[(k / Up) * kUMax + (k % Up)] = 0.f;
-        __syncthreads();
-        for (int k = tid; k < DCH * TP; k += 256) {
-          const float2 sp = L.samp[k];
-          if (!(sp.x == sp.x)) continue;
-          const int i = k & (TP - 1), d = d0 + (k >> 4);
-          const float g = dcost[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i] * scale;
-          const float fx0 = floorf(sp.x), fy0 = floorf(sp.y);
-          const int tx0 = (int)fx0, ty0 = (int)fy0;
-          const float wx0 = (float)(tx0 + 1) - sp.x, wx1 = sp.x - fx0, wy0 = (float)(ty0 + 1) - sp.y,
-                      wy1 = sp.y - fy0;
-          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
-            if (tx >= 0 && tx < W && ty >= 0 && ty < H) atomicAdd(&Gm[i * kUMax + tap_rank(L, ty * W + tx)], g * wt[t]);
-          }
-        }
-        __syncthreads();
-        // dref[16 x C] += G[16 x U] . T[U x C]: blocks of 16 channels, K = taps (4 per MFMA)
-        for (int cb = wv * 16; cb < C; cb += 64) {
-          f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
-          for (int u0 = 0; u0 < Up; u0 += 4) {
-            const int u = u0 + (lane >> 4);
-            const float a = Gm[(lane & 15) * kUMax + u];
-            const float bv = u < U ? tg[(size_t)L.list[u] * C + cb + (lane & 15)] : 0.f;
-            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc4, 0, 0, 0);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) dacc[(4 * (lane >> 4) + r) * C + cb + (lane & 15)] += acc4[r];
-        }
-        // dtgt[U x C] += G^T[U x 16] . aref[16 x C]: blocks of 16 taps x 16 channels, K = pixels
-        const int nub = Up / 16, ncb = C / 16;
-        for (int blk = wv; blk < nub * ncb; blk += 4) {
-          const int ub = (blk / ncb) * 16, cb = (blk % ncb) * 16;
-          f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) {
-            const int i = 4 * s2 + (lane >> 4);
-            const float a = Gm[i * kUMax + ub + (lane & 15)];
-            const float bv = L.aref[i * C + cb + (lane & 15)];
-            acc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc4, 0, 0, 0);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int u = ub + 4 * (lane >> 4) + r;
-            if (u < U && acc4[r] != 0.f) atomicAdd(&dtg[(size_t)L.list[u] * C + cb + (lane & 15)], acc4[r]);
-          }
-        }
-      } else {
-        // direct scatter (very wide tap sets): per sample and tap, all channels
-        for (int k = tid; k < DCH * TP; k += 256) {
-          const float2 sp = L.samp[k];
-          if (!(sp.x == sp.x)) continue;
-          const int i = k & (TP - 1), d = d0 + (k >> 4);
-          const float g = dcost[((size_t)b * D + d) * HW + (size_t)y * W + x0 + i] * scale;
-          const float fx0 = floorf(sp.x), fy0 = floorf(sp.y);
-          const int tx0 = (int)fx0, ty0 = (int)fy0;
-          const float wx0 = (float)(tx0 + 1) - sp.x, wx1 = sp.x - fx0, wy0 = (float)(ty0 + 1) - sp.y,
-                      wy1 = sp.y - fy0;
-          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
-          for (int t = 0; t < 4; ++t) {
-            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
-            if (!(tx >= 0 && tx < W && ty >= 0 && ty < H)) continue;
-            const float gw = g * wt[t];
-            const size_t row = (size_t)(ty * W + tx) * C;
-            for (int c = 0; c < C; ++c) {
-              atomicAdd(&dacc[i * C + c], gw * tg[row + c]);
-              atomicAdd(&dtg[row + c], gw * L.aref[i * C + c]);
-            }
-          }
-        }
-      }
-      __syncthreads();
+    uint32_t off = incl - tot, offz = inz - nz;
+    for (int k = 0; k < wv; ++k) {
+      off += L.misc[k];
+      offz += L.misc[8 + k];
+    }
+    for (int w = w0; w < w1; ++w) {
+      const uint32_t bits = L.wb[w].x;
+      L.wb[w].y = off;
+      off += __popc(bits);
+      if (bits) L.nzw[offz++] = w;
+    }
+    if (tid == 255) {
+      L.misc[4] = off;
+      L.misc[5] = offz;
     }
   }
-  for (int k = tid; k < TP * C; k += 256) {
-    const int i = k & (TP - 1), c = k >> 4;
-    if (x0 + i < W) dref[((size_t)b * C + c) * HW + (size_t)y * W + x0 + i] = dacc[i * C + c];
+  __syncthreads();
+  return (int)L.misc[4];
+}
+
+// list[] = the target row of band ranks [r0, r0 + n): the image pixel, or HW (the all-zero
+// padding row of the channel-last copy) for positions outside the image and for the slots
+// [n, round_up(n, kEPad)) past the band. 32 lanes per non-zero word, one bit each.
+constexpr int kEPad = 32;
+__device__ __forceinline__ int epi_padded(int n) { return (n + kEPad - 1) / kEPad * kEPad; }
+__device__ __forceinline__ void epi_list(const EpiLds& L, int H, int W, int r0, int n) {
+  const int Wx = W + 2, nnz = (int)L.misc[5], bit = threadIdx.x & 31, HW = H * W;
+  if ((int)threadIdx.x < epi_padded(n) - n) L.list[n + threadIdx.x] = HW;
+  const float rWx = 1.0f / (float)Wx;
+  for (int k = threadIdx.x >> 5; k < nnz; k += 8) {
+    const int w = L.nzw[k];
+    const uint2 wv2 = L.wb[w];
+    const uint32_t bits = wv2.x;
+    if (!((bits >> bit) & 1u)) continue;
+    const int r = (int)(wv2.y + __popc(bits & ((1u << bit) - 1u)));
+    if (r < r0 || r >= r0 + n) continue;
+    const int e = w * 32 + bit;
+    int ye = (int)((float)e * rWx), xe = e - ye * Wx;  // the float quotient is within 1 of e / Wx
+    if (xe < 0) {
+      --ye;
+      xe += Wx;
+    } else if (xe >= Wx) {
+      ++ye;
+      xe -= Wx;
+    }
+    const int x = xe - 1, y = ye - 1;
+    L.list[r - r0] = (x >= 0 && x < W && y >= 0 && y < H) ? y * W + x : HW;
   }
 }
-
-// ---- forward on the matrix cores, band form (dcv_cost_volume_fwd) ----------------------
-// One workgroup per (16 reference pixels of a row, 64 depth hypotheses): thread t owns pixel
-// t & 15 and depths (t >> 4) + 16 s, s < 4, and keeps those samples' positions in registers.
-// Per source view the workgroup takes the bounding box of every target pixel its samples tap
-// (a block min / max: no LDS atomics, no bitmap), computes the correlations of its 16
-// reference pixels with ALL box pixels as one exact-f32 GEMM on v_mfma_f32_16x16x4_f32
-// (A = the reference tile, loaded once into registers straight from [B,C,H,W]; B = target
-// columns loaded straight from [B,J,C,H,W], no channel-last copy), and finishes with the
-// 4-tap bilinear gather from LDS. A small-baseline epipolar band fills its box (a few tens
-// to a few hundred pixels at these scales); a box above kBandMax pixels is computed by direct
-// dot products from global memory instead (wide, scattered taps; rare).
-constexpr int BTP = 16;                       // reference pixels per workgroup
-constexpr int BDCH = 64;                      // depth hypotheses per workgroup
-constexpr int BSPT = BTP * BDCH / 256;        // samples per thread
-constexpr int kBandMax = 512;                 // box pixels whose correlations fit in LDS (33 KB:
-                                              // 4 workgroups per CU, all of config B's in one round)
-constexpr int kCorrStride = kBandMax + 1;     // odd row stride: the gather's lanes spread over banks
-
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
-  return v;
-}
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
-  return v;
+__device__ __forceinline__ int epi_rank(const EpiLds& L, int e) {
+  const uint2 w = L.wb[e >> 5];
+  return (int)(w.y + __popc(w.x & ((1u << (e & 31)) - 1u)));
 }
 
-template <int NK>  // NK = C / 4 matrix-core steps
-__global__ __launch_bounds__(256) void k_cost_band(int J, int H, int W, int D, int depth_per_pixel,
-                                                   const float* __restrict__ ref, const float* __restrict__ tgt,
-                                                   const float* __restrict__ intr, const float* __restrict__ pose,
-                                                   const float* __restrict__ depth, float clampz,
-                                                   float* __restrict__ cost) {
+// Forward, view j: grid.x = 8 * ceil(B * ngroups / 8) (XCD-contiguous), grid.y = D chunks of
+// 16 * SPT. Writes (accumulate = 0) or adds (accumulate = 1: views after the first, launched in
+// view order, so the sum over views is deterministic) scale * sum_taps w * corr.
+// ref_hwc [B][HW + 1][C], tgt_hwc [B][J][HW + 1][C]: channel-last copies, row HW zero.
+template <int NK, int SPT>
+__global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
+                                                  int accumulate, const float* __restrict__ ref_hwc,
+                                                  const float* __restrict__ tgt_hwc, const int* __restrict__ groups,
+                                                  const float* __restrict__ geom, const float* __restrict__ depth,
+                                                  float clampz, float scale, float* __restrict__ cost) {
   constexpr int C = 4 * NK;
   extern __shared__ __attribute__((aligned(16))) float cv_lds[];
-  float* s_corr = cv_lds;                                           // [BTP][kCorrStride]
-  int* s_box = reinterpret_cast<int*>(cv_lds + BTP * kCorrStride);  // [4 waves][4]
-  const int HW = H * W;
+  const int HW = H * W, ngroups = (HW + EG - 1) / EG, Wx = W + 2;
+  int b, g;
+  if (!epi_item(B, ngroups, b, g)) return;
+  const EpiLds L = epi_lds(cv_lds, C, epi_words(H, W), false);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int tpr = (W + BTP - 1) / BTP;
-  const int y = blockIdx.x / tpr, x0 = (blockIdx.x % tpr) * BTP;
-  const int b = blockIdx.y, d0 = blockIdx.z * BDCH;
-  const int i = tid & (BTP - 1), dl = tid >> 4;
-  const int px = x0 + i;
-  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-  // A operand (v_mfma_f32_16x16x4f32: lane l holds A[l & 15][l >> 4]): channel 4 s + (l >> 4) of
-  // reference pixel x0 + (l & 15), for every step s — the whole 16 x C tile in NK registers
-  float a[NK];
-  {
-    const int ax = x0 + (lane & 15);
-    const float* rp = ref + ((size_t)b * C + (lane >> 4)) * HW + (size_t)y * W + ax;
+  const int i = tid & (EG - 1), dl = tid >> 4, d0 = blockIdx.y * 16 * SPT;
+  const size_t bj = (size_t)b * J + j;
+  __shared__ int s_gid[EG];
+  if (tid < EG) s_gid[tid] = g * EG + tid < HW ? groups[bj * HW + g * EG + tid] : -1;
+  __syncthreads();
+  epi_aref<NK>(L, HW, b, s_gid, ref_hwc);
+  const int pix = s_gid[i];  // -1: past the last pixel
+  const EpiRay ry = epi_ray(geom + bj * 12, pix >= 0 ? (float)(pix % W) : 0.f, pix >= 0 ? (float)(pix / W) : 0.f);
+  float sx[SPT], sy[SPT];
+  int es[SPT];
+  const int U = epi_front<SPT>(L, H, W, HW, D, depth_per_pixel, b, d0, pix, ry, depth, clampz, sx, sy, es);
+  // per sample: sum over its taps of grid_sample's weight x correlation, taps in a fixed order
+  // (a band of more than kEUMax positions takes several passes, each adding its taps)
+  float* cb = cost + (size_t)b * D * HW;  // this scene's cost volume (< 2^32 elements)
+  float acc[SPT], prev[SPT];
 #pragma unroll
-    for (int s = 0; s < NK; ++s) a[s] = ax < W ? rp[(size_t)4 * s * HW] : 0.f;
-  }
-  float acc[BSPT];
+  for (int s = 0; s < SPT; ++s) acc[s] = prev[s] = 0.f;
+  auto load_prev = [&]() {
+    int pc = max(pix, 0);
+    asm volatile("" : "+v"(pc));  // addresses formed here, not hoisted (register pressure)
 #pragma unroll
-  for (int s = 0; s < BSPT; ++s) acc[s] = 0.f;
-  for (int j = 0; j < J; ++j) {
-    Cam cam;
-    load_cam(intr + ((size_t)b * J + j) * 9, pose + ((size_t)b * J + j) * 16, cam);
-    // sample positions (reference operation order, as k_cost_mfma) and the taps' bounding box
-    float sx[BSPT], sy[BSPT];
-    int bx0 = 0x7fffffff, bx1 = -1, by0 = 0x7fffffff, by1 = -1;
-    {
-      const float fpx = (float)px, fpy = (float)y;
-      const float qx = cam.Kinv[0] * fpx + cam.Kinv[1] * fpy + cam.Kinv[2];
-      const float qy = cam.Kinv[3] * fpx + cam.Kinv[4] * fpy + cam.Kinv[5];
-      const float qz = cam.Kinv[6] * fpx + cam.Kinv[7] * fpy + cam.Kinv[8];
-      const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
-      const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
-      const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
+    for (int s = 0; s < SPT; ++s) prev[s] = cb[(uint32_t)(min(d0 + dl + 16 * s, D - 1) * HW + pc)];
+  };
+  const float* tg = tgt_hwc + bj * (size_t)(HW + 1) * C;
+  for (int r0 = 0; r0 < U; r0 += kEUMax) {
+    const int n = min(kEUMax, U - r0);
+    epi_list(L, H, W, r0, n);
+    __syncthreads();
+    // corr[16 x n] = aref[16 x C] . tgt[n x C]^T; per 16-channel step lane l feeds channels
+    // cb + 4 (l >> 4) + s to MFMA s (A and B permuted alike). The C / 16 row loads of a
+    // block are issued together.
+#ifndef DCV_X_NOGEMM
+    for (int blk = wv; blk * 16 < n; blk += 4) {
+#else
+    for (int blk = wv; blk * 16 < 0; blk += 4) {
+#endif
+      const int u = blk * 16 + (lane & 15);
+      const float* brow = tg + (size_t)L.list[u] * C + 4 * (lane >> 4);
+      float4 bv[NK / 4];
 #pragma unroll
-      for (int s = 0; s < BSPT; ++s) {
-        const int d = d0 + dl + 16 * s;
-        sx[s] = __int_as_float(0x7fc00000);
-        sy[s] = 0.f;
-        if (d < D && px < W) {
-          const float dep = depth_per_pixel ? depth[((size_t)b * D + d) * HW + (size_t)y * W + px]
-                                            : depth[(size_t)b * D + d];
-          const float X = prx * dep + cam.t[0];
-          const float Y = pry * dep + cam.t[1];
-          const float Z = prz * dep + cam.t[2];
-          const float xx = cam.K[0] * X + cam.K[1] * Y + cam.K[2] * Z;
-          const float yy = cam.K[3] * X + cam.K[4] * Y + cam.K[5] * Z;
-          const float zz = fmaxf(cam.K[6] * X + cam.K[7] * Y + cam.K[8] * Z, clampz);
-          const float u = xx / zz, v = yy / zz;
-          const float gxn = 2 * u / (W - 1) - 1;
-          const float gyn = 2 * v / (H - 1) - 1;
-          const float ix = ((gxn + 1) / 2) * (W - 1);
-          const float iy = ((gyn + 1) / 2) * (H - 1);
-          if (ix > -2.f && ix < (float)W + 1.f && iy > -2.f && iy < (float)H + 1.f) {
-            sx[s] = ix;
-            sy[s] = iy;
-            const int tx = (int)floorf(ix), ty = (int)floorf(iy);
-            const int cx0 = max(tx, 0), cx1 = min(tx + 1, W - 1), cy0 = max(ty, 0), cy1 = min(ty + 1, H - 1);
-            if (cx0 <= cx1 && cy0 <= cy1) {
-              bx0 = min(bx0, cx0);
-              bx1 = max(bx1, cx1);
-              by0 = min(by0, cy0);
-              by1 = max(by1, cy1);
-            }
-          }
-        }
+      for (int t = 0; t < NK / 4; ++t) bv[t] = *reinterpret_cast<const float4*>(brow + 16 * t);
+      const float* arow = L.aref + (lane & 15) * (C + 4) + 4 * (lane >> 4);
+      f32x4 c4[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int t = 0; t < NK / 4; ++t) {
+        const float4 av = *reinterpret_cast<const float4*>(arow + 16 * t);
+        f32x4& a4 = c4[t & 1];  // two independent accumulation chains
+        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[t].x, a4, 0, 0, 0);
+        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[t].y, a4, 0, 0, 0);
+        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[t].z, a4, 0, 0, 0);
+        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[t].w, a4, 0, 0, 0);
       }
-    }
-    bx0 = wave_min_i(bx0);
-    by0 = wave_min_i(by0);
-    bx1 = wave_max_i(bx1);
-    by1 = wave_max_i(by1);
-    if (lane == 0) {
-      s_box[wv * 4] = bx0;
-      s_box[wv * 4 + 1] = bx1;
-      s_box[wv * 4 + 2] = by0;
-      s_box[wv * 4 + 3] = by1;
+      // D[row][col]: col = lane & 15 (band position u), row = 4 (lane >> 4) + r (reference pixel)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) L.corr[(4 * (lane >> 4) + r) * kECorr + u] = c4[0][r] + c4[1][r];
     }
     __syncthreads();
+    if (r0 == 0 && accumulate) load_prev();  // the earlier views' sum, in flight across the gather
+    const float* crow = L.corr + i * kECorr;
+#ifdef DCV_X_NOGATHER
+    if (n == U) {
+    } else
+#endif
+    if (n == U) {
+      // the one pass holds every tap: straight-line gather; a zero sample reads ranks 0 / 1
+      // (written: the first 16 columns always are) with zero weights
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      bx0 = min(bx0, s_box[k * 4]);
-      bx1 = max(bx1, s_box[k * 4 + 1]);
-      by0 = min(by0, s_box[k * 4 + 2]);
-      by1 = max(by1, s_box[k * 4 + 3]);
-    }
-    const float* tg = tgt + ((size_t)b * J + j) * (size_t)C * HW;
-    if (bx1 >= bx0) {  // uniform: some sample taps the image
-      const int bw = bx1 - bx0 + 1, U = bw * (by1 - by0 + 1);
-      if (U <= kBandMax) {
-        // corr[16 x U] on the matrix cores: wave wv takes column blocks wv, wv + 4, ...
-        const int nblk = (U + 15) / 16;
-        for (int blk = wv; blk < nblk; blk += 4) {
-          const int u = blk * 16 + (lane & 15);
-          int q = -1;
-          if (u < U) {
-            const int r = u / bw;
-            q = (by0 + r) * W + bx0 + (u - r * bw);
-          }
-          float bv[NK];
-          const float* bp = tg + (size_t)(lane >> 4) * HW + (q < 0 ? 0 : q);
+      for (int s = 0; s < SPT; ++s) {
+        const bool ok = es[s] >= 0;
+        float x = ok ? sx[s] : 0.f, y = ok ? sy[s] : 0.f;
+        int e = ok ? es[s] : 0;
+        asm volatile("" : "+v"(x), "+v"(y), "+v"(e));  // weights formed here, not kept live across the GEMM
+        int ra = epi_rank(L, e), rb = epi_rank(L, e + Wx);  // taps (0, 1), (2, 3)
+        asm volatile("" : "+v"(ra), "+v"(rb));             // both reads issued, no branch
+        ra = ok ? ra : 0;
+        rb = ok ? rb : 0;
+        const float fx0 = floorf(x), fy0 = floorf(y);
+        const float wx0 = (fx0 + 1.f) - x, wx1 = x - fx0;
+        const float wy0 = ok ? (fy0 + 1.f) - y : 0.f, wy1 = ok ? y - fy0 : 0.f;
+        acc[s] = wx0 * wy0 * crow[ra] + wx1 * wy0 * crow[ra + 1] + wx0 * wy1 * crow[rb] + wx1 * wy1 * crow[rb + 1];
+      }
+    } else {
 #pragma unroll
-          for (int s = 0; s < NK; ++s) bv[s] = q >= 0 ? bp[(size_t)4 * s * HW] : 0.f;
-          // four independent accumulation chains (a dependent v_mfma_f32_16x16x4f32 waits ~40
-          // cycles for its accumulator), summed at the end
-          f32x4 c4[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) c4[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s = 0; s < NK; ++s) c4[s & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bv[s], c4[s & 3], 0, 0, 0);
-          c4[0] = (c4[0] + c4[1]) + (c4[2] + c4[3]);
-          // D[row][col]: col = lane & 15 (box pixel u), row = 4 (lane >> 4) + r (reference pixel)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s_corr[(4 * (lane >> 4) + r) * kCorrStride + u] = c4[0][r];
-        }
-        __syncthreads();
-        const float* crow = s_corr + i * kCorrStride;
-#pragma unroll
-        for (int s = 0; s < BSPT; ++s) {
-          if (!(sx[s] == sx[s])) continue;
-          const float fx0 = floorf(sx[s]), fy0 = floorf(sy[s]);
-          const int tx0 = (int)fx0, ty0 = (int)fy0;
-          const float wx0 = (float)(tx0 + 1) - sx[s], wx1 = sx[s] - fx0, wy0 = (float)(ty0 + 1) - sy[s],
-                      wy1 = sy[s] - fy0;
-          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
-          float sum = 0.f;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
-            if (tx >= 0 && tx < W && ty >= 0 && ty < H) sum += wt[t] * crow[(ty - by0) * bw + (tx - bx0)];
-          }
-          acc[s] += sum;
-        }
-      } else {
-        // the box is too large for LDS: each tap's dot product over C straight from memory
-#pragma unroll
-        for (int s = 0; s < BSPT; ++s) {
-          if (!(sx[s] == sx[s])) continue;
-          const float fx0 = floorf(sx[s]), fy0 = floorf(sy[s]);
-          const int tx0 = (int)fx0, ty0 = (int)fy0;
-          const float wx0 = (float)(tx0 + 1) - sx[s], wx1 = sx[s] - fx0, wy0 = (float)(ty0 + 1) - sy[s],
-                      wy1 = sy[s] - fy0;
-          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
-          float sum = 0.f;
-          for (int t = 0; t < 4; ++t) {
-            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
-            if (!(tx >= 0 && tx < W && ty >= 0 && ty < H)) continue;
-            const float* rp = ref + (size_t)b * C * HW + (size_t)y * W + px;
-            const float* qp = tg + (size_t)ty * W + tx;
-            float dot = 0.f;
-            for (int c = 0; c < C; ++c) dot += rp[(size_t)c * HW] * qp[(size_t)c * HW];
-            sum += wt[t] * dot;
-          }
-          acc[s] += sum;
-        }
+      for (int s = 0; s < SPT; ++s) {
+        if (es[s] < 0) continue;
+        float x = sx[s], y = sy[s];
+        int e = es[s];
+        asm volatile("" : "+v"(x), "+v"(y), "+v"(e));
+        const int ra = epi_rank(L, e) - r0, rb = epi_rank(L, e + Wx) - r0;
+        const float fx0 = floorf(x), fy0 = floorf(y);
+        const float wx0 = (fx0 + 1.f) - x, wx1 = x - fx0, wy0 = (fy0 + 1.f) - y, wy1 = y - fy0;
+        if (ra >= 0 && ra < n) acc[s] += wx0 * wy0 * crow[ra];
+        if (ra + 1 >= 0 && ra + 1 < n) acc[s] += wx1 * wy0 * crow[ra + 1];
+        if (rb >= 0 && rb < n) acc[s] += wx0 * wy1 * crow[rb];
+        if (rb + 1 >= 0 && rb + 1 < n) acc[s] += wx1 * wy1 * crow[rb + 1];
       }
     }
-    __syncthreads();  // s_corr / s_box reused by the next view
+    __syncthreads();  // list / corr reused by the next pass
   }
+  if (pix < 0) return;
+  if (U == 0 && accumulate) load_prev();  // no pass ran: no tap of this group is inside view j
 #pragma unroll
-  for (int s = 0; s < BSPT; ++s) {
+  for (int s = 0; s < SPT; ++s) {
     const int d = d0 + dl + 16 * s;
-    if (d < D && px < W) cost[((size_t)b * D + d) * HW + (size_t)y * W + px] = acc[s] * scale;
+    if (d < D) cb[(uint32_t)(d * HW + pix)] = accumulate ? prev[s] + acc[s] * scale : acc[s] * scale;
   }
 }
 
-size_t cost_band_lds_bytes() { return (size_t)(BTP * kCorrStride + 16) * sizeof(float); }
-
-size_t cost_mfma_bwd_lds_bytes(int C, int HW) {
-  const int NW = (HW + 31) / 32;
-  return sizeof(float) * ((size_t)2 * TP * C + 2 * DCH * TP + TP * kUMax + kUMax + 2 * NW + 8);
-}
-
-size_t cost_mfma_lds_bytes(int C, int HW) {
-  const int NW = (HW + 31) / 32;
-  return sizeof(float) * ((size_t)TP * C + 2 * DCH * TP + DCH * TP + TP * kUMax + kUMax + 2 * NW + 8);
+// Backward, view j (grid.x as the forward; depth chunks looped inside): per group the gradient
+// weights G[p][u] = sum over its samples' taps of dcost * scale * w (LDS), then
+// dref[p] += G[p, :] . tgt[band]  (MFMA, K = band) and dtgt[band] += G^T . aref  (MFMA,
+// K = 16 pixels; global float atomics: target pixels are shared between groups, so their
+// gradients arrive in any order). dref_hwc [B][HW][C] is written (view 0) or added to (views
+// after it, in launch order): each pixel is in exactly one group per view.
+template <int NK, int SPT>
+__global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
+                                                      int accumulate, const float* __restrict__ ref_hwc,
+                                                      const float* __restrict__ tgt_hwc,
+                                                      const int* __restrict__ groups, const float* __restrict__ geom,
+                                                      const float* __restrict__ depth,
+                                                      float clampz, float scale, const float* __restrict__ dcost,
+                                                      float* __restrict__ dref_hwc, float* __restrict__ dtgt_hwc) {
+  constexpr int C = 4 * NK;
+  extern __shared__ __attribute__((aligned(16))) float cv_lds[];
+  const int HW = H * W, ngroups = (HW + EG - 1) / EG, Wx = W + 2;
+  int b, g;
+  if (!epi_item(B, ngroups, b, g)) return;
+  const EpiLds L = epi_lds(cv_lds, C, epi_words(H, W), true);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = tid & (EG - 1), dl = tid >> 4;
+  const size_t bj = (size_t)b * J + j;
+  __shared__ int s_gid[EG];
+  if (tid < EG) s_gid[tid] = g * EG + tid < HW ? groups[bj * HW + g * EG + tid] : -1;
+  for (int k = tid; k < EG * (C + 4); k += 256) L.dacc[k] = 0.f;
+  __syncthreads();
+  epi_aref<NK>(L, HW, b, s_gid, ref_hwc);
+  const int pix = s_gid[i];
+  const EpiRay ry = epi_ray(geom + bj * 12, pix >= 0 ? (float)(pix % W) : 0.f, pix >= 0 ? (float)(pix / W) : 0.f);
+  const float* tg = tgt_hwc + bj * (size_t)(HW + 1) * C;
+  float* dtg = dtgt_hwc + bj * (size_t)(HW + 1) * C;
+  for (int d0 = 0; d0 < D; d0 += 16 * SPT) {  // depth chunks in turn: dacc is this workgroup's alone
+    float gs[SPT];
+    {
+      const float* gp = dcost + (size_t)b * D * HW;
+#pragma unroll
+      for (int s = 0; s < SPT; ++s) gs[s] = gp[(uint32_t)(min(d0 + dl + 16 * s, D - 1) * HW + max(pix, 0))];
+    }
+    float sx[SPT], sy[SPT];
+    int es[SPT];
+    const int U = epi_front<SPT>(L, H, W, HW, D, depth_per_pixel, b, d0, pix, ry, depth, clampz, sx, sy, es);
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) gs[s] = es[s] >= 0 ? gs[s] * scale : 0.f;
+    for (int r0 = 0; r0 < U; r0 += kEUMax) {
+      const int n = min(kEUMax, U - r0), np = epi_padded(n);
+      for (int k = tid; k < EG * np; k += 256) L.corr[(k & (EG - 1)) * kECorr + (k >> 4)] = 0.f;
+      epi_list(L, H, W, r0, n);
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < SPT; ++s) {
+        if (gs[s] == 0.f) continue;
+        float x = sx[s], y = sy[s];
+        int e = es[s];
+        asm volatile("" : "+v"(x), "+v"(y), "+v"(e));
+        const float fx0 = floorf(x), fy0 = floorf(y);
+        const float wx0 = (fx0 + 1.f) - x, wx1 = x - fx0, wy0 = (fy0 + 1.f) - y, wy1 = y - fy0;
+        const int ra = epi_rank(L, e) - r0, rb = epi_rank(L, e + Wx) - r0;
+        float* grow = L.corr + i * kECorr;
+        if (ra >= 0 && ra < n) atomicAdd(&grow[ra], gs[s] * (wx0 * wy0));
+        if (ra + 1 >= 0 && ra + 1 < n) atomicAdd(&grow[ra + 1], gs[s] * (wx1 * wy0));
+        if (rb >= 0 && rb < n) atomicAdd(&grow[rb], gs[s] * (wx0 * wy1));
+        if (rb + 1 >= 0 && rb + 1 < n) atomicAdd(&grow[rb + 1], gs[s] * (wx1 * wy1));
+      }
+      __syncthreads();
+      // dref[16 x C] += G[16 x np] . tgt[np x C]: wave wv owns channel blocks wv, wv + 4, ...
+      // (one writer per element: a fixed summation order); 32 band positions (8 MFMAs) per
+      // batch of loads
+      for (int cbk = wv; cbk < C / 16; cbk += 4) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* tcol = tg + cbk * 16 + (lane & 15);
+        for (int u0 = 0; u0 < np; u0 += kEPad) {
+          float av[kEPad / 4], bv[kEPad / 4];
+#pragma unroll
+          for (int t = 0; t < kEPad / 4; ++t) {
+            const int u = u0 + 4 * t + (lane >> 4);
+            bv[t] = tcol[(size_t)L.list[u] * C];
+            av[t] = L.corr[(lane & 15) * kECorr + u];
+          }
+#pragma unroll
+          for (int t = 0; t < kEPad / 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) L.dacc[(4 * (lane >> 4) + r) * (C + 4) + cbk * 16 + (lane & 15)] += acc[r];
+      }
+      // dtgt[n x C] += G^T[n x 16] . aref[16 x C]: (band block, channel block) pairs over the waves
+      const int nub = np / 16;
+      for (int pr = wv; pr < nub * (C / 16); pr += 4) {
+        const int ub = pr / (C / 16), cbk = pr - ub * (C / 16);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k0 = 0; k0 < EG; k0 += 4) {
+          const int u = ub * 16 + (lane & 15), p = k0 + (lane >> 4);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(L.corr[p * kECorr + u], L.aref[p * (C + 4) + cbk * 16 + (lane & 15)],
+                                                     acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = L.list[ub * 16 + 4 * (lane >> 4) + r];
+          if (q < HW && acc[r] != 0.f) atomicAdd(&dtg[(size_t)q * C + cbk * 16 + (lane & 15)], acc[r]);
+        }
+      }
+      __syncthreads();  // corr / list / dacc rows reused by the next pass
+    }
+  }
+  // the group's reference-gradient rows, channel-last (16-byte vectors)
+  for (int k = tid; k < EG * C / 4; k += 256) {
+    const int r = k / (C / 4), c4 = k - r * (C / 4), p = s_gid[r];
+    if (p < 0) continue;
+    const float4 v = *reinterpret_cast<const float4*>(L.dacc + r * (C + 4) + 4 * c4);
+    float4* o = reinterpret_cast<float4*>(dref_hwc + ((size_t)b * HW + p) * C + 4 * c4);
+    if (accumulate) {
+      const float4 o0 = *o;
+      *o = make_float4(o0.x + v.x, o0.y + v.y, o0.z + v.z, o0.w + v.w);
+    } else {
+      *o = v;
+    }
+  }
 }
 
 // Backward: one wave per (b, pixel); lanes over channels.
@@ -882,8 +857,8 @@ __global__ __launch_bounds__(256) void k_cost_bwd(int J, int C, int H, int W, in
       const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
       const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
       const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
-      const float* tg = tgt_hwc + ((size_t)b * J + j) * HW * C;
-      float* dtg = dtgt_hwc + ((size_t)b * J + j) * HW * C;
+      const float* tg = tgt_hwc + ((size_t)b * J + j) * (HW + 1) * C;
+      float* dtg = dtgt_hwc + ((size_t)b * J + j) * (HW + 1) * C;
       for (int d = 0; d < D; ++d) {
         const float g = dcost[((size_t)b * D + d) * HW + p] * scale;
         if (g == 0.f) continue;
@@ -981,60 +956,74 @@ int dcv_warp_bwd(int B, int C, int H, int W, int D, const float* dout, const flo
   return dsplat::check_launch("k_warp_bwd");
 }
 
+// forward workspace: tgt_hwc [B][J][HW + 1][C] | ref_hwc [B][HW + 1][C] | groups [B][J][HW] | geom [B][J][12]
+size_t dcv_cost_volume_workspace_size(int B, int J, int C, int H, int W) {
+  if (B <= 0 || J <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  const size_t rows = (size_t)H * W + 1;
+  return ((size_t)B * J * rows * C + (size_t)B * rows * C + (size_t)B * J * 12) * sizeof(float) +
+         (size_t)B * J * H * W * sizeof(int32_t);
+}
+// backward workspace: dtgt_hwc [B][J][HW + 1][C] | dref_hwc [B][HW][C]
+size_t dcv_cost_volume_bwd_workspace_size(int B, int J, int C, int H, int W) {
+  if (B <= 0 || J <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  return ((size_t)B * J * ((size_t)H * W + 1) * C + (size_t)B * H * W * C) * sizeof(float);
+}
+
+static bool epi_path(int C, int H, int W, bool bwd) {
+  return C % 16 == 0 && C <= 128 && epi_lds_bytes(C, H, W, bwd) <= 160 * 1024;
+}
+
 int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref,
                         const float* tgt, const float* intr, const float* pose, const float* depth,
-                        float clamp_min_depth, float* tgt_hwc, float* cost, void* stream) {
+                        float clamp_min_depth, void* workspace, float* cost, void* stream) {
   DSPLAT_REQUIRE(B > 0 && J > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_cost_volume_fwd: bad sizes B=%d J=%d C=%d H=%d W=%d D=%d", B, J, C, H, W, D);
-  DSPLAT_REQUIRE(ref && tgt && intr && pose && depth && cost, "dcv_cost_volume_fwd: null pointer");
+  DSPLAT_REQUIRE(ref && tgt && intr && pose && depth && workspace && cost, "dcv_cost_volume_fwd: null pointer");
   hipStream_t st = (hipStream_t)stream;
   const int HW = H * W;
-  // channel-last copy of the target features: only for the backward (when asked for) and the
-  // generic-C paths below; the band kernel reads [B,J,C,H,W] directly
-  const bool band = C == 16 || C == 32 || C == 64 || C == 128;
-  if (tgt_hwc || !band) {
-    DSPLAT_REQUIRE(tgt_hwc != nullptr, "dcv_cost_volume_fwd: C=%d needs the tgt_hwc workspace", C);
-    k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, tgt, tgt_hwc);
-    if (int e = dsplat::check_launch("k_to_hwc")) return e;
-  }
-  if (band) {
-    static bool attr = false;
-    const size_t lds = cost_band_lds_bytes();
-    if (!attr) {
-#define DCV_ATTR(NK)                                                                                          \
-  if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_cost_band<NK>,                             \
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), \
-                                "hipFuncSetAttribute(k_cost_band)"))                                         \
-    return e;
-      DCV_ATTR(4) DCV_ATTR(8) DCV_ATTR(16) DCV_ATTR(32)
-#undef DCV_ATTR
-      attr = true;
-    }
-    const dim3 grid((unsigned)(((W + BTP - 1) / BTP) * H), (unsigned)B, (unsigned)((D + BDCH - 1) / BDCH));
-#define DCV_BAND(NK)                                                                                             \
-  k_cost_band<NK><<<grid, 256, lds, st>>>(J, H, W, D, depth_per_pixel, ref, tgt, intr, pose, depth, clamp_min_depth, \
-                                          cost)
-    switch (C) {
-      case 16: DCV_BAND(4); break;
-      case 32: DCV_BAND(8); break;
-      case 64: DCV_BAND(16); break;
-      default: DCV_BAND(32); break;
-    }
-#undef DCV_BAND
-    return dsplat::check_launch("k_cost_band");
-  }
-  const size_t lds = cost_mfma_lds_bytes(C, HW);
-  if (C % 16 == 0 && lds <= 160 * 1024) {  // matrix-core path over the exact tapped set
+  float* tgt_hwc = static_cast<float*>(workspace);
+  float* ref_hwc = tgt_hwc + (size_t)B * J * (HW + 1) * C;
+  int* groups = reinterpret_cast<int*>(ref_hwc + (size_t)B * (HW + 1) * C);
+  float* geom = reinterpret_cast<float*>(groups + (size_t)B * J * HW);
+  // channel-last copies: a band pixel's C channels are one contiguous row for the GEMM's
+  // operands; row HW of each image is zero (the padding / out-of-image row)
+  k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc);
+  if (int e = dsplat::check_launch("k_to_hwc")) return e;
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  if (epi_path(C, H, W, false)) {
+    k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW + 1, ref, ref_hwc);
+    if (int e = dsplat::check_launch("k_to_hwc(ref)")) return e;
+    k_epi_groups<<<dim3(B, J), 1024, 0, st>>>(J, H, W, intr, pose, groups, geom);
+    if (int e = dsplat::check_launch("k_epi_groups")) return e;
+    const size_t lds = epi_lds_bytes(C, H, W, false);
     static size_t attr = 0;
-    if (lds > 64 * 1024 && lds > attr) {
-      if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_cost_mfma,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                                    "hipFuncSetAttribute(k_cost_mfma)"))
-        return e;
+    if (lds > attr) {
+#define DCV_ATTR(NK, SPT)                                                                                    \
+  if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_cost_epi<NK, SPT>,                        \
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), \
+                                "hipFuncSetAttribute(k_cost_epi)"))                                         \
+    return e;
+      DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
+      DCV_ATTR(4, 8) DCV_ATTR(8, 8) DCV_ATTR(16, 8) DCV_ATTR(32, 8)
+#undef DCV_ATTR
       attr = lds;
     }
-    k_cost_mfma<<<dim3((unsigned)(((W + TP - 1) / TP) * H), B), 256, lds, st>>>(
-        J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose, depth, clamp_min_depth, cost);
-    return dsplat::check_launch("k_cost_mfma");
+    const int ngroups = (HW + EG - 1) / EG;
+    const int spt = D <= 32 ? 2 : 8;
+    const dim3 grid(8u * (unsigned)((B * ngroups + 7) / 8), (unsigned)((D + 16 * spt - 1) / (16 * spt)));
+    for (int j = 0; j < J; ++j) {  // views in order: the sum over views is deterministic
+#define DCV_EPI(NK)                                                                                           \
+  (spt == 2 ? k_cost_epi<NK, 2> : k_cost_epi<NK, 8>)<<<grid, 256, lds, st>>>(B, j, J, H, W, D, depth_per_pixel, j > 0, ref_hwc, tgt_hwc, groups, geom, \
+                                         depth, clamp_min_depth, scale, cost)
+      switch (C) {
+        case 16: DCV_EPI(4); break;
+        case 32: DCV_EPI(8); break;
+        case 64: DCV_EPI(16); break;
+        default: DCV_EPI(32); break;
+      }
+#undef DCV_EPI
+      if (int e = dsplat::check_launch("k_cost_epi")) return e;
+    }
+    return 0;
   }
   k_cost_fwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
                                                    depth, clamp_min_depth, cost);
@@ -1042,34 +1031,59 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
 }
 
 int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref,
-                        const float* tgt_hwc, const float* intr, const float* pose, const float* depth,
-                        float clamp_min_depth, const float* dcost, float* dref, float* dtgt, float* dtgt_hwc,
+                        const void* workspace, const float* intr, const float* pose, const float* depth,
+                        float clamp_min_depth, const float* dcost, float* dref, float* dtgt, void* bwd_workspace,
                         void* stream) {
   DSPLAT_REQUIRE(B > 0 && J > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_cost_volume_bwd: bad sizes");
-  DSPLAT_REQUIRE(ref && tgt_hwc && intr && pose && depth && dcost && dref && dtgt && dtgt_hwc,
+  DSPLAT_REQUIRE(ref && workspace && intr && pose && depth && dcost && dref && dtgt && bwd_workspace,
                  "dcv_cost_volume_bwd: null pointer");
   hipStream_t st = (hipStream_t)stream;
   const int HW = H * W;
-  if (int e = dsplat::zero_async(dtgt_hwc, (size_t)B * J * HW * C * 4, st, "zero dtgt_hwc")) return e;
-  const size_t lds = cost_mfma_bwd_lds_bytes(C, HW);
-  if (C % 16 == 0 && lds <= 160 * 1024) {  // matrix-core path
+  const float* tgt_hwc = static_cast<const float*>(workspace);
+  const float* ref_hwc = tgt_hwc + (size_t)B * J * (HW + 1) * C;
+  const int* groups = reinterpret_cast<const int*>(ref_hwc + (size_t)B * (HW + 1) * C);
+  const float* geom = reinterpret_cast<const float*>(groups + (size_t)B * J * HW);
+  float* dtgt_hwc = static_cast<float*>(bwd_workspace);
+  float* dref_hwc = dtgt_hwc + (size_t)B * J * (HW + 1) * C;
+  if (int e = dsplat::zero_async(dtgt_hwc, (size_t)B * J * (HW + 1) * C * 4, st, "zero dtgt_hwc")) return e;
+  if (epi_path(C, H, W, true) && epi_path(C, H, W, false)) {
+    const size_t lds = epi_lds_bytes(C, H, W, true);
     static size_t attr = 0;
-    if (lds > 64 * 1024 && lds > attr) {
-      if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_cost_mfma_bwd,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                                    "hipFuncSetAttribute(k_cost_mfma_bwd)"))
-        return e;
+    if (lds > attr) {
+#define DCV_ATTR(NK, SPT)                                                                                    \
+  if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_cost_epi_bwd<NK, SPT>,                    \
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), \
+                                "hipFuncSetAttribute(k_cost_epi_bwd)"))                                     \
+    return e;
+      DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
+      DCV_ATTR(4, 8) DCV_ATTR(8, 8) DCV_ATTR(16, 8) DCV_ATTR(32, 8)
+#undef DCV_ATTR
       attr = lds;
     }
-    k_cost_mfma_bwd<<<dim3((unsigned)(((W + TP - 1) / TP) * H), B), 256, lds, st>>>(
-        J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose, depth, clamp_min_depth, dcost, dref, dtgt_hwc);
-    if (int e = dsplat::check_launch("k_cost_mfma_bwd")) return e;
+    const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+    const int ngroups = (HW + EG - 1) / EG, spt = D <= 32 ? 2 : 8;
+    const dim3 grid(8u * (unsigned)((B * ngroups + 7) / 8));
+    for (int j = 0; j < J; ++j) {
+#define DCV_EPIB(NK)                                                                                           \
+  (spt == 2 ? k_cost_epi_bwd<NK, 2> : k_cost_epi_bwd<NK, 8>)<<<grid, 256, lds, st>>>(B, j, J, H, W, D, depth_per_pixel, j > 0, ref_hwc, tgt_hwc, groups, \
+                                             geom, depth, clamp_min_depth, scale, dcost, dref_hwc, dtgt_hwc)
+      switch (C) {
+        case 16: DCV_EPIB(4); break;
+        case 32: DCV_EPIB(8); break;
+        case 64: DCV_EPIB(16); break;
+        default: DCV_EPIB(32); break;
+      }
+#undef DCV_EPIB
+      if (int e = dsplat::check_launch("k_cost_epi_bwd")) return e;
+    }
+    k_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW, dref_hwc, dref);
+    if (int e = dsplat::check_launch("k_to_chw(dref)")) return e;
   } else {
     k_cost_bwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
                                                      depth, clamp_min_depth, dcost, dref, dtgt_hwc);
     if (int e = dsplat::check_launch("k_cost_bwd")) return e;
   }
-  k_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, dtgt_hwc, dtgt);
+  k_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_hwc, dtgt);
   return dsplat::check_launch("k_to_chw");
 }
 

@@ -77,29 +77,28 @@ class _CostVolume(torch.autograd.Function):
         D = depth.shape[1]
         dev = ref.device
         st = _lib.stream_of(dev)
-        # the channel-last copy of the targets is only made for the backward (and for channel
-        # counts the band kernel does not take); inference reads [B,J,C,H,W] directly
-        need_hwc = ctx.needs_input_grad[0] or ctx.needs_input_grad[1] or C not in (16, 32, 64, 128)
-        tgt_hwc = torch.empty((B, J, H, W, C), dtype=torch.float32, device=dev) if need_hwc else None
+        # channel-last copies of the features + the epipolar pixel groups (the backward reuses them)
+        ws = torch.empty(lib.dcv_cost_volume_workspace_size(B, J, C, H, W), dtype=torch.uint8, device=dev)
         cost = torch.empty((B, D, H, W), dtype=torch.float32, device=dev)
         _lib.check(lib.dcv_cost_volume_fwd(B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), tgt.data_ptr(),
                                            intrinsics.data_ptr(), pose.data_ptr(), depth.data_ptr(), clamp,
-                                           _lib.ptr(tgt_hwc), cost.data_ptr(), st), "dcv_cost_volume_fwd")
-        ctx.save_for_backward(ref, tgt_hwc, intrinsics, pose, depth)
+                                           ws.data_ptr(), cost.data_ptr(), st), "dcv_cost_volume_fwd")
+        ctx.save_for_backward(ref, ws, intrinsics, pose, depth)
         ctx.meta = (B, J, C, H, W, D, per_pixel, clamp)
         return cost
 
     @staticmethod
     def backward(ctx, dcost):
-        ref, tgt_hwc, intrinsics, pose, depth = ctx.saved_tensors
+        ref, ws, intrinsics, pose, depth = ctx.saved_tensors
         B, J, C, H, W, D, per_pixel, clamp = ctx.meta
         dev = ref.device
         dcost = _f(dcost)
         dref = torch.empty_like(ref)
         dtgt = torch.empty((B, J, C, H, W), dtype=torch.float32, device=dev)
-        scratch = torch.empty((B, J, H, W, C), dtype=torch.float32, device=dev)
-        _lib.check(_lib.load().dcv_cost_volume_bwd(
-            B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), tgt_hwc.data_ptr(), intrinsics.data_ptr(),
+        lib = _lib.load()
+        scratch = torch.empty(lib.dcv_cost_volume_bwd_workspace_size(B, J, C, H, W), dtype=torch.uint8, device=dev)
+        _lib.check(lib.dcv_cost_volume_bwd(
+            B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), ws.data_ptr(), intrinsics.data_ptr(),
             pose.data_ptr(), depth.data_ptr(), clamp, dcost.data_ptr(), dref.data_ptr(), dtgt.data_ptr(),
             scratch.data_ptr(), _lib.stream_of(dev)), "dcv_cost_volume_bwd")
         return dref, dtgt, None, None, None, None, None
