@@ -128,7 +128,14 @@ int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, in
                             const float* intrinsics, const float* near, const float* far,
                             const float* bg, const int32_t* view_scene, int scale_invariant,
                             dsr_camera* cams, float* geom, int32_t* radii, int64_t* dgeom_zero,
-                            uint32_t* seg_count, uint64_t* keys, int layout, void* stream);
+                            uint32_t* seg_count, uint64_t* keys, uint32_t seg_capacity, int layout,
+                            void* stream);
+/* seg_capacity (bounded key memory; 0 = G): segment (v, t) = keys[(v*T + t) * seg_capacity ...],
+ * keys / scratch hold V*T*seg_capacity entries. A tile that receives more entries keeps the
+ * first seg_capacity of them while seg_count goes on counting; dsr_sort_render (seg_stride =
+ * seg_capacity) recognises such a segment (count > stride) and rebuilds its list from the
+ * geometry records (the binning test is a function of one record), so images are identical
+ * for every capacity — a capacity above the largest tile list only saves the rebuild. */
 
 /* Exclusive scan of seg_count[V*T] -> seg_start[V*T+1], seg_cursor[V*T] (= seg_start),
  * totals[0] = N (num_rendered over all views), totals[1] = max entries in one tile,
@@ -260,9 +267,15 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                     const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
                     uint64_t* scratch, int write_keys, int clear_counts, uint32_t max_count_hint,
-                    float* out_color, float* final_T, uint32_t* n_contrib, void* stream);
+                    int binning_layout, float* out_color, float* final_T, uint32_t* n_contrib,
+                    void* stream);
 /* clear_counts != 0 (fixed-capacity layout only): seg_count is zeroed as it is consumed, so
- * the buffer can serve the next dsr_project_bin_cameras call as already-zeroed counters. */
+ * the buffer can serve the next dsr_project_bin_cameras call as already-zeroed counters.
+ * Bounded capacity (dsr_project_bin_cameras seg_capacity < G, seg_stride = that capacity): a
+ * segment with seg_count[s] > seg_stride is rebuilt by its workgroup from the view's geometry
+ * records with the binning test of `binning_layout` (the layout bits of the binning call:
+ * DSR_LAYOUT_RECT_BINNING = 3-sigma rects, else the exact test) and composited in depth
+ * windows of the LDS capacity (slow, exact). write_keys requires seg_stride >= G. */
 
 /* ---- rasterizer backward -----------------------------------------------------------
  * Deterministic: every per-Gaussian gradient is a sum over (tile, sub-tile wave) partials,

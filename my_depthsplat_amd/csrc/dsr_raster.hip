@@ -52,15 +52,19 @@ struct F3 {
   float x, y, z;
 };
 
+// The projection chain is written with explicit FMAs in a fixed order (the file is compiled
+// with -ffp-contract=off, so no other contraction happens); oracle/dsr_oracle.cpp evaluates
+// the same sequence with std::fma, which keeps depth, radius, xy, conic, rgb and the tile
+// lists bit-identical while each multiply-add is one instruction.
 __device__ __forceinline__ F3 xform43(const float* m, F3 p) {
   F3 r;
-  r.x = m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12];
-  r.y = m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13];
-  r.z = m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14];
+  r.x = fmaf(m[0], p.x, fmaf(m[4], p.y, fmaf(m[8], p.z, m[12])));
+  r.y = fmaf(m[1], p.x, fmaf(m[5], p.y, fmaf(m[9], p.z, m[13])));
+  r.z = fmaf(m[2], p.x, fmaf(m[6], p.y, fmaf(m[10], p.z, m[14])));
   return r;
 }
 __device__ __forceinline__ float xform44w(const float* m, F3 p) {
-  return m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15];
+  return fmaf(m[3], p.x, fmaf(m[7], p.y, fmaf(m[11], p.z, m[15])));
 }
 __device__ __forceinline__ float ndc2pix(float v, int S) {
   return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
@@ -198,43 +202,52 @@ __device__ __forceinline__ void cov2d(F3 mean, float fx, float fy, float tanx, f
   const float W00 = view[0], W01 = view[4], W02 = view[8];
   const float W10 = view[1], W11 = view[5], W12 = view[9];
   const float W20 = view[2], W21 = view[6], W22 = view[10];
-  w.T[0][0] = j00 * W00 + j02 * W20;
-  w.T[0][1] = j00 * W01 + j02 * W21;
-  w.T[0][2] = j00 * W02 + j02 * W22;
-  w.T[1][0] = j11 * W10 + j12 * W20;
-  w.T[1][1] = j11 * W11 + j12 * W21;
-  w.T[1][2] = j11 * W12 + j12 * W22;
+  w.T[0][0] = fmaf(j00, W00, j02 * W20);
+  w.T[0][1] = fmaf(j00, W01, j02 * W21);
+  w.T[0][2] = fmaf(j00, W02, j02 * W22);
+  w.T[1][0] = fmaf(j11, W10, j12 * W20);
+  w.T[1][1] = fmaf(j11, W11, j12 * W21);
+  w.T[1][2] = fmaf(j11, W12, j12 * W22);
   const float V[3][3] = {{c6[0], c6[1], c6[2]}, {c6[1], c6[3], c6[4]}, {c6[2], c6[4], c6[5]}};
   float U[2][3];
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) U[r][c] = w.T[r][0] * V[0][c] + w.T[r][1] * V[1][c] + w.T[r][2] * V[2][c];
-  const float a = U[0][0] * w.T[0][0] + U[0][1] * w.T[0][1] + U[0][2] * w.T[0][2];
-  const float b = U[0][0] * w.T[1][0] + U[0][1] * w.T[1][1] + U[0][2] * w.T[1][2];
-  const float c = U[1][0] * w.T[1][0] + U[1][1] * w.T[1][1] + U[1][2] * w.T[1][2];
+    for (int c = 0; c < 3; ++c) U[r][c] = fmaf(w.T[r][0], V[0][c], fmaf(w.T[r][1], V[1][c], w.T[r][2] * V[2][c]));
+  const float a = fmaf(U[0][0], w.T[0][0], fmaf(U[0][1], w.T[0][1], U[0][2] * w.T[0][2]));
+  const float b = fmaf(U[0][0], w.T[1][0], fmaf(U[0][1], w.T[1][1], U[0][2] * w.T[1][2]));
+  const float c = fmaf(U[1][0], w.T[1][0], fmaf(U[1][1], w.T[1][1], U[1][2] * w.T[1][2]));
   w.a = a + 0.3f;
   w.b = b;
   w.c = c + 0.3f;
 }
 
 // SH (degree DEG) -> one colour channel; s(k) = coefficient k of this channel.
+// The basis values (channel-independent) are formed first, then each channel is accumulated
+// coefficient by coefficient with one FMA each (oracle: sh_to_rgb, same order).
 template <int DEG>
 __device__ __forceinline__ float sh_eval(const float* sh, int ch, float x, float y, float z) {
   auto s = [&](int k) { return sh[k * 3 + ch]; };
   float v = SH_C0 * s(0);
   if constexpr (DEG > 0) {
-    v = v - SH_C1 * y * s(1) + SH_C1 * z * s(2) - SH_C1 * x * s(3);
+    v = fmaf(-(SH_C1 * y), s(1), v);
+    v = fmaf(SH_C1 * z, s(2), v);
+    v = fmaf(-(SH_C1 * x), s(3), v);
     if constexpr (DEG > 1) {
       const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-      v = v + SH_C2_0 * xy * s(4) + SH_C2_1 * yz * s(5) + SH_C2_2 * (2.0f * zz - xx - yy) * s(6) +
-          SH_C2_3 * xz * s(7) + SH_C2_4 * (xx - yy) * s(8);
+      v = fmaf(SH_C2_0 * xy, s(4), v);
+      v = fmaf(SH_C2_1 * yz, s(5), v);
+      v = fmaf(SH_C2_2 * (2.0f * zz - xx - yy), s(6), v);
+      v = fmaf(SH_C2_3 * xz, s(7), v);
+      v = fmaf(SH_C2_4 * (xx - yy), s(8), v);
       if constexpr (DEG > 2) {
-        v = v + SH_C3_0 * y * (3.0f * xx - yy) * s(9) + SH_C3_1 * xy * z * s(10) +
-            SH_C3_2 * y * (4.0f * zz - xx - yy) * s(11) +
-            SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * s(12) +
-            SH_C3_4 * x * (4.0f * zz - xx - yy) * s(13) + SH_C3_5 * z * (xx - yy) * s(14) +
-            SH_C3_6 * x * (xx - 3.0f * yy) * s(15);
+        v = fmaf(SH_C3_0 * y * (3.0f * xx - yy), s(9), v);
+        v = fmaf(SH_C3_1 * xy * z, s(10), v);
+        v = fmaf(SH_C3_2 * y * (4.0f * zz - xx - yy), s(11), v);
+        v = fmaf(SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy), s(12), v);
+        v = fmaf(SH_C3_4 * x * (4.0f * zz - xx - yy), s(13), v);
+        v = fmaf(SH_C3_5 * z * (xx - yy), s(14), v);
+        v = fmaf(SH_C3_6 * x * (xx - 3.0f * yy), s(15), v);
       }
     }
   }
@@ -533,11 +546,11 @@ __device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_c
     const float fy = H / (2.0f * cam->tanfovy);
     Cov2D w;
     cov2d(p, fx, fy, cam->tanfovx, cam->tanfovy, c6, view, w);
-    const float det = w.a * w.c - w.b * w.b;
+    const float det = fmaf(w.a, w.c, -(w.b * w.b));
     if (det != 0.0f) {
       const float det_inv = 1.f / det;
       const float mid = 0.5f * (w.a + w.c);
-      const float disc = sqrtf(fmaxf(0.1f, mid * mid - det));
+      const float disc = sqrtf(fmaxf(0.1f, fmaf(mid, mid, -det)));
       const float l1 = mid + disc, l2 = mid - disc;
       const int rr = (int)ceilf(3.f * sqrtf(fmaxf(l1, l2)));
       const float px = ndc2pix(ndx, W), py = ndc2pix(ndy, H);
@@ -549,7 +562,7 @@ __device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_c
           float sh[GaussIn<DEG>::NC * 3];
           load_sh<GaussIn<DEG>::NC>(shs, in.sg, M, layout, sh);
           float dx = p.x - cam->campos[0], dy = p.y - cam->campos[1], dz = p.z - cam->campos[2];
-          const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+          const float len = sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
           dx = dx / len;
           dy = dy / len;
           dz = dz / len;
@@ -755,7 +768,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
                                                      float* __restrict__ geom, int32_t* __restrict__ radii,
                                                      long long* __restrict__ dzero,
                                                      uint32_t* __restrict__ seg_count,
-                                                     uint64_t* __restrict__ keys, int layout, CamIn ci) {
+                                                     uint64_t* __restrict__ keys, uint32_t cap, int layout,
+                                                     CamIn ci) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
@@ -826,13 +840,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
     if (c) s_hist[t] = atomicAdd(&gcount[t], c);
   }
   __syncthreads();
-  uint64_t* vkeys = keys + (size_t)v * T * G;
+  // segment (v, t) = keys[(v T + t) cap ...]: cap = G holds every entry a tile can get; a
+  // smaller capacity (bounded key memory) keeps the first cap arrivals, the count goes on,
+  // and dsr_sort_render rebuilds such a segment from the geometry records
+  uint64_t* vkeys = keys + (size_t)v * T * cap;
   if (!s_ovf) {  // workgroup-uniform
     for (uint32_t j = (uint32_t)lane; j < wtotal; j += 64u) {
       const uint32_t p = wp[j];
       if (EXACT && p == 0xFFFFFFFFu) continue;
       const uint32_t t = p & 0xFFFFu;
-      vkeys[(size_t)t * G + s_hist[t] + ((p >> 16) & 0xFFu)] = wkey[p >> 24];
+      const uint32_t off = s_hist[t] + ((p >> 16) & 0xFFu);
+      if (off < cap) vkeys[(size_t)t * cap + off] = wkey[p >> 24];
     }
     return;
   }
@@ -844,7 +862,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
     if constexpr (EXACT) {
       if (!tile_reach(oe, tx, ty)) return;
     }
-    vkeys[(size_t)t * G + atomicAdd(&s_hist[t], 1u)] = wkey[o];
+    const uint32_t off = atomicAdd(&s_hist[t], 1u);
+    if (off < cap) vkeys[(size_t)t * cap + off] = wkey[o];
   }, fetch);
 }
 
@@ -2508,12 +2527,158 @@ constexpr size_t sort_render_lds_bytes() {
   return (size_t)(NT * KMAX + NT) * 8 + (size_t)sort_render_aux_words<NBL>() * 4 + 64 * 4;
 }
 
+// ---- bounded-capacity segments ---------------------------------------------------------
+// dsr_project_bin_cameras with seg_capacity < G keeps only the first `capacity` entries a tile
+// receives (the count goes on). Such a tile's list is rebuilt from the view's geometry records:
+// the binning test is a function of one record, so evaluating it for every Gaussian of the
+// view gives the tile's full entry set. record_hits_tile is k_project_emit's keep test (the
+// 3-sigma rect; with EXACT the alpha >= 1/255 rect and tile_reach) on the stored fields.
+__device__ __forceinline__ bool record_hits_tile(float4 q, float4 rr, float4 z, int gx, int gy, int tx, int ty,
+                                                 bool exact) {
+  const int r = __float_as_int(z.z);  // rec[10]
+  if (r <= 0) return false;
+  int x0, y0, x1, y1;
+  tile_rect(q.x, q.y, r, gx, gy, x0, y0, x1, y1);
+  if (!exact) return tx >= x0 && tx < x1 && ty >= y0 && ty < y1;
+  const float rec[6] = {q.x, q.y, q.z, q.w, rr.x, rr.y};
+  const TileEll e = tile_ell(rec, r);
+  tile_rect_alpha(e, x0, y0, x1, y1);
+  if (!(tx >= x0 && tx < x1 && ty >= y0 && ty < y1)) return false;
+  return tile_reach(e, tx, ty);
+}
+
+// Rank selection over a per-digit histogram (NB u32 bins in LDS, NB / NT per thread): the
+// digit d holding the r-th candidate (1-based) and the number of candidates in lower digits;
+// d = 0xffffffff when fewer than r candidates exist. Block-uniform results (flag[0..1]).
+template <int NB>
+__device__ __forceinline__ void hist_select(const uint32_t* hist, uint32_t r, uint32_t* wsum, uint32_t* flag,
+                                            uint32_t& d, uint32_t& below) {
+  constexpr int BPT = NB / NT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t c[BPT], tot = 0;
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    c[i] = hist[tid * BPT + i];
+    tot += c[i];
+  }
+  const uint32_t incl = dsplat::wave_incl_add_dpp(tot);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t off = incl - tot;
+  for (int k = 0; k < w; ++k) off += wsum[k];
+  if (r > off && r <= off + tot) {
+    uint32_t acc = off;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      if (r > acc && r <= acc + c[i]) {
+        flag[0] = (uint32_t)(tid * BPT + i);
+        flag[1] = acc;
+      }
+      acc += c[i];
+    }
+  }
+  __syncthreads();
+  d = flag[0];
+  below = flag[1];
+  __syncthreads();
+}
+
+// Composite a rebuilt tile: its entries (keys above `lo`, in key order) are taken in windows
+// of at most the LDS capacity — the window's last key found by a radix select over 11-bit
+// digits of the 64-bit keys (one pass over the view's records per digit; a pass stops the
+// descent once half a window is certain) — each window sorted in LDS (count_sort) and
+// composited before the next, until every pixel has stopped or the list is exhausted.
+// Entries are blended in exactly the full list's order, so the image equals the unbounded
+// layout's. LAST: n_contrib positions count from the list's start.
+template <int KMAX, bool LAST, int NBL>
+__device__ __attribute__((noinline)) void render_rebuilt(int G, int gx, int gy, int tx, int ty, bool exact, const float* __restrict__ gv,
+                               uint64_t* A, uint16_t* cnt, uint32_t* wsum, uint32_t* flag, int id_bits, float fx0,
+                               float fy0, const PixUV2& pp, int lane, uint64_t lt, WaveList* plist, float& Tr, f2v& C01,
+                               float& C2, uint32_t& last, bool& alive) {
+  constexpr uint32_t capl = NT * KMAX;
+  constexpr int kNB = 2048;  // 11-bit digits
+  static_assert((NT * KMAX + NT) * 2 >= kNB, "digit histogram fits the key array");
+  uint32_t* hist = reinterpret_cast<uint32_t*>(A);
+  const int tid = threadIdx.x;
+  auto key_of = [&](uint32_t g, uint64_t& key) -> bool {
+    const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)g * GS);
+    const float4 q = rec[0], rr = rec[1], z = rec[2];
+    if (!record_hits_tile(q, rr, z, gx, gy, tx, ty, exact)) return false;
+    key = ((uint64_t)__float_as_uint(z.y) << 32) | g;  // (depth rec[9], id): k_project_emit's key
+    return true;
+  };
+  uint64_t lo = 0ull;  // exclusive: every key is > 0 (depth > 0.2)
+  uint32_t base = 0;
+  for (;;) {
+    uint64_t hi = ~0ull;
+    {
+      uint64_t prefix = 0ull;
+      int pbits = 0;
+      uint32_t r = capl, taken = 0;
+      for (int shift = 53;; shift = max(shift - 11, 0)) {
+        const int width = 64 - pbits - shift;
+        for (int i = tid; i < kNB; i += NT) hist[i] = 0u;
+        if (tid == 0) flag[0] = 0xffffffffu;
+        __syncthreads();
+        for (uint32_t g = (uint32_t)tid; g < (uint32_t)G; g += NT) {
+          uint64_t key;
+          if (!key_of(g, key) || key <= lo) continue;
+          if (pbits != 0 && (key >> (64 - pbits)) != prefix) continue;
+          atomicAdd(&hist[(uint32_t)(key >> shift) & ((1u << width) - 1u)], 1u);
+        }
+        __syncthreads();
+        uint32_t d, below;
+        hist_select<kNB>(hist, r, wsum, flag, d, below);
+        if (d == 0xffffffffu) break;  // (level 0 only) the rest of the list fits one window: hi = ~0
+        taken += below;
+        r -= below;
+        const uint64_t cell = (prefix << width) | d;
+        if (shift == 0) {  // digits exhausted: the r-th candidate itself closes the window
+          hi = cell;
+          break;
+        }
+        if (taken >= capl / 2 && cell != 0ull) {  // every key below digit d: at least half a window
+          hi = (cell << shift) - 1ull;
+          break;
+        }
+        prefix = cell;
+        pbits += width;
+      }
+    }
+    if (tid == 0) flag[2] = 0u;
+    __syncthreads();
+    for (uint32_t g = (uint32_t)tid; g < (uint32_t)G; g += NT) {
+      uint64_t key;
+      if (!key_of(g, key) || key <= lo || key > hi) continue;
+      A[padi<KMAX>(atomicAdd(&flag[2], 1u))] = key;
+    }
+    __syncthreads();
+    const uint32_t n = flag[2];
+    uint64_t tmp[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      const uint32_t idx = tid + (uint32_t)i * NT;
+      tmp[i] = idx < n ? A[padi<KMAX>(idx)] : 0ull;
+    }
+    __syncthreads();
+    if (n > 1) count_sort<KMAX, NT, NBL>(tmp, n, A, id_bits, cnt, wsum, flag);
+    uint32_t wl = 0;
+    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)A[padi<KMAX>(i)]; }, 0u, n, gv, fx0, fy0, pp, lane, lt,
+                         plist, Tr, C01, C2, wl, alive);
+    if (LAST && wl) last = base + wl;
+    const bool more = __syncthreads_or(alive);
+    if (!more || hi == ~0ull) break;
+    lo = hi;
+    base += n;
+  }
+}
+
 template <int KMAX, bool LAST, int NBL, int WPE>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_sort_render(
     int G, int H, int W, int gx, int T, const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
     const uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_count, uint32_t stride,
     uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits, int write_keys, int clear_counts,
-    float* __restrict__ out, float* __restrict__ finalT, uint32_t* __restrict__ ncontrib) {
+    int exact_rebuild, float* __restrict__ out, float* __restrict__ finalT, uint32_t* __restrict__ ncontrib) {
   constexpr uint32_t cap = NT * KMAX;
   constexpr uint32_t padded = cap + cap / KMAX;
   extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
@@ -2527,6 +2692,26 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   int tx, ty;
   const int v = tile_xcd(gx, T / gx, tx, ty);  // kbench: 3 views -4.7 %, 24 / 64 views -0.6 %
   const int seg = v * T + ty * gx + tx;
+  if (stride != 0u && stride != kSegEnds && seg_count[seg] > stride) {  // bounded segment that overflowed
+    const int sx0 = tx * BX + (w & 1) * SUB, sy0 = ty * BY + (w >> 1) * SUB;
+    const int px = sx0 + (lane & (SUB - 1)), py = sy0 + (lane >> 3);
+    const bool inside = px < W && py < H;
+    const PixUV2 pp = pix_uv2(pix_uv(px, py, (float)sx0, (float)sy0));
+    f2v C01 = {0.f, 0.f};
+    float Tr = 1.0f, C2 = 0.f;
+    bool alive = inside;
+    uint32_t last = 0;
+    render_rebuilt<KMAX, LAST, NBL>(G, gx, T / gx, tx, ty, exact_rebuild != 0, geom + (size_t)v * G * GS, s_keys,
+                                    reinterpret_cast<uint16_t*>(reinterpret_cast<uint32_t*>(s_keys + padded)),
+                                    reinterpret_cast<uint32_t*>(s_keys + padded) + sort_render_aux_words<NBL>(),
+                                    reinterpret_cast<uint32_t*>(s_keys + padded) + sort_render_aux_words<NBL>() + 16,
+                                    id_bits, (float)sx0, (float)sy0, pp, lane, dsplat::lanemask_lt(lane),
+                                    reinterpret_cast<WaveList*>(reinterpret_cast<uint32_t*>(s_keys + padded)) + w, Tr,
+                                    C01, C2, last, alive);
+    if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
+    if (clear_counts && tid == 0) seg_count[seg] = 0u;
+    return;
+  }
   uint32_t b, e;
   seg_bounds(seg_start, seg_count, stride, seg, b, e);
   const uint32_t n = e - b;
@@ -3238,7 +3423,7 @@ namespace {
 int project_bin_impl(const char* who, int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                      const float* shs, const float* colors, const float* opacities, const float* cov6,
                      dsr_camera* cams, const CamIn* ci, float* geom, int32_t* radii, long long* dzero,
-                     uint32_t* seg_count, uint64_t* keys, int layout, void* stream) {
+                     uint32_t* seg_count, uint64_t* keys, uint32_t cap, int layout, void* stream) {
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "%s: bad sizes S=%d G=%d V=%d H=%d W=%d", who, S, G, V, H, W);
   DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "%s: exactly one of shs/colors must be given", who);
   DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
@@ -3246,7 +3431,9 @@ int project_bin_impl(const char* who, int S, int G, int V, int H, int W, int sh_
   DSPLAT_REQUIRE(means && opacities && cov6 && cams && geom && radii && seg_count && keys, "%s: null pointer", who);
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H), T = gx * gy;
   DSPLAT_REQUIRE(T <= kHistLdsMax, "%s: %d tiles per view exceed the LDS histogram (%d)", who, T, kHistLdsMax);
-  DSPLAT_REQUIRE((uint64_t)V * T * G < (1ull << 32), "%s: V*tiles*G must fit 32-bit key offsets", who);
+  if (cap == 0) cap = (uint32_t)G;
+  DSPLAT_REQUIRE(cap <= (uint32_t)G, "%s: segment capacity %u above G = %d", who, cap, G);
+  DSPLAT_REQUIRE((uint64_t)V * T * cap < (1ull << 32), "%s: V*tiles*capacity must fit 32-bit key offsets", who);
   hipStream_t st = (hipStream_t)stream;
   if (!(layout & kLayoutCountsZeroed))
     if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
@@ -3257,19 +3444,19 @@ int project_bin_impl(const char* who, int S, int G, int V, int H, int W, int sh_
     if (ci && !(layout & kLayoutRectBinning))                                                                  \
       k_project_emit<D, true, true><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,         \
                                                              opacities, cov6, cams, geom, radii, dzero, seg_count,     \
-                                                             keys, layout, *ci);                                \
+                                                             keys, cap, layout, *ci);                                \
     else if (ci)                                                                                               \
       k_project_emit<D, true, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,        \
                                                               opacities, cov6, cams, geom, radii, dzero, seg_count,    \
-                                                              keys, layout, *ci);                               \
+                                                              keys, cap, layout, *ci);                               \
     else if (layout & kLayoutExactBinning)                                                                     \
       k_project_emit<D, false, true><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,        \
                                                               opacities, cov6, cams, geom, radii, dzero, seg_count,    \
-                                                              keys, layout, CamIn{});                           \
+                                                              keys, cap, layout, CamIn{});                           \
     else                                                                                                       \
       k_project_emit<D, false, false><<<grid, NT, T * 4, st>>>(G, V, H, W, gx, gy, M, means, shs, colors,       \
                                                                opacities, cov6, cams, geom, radii, dzero, seg_count,   \
-                                                               keys, layout, CamIn{});                          \
+                                                               keys, cap, layout, CamIn{});                          \
   } while (0)
   switch (deg) {
     case -1: DSR_PB(-1); break;
@@ -3290,7 +3477,7 @@ int dsr_project_bin(int S, int G, int V, int H, int W, int sh_degree, int M, con
                     void* stream) {
   return project_bin_impl("dsr_project_bin", S, G, V, H, W, sh_degree, M, means, shs, colors, opacities, cov6,
                           const_cast<dsr_camera*>(cams), nullptr, geom, radii,
-                          reinterpret_cast<long long*>(dgeom_zero), seg_count, keys, layout, stream);
+                          reinterpret_cast<long long*>(dgeom_zero), seg_count, keys, (uint32_t)G, layout, stream);
 }
 
 int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
@@ -3298,13 +3485,13 @@ int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, in
                             const float* extrinsics, const float* intrinsics, const float* near, const float* far,
                             const float* bg, const int32_t* view_scene, int scale_invariant, dsr_camera* cams,
                             float* geom, int32_t* radii, int64_t* dgeom_zero, uint32_t* seg_count, uint64_t* keys,
-                            int layout, void* stream) {
+                            uint32_t seg_capacity, int layout, void* stream) {
   DSPLAT_REQUIRE(extrinsics && intrinsics && near && far && bg && view_scene,
                  "dsr_project_bin_cameras: null camera input");
   const CamIn ci{extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant};
   return project_bin_impl("dsr_project_bin_cameras", S, G, V, H, W, sh_degree, M, means, shs, colors, opacities,
                           cov6, cams, &ci, geom, radii, reinterpret_cast<long long*>(dgeom_zero), seg_count, keys,
-                          layout, stream);
+                          seg_capacity, layout, stream);
 }
 
 int dsr_bin_scan(int V, int H, int W, const uint32_t* seg_count, uint32_t* seg_start, uint32_t* seg_cursor,
@@ -3576,8 +3763,10 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                     const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
                     uint64_t* scratch, int write_keys, int clear_counts, uint32_t max_count_hint,
-                    float* out_color, float* final_T, uint32_t* n_contrib, void* stream) {
+                    int binning_layout, float* out_color, float* final_T, uint32_t* n_contrib, void* stream) {
   DSPLAT_REQUIRE(!clear_counts || seg_stride > 0, "dsr_sort_render: clear_counts needs the fixed-capacity layout");
+  DSPLAT_REQUIRE(!write_keys || seg_stride == 0 || seg_stride == kSegEnds || (uint32_t)G <= seg_stride,
+                 "dsr_sort_render: write_keys needs segments that hold every entry (seg_stride >= G)");
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_sort_render: bad sizes");
   DSPLAT_REQUIRE(cams && geom && keys && scratch && seg_ptrs_ok(seg_start, seg_count, seg_stride) && out_color &&
                      final_T,
@@ -3627,8 +3816,9 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
   hipStream_t st = (hipStream_t)stream;
 #define DSR_SR_LAUNCH(K, L, NB, WP)                                                                          \
   k_sort_render<K, L, NB, WP><<<grid, NT, lds, st>>>(G, H, W, gx, T, cams, geom, seg_start, seg_count, seg_stride, \
-                                                     keys, scratch, id_bits, write_keys, clear_counts, out_color,  \
-                                                     final_T, n_contrib)
+                                                     keys, scratch, id_bits, write_keys, clear_counts,             \
+                                                     !(binning_layout & kLayoutRectBinning), out_color, final_T,   \
+                                                     n_contrib)
   // n_contrib is optional (inference: LAST = false)
   const bool wide = (int64_t)V * T >= kWide;
   switch (ci * 2 + (n_contrib ? 1 : 0)) {

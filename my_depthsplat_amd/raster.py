@@ -187,6 +187,14 @@ _kb_env = os.environ.get("DSPLAT_KEY_BUDGET_GB")
 KEY_BUDGET_BYTES = None if _kb_env is None else int(float(_kb_env) * (1 << 30))
 
 
+# Segment capacity of the inference fast path (bounded key memory): None = automatic per
+# RasterContext — twice the largest tile list of the context's earlier calls rounded up to a
+# power of two, at least 4096 (16384 before any call), at most G. A tile that gets more
+# entries than its capacity is rebuilt from the geometry records by dsr_sort_render (exact,
+# slow), so the capacity affects memory and speed only. Keys + sort scratch then take
+# 16 B x views x tiles x capacity (0.8 GB at 16 scenes of config B) instead of x G (26 GB).
+SEG_CAPACITY = None if os.environ.get("DSPLAT_SEG_CAPACITY") is None else int(os.environ["DSPLAT_SEG_CAPACITY"])
+
 # Segments larger than this many entries (only when some exceed the LDS sort) get only their
 # nearest SORT_PREFIX entries put in order (dsr_bin_sort prefix mode): at 6x448x768 the
 # compositor uses at most ~1.2K of 30-40K entries per tile. 0 sorts everything.
@@ -226,6 +234,7 @@ LAYOUT_EXACT_BINNING = 16
 # copy and the key stores; the product never sets it.
 DEBUG_KEEP_FAST_LISTS = False
 SEG_ENDS = 0xFFFFFFFF  # DSR_SEG_ENDS
+_HIST_LDS_MAX = 32768  # tiles per view binned in k_project_emit's LDS histogram (kHistLdsMax)
 
 
 class RasterContext:
@@ -239,7 +248,9 @@ class RasterContext:
       exact_binning (inference path), stateful_exact_binning (training path),
       fused_sort_render, sort_render_hint, inkernel_cameras, sort_prefix, cut_prefix,
       debug_keep_fast_lists, key_budget_bytes (None and no module override: automatic,
-      min(48 GiB, 40 % of the device, half of its memory free when first asked)).
+      min(48 GiB, 40 % of the device, half of its memory free when first asked)),
+      seg_capacity (inference fast path: entries per (view, tile) segment; None = from the
+      hints, see SEG_CAPACITY).
     hints: max_count (largest tile list seen: picks the fused sort's LDS class),
       two_phase_max (largest list of the last two-phase call: plans the depth cut).
     adapt_hints False freezes the hints (tests pin a class)."""
@@ -247,7 +258,8 @@ class RasterContext:
     _OPTS = {"exact_binning": "EXACT_BINNING", "stateful_exact_binning": "STATEFUL_EXACT_BINNING",
              "fused_sort_render": "FUSED_SORT_RENDER", "sort_render_hint": "SORT_RENDER_HINT",
              "inkernel_cameras": "INKERNEL_CAMERAS", "sort_prefix": "SORT_PREFIX", "cut_prefix": "CUT_PREFIX",
-             "debug_keep_fast_lists": "DEBUG_KEEP_FAST_LISTS", "key_budget_bytes": "KEY_BUDGET_BYTES"}
+             "debug_keep_fast_lists": "DEBUG_KEEP_FAST_LISTS", "key_budget_bytes": "KEY_BUDGET_BYTES",
+             "seg_capacity": "SEG_CAPACITY"}
 
     def __init__(self, **options):
         unknown = set(options) - set(self._OPTS)
@@ -272,6 +284,14 @@ class RasterContext:
             raise TypeError(f"unknown rasterizer options {sorted(unknown)}")
         self.options.update(options)
         return self
+
+    def seg_capacity(self, G: int) -> int:
+        """Segment capacity of the inference fast path (SEG_CAPACITY)."""
+        c = self.opt("seg_capacity")
+        if c is None:
+            m = self.hints["max_count"]
+            c = 16384 if m == 0 else max(4096, 1 << max(0, 2 * m - 1).bit_length())
+        return max(1, min(int(c), G))
 
     def key_budget(self, device) -> int:
         b = self.opt("key_budget_bytes")
@@ -518,14 +538,20 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
     radii = torch.empty((V, G), dtype=torch.int32, device=dev)
     lds_cap = lib.dsr_sort_lds_capacity()
-    fixed = bool(workspace(G, H, W, V, dev, ctx).fixed_capacity)
     maxc_hint = spec["max_count"] or lds_cap
-    fused = fixed and ctx.opt("fused_sort_render") and maxc_hint <= FUSED_MAX
     # eager inference fast path: cameras set up inside the binning kernel, counters taken zeroed
-    # from the previous call's sort + composite (two launches per forward)
-    fast = fused and ctx.opt("inkernel_cameras") and cam_in is not None and not need_state and zeroed_counts is None
+    # from the previous call's sort + composite (two launches per forward), segments of bounded
+    # capacity (keys + scratch: 16 B per (view, tile, capacity slot))
+    debug_lists = ctx.opt("debug_keep_fast_lists")
+    cap = G if debug_lists else ctx.seg_capacity(G)
+    fast = (ctx.opt("fused_sort_render") and maxc_hint <= FUSED_MAX and ctx.opt("inkernel_cameras")
+            and cam_in is not None and not need_state and zeroed_counts is None and T <= _HIST_LDS_MAX
+            and V * T * cap < (1 << 32) and 16 * V * T * cap <= ctx.key_budget(dev))
     clean = ctx.take_clean_counts(V * T, dev, st) if fast else None
     fast = clean is not None
+    fixed = fast or bool(workspace(G, H, W, V, dev, ctx).fixed_capacity)
+    fused = fixed and ctx.opt("fused_sort_render") and maxc_hint <= FUSED_MAX
+    stride = cap if fast else G
     if fast:
         seg_count = clean
         layout |= LAYOUT_COUNTS_ZEROED
@@ -544,17 +570,17 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                              zero_counts=None if layout & LAYOUT_COUNTS_ZEROED else seg_count)
         layout |= LAYOUT_COUNTS_ZEROED
     if fixed:
-        keys = torch.empty(V * T * G, dtype=torch.int64, device=dev)
+        keys = torch.empty(V * T * stride, dtype=torch.int64, device=dev)
         # scratch for segments above the LDS sort (their size is unknown before the sort)
-        scratch = torch.empty(V * T * G, dtype=torch.int64, device=dev)
+        scratch = torch.empty(V * T * stride, dtype=torch.int64, device=dev)
         if fast:
             ci = cam_in
             _lib.check(_timed("k_project_emit", lib.dsr_project_bin_cameras,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                 ci.extrinsics.data_ptr(), ci.intrinsics.data_ptr(), ci.near.data_ptr(), ci.far.data_ptr(),
                 ci.bg.data_ptr(), ci.view_scene.data_ptr(), int(ci.scale_invariant), cams.data_ptr(),
-                geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(), keys.data_ptr(), layout,
-                st),
+                geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(), keys.data_ptr(), stride,
+                layout, st),
                 "dsr_project_bin_cameras")
         else:
             if ctx.opt("stateful_exact_binning"):
@@ -563,7 +589,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                 cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(),
                 keys.data_ptr(), layout, st), "dsr_project_bin")
-        seg_start, stride = None, G
+        seg_start = None
         seg_sorted = None
         if not fused:
             ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
@@ -638,7 +664,6 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     final_T = torch.empty((V, H, W), dtype=torch.float32, device=dev)
     # n_contrib (the last blended position, read only by the backward) is skipped on the
     # inference fast path: not tracking it takes ~4 VALU instructions off every (pixel, entry)
-    debug_lists = ctx.opt("debug_keep_fast_lists")
     keep_nc = not fast or need_state or debug_lists
     n_contrib = torch.empty((V, H, W), dtype=torch.int32, device=dev) if keep_nc else None
     outs = (color.data_ptr(), final_T.data_ptr(), _ptr(n_contrib), st)
@@ -647,7 +672,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(), None,
                           seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(),
                           int(bool(need_state) or snap is not None), int(fast),
-                          ctx.opt("sort_render_hint") or spec["max_count"], *outs), "dsr_sort_render")
+                          ctx.opt("sort_render_hint") or spec["max_count"], layout, *outs), "dsr_sort_render")
         state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, cams=cams)
         if fast:  # the counters are zero again once the launch above has run
             ctx.give_back_clean_counts(seg_count, dev, st)

@@ -28,7 +28,9 @@
 //
 // Floating-point order: every expression that feeds the bit-exact outputs (depth,
 // radius, xy, tile rect) is written with a fixed evaluation order and compiled with
-// -ffp-contract=off, matching the HIP kernels in my_depthsplat_amd/csrc/.
+// -ffp-contract=off, matching the HIP kernels in my_depthsplat_amd/csrc/; the multiply-adds
+// of the projection chain (transforms, EWA, eigenvalues, SH) are explicit std::fma calls in
+// the kernels' order (upstream nvcc contracts such expressions into FMAs by default too).
 
 #include <algorithm>
 #include <cmath>
@@ -60,12 +62,14 @@ using V3 = V3T<float>;
 template <typename R>
 inline V3T<R> xform43(const float* m, V3T<R> p) {
   V3T<R> r;
-  r.x = m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12];
-  r.y = m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13];
-  r.z = m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14];
+  r.x = std::fma(R(m[0]), p.x, std::fma(R(m[4]), p.y, std::fma(R(m[8]), p.z, R(m[12]))));
+  r.y = std::fma(R(m[1]), p.x, std::fma(R(m[5]), p.y, std::fma(R(m[9]), p.z, R(m[13]))));
+  r.z = std::fma(R(m[2]), p.x, std::fma(R(m[6]), p.y, std::fma(R(m[10]), p.z, R(m[14]))));
   return r;
 }
-inline float xform44w(const float* m, V3 p) { return m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]; }
+inline float xform44w(const float* m, V3 p) {
+  return std::fma(m[3], p.x, std::fma(m[7], p.y, std::fma(m[11], p.z, m[15])));
+}
 
 inline float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5); }
 
@@ -104,21 +108,22 @@ inline void cov2d(V3T<R> mean, R fx, R fy, R tanx, R tany, const float* c6, cons
   const R W10 = view[1], W11 = view[5], W12 = view[9];
   const R W20 = view[2], W21 = view[6], W22 = view[10];
   // T = J * Wr  (2x3)
-  w.T[0][0] = j00 * W00 + j02 * W20;
-  w.T[0][1] = j00 * W01 + j02 * W21;
-  w.T[0][2] = j00 * W02 + j02 * W22;
-  w.T[1][0] = j11 * W10 + j12 * W20;
-  w.T[1][1] = j11 * W11 + j12 * W21;
-  w.T[1][2] = j11 * W12 + j12 * W22;
+  w.T[0][0] = std::fma(j00, W00, j02 * W20);
+  w.T[0][1] = std::fma(j00, W01, j02 * W21);
+  w.T[0][2] = std::fma(j00, W02, j02 * W22);
+  w.T[1][0] = std::fma(j11, W10, j12 * W20);
+  w.T[1][1] = std::fma(j11, W11, j12 * W21);
+  w.T[1][2] = std::fma(j11, W12, j12 * W22);
   // V = Sigma (symmetric from cov6 = xx, xy, xz, yy, yz, zz)
   const R V[3][3] = {{c6[0], c6[1], c6[2]}, {c6[1], c6[3], c6[4]}, {c6[2], c6[4], c6[5]}};
   // U = T * V (2x3), cov = U * T^T
   R U[2][3];
   for (int r = 0; r < 2; ++r)
-    for (int c = 0; c < 3; ++c) U[r][c] = w.T[r][0] * V[0][c] + w.T[r][1] * V[1][c] + w.T[r][2] * V[2][c];
-  const R a = U[0][0] * w.T[0][0] + U[0][1] * w.T[0][1] + U[0][2] * w.T[0][2];
-  const R b = U[0][0] * w.T[1][0] + U[0][1] * w.T[1][1] + U[0][2] * w.T[1][2];
-  const R c = U[1][0] * w.T[1][0] + U[1][1] * w.T[1][1] + U[1][2] * w.T[1][2];
+    for (int c = 0; c < 3; ++c)
+      U[r][c] = std::fma(w.T[r][0], V[0][c], std::fma(w.T[r][1], V[1][c], w.T[r][2] * V[2][c]));
+  const R a = std::fma(U[0][0], w.T[0][0], std::fma(U[0][1], w.T[0][1], U[0][2] * w.T[0][2]));
+  const R b = std::fma(U[0][0], w.T[1][0], std::fma(U[0][1], w.T[1][1], U[0][2] * w.T[1][2]));
+  const R c = std::fma(U[1][0], w.T[1][0], std::fma(U[1][1], w.T[1][1], U[1][2] * w.T[1][2]));
   w.a = a + R(0.3f);
   w.b = b;
   w.c = c + R(0.3f);
@@ -126,25 +131,33 @@ inline void cov2d(V3T<R> mean, R fx, R fy, R tanx, R tany, const float* c6, cons
 
 inline V3 sh_to_rgb(int deg, const float* sh /*[M][3]*/, V3 pos, const float* campos, uint8_t* clamped) {
   V3 dir = {pos.x - campos[0], pos.y - campos[1], pos.z - campos[2]};
-  const float len = std::sqrt(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
+  const float len = std::sqrt(std::fma(dir.x, dir.x, std::fma(dir.y, dir.y, dir.z * dir.z)));
   dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
   float r[3];
   for (int ch = 0; ch < 3; ++ch) {
     auto s = [&](int k) { return sh[k * 3 + ch]; };
+    // basis values first, then one fused multiply-add per coefficient (the kernels' order)
     float v = SH_C0 * s(0);
     if (deg > 0) {
       const float x = dir.x, y = dir.y, z = dir.z;
-      v = v - SH_C1 * y * s(1) + SH_C1 * z * s(2) - SH_C1 * x * s(3);
+      v = std::fma(-(SH_C1 * y), s(1), v);
+      v = std::fma(SH_C1 * z, s(2), v);
+      v = std::fma(-(SH_C1 * x), s(3), v);
       if (deg > 1) {
         const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-        v = v + SH_C2[0] * xy * s(4) + SH_C2[1] * yz * s(5) + SH_C2[2] * (2.0f * zz - xx - yy) * s(6) +
-            SH_C2[3] * xz * s(7) + SH_C2[4] * (xx - yy) * s(8);
+        v = std::fma(SH_C2[0] * xy, s(4), v);
+        v = std::fma(SH_C2[1] * yz, s(5), v);
+        v = std::fma(SH_C2[2] * (2.0f * zz - xx - yy), s(6), v);
+        v = std::fma(SH_C2[3] * xz, s(7), v);
+        v = std::fma(SH_C2[4] * (xx - yy), s(8), v);
         if (deg > 2) {
-          v = v + SH_C3[0] * y * (3.0f * xx - yy) * s(9) + SH_C3[1] * xy * z * s(10) +
-              SH_C3[2] * y * (4.0f * zz - xx - yy) * s(11) +
-              SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * s(12) +
-              SH_C3[4] * x * (4.0f * zz - xx - yy) * s(13) + SH_C3[5] * z * (xx - yy) * s(14) +
-              SH_C3[6] * x * (xx - 3.0f * yy) * s(15);
+          v = std::fma(SH_C3[0] * y * (3.0f * xx - yy), s(9), v);
+          v = std::fma(SH_C3[1] * xy * z, s(10), v);
+          v = std::fma(SH_C3[2] * y * (4.0f * zz - xx - yy), s(11), v);
+          v = std::fma(SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy), s(12), v);
+          v = std::fma(SH_C3[4] * x * (4.0f * zz - xx - yy), s(13), v);
+          v = std::fma(SH_C3[5] * z * (xx - yy), s(14), v);
+          v = std::fma(SH_C3[6] * x * (xx - 3.0f * yy), s(15), v);
         }
       }
     }
@@ -189,11 +202,11 @@ void preprocess(State& s) {
     const float ndx = ph.x * pw, ndy = ph.y * pw;
     Cov2DWork w;
     cov2d(p, fx, fy, s.tanx, s.tany, &s.cov6[6 * i], s.view.data(), w);
-    const float det = w.a * w.c - w.b * w.b;
+    const float det = std::fma(w.a, w.c, -(w.b * w.b));
     if (det == 0.0f) continue;
     const float det_inv = 1.f / det;
     const float mid = 0.5f * (w.a + w.c);
-    const float disc = std::sqrt(std::max(0.1f, mid * mid - det));
+    const float disc = std::sqrt(std::max(0.1f, std::fma(mid, mid, -det)));
     const float l1 = mid + disc, l2 = mid - disc;
     const float radius = std::ceil(3.f * std::sqrt(std::max(l1, l2)));
     const int r = (int)radius;
