@@ -2221,19 +2221,27 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, const PixUV2& p
   a.x = fminf(np2.x, over.x) >= 0.f ? alpha.x : 0.f;
   a.y = fminf(np2.y, over.y) >= 0.f ? alpha.y : 0.f;
   const f2v om = f2v{1.f, 1.f} - a;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const float testT = Tr * om[j];
-    const bool stop = testT < 0.0001f;  // always once stopped (test T <= 0)
-    const float wgt = stop ? 0.f : a[j] * Tr;
-    const f2v rg = P.rg[j];
-    f2v w2;
-    w2.x = wgt;
-    w2.y = wgt;
-    C01 = __builtin_elementwise_fma(rg, w2, C01);
-    C2 = fmaf(P.b[j], wgt, C2);
-    Tr = stop ? -fabsf(Tr) : testT;
-    if (LAST) lastk = wgt > 0.f ? k0 + j : lastk;  // blended <=> wgt > 0 (alpha >= 1/255, T >= 1e-4)
+  // both entries' test T up front (T1 = T (1 - a0), T2 = T1 (1 - a1): the same products as
+  // entry-by-entry), their weights as one packed multiply, then the stop selects: entry 1 stops
+  // whenever entry 0 did (T2 <= T1 < 1e-4, or T1 <= 0 for a stopped pixel), so the pixel's new
+  // state is -|T| (stopped at 0), -|T1| (stopped at 1) or T2.
+  const float T1 = Tr * om.x;
+  const float T2 = T1 * om.y;
+  const bool s0 = T1 < 0.0001f, s1 = T2 < 0.0001f;  // always once stopped (test T <= 0)
+  const f2v wv = a * f2v{Tr, T1};
+  const float w0 = s0 ? 0.f : wv.x, w1 = s1 ? 0.f : wv.y;
+  C01 = __builtin_elementwise_fma(P.rg[0], f2v{w0, w0}, C01);
+  C2 = fmaf(P.b[0], w0, C2);
+  C01 = __builtin_elementwise_fma(P.rg[1], f2v{w1, w1}, C01);
+  C2 = fmaf(P.b[1], w1, C2);
+  // -|x| as a sign-bit OR, two flat selects (no branches)
+  const float n0 = __int_as_float(__float_as_int(Tr) | (int)0x80000000);
+  const float n1 = __int_as_float(__float_as_int(T1) | (int)0x80000000);
+  const float t = s1 ? n1 : T2;
+  Tr = s0 ? n0 : t;
+  if (LAST) {  // blended <=> weight > 0 (alpha >= 1/255, T >= 1e-4)
+    lastk = w0 > 0.f ? k0 : lastk;
+    lastk = w1 > 0.f ? k0 + 1 : lastk;
   }
 }
 
@@ -3175,17 +3183,17 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     const float fy = H / (2.0f * cam->tanfovy);
     Cov2D w;
     cov2d(m, fx, fy, cam->tanfovx, cam->tanfovy, c6, cam->viewmatrix, w);
-    // conic = inverse(cov2D): gradient w.r.t. (a, b, c); gb carries half the
-    // off-diagonal derivative (see oracle/dsr_oracle.cpp).
-    const float a = w.a, b = w.b, c = w.c;
-    const float denom = a * c - b * b;
-    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
-    if (denom2inv != 0.f) {
-      dL_da = denom2inv * (-c * c * ga + 2 * b * c * gb + (denom - a * c) * gc);
-      dL_dc = denom2inv * (-a * a * gc + 2 * a * b * gb + (denom - a * c) * ga);
-      dL_db = denom2inv * 2 * (b * c * ga - (denom + 2 * b * b) * gb + a * b * gc);
-    }
+    // conic S = inverse(cov2D): dL/dcov2D = -S (dL/dS) S with the conic the forward stored
+    // (no det(cov2D)^2: its a c - b^2 cancels for needle-shaped Gaussians and cost up to ~2e-3
+    // of the largest dL/dmean3D in float); gb carries half the off-diagonal derivative, so
+    // dL/db = 2 M01 (oracle/dsr_oracle.cpp, same formula).
+    const float4 rec0 = reinterpret_cast<const float4*>(geom + vg * GS)[0];  // x, y, conic A, B
+    const float SA = rec0.z, SB = rec0.w, SC = geom[vg * GS + 4];
+    const float sg00 = SA * ga + SB * gb, sg01 = SA * gb + SB * gc;
+    const float sg10 = SB * ga + SC * gb, sg11 = SB * gb + SC * gc;
+    const float dL_da = -(sg00 * SA + sg01 * SB);
+    const float dL_dc = -(sg10 * SB + sg11 * SC);
+    const float dL_db = -2.f * (sg00 * SB + sg01 * SC);
     const auto& Tm = w.T;
     float dcv[6];
     dcv[0] = Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc;

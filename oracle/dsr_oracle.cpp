@@ -404,19 +404,18 @@ void backward_t(State& s, const float* dL_dpix, float* dmean2D, float* dconic, f
     for (int r = 0; r < 2; ++r)
       for (int c = 0; c < 3; ++c) w.T[r][c] = wf.T[r][c];
     w.a = wf.a; w.b = wf.b; w.c = wf.c; w.tx = wf.tx; w.ty = wf.ty; w.tz = wf.tz; w.xmul = wf.xmul; w.ymul = wf.ymul;
-    // conic = inverse(cov2D); gradient of the symmetric-matrix inverse. The render bwd
-    // accumulates dconic.y as HALF the derivative w.r.t. the off-diagonal entry (it appears
-    // twice in the quadratic form), so the off-diagonal weight below is 2.
-    const R a = w.a, b = w.b, c = w.c;
+    // conic = inverse(cov2D); gradient of the symmetric-matrix inverse, dL/dcov2D =
+    // -S dL/dS S with S the conic the forward stored (conic_gradient: the same formula as the
+    // kernels; upstream writes it through det(cov2D)^2 + 1e-7, whose a c - b^2 cancels for
+    // needle-shaped Gaussians — the forms agree to 1e-7 / det^2 <= 1.2e-5 relative since
+    // cov2D >= 0.3 I). The render bwd accumulates dconic.y as HALF the derivative w.r.t. the
+    // off-diagonal entry (it appears twice in the quadratic form), so dL/db = 2 M01.
     const R ga = R(acc_con[3 * i]), gb = R(acc_con[3 * i + 1]), gc = R(acc_con[3 * i + 2]);
-    const R denom = a * c - b * b;
-    const R denom2inv = R(1) / ((denom * denom) + R(0.0000001f));
-    R dL_da = 0, dL_db = 0, dL_dc = 0;
-    if (denom2inv != 0) {
-      dL_da = denom2inv * (-c * c * ga + 2 * b * c * gb + (denom - a * c) * gc);
-      dL_dc = denom2inv * (-a * a * gc + 2 * a * b * gb + (denom - a * c) * ga);
-      dL_db = denom2inv * 2 * (b * c * ga - (denom + 2 * b * b) * gb + a * b * gc);
-    }
+    const R A = R(s.conic_o[4 * i]), B = R(s.conic_o[4 * i + 1]), C = R(s.conic_o[4 * i + 2]);
+    const R sg00 = A * ga + B * gb, sg01 = A * gb + B * gc, sg10 = B * ga + C * gb, sg11 = B * gb + C * gc;
+    const R dL_da = -(sg00 * A + sg01 * B);
+    const R dL_dc = -(sg10 * B + sg11 * C);
+    const R dL_db = -2 * (sg00 * B + sg01 * C);
     // cov2D = T V T^T  (a = T0 V T0^T, b = T0 V T1^T, c = T1 V T1^T)
     const R (*T)[3] = w.T;
     // dL/dV (symmetric, cov6 order xx, xy, xz, yy, yz, zz; off-diagonals carry both halves)
