@@ -66,8 +66,12 @@ __device__ __forceinline__ F3 xform43(const float* m, F3 p) {
 __device__ __forceinline__ float xform44w(const float* m, F3 p) {
   return fmaf(m[3], p.x, fmaf(m[7], p.y, fmaf(m[11], p.z, m[15])));
 }
+// Upstream (and the oracle) evaluate ((v + 1.0) * S - 1.0) * 0.5 in double: every step is exact
+// there (a float v, an integer S < 2^24), so the result is the exact value rounded once to
+// float. One float FMA gives the same single rounding of (v + 1) S - 1 = v S + (S - 1), and the
+// halving is exact: bit-identical, two float instructions instead of six double ones.
 __device__ __forceinline__ float ndc2pix(float v, int S) {
-  return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
+  return 0.5f * fmaf(v, (float)S, (float)(S - 1));
 }
 __device__ __forceinline__ void tile_rect(float px, float py, int r, int gx, int gy, int& x0, int& y0,
                                           int& x1, int& y1) {
@@ -2221,27 +2225,19 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, const PixUV2& p
   a.x = fminf(np2.x, over.x) >= 0.f ? alpha.x : 0.f;
   a.y = fminf(np2.y, over.y) >= 0.f ? alpha.y : 0.f;
   const f2v om = f2v{1.f, 1.f} - a;
-  // both entries' test T up front (T1 = T (1 - a0), T2 = T1 (1 - a1): the same products as
-  // entry-by-entry), their weights as one packed multiply, then the stop selects: entry 1 stops
-  // whenever entry 0 did (T2 <= T1 < 1e-4, or T1 <= 0 for a stopped pixel), so the pixel's new
-  // state is -|T| (stopped at 0), -|T1| (stopped at 1) or T2.
-  const float T1 = Tr * om.x;
-  const float T2 = T1 * om.y;
-  const bool s0 = T1 < 0.0001f, s1 = T2 < 0.0001f;  // always once stopped (test T <= 0)
-  const f2v wv = a * f2v{Tr, T1};
-  const float w0 = s0 ? 0.f : wv.x, w1 = s1 ? 0.f : wv.y;
-  C01 = __builtin_elementwise_fma(P.rg[0], f2v{w0, w0}, C01);
-  C2 = fmaf(P.b[0], w0, C2);
-  C01 = __builtin_elementwise_fma(P.rg[1], f2v{w1, w1}, C01);
-  C2 = fmaf(P.b[1], w1, C2);
-  // -|x| as a sign-bit OR, two flat selects (no branches)
-  const float n0 = __int_as_float(__float_as_int(Tr) | (int)0x80000000);
-  const float n1 = __int_as_float(__float_as_int(T1) | (int)0x80000000);
-  const float t = s1 ? n1 : T2;
-  Tr = s0 ? n0 : t;
-  if (LAST) {  // blended <=> weight > 0 (alpha >= 1/255, T >= 1e-4)
-    lastk = w0 > 0.f ? k0 : lastk;
-    lastk = w1 > 0.f ? k0 + 1 : lastk;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float testT = Tr * om[j];
+    const bool stop = testT < 0.0001f;  // always once stopped (test T <= 0)
+    const float wgt = stop ? 0.f : a[j] * Tr;
+    const f2v rg = P.rg[j];
+    f2v w2;
+    w2.x = wgt;
+    w2.y = wgt;
+    C01 = __builtin_elementwise_fma(rg, w2, C01);
+    C2 = fmaf(P.b[j], wgt, C2);
+    Tr = stop ? -fabsf(Tr) : testT;
+    if (LAST) lastk = wgt > 0.f ? k0 + j : lastk;  // blended <=> wgt > 0 (alpha >= 1/255, T >= 1e-4)
   }
 }
 
