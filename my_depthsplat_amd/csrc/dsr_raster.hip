@@ -3004,16 +3004,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           dL_dalpha *= Tr;
           last_alpha = alpha;
           dL_dalpha += (-Tfin * inv1ma) * bg_dot;
-          const float dL_dG = cur.r.y * dL_dalpha;
-          const float gdx = Gs * dx, gdy = Gs * dy;
-          const float dG_ddelx = -gdx * cur.s.y - gdy * cur.s.z;
-          const float dG_ddely = -gdy * cur.s.w - gdx * cur.s.z;
-          g[j][0] = dL_dG * dG_ddelx * ddelx_dx;
-          g[j][1] = dL_dG * dG_ddely * ddely_dy;
-          g[j][2] = -0.5f * gdx * dx * dL_dG;
-          g[j][3] = -0.5f * gdx * dy * dL_dG;
-          g[j][4] = -0.5f * gdy * dy * dL_dG;
-          g[j][5] = Gs * dL_dalpha;
+          // per pixel only the factors that vary over the pixels: with h = G dL/dalpha the
+          // entry's sums are S(h dx), S(h dy), S(h dx^2), S(h dx dy), S(h dy^2), S(h); the
+          // conic, opacity and ndc factors multiply the sums once per entry (finish_grads)
+          const float h = Gs * dL_dalpha;
+          const float hx = h * dx, hy = h * dy;
+          g[j][0] = hx;
+          g[j][1] = hy;
+          g[j][2] = hx * dx;
+          g[j][3] = hx * dy;
+          g[j][4] = hy * dy;
+          g[j][5] = h;
         }
       }
       if (__ballot(any) != 0ull) {
@@ -3024,9 +3025,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           const int row = lane >> 4;
           const int kk = k - ((row & 1) * 2 + (row >> 1));
           if (kk >= 0) {
+            // dL/dmean2D = o S(h dG/dd) (ndc scale), dL/dconic = -o/2 S(h d d^T), dL/do = S(h)
+            // (upstream renderCUDA backward, its per-pixel products regrouped)
+            const float4 cs = list[kk].s;  // (blue, conic a, b, c)
+            const float o = list[kk].r.y;
             float* a9 = acc + kk * 9;
+            a9[0] = -o * (cs.y * R[0] + cs.z * R[1]) * ddelx_dx;
+            a9[1] = -o * (cs.w * R[1] + cs.z * R[0]) * ddely_dy;
+            a9[2] = -0.5f * o * R[2];
+            a9[3] = -0.5f * o * R[3];
+            a9[4] = -0.5f * o * R[4];
 #pragma unroll
-            for (int c = 0; c < 9; ++c) a9[c] = R[c];
+            for (int c = 5; c < 9; ++c) a9[c] = R[c];
           }
         }
       } else if ((lane & 15) == 15) {

@@ -15,9 +15,9 @@
 The oracle is fed the camera blocks the device built (state.cams / build_cameras), so the
 comparison isolates the rasterizer. The gradient reference is the oracle's backward evaluated in
 double (orc_backward_f64): on these scenes the per-pixel terms cancel heavily, and the float
-oracle itself sits ~1e-3 of the largest dL/dmean3D away from the exact gradient at config D.
+oracle and the device sit within 5e-4 of the largest dL/dmean3D of it at config D.
 Bars (north_star): mean L1 < 1e-4 and PSNR delta < 0.01 dB per image; gradients within
-1e-3 of each tensor's largest magnitude (GRAD_BAR below).
+5e-4 of each tensor's largest magnitude (GRAD_BAR below).
 """
 from __future__ import annotations
 
@@ -32,13 +32,13 @@ from test_fullsize_parity import _image_bars, _report, _segments
 
 pytestmark = pytest.mark.gpu
 
-# Gradient bar at these sizes: 1e-3 of each tensor's largest magnitude. The scenes hold huge,
-# needle-shaped Gaussians (radius ~375 px, det(cov2D) ~1e-3 of a*c) whose dL/dmean3D is a sum
-# of ~1e5 cancelling per-pixel terms through an ill-conditioned conic inverse: any float32
-# evaluation carries ~5e-4 there (device: 4.4e-4 at config C, 4.7e-4 at config D; the float
-# oracle itself is 1.03e-3 from the double reference at config D). Other gradients stay below
-# 2.3e-4; the smaller scenes' tests keep 5e-4. A wrong term moves a gradient by O(1).
-GRAD_BAR = 1e-3
+# Gradient bar at these sizes: 5e-4 of each tensor's largest magnitude, the bar of the smaller
+# scenes' tests. The scenes hold huge, needle-shaped Gaussians (radius ~375 px, det(cov2D) ~1e-3
+# of a*c) whose dL/dmean3D is a sum of ~1e5 cancelling per-pixel terms; since the conic
+# inverse's gradient is taken as -S (dL/dS) S with the stored conic (no det^2 cancellation),
+# the device sits at 9e-5 (config C) and 4.3e-4 (config D) for dL/dmean3D and below 2.6e-4 for
+# every other gradient (profiles/r03d_parity.jsonl). A wrong term moves a gradient by O(1).
+GRAD_BAR = 5e-4
 
 
 def _oracle_view(means, shs, opac, cov6, cams, i, H, W):
