@@ -630,11 +630,7 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
     // corr[16 x n] = aref[16 x C] . tgt[n x C]^T; per 16-channel step lane l feeds channels
     // cb + 4 (l >> 4) + s to MFMA s (A and B permuted alike). The C / 16 row loads of a
     // block are issued together.
-#ifndef DCV_X_NOGEMM
     for (int blk = wv; blk * 16 < n; blk += 4) {
-#else
-    for (int blk = wv; blk * 16 < 0; blk += 4) {
-#endif
       const int u = blk * 16 + (lane & 15);
       const float* brow = tg + (size_t)L.list[u] * C + 4 * (lane >> 4);
       float4 bv[NK / 4];
@@ -658,10 +654,6 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
     __syncthreads();
     if (r0 == 0 && accumulate) load_prev();  // the earlier views' sum, in flight across the gather
     const float* crow = L.corr + i * kECorr;
-#ifdef DCV_X_NOGATHER
-    if (n == U) {
-    } else
-#endif
     if (n == U) {
       // the one pass holds every tap: straight-line gather; a zero sample reads ranks 0 / 1
       // (written: the first 16 columns always are) with zero weights
