@@ -321,8 +321,9 @@ def main():
     # every capture in use rendered its own scenes exactly as an eager call does
     for i in range(lanes_used if graphs else 0):
         assert torch.equal(graphs[i].out.color, steps[B][i]().color), f"lane {i} of {mode} differs from eager"
-    # the captures' buffers (keys + sort scratch: V T G x 16 B per lane, ~26 GB per lane at 16
-    # scenes) are released before the reference-binning captures are made
+    # the captures' buffers (keys + sort scratch: 16 B x views x tiles x segment capacity per
+    # lane, ~0.8 GB at 16 scenes with the bounded capacity) are released before the
+    # reference-binning captures are made
     color_lane0 = graphs[0].out.color.clone() if graphs else None
     runner = None
     del graphs, modes

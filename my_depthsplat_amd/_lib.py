@@ -14,7 +14,7 @@ from pathlib import Path
 
 import torch  # noqa: F401  (must be loaded before the HIP library)
 
-# (DSPLAT_LIB: another build of the same ABI, e.g. a tools/variants.py experiment)
+# (DSPLAT_LIB: another build of the same ABI, e.g. a tools/ab_build.py A/B variant)
 LIB_PATH = Path(os.environ.get("DSPLAT_LIB") or Path(__file__).resolve().parent / "lib" / "libdsplat_hip.so")
 
 # name -> (restype, argtypes); mirrors include/dsplat_hip.h exactly.
