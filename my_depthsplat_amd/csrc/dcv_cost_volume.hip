@@ -474,26 +474,29 @@ __device__ __forceinline__ int epi_sample(const EpiRay& ry, float dep, float cla
   return ty0 * (W + 2) + tx0 + (W + 3);
 }
 
-// Front half shared by the forward and the backward: the samples' top-left taps into the
-// base bitmap, the tapped set (base | shifted copies), its exclusive popcount prefix and
-// its non-zero words; returns U (band positions). es[s]: extended index of sample s's
-// top-left tap (-1: zero sample). Global loads are issued unconditionally (clamped indices),
-// all before their first use, so their latencies overlap.
+// Front half shared by the forward and the backward, in three steps:
+//   epi_depths  the samples' depth candidates (global loads, issued early: their latency runs
+//               under the reference tile load in the forward);
+//   epi_taps    the samples' top-left taps into the base bitmap (LDS atomics; base must have
+//               been cleared before the last barrier);
+//   epi_band    after a barrier: the tapped set (base | shifted copies) of each thread's own
+//               contiguous run of words, its popcount prefix (wave scans) and the non-zero
+//               words; returns U (band positions). Two barriers.
+// es[s]: extended index of sample s's top-left tap (-1: zero sample).
 template <int SPT>
-__device__ __forceinline__ int epi_front(const EpiLds& L, int H, int W, int HW, int D, int depth_per_pixel, int b,
-                                         int d0, int pix, const EpiRay& ry, const float* __restrict__ depth,
-                                         float clampz, float (&sx)[SPT], float (&sy)[SPT], int (&es)[SPT]) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int dl = tid >> 4, Wx = W + 2, NWx = epi_words(H, W);
-  float dep[SPT];
-  {
-    const float* dp = depth + (size_t)b * D * (depth_per_pixel ? HW : 1);
-    const int dstride = depth_per_pixel ? HW : 1, pc = depth_per_pixel ? max(pix, 0) : 0;
+__device__ __forceinline__ void epi_depths(int HW, int D, int depth_per_pixel, int b, int d0, int pix,
+                                           const float* __restrict__ depth, float (&dep)[SPT]) {
+  const int dl = threadIdx.x >> 4;
+  const float* dp = depth + (size_t)b * D * (depth_per_pixel ? HW : 1);
+  const int dstride = depth_per_pixel ? HW : 1, pc = depth_per_pixel ? max(pix, 0) : 0;
 #pragma unroll
-    for (int s = 0; s < SPT; ++s) dep[s] = dp[(uint32_t)(min(d0 + dl + 16 * s, D - 1) * dstride + pc)];
-  }
-  for (int w = tid; w < NWx; w += 256) L.base[w] = 0u;
-  __syncthreads();
+  for (int s = 0; s < SPT; ++s) dep[s] = dp[(uint32_t)(min(d0 + dl + 16 * s, D - 1) * dstride + pc)];
+}
+template <int SPT>
+__device__ __forceinline__ void epi_taps(const EpiLds& L, int H, int W, int D, int d0, int pix, const EpiRay& ry,
+                                         const float (&dep)[SPT], float clampz, float (&sx)[SPT], float (&sy)[SPT],
+                                         int (&es)[SPT]) {
+  const int dl = threadIdx.x >> 4;
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
     const int d = d0 + dl + 16 * s;
@@ -501,7 +504,10 @@ __device__ __forceinline__ int epi_front(const EpiLds& L, int H, int W, int HW, 
     if (pix < 0 || d >= D) es[s] = -1;
     if (es[s] >= 0) atomicOr(&L.base[es[s] >> 5], 1u << (es[s] & 31));
   }
-  __syncthreads();
+}
+__device__ __forceinline__ int epi_band(const EpiLds& L, int H, int W) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int Wx = W + 2, NWx = epi_words(H, W);
   // tapped = base | base << 1 | base << Wx | base << (Wx + 1) (bit shifts across the words)
   auto shl = [&](int w, int sft) -> uint32_t {
     const int wo = sft >> 5, bo = sft & 31;
@@ -510,42 +516,57 @@ __device__ __forceinline__ int epi_front(const EpiLds& L, int H, int W, int HW, 
     const uint32_t hi = w - wo - 1 >= 0 ? L.base[w - wo - 1] : 0u;
     return (lo << bo) | (hi >> (32 - bo));
   };
-  for (int w = tid; w < NWx; w += 256) L.wb[w].x = shl(w, 0) | shl(w, 1) | shl(w, Wx) | shl(w, Wx + 1);
+  // thread t owns the contiguous words [t per, (t + 1) per): it forms them and counts them, so
+  // no barrier separates the two
+  const int per = (NWx + 255) / 256;
+  const int w0 = tid * per, w1 = min(NWx, w0 + per);
+  uint32_t tot = 0, nz = 0;
+  for (int w = w0; w < w1; ++w) {
+    const uint32_t bits = shl(w, 0) | shl(w, 1) | shl(w, Wx) | shl(w, Wx + 1);
+    L.wb[w].x = bits;
+    const uint32_t c = __popc(bits);
+    tot += c;
+    nz += c != 0u;
+  }
+  const uint32_t incl = dsplat::wave_incl_add_dpp(tot), inz = dsplat::wave_incl_add_dpp(nz);
+  if (lane == 63) {
+    L.misc[wv] = incl;
+    L.misc[8 + wv] = inz;
+  }
   __syncthreads();
-  {  // exclusive prefix of the popcounts and compaction of the non-zero words (thread t owns
-     // a contiguous run of words)
-    const int per = (NWx + 255) / 256;
-    const int w0 = tid * per, w1 = min(NWx, w0 + per);
-    uint32_t tot = 0, nz = 0;
-    for (int w = w0; w < w1; ++w) {
-      const uint32_t c = __popc(L.wb[w].x);
-      tot += c;
-      nz += c != 0u;
-    }
-    const uint32_t incl = dsplat::wave_incl_add_dpp(tot), inz = dsplat::wave_incl_add_dpp(nz);
-    if (lane == 63) {
-      L.misc[wv] = incl;
-      L.misc[8 + wv] = inz;
-    }
-    __syncthreads();
-    uint32_t off = incl - tot, offz = inz - nz;
-    for (int k = 0; k < wv; ++k) {
-      off += L.misc[k];
-      offz += L.misc[8 + k];
-    }
-    for (int w = w0; w < w1; ++w) {
-      const uint32_t bits = L.wb[w].x;
-      L.wb[w].y = off;
-      off += __popc(bits);
-      if (bits) L.nzw[offz++] = w;
-    }
-    if (tid == 255) {
-      L.misc[4] = off;
-      L.misc[5] = offz;
-    }
+  uint32_t off = incl - tot, offz = inz - nz;
+  for (int k = 0; k < wv; ++k) {
+    off += L.misc[k];
+    offz += L.misc[8 + k];
+  }
+  for (int w = w0; w < w1; ++w) {
+    const uint32_t bits = L.wb[w].x;
+    L.wb[w].y = off;
+    off += __popc(bits);
+    if (bits) L.nzw[offz++] = w;
+  }
+  if (tid == 255) {
+    L.misc[4] = off;
+    L.misc[5] = offz;
   }
   __syncthreads();
   return (int)L.misc[4];
+}
+__device__ __forceinline__ void epi_clear_base(const EpiLds& L, int H, int W) {
+  for (int w = threadIdx.x, NWx = epi_words(H, W); w < NWx; w += 256) L.base[w] = 0u;
+}
+// the three steps with their own clear + barrier (the backward's per-depth-chunk loop)
+template <int SPT>
+__device__ __forceinline__ int epi_front(const EpiLds& L, int H, int W, int HW, int D, int depth_per_pixel, int b,
+                                         int d0, int pix, const EpiRay& ry, const float* __restrict__ depth,
+                                         float clampz, float (&sx)[SPT], float (&sy)[SPT], int (&es)[SPT]) {
+  float dep[SPT];
+  epi_depths<SPT>(HW, D, depth_per_pixel, b, d0, pix, depth, dep);
+  epi_clear_base(L, H, W);
+  __syncthreads();
+  epi_taps<SPT>(L, H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
+  __syncthreads();
+  return epi_band(L, H, W);
 }
 
 // list[] = the target row of band ranks [r0, r0 + n): the image pixel, or HW (the all-zero
@@ -603,13 +624,20 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
   const size_t bj = (size_t)b * J + j;
   __shared__ int s_gid[EG];
   if (tid < EG) s_gid[tid] = g * EG + tid < HW ? groups[bj * HW + g * EG + tid] : -1;
+  epi_clear_base(L, H, W);
   __syncthreads();
-  epi_aref<NK>(L, HW, b, s_gid, ref_hwc);
+  // depth loads, then the reference tile's loads, all in flight together; the taps go into the
+  // base bitmap while the tile's LDS stores drain, and one barrier covers both
   const int pix = s_gid[i];  // -1: past the last pixel
+  float dep[SPT];
+  epi_depths<SPT>(HW, D, depth_per_pixel, b, d0, pix, depth, dep);
+  epi_aref<NK>(L, HW, b, s_gid, ref_hwc);
   const EpiRay ry = epi_ray(geom + bj * 12, pix >= 0 ? (float)(pix % W) : 0.f, pix >= 0 ? (float)(pix / W) : 0.f);
   float sx[SPT], sy[SPT];
   int es[SPT];
-  const int U = epi_front<SPT>(L, H, W, HW, D, depth_per_pixel, b, d0, pix, ry, depth, clampz, sx, sy, es);
+  epi_taps<SPT>(L, H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
+  __syncthreads();
+  const int U = epi_band(L, H, W);
   // per sample: sum over its taps of grid_sample's weight x correlation, taps in a fixed order
   // (a band of more than kEUMax positions takes several passes, each adding its taps)
   float* cb = cost + (size_t)b * D * HW;  // this scene's cost volume (< 2^32 elements)
