@@ -2111,8 +2111,11 @@ constexpr int CH = 64;  // list entries per chunk (one per lane)
 // Chunks whose records a wave gathers in one batch before compositing. A record gather is a
 // random read that mostly hits the MALL (the views' geometry does not fit one XCD's L2), and a
 // wave walks ~160 entries (p99 ~280, 3-5 chunks) of its tile at config B, so with only the
-// next chunk prefetched the walk was a chain of one memory round trip per chunk.
-constexpr int PD = 4;
+// next chunk prefetched the walk was a chain of one memory round trip per chunk. Two chunks
+// (then one ahead): the round-3 A/B at 16 scenes per launch measured PD = 4 / 3 / 2 / 1 at
+// 0.307 / 0.296 / 0.291 / 0.294 ms per sort_render launch and config C 3.22 / 3.19 / 3.17 /
+// 3.22 ms (fewer live registers at 5 waves per EU outweigh the deeper batch).
+constexpr int PD = 2;
 typedef float f2v __attribute__((ext_vector_type(2)));
 // The falloff as a polynomial in the pixel's offset (u, v) from its 8x8 sub-tile's centre
 // (cx, cy) = (x0 + 3.5, y0 + 3.5): with X = x - cx, Y = y - cy (the Gaussian's centre),
