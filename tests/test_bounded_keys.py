@@ -81,3 +81,35 @@ def test_automatic_capacity_from_hints():
     ctx.hints["max_count"] = 1800
     V, T = 48, 256
     assert 16 * V * T * ctx.seg_capacity(131072) < (1 << 30)
+
+
+@pytest.mark.gpu
+def test_bounded_capacity_under_graph_capture(gpu):
+    """A decoder whose capacity is frozen into a hipGraph below its scenes' longest tile lists
+    (the rebuild path runs inside the graph): every replay equals an eager render of the
+    unbounded layout bit for bit, and the counters the captured sort + composite clears serve
+    the next replay."""
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.graphs import GraphedCall
+    from my_depthsplat_amd.synthetic import make_scene
+    H = W = 96
+    sc = make_scene(batch=2, n_context=2, n_targets=3, height=H, width=W, seed=43, device=gpu)
+    cfg, ds = DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.1, 0.2, 0.3]}
+    G = sc.gaussians.means.shape[1]
+    ref_dec = DecoderSplattingCUDA(cfg, ds, seg_capacity=G).to(gpu)
+    dec = DecoderSplattingCUDA(cfg, ds, seg_capacity=64).to(gpu)
+    for d in (ref_dec, dec):
+        d.raster_ctx.hints["max_count"] = 2048
+        d.raster_ctx.adapt_hints = False
+
+    def call(d):
+        with torch.no_grad():
+            return d(sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near, sc.far, (H, W)).color
+
+    want = call(ref_dec).clone()
+    g = GraphedCall(lambda: call(dec), warmup=2)
+    assert dec.raster_ctx.last_stats()["max_count"] > 64  # the frozen capacity overflows
+    for _ in range(3):
+        got = g()
+        torch.cuda.synchronize()
+        assert torch.equal(got, want)
