@@ -423,7 +423,10 @@ struct CamIn {
 // occupancy from 8 to 2 waves/SIMD). Lane i < 16 owns E[i] and the cofactor (r, c) = (i / 4,
 // i % 4) of the 4x4 inverse; lanes 16..24 own K and the cofactors of the 3x3 inverse. Values
 // move between lanes with ds_bpermute (__shfl), which every lane of the wave executes.
-__device__ void make_camera_wave(int v, const CamIn& ci, int lane, dsr_camera& c) {
+// focal (optional): (W / (2 tanfovx), H / (2 tanfovy)) of the camera, the projection's two
+// per-camera divisions done once here instead of by every lane of every workgroup.
+__device__ void make_camera_wave(int v, const CamIn& ci, int lane, dsr_camera& c, int H = 0, int W = 0,
+                                 float2* focal = nullptr) {
   const float sc = ci.scale_invariant ? 1.0f / ci.near[v] : 1.0f;
   float x = 0.f;
   if (lane < 16) {
@@ -496,6 +499,7 @@ __device__ void make_camera_wave(int v, const CamIn& ci, int lane, dsr_camera& c
     c.scale = sc;
     c._pad[0] = 0;
     c._pad[1] = 0;
+    if (focal) *focal = make_float2(W / (2.0f * tx), H / (2.0f * ty));
   }
 }
 
@@ -523,10 +527,15 @@ __device__ __forceinline__ void load_gauss(GaussIn<DEG>& in, size_t sg, const fl
   in.sg = sg;
 }
 
+// The camera's focal lengths in pixels (cuda_splatting's rasterizer: W / (2 tan(fovx / 2))).
+__device__ __forceinline__ float2 focal_of(const dsr_camera* cam, int H, int W) {
+  return make_float2(W / (2.0f * cam->tanfovx), H / (2.0f * cam->tanfovy));
+}
 // Fills rec (GS floats, zero when culled) and the tile rect; returns the radius (0 = culled).
+// focal = focal_of(cam, H, W) (precomputed once per camera where the kernel has it).
 template <int DEG>
-__device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_camera* __restrict__ cam, int H,
-                                             int W, int gx, int gy, int M, const float* __restrict__ shs,
+__device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_camera* __restrict__ cam, float2 focal,
+                                             int H, int W, int gx, int gy, int M, const float* __restrict__ shs,
                                              const float* __restrict__ colors, int layout, float* rec, int& x0,
                                              int& y0, int& x1, int& y1) {
   int r = 0;
@@ -546,10 +555,8 @@ __device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_c
     const float gsc2 = gsc * gsc;
 #pragma unroll
     for (int k = 0; k < 6; ++k) c6[k] = in.c6[k] * gsc2;
-    const float fx = W / (2.0f * cam->tanfovx);
-    const float fy = H / (2.0f * cam->tanfovy);
     Cov2D w;
-    cov2d(p, fx, fy, cam->tanfovx, cam->tanfovy, c6, view, w);
+    cov2d(p, focal.x, focal.y, cam->tanfovx, cam->tanfovy, c6, view, w);
     const float det = fmaf(w.a, w.c, -(w.b * w.b));
     if (det != 0.0f) {
       const float det_inv = 1.f / det;
@@ -671,8 +678,13 @@ __device__ __forceinline__ void tile_rect_alpha(const TileEll& e, int& x0, int& 
     y1 = y0;
     return;
   }
+  // only a candidate box for tile_reach (which decides): hardware reciprocal and square root
+  // (1 ulp each) sit far inside the 1.002 / +0.05 margin, and count, emission and the
+  // bounded-capacity rebuild all evaluate this same function
   const float det = e.a * e.c - e.b * e.b;
-  const float hx = sqrtf(e.t2 * e.c / det) * 1.002f + 0.05f, hy = sqrtf(e.t2 * e.a / det) * 1.002f + 0.05f;
+  const float rdet = __builtin_amdgcn_rcpf(det);
+  const float hx = __builtin_amdgcn_sqrtf(e.t2 * e.c * rdet) * 1.002f + 0.05f;
+  const float hy = __builtin_amdgcn_sqrtf(e.t2 * e.a * rdet) * 1.002f + 0.05f;
   if (!(e.a > 0.f && e.c > 0.f && det > 0.f) || !(hx == hx) || !(hy == hy)) return;
   const float lim = 65536.f;
   x0 = max(x0, (int)floorf(fminf(fmaxf((e.x - hx) * (1.0f / BX), -1.f), lim)));
@@ -715,7 +727,8 @@ __global__ __launch_bounds__(NT) void k_preprocess(int G, int V, int H, int W, i
     GaussIn<DEG> in;
     load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
     float rec[GS];
-    r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
+    r = project_gauss<DEG>(in, cam, focal_of(cam, H, W), H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1,
+                           y1);
     store_geom(geom, radii, (size_t)v * G + g, rec, r, dzero);
     if constexpr (EXACT) {  // same terms as k_scatter<true> recomputes from the stored record
       ell = tile_ell(rec, r);
@@ -778,6 +791,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
   __shared__ WaveRects s_wr[NT / 64];
   __shared__ uint64_t s_key[NT];
   __shared__ dsr_camera s_cam[1];  // CAM only
+  __shared__ float2 s_focal;       // CAM only
   __shared__ uint32_t s_pairs[NT / 64][kPairCapW];
   __shared__ uint32_t s_ovf;
   int v, blk;
@@ -797,7 +811,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
   if constexpr (CAM) {
     // every workgroup sets up its view's camera while its Gaussians load (no separate
     // launch); the first block of each view also stores it for the later kernels
-    if (w == 0) make_camera_wave(v, ci, lane, s_cam[0]);
+    if (w == 0) make_camera_wave(v, ci, lane, s_cam[0], H, W, &s_focal);
     __syncthreads();
     if (blk == 0 && tid < (int)(sizeof(dsr_camera) / 4))
       reinterpret_cast<uint32_t*>(cams + v)[tid] = reinterpret_cast<const uint32_t*>(s_cam)[tid];
@@ -805,7 +819,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
   }
   if (g < G) {
     float rec[GS];
-    r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
+    r = project_gauss<DEG>(in, cam, CAM ? s_focal : focal_of(cam, H, W), H, W, gx, gy, M, shs, colors, layout, rec,
+                           x0, y0, x1, y1);
     store_geom(geom, radii, (size_t)v * G + g, rec, r, dzero);
     key = ((uint64_t)__float_as_uint(rec[9]) << 32) | (uint32_t)g;
     if constexpr (EXACT) {
@@ -1146,7 +1161,8 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
       GaussIn<DEG> in;
       load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
       float rec[GS];
-      r = project_gauss<DEG>(in, cam, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
+      r = project_gauss<DEG>(in, cam, focal_of(cam, H, W), H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1,
+                           y1);
       store_geom(geom, radii, (size_t)v * G + g, rec, r, dzero);
       zb = __float_as_uint(rec[9]);
     }
