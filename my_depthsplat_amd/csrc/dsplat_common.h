@@ -82,7 +82,11 @@ int zero_async(void* p, size_t bytes, hipStream_t st, const char* what);
 // 9 / 27 / 37 floats accessed directly make every load instruction touch ~64 cache lines.
 // The LDS side moves 16 B per lane too (ds_write_b128 / ds_read_b128: consecutive lanes,
 // consecutive 16-B slots, no bank conflict; four scalar ds ops at a 16-B lane stride were a
-// 4-way conflict each). `lds` must be 16-byte aligned.
+// 4-way conflict each). `lds` must be 16-byte aligned. The loads go out in batches of
+// kStageBatch per thread before any LDS store: a plain copy loop waits for every load before
+// its store (one memory round trip per iteration: ~10 serial round trips for a block's
+// 37-float head rows).
+constexpr int kStageBatch = 8;
 template <int NTH>
 __device__ __forceinline__ void stage_in(const float* __restrict__ src, size_t nfloat, float* lds) {
   const uintptr_t addr = reinterpret_cast<uintptr_t>(src);
@@ -90,10 +94,28 @@ __device__ __forceinline__ void stage_in(const float* __restrict__ src, size_t n
     const size_t n4 = nfloat / 4;
     const float4* s4 = reinterpret_cast<const float4*>(src);
     float4* l4 = reinterpret_cast<float4*>(lds);
-    for (size_t i = threadIdx.x; i < n4; i += NTH) l4[i] = s4[i];
+    for (size_t i0 = threadIdx.x; i0 < n4; i0 += (size_t)kStageBatch * NTH) {
+      float4 v[kStageBatch];  // unconditional loads (clamped index) keep v in registers
+#pragma unroll
+      for (int k = 0; k < kStageBatch; ++k) v[k] = s4[min(i0 + (size_t)k * NTH, n4 - 1)];
+#pragma unroll
+      for (int k = 0; k < kStageBatch; ++k) {
+        const size_t i = i0 + (size_t)k * NTH;
+        if (i < n4) l4[i] = v[k];
+      }
+    }
     for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NTH) lds[i] = src[i];
   } else {
-    for (size_t i = threadIdx.x; i < nfloat; i += NTH) lds[i] = src[i];
+    for (size_t i0 = threadIdx.x; i0 < nfloat; i0 += (size_t)kStageBatch * NTH) {
+      float v[kStageBatch];
+#pragma unroll
+      for (int k = 0; k < kStageBatch; ++k) v[k] = src[min(i0 + (size_t)k * NTH, nfloat - 1)];
+#pragma unroll
+      for (int k = 0; k < kStageBatch; ++k) {
+        const size_t i = i0 + (size_t)k * NTH;
+        if (i < nfloat) lds[i] = v[k];
+      }
+    }
   }
 }
 template <int NTH>
