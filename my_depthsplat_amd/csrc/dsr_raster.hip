@@ -176,6 +176,44 @@ __device__ __forceinline__ uint32_t for_each_rect_tile(WaveRects& wr, int lane, 
   return total;
 }
 
+// The same balanced hand-out, with f(valid, tile, owner, tile x, tile y) called on EVERY lane of
+// each 64-pair window (valid: this lane holds a pair), so f may itself run wave-wide code (a
+// nested for_each_rect_tile over a second WaveRects).
+template <typename F>
+__device__ __forceinline__ void for_each_rect_window(WaveRects& wr, int lane, int x0, int y0, int x1, int y1,
+                                                     bool has, int gx, F f) {
+  const uint32_t area = has ? (uint32_t)((x1 - x0) * (y1 - y0)) : 0u;
+  const uint32_t incl = dsplat::wave_incl_add_dpp(area);
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  const uint32_t ex = incl - area;
+  wr.ex[lane] = ex;
+  wr.org[lane] = (uint32_t)x0 | ((uint32_t)y0 << 16);
+  wr.wid[lane] = (uint32_t)max(x1 - x0, 1);
+  uint32_t carry = 0u;
+  for (uint32_t base = 0; base < total; base += 64) {
+    wr.mark[lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (area != 0u && ex - base < 64u) wr.mark[ex - base] = (uint32_t)lane + 1u;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t m = wr.mark[lane];
+    if (lane == 0) m = max(m, carry);
+    const uint32_t own = dsplat::wave_incl_max_dpp(m);
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
+    const uint32_t j = base + (uint32_t)lane;
+    const int o = max((int)own - 1, 0);
+    const uint32_t local = j < total ? j - wr.ex[o] : 0u;
+    const uint32_t wd = wr.wid[o];
+    uint32_t dy = (uint32_t)(((float)local + 0.5f) * __builtin_amdgcn_rcpf((float)wd));
+    if (dy * wd > local) --dy;
+    if ((dy + 1) * wd <= local) ++dy;
+    const uint32_t og = wr.org[o];
+    const int tx = (int)((og & 0xFFFFu) + local - dy * wd), ty = (int)((og >> 16) + dy);
+    __builtin_amdgcn_wave_barrier();
+    f(j < total, ty * gx + tx, o, tx, ty);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 struct Cov2D {
   float T[2][3];
   float a, b, c;
@@ -1029,7 +1067,8 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
 // kept entry takes its slot with one global atomic on its segment cursor, and a persistent
 // grid (one view and a run of blocks per workgroup, no workgroup barrier in the loop) walks
 // the Gaussians. A whole-Gaussian pre-test over the super-blocks its rect touches skips the
-// expansion of Gaussians no tile keeps (most of them).
+// expansion of Gaussians no tile keeps (most of them) and clips the others' rects to the
+// super-blocks that keep something.
 template <int NTH>
 __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int gy, const float* __restrict__ geom,
                                                      uint32_t* __restrict__ cursor, uint64_t* __restrict__ keys,
@@ -1040,6 +1079,9 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
   __shared__ uint32_t s_cut[kCutMaxSB];
   __shared__ WaveRects s_wr[NW];
   __shared__ uint64_t s_key[NTH];
+  __shared__ uint32_t s_rx[NW][64], s_ry[NW][64];  // tile rect x0 | x1 << 16, y0 | y1 << 16
+  __shared__ WaveRects s_wr2[NW];                   // inner expansion of the large rects
+  __shared__ uint64_t s_k2[NW][64];
   const int T = gx * gy;
   if (tail && seg_overflow[(size_t)V * T] == 0u) return;  // no tile flagged (uniform)
   const int v = blockIdx.x / per_view, p = blockIdx.x - v * per_view;
@@ -1060,12 +1102,13 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
   for (int blk = p; blk < nblk; blk += per_view) {
     const int g = blk * NTH + tid;
     int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    int sx0 = 0, sx1 = 0, sy0 = 0, sy1 = 0;
+    bool big = false;  // rect over more than 16 super-blocks: tested per (Gaussian, super-block) below
     uint64_t key = 0;
     if (g < G) {
       // whole-Gaussian pre-test over the super-blocks its rect touches: from the 8-byte compact
-      // record when given (most Gaussians fail it: only ~4-9 % of the entries are kept), the
+      // record when given (most Gaussians fail it: only ~2-7 % of the entries are kept), the
       // 48-byte geometry record is read only by the survivors
-      int sx0 = 0, sx1 = 0, sy0 = 0, sy1 = 0;
       uint32_t zb = 0u;
       const float* rec = gv + (size_t)g * GS;
       if (cut_rec) {
@@ -1084,28 +1127,60 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
           zb = __float_as_uint(rec[9]);
         }
       }
-      if (r > 0 && (sx1 - sx0) * (sy1 - sy0) <= 16) {
-        bool any = false;
+      // the super-blocks that pass: their bounding box (in super-blocks) clips the expansion,
+      // since every tile outside it lies in a super-block whose tiles the keep test rejects
+      int bx0 = sx1, bx1 = sx0 - 1, by0 = sy1, by1 = sy0 - 1;
+      big = r > 0 && (sx1 - sx0) * (sy1 - sy0) > 16;
+      if (r > 0 && !big) {
         for (int sy = sy0; sy < sy1; ++sy)
           for (int sx = sx0; sx < sx1; ++sx) {
             const bool nearer = zb <= s_cut[sy * nsx + sx];
-            any |= tail ? (!nearer && sbov[sy * nsx + sx] != 0u) : nearer;
+            if (tail ? (!nearer && sbov[sy * nsx + sx] != 0u) : nearer) {
+              bx0 = min(bx0, sx);
+              bx1 = max(bx1, sx);
+              by0 = min(by0, sy);
+              by1 = max(by1, sy);
+            }
           }
-        if (!any) r = 0;
+        if (bx1 < bx0) r = 0;
       }
       if (r > 0) {
         if (cut_rec) {
           r = __float_as_int(rec[10]);
           tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
         }
+        if (!big) {
+          x0 = max(x0, bx0 << sbl);
+          x1 = min(x1, (bx1 + 1) << sbl);
+          y0 = max(y0, by0 << sbl);
+          y1 = min(y1, (by1 + 1) << sbl);
+        }
         key = ((uint64_t)zb << 32) | (uint32_t)g;
       }
     }
     s_key[tid] = key;
-    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0, gx, [&](int t, int o, int tx, int ty) {
+    s_rx[w][lane] = (uint32_t)x0 | ((uint32_t)x1 << 16);
+    s_ry[w][lane] = (uint32_t)y0 | ((uint32_t)y1 << 16);
+    for_each_rect_tile(wr, lane, x0, y0, x1, y1, r > 0 && !big, gx, [&](int t, int o, int tx, int ty) {
       const uint64_t k = wkey[o];
       const bool nearer = (uint32_t)(k >> 32) <= s_cut[(ty >> sbl) * nsx + (tx >> sbl)];
       if (tail ? (!nearer && vov[t] != 0u) : nearer) keys[atomicAdd(&gcur[t], 1u)] = k;
+    });
+    // large rects (a few % of the Gaussians, but most of the rect tiles at 12x512x960):
+    // (Gaussian, super-block) pairs balanced over the wave; the tiles of the pairs that pass (the
+    // rect clipped to the super-block; the first pass keeps all of them) are then expanded
+    // balanced again, 64 pairs at a time
+    for_each_rect_window(wr, lane, sx0, sy0, sx1, sy1, big, nsx, [&](bool valid, int s, int o, int sx, int sy) {
+      const uint64_t k = wkey[o];
+      const bool nearer = (uint32_t)(k >> 32) <= s_cut[s];
+      const bool pass = valid && (tail ? (!nearer && sbov[s] != 0u) : nearer);
+      const uint32_t rx = s_rx[w][o], ry = s_ry[w][o];
+      const int tx0 = max((int)(rx & 0xFFFFu), sx << sbl), tx1 = min((int)(rx >> 16), (sx + 1) << sbl);
+      const int ty0 = max((int)(ry & 0xFFFFu), sy << sbl), ty1 = min((int)(ry >> 16), (sy + 1) << sbl);
+      s_k2[w][lane] = k;
+      for_each_rect_tile(s_wr2[w], lane, tx0, ty0, tx1, ty1, pass, gx, [&](int t, int o2, int, int) {
+        if (!tail || vov[t] != 0u) keys[atomicAdd(&gcur[t], 1u)] = s_k2[w][o2];
+      });
     });
   }
 }

@@ -148,6 +148,8 @@ class RasterState:
     pruned_lists: bool = False
     # the backward's int64 gradient accumulator, its rendered rows zeroed by the forward
     dgeom: torch.Tensor | None = None
+    # depth-cut binning: (cut thresholds [V * super-blocks], compact records or None, super-block size)
+    cut_plan: tuple | None = None
 
     @property
     def counts(self) -> torch.Tensor:
@@ -708,6 +710,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, seg_sorted, overflow,
                         tile_count if stride == SEG_ENDS else None, cams=cams)
     state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING) and stride != SEG_ENDS
+    if stride == SEG_ENDS:  # the depth-cut plan (tools/cut_case.py statistics)
+        state.cut_plan = (cut, cut_rec, lib.dsr_cut_superblock(H, W))
     ctx._last["counts"] = state.counts
     return color, state
 

@@ -453,6 +453,50 @@ def test_depth_cut_multiview_scene_vs_oracle(gpu, monkeypatch):
         o.close()
 
 
+@pytest.mark.parametrize("opacity", ["default", "faint"])
+def test_depth_cut_large_rects(gpu, opacity, monkeypatch):
+    """Depth cut with Gaussians whose 3-sigma rects cover more than 16 super-blocks (the
+    scatter tests those per (Gaussian, super-block) pair and visits only the tiles of the
+    super-blocks that pass): 320x320 (5x5 super-blocks of 4x4 tiles), every 50th Gaussian blown
+    up over the whole image. Images equal the full scatter's bit for bit and the written heads
+    are the oracle's; faint: every cut tile is flagged and completed by the tail pass."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+    monkeypatch.setattr(raster, "SORT_PREFIX", 0)
+    sc = scene_inputs(h=320, w=320, n_ctx=2, n_tgt=2, seed=23)
+    g = sc.gaussians
+    scale = torch.ones_like(g.opacities)
+    scale[:, ::50] = 10000.0
+    g.covariances = g.covariances * scale[..., None, None]
+    if opacity == "faint":
+        g.opacities = torch.full_like(g.opacities, 0.0045)
+    st = settings_for(sc)
+    monkeypatch.setattr(raster, "CUT_PREFIX", 0)
+    full, _, _ = hip_forward(sc, st, gpu)
+    monkeypatch.setattr(raster, "CUT_PREFIX", 256)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)
+    color, state, _ = hip_forward(sc, st, gpu)
+    assert state.seg_stride == raster.SEG_ENDS
+    cut, _, sb = state.cut_plan
+    assert sb == 4
+    # some rects span more than 16 of the 25 super-blocks
+    r = state.radii.cpu()
+    assert int((r > 160).sum()) > 0
+    written, counts = state.written().cpu(), state.counts.cpu().long()
+    nseg = counts.numel()
+    flagged = state.seg_overflow.cpu()[:nseg] != 0
+    if opacity == "default":
+        assert int(written.sum()) < 0.8 * int(counts.sum())
+    else:
+        assert bool(flagged.any())
+        assert torch.equal(written[flagged], counts[flagged])
+    assert torch.equal(color.cpu(), full.cpu())
+    orcs = oracle_views(sc, st)
+    _check_segments_vs_oracle(state, orcs, 2, 20 * 20)
+    for o in orcs:
+        o.close()
+
+
 def test_empty_and_culled(gpu):
     """All Gaussians behind the camera -> background only, N = 0."""
     sc = scene_inputs(h=32, w=48, seed=6)
