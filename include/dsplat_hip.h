@@ -87,6 +87,9 @@ int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, c
 #define DSR_LAYOUT_EXACT_BINNING 16    /* dsr_project_bin / dsr_preprocess_fwd / dsr_bin_scatter:
                                           exact alpha >= 1/255 tile test (as dsr_project_bin_cameras;
                                           the count and scatter calls of one forward must agree)    */
+#define DSR_LAYOUT_DEFER_GEOM 32       /* dsr_preprocess_cut only: radii, counts, histogram and
+                                          cut_rec, but no geometry record and no colour (see
+                                          dsr_project_survivors); needs cut_rec, no dgeom_zero      */
 int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,
@@ -184,10 +187,9 @@ int dsr_bin_scatter(int G, int V, int H, int W, const float* geom, uint32_t* seg
 int dsr_cut_superblock(int H, int W);
 /* depth_hist [V, nsb, DSR_CUT_BUCKETS] uint32 (zeroed by this call), nsb = ceil(tiles_x/sb)
  * * ceil(tiles_y/sb); other arguments and outputs as dsr_preprocess_fwd.
- * cut_rec (optional, [V, G, 2] uint32): per (view, Gaussian) the super-block rect of its tile
- * rect (x0 | x1 << 8 | y0 << 16 | y1 << 24, 0 when culled) and its depth bits: 8 bytes the
- * scatter's whole-Gaussian pre-test reads instead of the 48-byte geometry record (requires
- * ceil(tiles/sb) <= 255 per axis; NULL skips it). */
+ * cut_rec (optional, [V, G, 2] uint32): per (view, Gaussian) its tile rect (x0 | x1 << 8 |
+ * y0 << 16 | y1 << 24, 0 when culled) and its depth bits: 8 bytes the scatter reads instead of
+ * the 48-byte geometry record (requires at most 255 tiles per axis; NULL skips it). */
 int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,
@@ -205,8 +207,26 @@ int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t pre
  * written. */
 int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor,
                         uint64_t* keys, const uint32_t* cut, int tail, const uint32_t* seg_overflow,
-                        const uint32_t* cut_rec, void* stream);
-/* cut_rec: dsr_preprocess_cut's compact records (or NULL: the pre-test reads geom). */
+                        const uint32_t* cut_rec, uint32_t* survivors, uint32_t* survivor_count,
+                        void* stream);
+/* cut_rec: dsr_preprocess_cut's compact records (or NULL: the pre-test reads geom).
+ * survivors / survivor_count (sizes from dsr_survivor_layout; the counters zeroed by the
+ * caller; both NULL: none): the Gaussians that may emit in this pass are listed, per view and
+ * per scatter workgroup (for dsr_project_survivors after a DSR_LAYOUT_DEFER_GEOM preprocess;
+ * requires cut_rec). */
+/* Sizes of the survivor lists for (G, V): *slots uint32 entries, *counters uint32 counters. */
+int dsr_survivor_layout(int G, int V, int64_t* slots, int* counters);
+
+/* Deferred geometry: after dsr_preprocess_cut with DSR_LAYOUT_DEFER_GEOM and a scatter pass
+ * that listed its survivors, project the listed Gaussians of every view in full (colour
+ * included) and write their geometry records (bit-identical to dsr_preprocess_fwd's). At
+ * 12x512x960 the scatter keeps ~3 % of the (view, Gaussian) pairs: the preprocess skips the SH
+ * reads, the colour and the 48-byte record of the others. Arguments as dsr_preprocess_fwd. */
+int dsr_project_survivors(int S, int G, int V, int H, int W, int sh_degree, int M,
+                          const float* means, const float* shs, const float* colors,
+                          const float* opacities, const float* cov6, const dsr_camera* cams,
+                          const uint32_t* survivors, const uint32_t* survivor_count, float* geom,
+                          int32_t* radii, int layout, void* stream);
 
 /* Sort every segment by (depth, id) ascending — identical to upstream's stable radix
  * sort of (tile << 32 | depth) with emission-order ties (K4/K5). max_count sizes the LDS

@@ -30,7 +30,9 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_preprocess_cut": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I,
                                 _P]),
     "dsr_bin_cutoff": (_I, [_I, _I, _I, _P, c_uint32, _P, _P]),
-    "dsr_bin_scatter_cut": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "dsr_bin_scatter_cut": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P]),
+    "dsr_survivor_layout": (_I, [_I, _I, _P, _P]),
+    "dsr_project_survivors": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dsr_bin_sort": (_I, [_I, _I, _I, _I, _P, _P, c_uint32, _P, _P, c_uint32, _P, c_uint32, _P, _P, _P]),
     "dsr_bin_sort_workspace_size": (ctypes.c_size_t, [_I, _I, _I, c_uint32]),
     "dsr_workspace_size": (_I, [_I, _I, _I, _I, ctypes.c_uint64, _P]),

@@ -32,5 +32,5 @@ int zero_async(void* p, size_t bytes, hipStream_t st, const char* what) {
 
 extern "C" {
 const char* dsplat_last_error(void) { return g_err; }
-int dsplat_abi_version(void) { return 11; }
+int dsplat_abi_version(void) { return 12; }
 }

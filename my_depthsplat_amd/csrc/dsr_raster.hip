@@ -302,7 +302,7 @@ __device__ __forceinline__ float sh_eval(const float* sh, int ch, float x, float
 // what cuda_splatting.py:114,122's triu gather hands the rasterizer.
 constexpr int kLayoutShChannelMajor = DSR_LAYOUT_SH_CHANNEL_MAJOR, kLayoutCovFull = DSR_LAYOUT_COV_FULL,
               kLayoutCountsZeroed = DSR_LAYOUT_COUNTS_ZEROED, kLayoutRectBinning = DSR_LAYOUT_RECT_BINNING,
-              kLayoutExactBinning = DSR_LAYOUT_EXACT_BINNING;
+              kLayoutExactBinning = DSR_LAYOUT_EXACT_BINNING, kLayoutDeferGeom = DSR_LAYOUT_DEFER_GEOM;
 __device__ __forceinline__ float load_cov(const float* cov, size_t sg, int k, int layout) {
   if (layout & kLayoutCovFull) {
     constexpr int idx[6] = {0, 1, 2, 4, 5, 8};
@@ -571,7 +571,8 @@ __device__ __forceinline__ float2 focal_of(const dsr_camera* cam, int H, int W) 
 }
 // Fills rec (GS floats, zero when culled) and the tile rect; returns the radius (0 = culled).
 // focal = focal_of(cam, H, W) (precomputed once per camera where the kernel has it).
-template <int DEG>
+// COLOR = false: the geometry only (rec[6..8] and the clamp bits stay zero, no SH read).
+template <int DEG, bool COLOR = true>
 __device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_camera* __restrict__ cam, float2 focal,
                                              int H, int W, int gx, int gy, int M, const float* __restrict__ shs,
                                              const float* __restrict__ colors, int layout, float* rec, int& x0,
@@ -607,7 +608,8 @@ __device__ __forceinline__ int project_gauss(const GaussIn<DEG>& in, const dsr_c
       if ((x1 - x0) * (y1 - y0) != 0) {
         r = rr;
         uint32_t clamp_bits = 0;
-        if constexpr (DEG >= 0) {
+        if constexpr (!COLOR) {
+        } else if constexpr (DEG >= 0) {
           float sh[GaussIn<DEG>::NC * 3];
           load_sh<GaussIn<DEG>::NC>(shs, in.sg, M, layout, sh);
           float dx = p.x - cam->campos[0], dy = p.y - cam->campos[1], dz = p.z - cam->campos[2];
@@ -1059,6 +1061,20 @@ __global__ __launch_bounds__(NT) void k_scatter(int G, int V, int gx, int gy, co
   }
 }
 
+// The depth-cut scatter's persistent grid: per_view workgroups of kScatterCutNTH threads per
+// view, workgroup p taking blocks p, p + per_view, ... Its survivor list (deferred geometry) is
+// its own slice of survivor_slice() entries with its own counter, so listing costs one LDS
+// atomic per wave and no global atomic (a per-view global counter, hit once per wave by every
+// workgroup of the view, serialised the scatter: 8x slower at 12x512x960).
+constexpr int kScatterCutNTH = 256;
+__host__ __device__ inline int scatter_cut_per_view(int G, int V) {
+  return max(1, min((G + kScatterCutNTH - 1) / kScatterCutNTH, (256 * 8) / V));
+}
+__host__ __device__ inline size_t survivor_slice(int G, int V) {
+  const int nblk = (G + kScatterCutNTH - 1) / kScatterCutNTH, pv = scatter_cut_per_view(G, V);
+  return (size_t)((nblk + pv - 1) / pv) * kScatterCutNTH;
+}
+
 // K3 under the depth cut (dsr_bin_scatter_cut): only the entries the cut keeps (tail == 0:
 // depth bits <= the threshold of the tile's super-block; tail == 1: the others, of flagged
 // tiles only).
@@ -1074,7 +1090,8 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
                                                      uint32_t* __restrict__ cursor, uint64_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ cut, int tail,
                                                      const uint32_t* __restrict__ seg_overflow,
-                                                     const uint2* __restrict__ cut_rec, int per_view) {
+                                                     const uint2* __restrict__ cut_rec, int per_view,
+                                                     uint32_t* __restrict__ surv, uint32_t* __restrict__ surv_count) {
   constexpr int NW = NTH / 64;
   __shared__ uint32_t s_cut[kCutMaxSB];
   __shared__ WaveRects s_wr[NW];
@@ -1088,10 +1105,35 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int sb = cut_superblock(gx, gy), sbl = __builtin_ctz((unsigned)sb);
   const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((gy + sb - 1) / sb);
-  for (int k = tid; k < nsb; k += NTH) s_cut[k] = cut[(size_t)v * nsb + k];
-  __syncthreads();
   const uint32_t* vov = seg_overflow ? seg_overflow + (size_t)v * T : nullptr;
   const uint32_t* sbov = seg_overflow ? seg_overflow + (size_t)V * T + 1 + (size_t)v * nsb : nullptr;
+  // tail: the bounding box of the view's flagged super-blocks (a flagged tile is usually one
+  // of a handful), so that the Gaussians whose rects miss it skip the per-super-block test
+  __shared__ int s_fb[4];
+  if (tail && tid == 0) {
+    s_fb[0] = nsx;
+    s_fb[1] = -1;
+    s_fb[2] = nsb;
+    s_fb[3] = -1;
+  }
+  if (tail) __syncthreads();
+  for (int k = tid; k < nsb; k += NTH) {
+    s_cut[k] = cut[(size_t)v * nsb + k];
+    if (tail && sbov[k] != 0u) {
+      const int sy = k / nsx, sx = k - sy * nsx;
+      atomicMin(&s_fb[0], sx);
+      atomicMax(&s_fb[1], sx);
+      atomicMin(&s_fb[2], sy);
+      atomicMax(&s_fb[3], sy);
+    }
+  }
+  __syncthreads();
+  const int fx0 = tail ? s_fb[0] : 0, fx1 = tail ? s_fb[1] : nsx, fy0 = tail ? s_fb[2] : 0, fy1 = tail ? s_fb[3] : nsb;
+  if (fx1 < fx0) return;  // tail, nothing flagged in this view (workgroup-uniform; counters stay 0)
+  __shared__ uint32_t s_nsurv;
+  uint32_t* wsurv = surv ? surv + ((size_t)v * per_view + p) * survivor_slice(G, V) : nullptr;
+  if (tid == 0) s_nsurv = 0u;
+  __syncthreads();
   uint32_t* gcur = cursor + (size_t)v * T;
   const float* gv = geom + (size_t)v * G * GS;
   WaveRects& wr = s_wr[w];
@@ -1106,26 +1148,33 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
     bool big = false;  // rect over more than 16 super-blocks: tested per (Gaussian, super-block) below
     uint64_t key = 0;
     if (g < G) {
-      // whole-Gaussian pre-test over the super-blocks its rect touches: from the 8-byte compact
-      // record when given (most Gaussians fail it: only ~2-7 % of the entries are kept), the
-      // 48-byte geometry record is read only by the survivors
+      // whole-Gaussian pre-test over the super-blocks its rect touches, from the 8-byte compact
+      // record when given (tile rect + depth: the 48-byte geometry record is never read, and
+      // with deferred geometry it does not exist yet), else from the geometry record
       uint32_t zb = 0u;
-      const float* rec = gv + (size_t)g * GS;
       if (cut_rec) {
         const uint2 cr = cut_rec[(size_t)v * G + g];
-        sx0 = (int)(cr.x & 0xFFu);
-        sx1 = (int)((cr.x >> 8) & 0xFFu);
-        sy0 = (int)((cr.x >> 16) & 0xFFu);
-        sy1 = (int)(cr.x >> 24);
+        x0 = (int)(cr.x & 0xFFu);
+        x1 = (int)((cr.x >> 8) & 0xFFu);
+        y0 = (int)((cr.x >> 16) & 0xFFu);
+        y1 = (int)(cr.x >> 24);
         zb = cr.y;
         r = cr.x != 0u ? 1 : 0;
       } else {
+        const float* rec = gv + (size_t)g * GS;
         r = __float_as_int(rec[10]);
         if (r > 0) {
           tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
-          sx0 = x0 >> sbl, sx1 = ((x1 - 1) >> sbl) + 1, sy0 = y0 >> sbl, sy1 = ((y1 - 1) >> sbl) + 1;
           zb = __float_as_uint(rec[9]);
         }
+      }
+      if (r > 0) sx0 = x0 >> sbl, sx1 = ((x1 - 1) >> sbl) + 1, sy0 = y0 >> sbl, sy1 = ((y1 - 1) >> sbl) + 1;
+      if (tail) {  // only flagged super-blocks can pass
+        sx0 = max(sx0, fx0);
+        sx1 = min(sx1, fx1 + 1);
+        sy0 = max(sy0, fy0);
+        sy1 = min(sy1, fy1 + 1);
+        if (sx1 <= sx0 || sy1 <= sy0) r = 0;
       }
       // the super-blocks that pass: their bounding box (in super-blocks) clips the expansion,
       // since every tile outside it lies in a super-block whose tiles the keep test rejects
@@ -1145,10 +1194,6 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
         if (bx1 < bx0) r = 0;
       }
       if (r > 0) {
-        if (cut_rec) {
-          r = __float_as_int(rec[10]);
-          tile_rect(rec[0], rec[1], r, gx, gy, x0, y0, x1, y1);
-        }
         if (!big) {
           x0 = max(x0, bx0 << sbl);
           x1 = min(x1, (bx1 + 1) << sbl);
@@ -1156,6 +1201,17 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
           y1 = min(y1, (by1 + 1) << sbl);
         }
         key = ((uint64_t)zb << 32) | (uint32_t)g;
+      }
+    }
+    if (wsurv) {  // deferred geometry: list the Gaussians that may emit (one LDS atomic per wave)
+      const uint64_t m = __ballot(r > 0);
+      if (m) {
+        uint32_t base = 0u;
+        if (lane == 0) base = atomicAdd(&s_nsurv, (uint32_t)__popcll(m));
+        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        if (r > 0)
+          wsurv[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+              (uint32_t)g;
       }
     }
     s_key[tid] = key;
@@ -1183,6 +1239,44 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
       });
     });
   }
+  if (wsurv) {
+    __syncthreads();
+    if (tid == 0) surv_count[(size_t)v * per_view + p] = s_nsurv;
+  }
+}
+
+// Deferred geometry (dsr_project_survivors): the full projection (colour included) and the
+// geometry record of every Gaussian listed by the scatter pass just before, for each view.
+// A persistent grid: (view, run) workgroups walk the view's list. The same project_gauss as
+// every other path, so the records are bit-identical to dsr_preprocess_fwd's.
+template <int DEG>
+__global__ __launch_bounds__(NT) void k_project_survivors(int G, int V, int H, int W, int gx, int gy, int M,
+                                                          const float* __restrict__ means,
+                                                          const float* __restrict__ shs,
+                                                          const float* __restrict__ colors,
+                                                          const float* __restrict__ opac,
+                                                          const float* __restrict__ cov6,
+                                                          const dsr_camera* __restrict__ cams,
+                                                          const uint32_t* __restrict__ surv,
+                                                          const uint32_t* __restrict__ surv_count,
+                                                          float* __restrict__ geom, int32_t* __restrict__ radii,
+                                                          int per_view, int layout) {
+  // workgroup (v, p) projects the slice the scatter's workgroup (v, p) listed
+  const int v = blockIdx.x / per_view, p = blockIdx.x - v * per_view;
+  const dsr_camera* cam = cams + v;
+  const size_t slice = survivor_slice(G, V);
+  const uint32_t n = min(surv_count[(size_t)v * per_view + p], (uint32_t)slice);
+  const uint32_t* ws = surv + ((size_t)v * per_view + p) * slice;
+  const float2 focal = focal_of(cam, H, W);
+  for (uint32_t i = threadIdx.x; i < n; i += NT) {
+    const uint32_t g = ws[i];
+    GaussIn<DEG> in;
+    load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
+    float rec[GS];
+    int x0, y0, x1, y1;
+    const int r = project_gauss<DEG>(in, cam, focal, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
+    store_geom(geom, radii, (size_t)v * G + g, rec, r, nullptr);
+  }
 }
 
 // K1 + depth histogram (dsr_preprocess_cut). NTH threads per workgroup; each workgroup owns
@@ -1195,7 +1289,7 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
 // (Gaussian, touched super-block) adds the number of its tiles inside that super-block to
 // the bucket of its depth (super-blocks, not tiles: at 6x448x768 a 16-tile super-block
 // keeps the whole view's histogram in 43 KiB of LDS).
-template <int DEG, int NTH>
+template <int DEG, int NTH, bool LAZY>
 __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int W, int gx, int gy, int M,
                                                         const float* __restrict__ means,
                                                         const float* __restrict__ shs,
@@ -1236,9 +1330,14 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
       GaussIn<DEG> in;
       load_gauss<DEG>(in, (size_t)cam->scene * G + g, means, opac, cov6, layout);
       float rec[GS];
-      r = project_gauss<DEG>(in, cam, focal_of(cam, H, W), H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1,
-                           y1);
-      store_geom(geom, radii, (size_t)v * G + g, rec, r, dzero);
+      // LAZY (deferred geometry): no colour, no record; dsr_project_survivors writes the
+      // records of the Gaussians the depth-cut scatter keeps (a few % of them)
+      r = project_gauss<DEG, !LAZY>(in, cam, focal_of(cam, H, W), H, W, gx, gy, M, shs, colors, layout, rec, x0, y0,
+                                    x1, y1);
+      if constexpr (LAZY)
+        radii[(size_t)v * G + g] = r;
+      else
+        store_geom(geom, radii, (size_t)v * G + g, rec, r, dzero);
       zb = __float_as_uint(rec[9]);
     }
     if (r > 0) {
@@ -1252,9 +1351,9 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
     s_bk[w][lane] = (uint32_t)depth_bucket(zb);
     const int sx0 = x0 >> sbl, sy0 = y0 >> sbl;
     const int sx1 = r > 0 ? ((x1 - 1) >> sbl) + 1 : sx0, sy1 = r > 0 ? ((y1 - 1) >> sbl) + 1 : sy0;
-    if (cut_rec && g < G)
+    if (cut_rec && g < G)  // tile rect (non-zero: x1 >= 1 when visible) and depth bits
       cut_rec[(size_t)v * G + g] =
-          make_uint2(r > 0 ? (uint32_t)sx0 | ((uint32_t)sx1 << 8) | ((uint32_t)sy0 << 16) | ((uint32_t)sy1 << 24) : 0u,
+          make_uint2(r > 0 ? (uint32_t)x0 | ((uint32_t)x1 << 8) | ((uint32_t)y0 << 16) | ((uint32_t)y1 << 24) : 0u,
                      zb);
     for_each_rect_tile(wr, lane, sx0, sy0, sx1, sy1, r > 0, nsx, [&](int s, int o, int sx, int sy) {
       const uint32_t rx = s_rx[w][o], ry = s_ry[w][o];
@@ -3645,8 +3744,11 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, 
   const int sb = cut_superblock(gx, gy);
   DSPLAT_REQUIRE(sb > 0, "dsr_preprocess_cut: %dx%d tiles exceed the LDS histograms", gx, gy);
   const int nsb = ((gx + sb - 1) / sb) * ((gy + sb - 1) / sb);
-  DSPLAT_REQUIRE(cut_rec == nullptr || ((gx + sb - 1) / sb <= 255 && (gy + sb - 1) / sb <= 255),
-                 "dsr_preprocess_cut: cut_rec needs at most 255 super-blocks per axis");
+  DSPLAT_REQUIRE(cut_rec == nullptr || (gx <= 255 && gy <= 255),
+                 "dsr_preprocess_cut: cut_rec needs at most 255 tiles per axis");
+  const bool lazy = (layout & kLayoutDeferGeom) != 0;
+  DSPLAT_REQUIRE(!lazy || (cut_rec != nullptr && dgeom_zero == nullptr),
+                 "dsr_preprocess_cut: DSR_LAYOUT_DEFER_GEOM needs cut_rec and no dgeom_zero");
   hipStream_t st = (hipStream_t)stream;
   if (!(layout & kLayoutCountsZeroed))
     if (int e = dsplat::zero_async(seg_count, (size_t)V * T * 4, st, "zero seg_count")) return e;
@@ -3658,29 +3760,37 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, 
   const int nblk = (G + kNTH - 1) / kNTH;
   const int per_view = max(1, min(nblk, (256 * per_cu) / V));
   const int deg = shs ? sh_degree : -1;
-#define DSR_PC(D)                                                                                            \
+#define DSR_PC(D, L)                                                                                         \
   do {                                                                                                       \
     static bool attr = false;                                                                                \
     if (!attr) {                                                                                             \
-      if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_preprocess_cut<D, kNTH>,              \
+      if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_preprocess_cut<D, kNTH, L>,           \
                                                         hipFuncAttributeMaxDynamicSharedMemorySize,          \
                                                         kCutLdsWords * 4),                                   \
                                     "hipFuncSetAttribute(k_preprocess_cut)"))                                \
         return e;                                                                                            \
       attr = true;                                                                                           \
     }                                                                                                        \
-    k_preprocess_cut<D, kNTH><<<xcd_grid(per_view, V), kNTH, lds, st>>>(                                     \
+    k_preprocess_cut<D, kNTH, L><<<xcd_grid(per_view, V), kNTH, lds, st>>>(                                  \
         G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, geom, radii, dzero, seg_count,      \
         depth_hist,                                                                                          \
         reinterpret_cast<uint2*>(cut_rec), per_view, layout);                                                \
   } while (0)
+#define DSR_PC2(D)          \
+  do {                      \
+    if (lazy)               \
+      DSR_PC(D, true);      \
+    else                    \
+      DSR_PC(D, false);     \
+  } while (0)
   switch (deg) {
-    case -1: DSR_PC(-1); break;
-    case 0: DSR_PC(0); break;
-    case 1: DSR_PC(1); break;
-    case 2: DSR_PC(2); break;
-    default: DSR_PC(3); break;
+    case -1: DSR_PC2(-1); break;
+    case 0: DSR_PC2(0); break;
+    case 1: DSR_PC2(1); break;
+    case 2: DSR_PC2(2); break;
+    default: DSR_PC2(3); break;
   }
+#undef DSR_PC2
 #undef DSR_PC
   return dsplat::check_launch("k_preprocess_cut");
 }
@@ -3698,18 +3808,58 @@ int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t pre
 
 int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor, uint64_t* keys,
                         const uint32_t* cut, int tail, const uint32_t* seg_overflow, const uint32_t* cut_rec,
-                        void* stream) {
+                        uint32_t* survivors, uint32_t* survivor_count, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_scatter_cut: bad sizes");
   DSPLAT_REQUIRE(geom && seg_cursor && keys && cut && (!tail || seg_overflow), "dsr_bin_scatter_cut: null pointer");
+  DSPLAT_REQUIRE((survivors == nullptr) == (survivor_count == nullptr) && (survivors == nullptr || cut_rec),
+                 "dsr_bin_scatter_cut: survivors and survivor_count go together and need cut_rec");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   DSPLAT_REQUIRE(cut_superblock(gx, gy) > 0, "dsr_bin_scatter_cut: %dx%d tiles exceed the LDS histograms", gx, gy);
-  constexpr int kNTH = 256;
-  const int per_view = max(1, min((G + kNTH - 1) / kNTH, (256 * 8) / V));
+  constexpr int kNTH = kScatterCutNTH;
+  const int per_view = scatter_cut_per_view(G, V);
   k_scatter_cut<kNTH><<<(unsigned)(V * per_view), kNTH, 0, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor,
                                                                                   keys, cut, tail, seg_overflow,
                                                                                   reinterpret_cast<const uint2*>(cut_rec),
-                                                                                  per_view);
+                                                                                  per_view, survivors, survivor_count);
   return dsplat::check_launch("k_scatter_cut");
+}
+
+int dsr_survivor_layout(int G, int V, int64_t* slots, int* counters) {
+  DSPLAT_REQUIRE(G > 0 && V > 0 && slots && counters, "dsr_survivor_layout: bad arguments");
+  const int pv = scatter_cut_per_view(G, V);
+  *counters = V * pv;
+  *slots = (int64_t)V * pv * (int64_t)survivor_slice(G, V);
+  return 0;
+}
+
+int dsr_project_survivors(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
+                          const float* shs, const float* colors, const float* opacities, const float* cov6,
+                          const dsr_camera* cams, const uint32_t* survivors, const uint32_t* survivor_count,
+                          float* geom, int32_t* radii, int layout, void* stream) {
+  DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_project_survivors: bad sizes S=%d G=%d V=%d H=%d W=%d", S, G, V, H, W);
+  DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "dsr_project_survivors: exactly one of shs/colors must be given");
+  DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
+                 "dsr_project_survivors: sh_degree=%d M=%d unsupported (degree 0..3, M >= (deg+1)^2)", sh_degree, M);
+  DSPLAT_REQUIRE(means && opacities && cov6 && cams && survivors && survivor_count && geom && radii,
+                 "dsr_project_survivors: null pointer");
+  const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
+  static_assert(NT == kScatterCutNTH, "one survivor slice per scatter workgroup");
+  const int per_view = scatter_cut_per_view(G, V);
+  const int deg = shs ? sh_degree : -1;
+  hipStream_t st = (hipStream_t)stream;
+#define DSR_PS(D)                                                                                            \
+  k_project_survivors<D><<<(unsigned)(V * per_view), NT, 0, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, \
+                                                                   opacities, cov6, cams, survivors,         \
+                                                                   survivor_count, geom, radii, per_view, layout)
+  switch (deg) {
+    case -1: DSR_PS(-1); break;
+    case 0: DSR_PS(0); break;
+    case 1: DSR_PS(1); break;
+    case 2: DSR_PS(2); break;
+    default: DSR_PS(3); break;
+  }
+#undef DSR_PS
+  return dsplat::check_launch("k_project_survivors");
 }
 
 size_t dsr_bin_sort_workspace_size(int V, int H, int W, uint32_t max_count) {

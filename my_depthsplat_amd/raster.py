@@ -10,6 +10,7 @@ needed to size the key buffer.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from dataclasses import dataclass
@@ -150,6 +151,9 @@ class RasterState:
     dgeom: torch.Tensor | None = None
     # depth-cut binning: (cut thresholds [V * super-blocks], compact records or None, super-block size)
     cut_plan: tuple | None = None
+    # False when the depth cut deferred the geometry (no backward): only the records of the
+    # Gaussians a scatter pass listed are written (every Gaussian some list entry refers to)
+    geom_complete: bool = True
 
     @property
     def counts(self) -> torch.Tensor:
@@ -206,6 +210,11 @@ SORT_PREFIX = int(os.environ.get("DSPLAT_SORT_PREFIX", "4096"))
 # not all saturate within them get the rest appended, sorted and rendered again. 0 = off.
 CUT_PREFIX = int(os.environ.get("DSPLAT_CUT_PREFIX", "2048"))
 CUT_SORT_HINT = 4096  # LDS sort size for the written parts (larger ones sort through HBM)
+# Depth cut without a backward (need_state False): the preprocess writes no geometry record and
+# evaluates no colour; each scatter pass lists the Gaussians that may emit and
+# dsr_project_survivors projects only those (~3 % of the (view, Gaussian) pairs at 12x512x960).
+DEFER_GEOM = os.environ.get("DSPLAT_DEFER_GEOM", "1") != "0"
+LAYOUT_DEFER_GEOM = 32
 # Fixed-capacity binning with tile lists up to FUSED_MAX entries (the hint from earlier calls)
 # sorts and composites in one launch (dsr_sort_render); longer lists take dsr_bin_sort +
 # dsr_render_fwd (MSD split, prefix sort). Either is exact for any list length.
@@ -252,7 +261,7 @@ class RasterContext:
       debug_keep_fast_lists, key_budget_bytes (None and no module override: automatic,
       min(48 GiB, 40 % of the device, half of its memory free when first asked)),
       seg_capacity (inference fast path: entries per (view, tile) segment; None = from the
-      hints, see SEG_CAPACITY).
+      hints, see SEG_CAPACITY), defer_geom (depth cut without a backward: see DEFER_GEOM).
     hints: max_count (largest tile list seen: picks the fused sort's LDS class),
       two_phase_max (largest list of the last two-phase call: plans the depth cut).
     adapt_hints False freezes the hints (tests pin a class)."""
@@ -261,7 +270,7 @@ class RasterContext:
              "fused_sort_render": "FUSED_SORT_RENDER", "sort_render_hint": "SORT_RENDER_HINT",
              "inkernel_cameras": "INKERNEL_CAMERAS", "sort_prefix": "SORT_PREFIX", "cut_prefix": "CUT_PREFIX",
              "debug_keep_fast_lists": "DEBUG_KEEP_FAST_LISTS", "key_budget_bytes": "KEY_BUDGET_BYTES",
-             "seg_capacity": "SEG_CAPACITY"}
+             "seg_capacity": "SEG_CAPACITY", "defer_geom": "DEFER_GEOM"}
 
     def __init__(self, **options):
         unknown = set(options) - set(self._OPTS)
@@ -602,6 +611,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         # the depth cut pays when tile lists are long; the previous two-phase call's largest
         # list (None on the first call) decides whether this one builds the depth histogram
         cut_prefix = ctx.opt("cut_prefix")
+        defer, surv, surv_n = False, None, None  # deferred geometry (set below when the cut is planned)
         prev = spec.get("two_phase_max")
         want_cut = cut_prefix > 0 and (prev is None or prev > 4 * cut_prefix)
         sb = lib.dsr_cut_superblock(H, W) if want_cut else 0
@@ -610,11 +620,13 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             hist = torch.empty(V * nsb * 128, dtype=torch.int32, device=dev)
             # 8 bytes per (view, Gaussian) for the scatter's pre-test instead of the 48-byte record
             cut_rec = torch.empty(V * G * 2, dtype=torch.int32, device=dev) \
-                if -(-gx // sb) <= 255 and -(-gy // sb) <= 255 else None
+                if gx <= 255 and gy <= 255 else None
+            defer = bool(ctx.opt("defer_geom")) and not need_state and cut_rec is not None and dgeom_zero is None
             _lib.check(_timed("k_preprocess_cut", lib.dsr_preprocess_cut,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                 cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(),
-                hist.data_ptr(), _ptr(cut_rec), layout, st), "dsr_preprocess_cut")
+                hist.data_ptr(), _ptr(cut_rec), layout | (LAYOUT_DEFER_GEOM if defer else 0), st),
+                "dsr_preprocess_cut")
         else:
             if ctx.opt("stateful_exact_binning"):  # the scatter below repeats the same test
                 layout |= LAYOUT_EXACT_BINNING
@@ -640,14 +652,32 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
         if sb > 0 and maxc <= 2 * cut_prefix:  # short lists after all: write everything
             sb = 0
+            if defer:  # the full scatter reads every record: project them all now
+                _project_all(lib, S, G, V, H, W, deg, M, means, shs_p, col_p, opacities, cov6, cams, geom, radii,
+                             layout, dev, st)
         if sb > 0:
             # depth cut: write only each tile's nearest entries (cursor ends at their end)
             scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev)  # only big segments touch it
             cut = torch.empty(V * nsb, dtype=torch.int32, device=dev)
             _lib.check(_timed("k_bin_cutoff", lib.dsr_bin_cutoff, V, H, W, hist.data_ptr(), cut_prefix,
                               cut.data_ptr(), st), "dsr_bin_cutoff")
+            # deferred geometry: per view a list of the Gaussians each scatter pass may emit
+            # (first pass: counts [0, V), tail: [V, 2V)), projected right after the pass
+            if defer:
+                slots, ncnt = ctypes.c_int64(), ctypes.c_int()
+                _lib.check(lib.dsr_survivor_layout(G, V, ctypes.byref(slots), ctypes.byref(ncnt)),
+                           "dsr_survivor_layout")
+                surv = torch.empty(slots.value, dtype=torch.int32, device=dev)
+                surv_n = torch.zeros(2 * ncnt.value, dtype=torch.int32, device=dev)
+            proj = (S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+                    cams.data_ptr())
             _lib.check(_timed("k_scatter", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
-                              keys.data_ptr(), cut.data_ptr(), 0, None, _ptr(cut_rec), st), "dsr_bin_scatter_cut")
+                              keys.data_ptr(), cut.data_ptr(), 0, None, _ptr(cut_rec), _ptr(surv), _ptr(surv_n), st),
+                       "dsr_bin_scatter_cut")
+            if defer:
+                _lib.check(_timed("k_project_survivors", lib.dsr_project_survivors, *proj, surv.data_ptr(),
+                                  surv_n.data_ptr(), geom.data_ptr(), radii.data_ptr(), layout, st),
+                           "dsr_project_survivors")
             tile_count, seg_count, stride = seg_count, cursor, SEG_ENDS
             _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), seg_count.data_ptr(),
                               stride, keys.data_ptr(), scratch.data_ptr(), CUT_SORT_HINT, None, 0, None, None, st),
@@ -698,9 +728,13 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         # tiles whose unsorted (or unwritten) tail would have blended: complete them, sort them
         # in full, render them again (every launch returns at once for unflagged tiles; no sync)
         if stride == SEG_ENDS:
+            tail_n = None if surv is None else surv_n[surv_n.numel() // 2:]
             _lib.check(lib.dsr_bin_scatter_cut(G, V, H, W, geom.data_ptr(), seg_count.data_ptr(), keys.data_ptr(),
-                                               cut.data_ptr(), 1, overflow.data_ptr(), _ptr(cut_rec), st),
-                       "dsr_bin_scatter_cut(tail)")
+                                               cut.data_ptr(), 1, overflow.data_ptr(), _ptr(cut_rec), _ptr(surv),
+                                               _ptr(tail_n), st), "dsr_bin_scatter_cut(tail)")
+            if surv is not None:
+                _lib.check(lib.dsr_project_survivors(*proj, surv.data_ptr(), tail_n.data_ptr(), geom.data_ptr(),
+                                                     radii.data_ptr(), layout, st), "dsr_project_survivors(tail)")
         _lib.check(lib.dsr_bin_sort(G, V, H, W, _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(),
                                     scratch.data_ptr(), 0, None, 0, _ptr(seg_sorted), overflow.data_ptr(), st),
                    "dsr_bin_sort(overflow)")
@@ -712,8 +746,27 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING) and stride != SEG_ENDS
     if stride == SEG_ENDS:  # the depth-cut plan (tools/cut_case.py statistics)
         state.cut_plan = (cut, cut_rec, lib.dsr_cut_superblock(H, W))
+        state.geom_complete = surv is None
     ctx._last["counts"] = state.counts
     return color, state
+
+
+def _project_all(lib, S, G, V, H, W, deg, M, means, shs_p, col_p, opacities, cov6, cams, geom, radii, layout, dev, st):
+    """Deferred geometry abandoned (the lists turned out short): every record, through the
+    survivor projection with lists that hold every Gaussian (slice p of a view: the blocks p,
+    p + per_view, ... that the scatter's workgroup p walks)."""
+    slots, ncnt = ctypes.c_int64(), ctypes.c_int()
+    _lib.check(lib.dsr_survivor_layout(G, V, ctypes.byref(slots), ctypes.byref(ncnt)), "dsr_survivor_layout")
+    pv, nt = ncnt.value // V, 256
+    cap = slots.value // ncnt.value
+    blk = torch.arange(cap // nt, device=dev)[None, :] * pv + torch.arange(pv, device=dev)[:, None]  # [pv, cap/nt]
+    g = (blk[:, :, None] * nt + torch.arange(nt, device=dev)).reshape(pv, cap)
+    n = (g < G).sum(1).to(torch.int32)  # the valid ids come first in every slice
+    ids = g.clamp(max=G - 1).to(torch.int32).repeat(V, 1).reshape(-1)
+    n = n.repeat(V)
+    _lib.check(lib.dsr_project_survivors(S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(),
+                                         cov6.data_ptr(), cams.data_ptr(), ids.data_ptr(), n.data_ptr(),
+                                         geom.data_ptr(), radii.data_ptr(), layout, st), "dsr_project_survivors(all)")
 
 
 def _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, max_count, ws, st, lds_cap,

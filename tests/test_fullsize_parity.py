@@ -310,18 +310,23 @@ def test_config_c_shape_forward_backward_vs_oracle(gpu):
 
 def test_config_d_shape_render_vs_oracle(gpu, monkeypatch):
     """6-view 448x768 context (G = 2,064,384), 2 target views: the product path at this size
-    (two-phase binning, depth cut: only each tile's nearest entries are written and sorted)
-    vs the oracle's full render; the written heads equal the heads of the oracle's lists."""
+    (two-phase binning, depth cut: only each tile's nearest entries are written and sorted;
+    without a backward the geometry of the listed Gaussians only) vs the oracle's full render;
+    the written heads equal the heads of the oracle's lists, the image the stateful path's."""
     from my_depthsplat_amd import raster
     monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)  # no short-list hint from earlier tests
     sc = scene_inputs(h=448, w=768, n_ctx=6, n_tgt=2, seed=2000)
     st = settings_for(sc)
     means, shs, opac, cov6 = flat_inputs(sc)
     cams = packed_cams(st, [0, 0]).to(gpu)
-    color, state = raster.forward_raw(means.to(gpu), shs.to(gpu), True, 2, opac.to(gpu), cov6.to(gpu), cams, 2,
-                                      448, 768)
+    args = (means.to(gpu), shs.to(gpu), True, 2, opac.to(gpu), cov6.to(gpu), cams, 2, 448, 768)
+    full, _ = raster.forward_raw(*args)  # stateful: every geometry record written by the preprocess
+    # inference (no backward): deferred geometry, only the Gaussians the scatter lists are projected
+    color, state = raster.forward_raw(*args, need_state=False)
     torch.cuda.synchronize()
     assert state.seg_stride == raster.SEG_ENDS  # the depth-cut layout ran
+    assert not state.geom_complete
+    assert torch.equal(color, full)
     T = 28 * 48
     col = color.cpu().numpy()
     begin, end, keys = _segments(state, 2, T)
@@ -352,10 +357,13 @@ def test_config_e_shape_render_vs_oracle(gpu, monkeypatch):
     st = settings_for(sc)
     means, shs, opac, cov6 = flat_inputs(sc)
     cams = packed_cams(st, [0]).to(gpu)
-    color, state = raster.forward_raw(means.to(gpu), shs.to(gpu), True, 2, opac.to(gpu), cov6.to(gpu), cams, 1,
-                                      512, 960)
+    args = (means.to(gpu), shs.to(gpu), True, 2, opac.to(gpu), cov6.to(gpu), cams, 1, 512, 960)
+    full, _ = raster.forward_raw(*args)
+    color, state = raster.forward_raw(*args, need_state=False)  # deferred geometry
     torch.cuda.synchronize()
     assert state.seg_stride == raster.SEG_ENDS  # the depth-cut layout ran
+    assert not state.geom_complete
+    assert torch.equal(color, full)
     T = 32 * 60
     begin, end, keys = _segments(state, 1, T)
     written = int((end - begin).sum())

@@ -28,7 +28,7 @@ def reference_lists(monkeypatch):
     monkeypatch.setattr(raster, "STATEFUL_EXACT_BINNING", False)
 
 
-def hip_forward(sc, st, gpu, use_sh=True, bg=(0.0, 0.0, 0.0)):
+def hip_forward(sc, st, gpu, use_sh=True, bg=(0.0, 0.0, 0.0), need_state=True):
     from my_depthsplat_amd import raster
     means, shs, opac, cov6 = flat_inputs(sc)
     B, v = sc.target_extrinsics.shape[:2]
@@ -38,7 +38,7 @@ def hip_forward(sc, st, gpu, use_sh=True, bg=(0.0, 0.0, 0.0)):
     deg = math.isqrt(shs.shape[2]) - 1
     h, w = sc.image_shape
     color, state = raster.forward_raw(means.to(gpu), feats.to(gpu), use_sh, deg, opac.to(gpu), cov6.to(gpu), cams,
-                                      B * v, h, w)
+                                      B * v, h, w, need_state=need_state)
     torch.cuda.synchronize()
     return color, state, cams
 
@@ -491,10 +491,35 @@ def test_depth_cut_large_rects(gpu, opacity, monkeypatch):
         assert bool(flagged.any())
         assert torch.equal(written[flagged], counts[flagged])
     assert torch.equal(color.cpu(), full.cpu())
+    # no backward: deferred geometry (the scatter passes list their Gaussians, only those are
+    # projected in full), including the tail pass's in the faint case
+    monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)
+    lazy, lst, _ = hip_forward(sc, st, gpu, need_state=False)
+    assert lst.seg_stride == raster.SEG_ENDS and not lst.geom_complete
+    assert torch.equal(lazy.cpu(), full.cpu())
     orcs = oracle_views(sc, st)
     _check_segments_vs_oracle(state, orcs, 2, 20 * 20)
     for o in orcs:
         o.close()
+
+
+def test_deferred_geometry_short_lists(gpu, monkeypatch):
+    """The depth cut planned with deferred geometry (no backward) but the lists turn out
+    short (the full scatter runs): every record is then projected through the survivor
+    lists holding every Gaussian; images equal the stateful path's bit for bit."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+    monkeypatch.setattr(raster, "CUT_PREFIX", 1024)
+    sc = scene_inputs(h=96, w=128, n_ctx=2, n_tgt=2, seed=24)
+    st = settings_for(sc)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)
+    full, fst, _ = hip_forward(sc, st, gpu)
+    monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)
+    lazy, lst, _ = hip_forward(sc, st, gpu, need_state=False)
+    assert fst.seg_stride == 0 and lst.seg_stride == 0  # lists short: no cut after all
+    assert int(lst.counts.max()) <= 2048
+    assert torch.equal(lazy, full)
+    assert torch.equal(lst.geom, fst.geom)  # every record written
 
 
 def test_empty_and_culled(gpu):

@@ -143,8 +143,11 @@ def main():
             out["superblocks_flagged"] = int(sbf.sum())
             out["superblocks"] = int(sbf.numel())
         out["entries_flagged_tiles"] = int(counts.view(V, T)[flags].sum())
-    if st.cut_plan is not None:
-        out.update(scatter_stats(st, V, H, W))
+    if st.cut_plan is not None:  # statistics from the full geometry records (no deferral)
+        with torch.no_grad():
+            _, st2 = raster.forward_raw(g.means, g.harmonics, True, deg, g.opacities, g.covariances, ci, V, H, W, lay,
+                                        need_state=False, ctx=raster.RasterContext(defer_geom=False))
+        out.update(scatter_stats(st2, V, H, W))
     print(json.dumps(out))
 
 
