@@ -1141,8 +1141,18 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
   const int nblk = (G + NTH - 1) / NTH;
   // blocks dealt round-robin (p, p + per_view, ...): neighbouring blocks (context-image rows)
   // carry similar loads, so contiguous runs left some workgroups with several times the work
+  // the next block's compact records are loaded one iteration ahead (software pipelining:
+  // the loop is a chain of short dependent steps, each waiting on memory)
+  const uint2* vrec = cut_rec ? cut_rec + (size_t)v * G : nullptr;
+  uint2 cr_next = make_uint2(0u, 0u);
+  if (vrec && p * NTH + tid < G) cr_next = vrec[p * NTH + tid];
   for (int blk = p; blk < nblk; blk += per_view) {
     const int g = blk * NTH + tid;
+    const uint2 cr_cur = cr_next;
+    if (vrec) {
+      const int gn = (blk + per_view) * NTH + tid;
+      cr_next = gn < G ? vrec[gn] : make_uint2(0u, 0u);
+    }
     int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     int sx0 = 0, sx1 = 0, sy0 = 0, sy1 = 0;
     bool big = false;  // rect over more than 16 super-blocks: tested per (Gaussian, super-block) below
@@ -1153,7 +1163,7 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
       // with deferred geometry it does not exist yet), else from the geometry record
       uint32_t zb = 0u;
       if (cut_rec) {
-        const uint2 cr = cut_rec[(size_t)v * G + g];
+        const uint2 cr = cr_cur;
         x0 = (int)(cr.x & 0xFFu);
         x1 = (int)((cr.x >> 8) & 0xFFu);
         y0 = (int)((cr.x >> 16) & 0xFFu);
