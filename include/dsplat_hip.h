@@ -288,7 +288,10 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
                     const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
                     uint64_t* scratch, int write_keys, int clear_counts, uint32_t max_count_hint,
                     int binning_layout, float* out_color, float* final_T, uint32_t* n_contrib,
-                    void* stream);
+                    uint32_t* seg_overflow, void* stream);
+/* seg_overflow (NULL: none; DSR_SEG_ENDS layout only): the depth cut's flags, written exactly
+ * as dsr_render_fwd writes them (tile, any-flag, super-block), so this launch can replace
+ * dsr_bin_sort + dsr_render_fwd for the written heads when no backward needs sorted keys. */
 /* clear_counts != 0 (fixed-capacity layout only): seg_count is zeroed as it is consumed, so
  * the buffer can serve the next dsr_project_bin_cameras call as already-zeroed counters.
  * Bounded capacity (dsr_project_bin_cameras seg_capacity < G, seg_stride = that capacity): a

@@ -2885,7 +2885,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     int G, int H, int W, int gx, int T, const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
     const uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_count, uint32_t stride,
     uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits, int write_keys, int clear_counts,
-    int exact_rebuild, float* __restrict__ out, float* __restrict__ finalT, uint32_t* __restrict__ ncontrib) {
+    int exact_rebuild, float* __restrict__ out, float* __restrict__ finalT, uint32_t* __restrict__ ncontrib,
+    uint32_t* __restrict__ seg_overflow) {
   constexpr uint32_t cap = NT * KMAX;
   constexpr uint32_t padded = cap + cap / KMAX;
   extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
@@ -2961,6 +2962,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     composite_tile<LAST>([&](uint32_t i) { return (uint32_t)keys[i]; }, b, e, gv, (float)sx0, (float)sy0, pp, lane, lt,
                          plist, Tr, C01, C2, last, alive);
   if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
+  // depth cut (seg_overflow given, DSR_SEG_ENDS): a pixel of this wave still live at the end
+  // of the written part while the tile has omitted entries -> flag the tile, the any-flag and
+  // the super-block, exactly as dsr_render_fwd does (the tail pass completes such tiles)
+  if (seg_overflow != nullptr && e < seg_start[seg + 1] && __any(alive) && lane == 0) {
+    seg_overflow[seg] = 1u;
+    seg_overflow[(size_t)gridDim.z * T] = 1u;
+    const int sb = cut_superblock(gx, T / gx), sbl = __builtin_ctz((unsigned)sb);
+    const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((T / gx + sb - 1) / sb);
+    seg_overflow[(size_t)gridDim.z * T + 1 + (size_t)v * nsb + (ty >> sbl) * nsx + (tx >> sbl)] = 1u;
+  }
   // counts handed back zeroed for the next call's binning (every thread read it before the
   // sort's first barrier)
   if (clear_counts && tid == 0) seg_count[seg] = 0u;
@@ -4031,8 +4042,11 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                     const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
                     uint64_t* scratch, int write_keys, int clear_counts, uint32_t max_count_hint,
-                    int binning_layout, float* out_color, float* final_T, uint32_t* n_contrib, void* stream) {
+                    int binning_layout, float* out_color, float* final_T, uint32_t* n_contrib,
+                    uint32_t* seg_overflow, void* stream) {
   DSPLAT_REQUIRE(!clear_counts || seg_stride > 0, "dsr_sort_render: clear_counts needs the fixed-capacity layout");
+  DSPLAT_REQUIRE(seg_overflow == nullptr || (seg_stride == kSegEnds && seg_start != nullptr),
+                 "dsr_sort_render: seg_overflow needs the DSR_SEG_ENDS layout (depth cut)");
   DSPLAT_REQUIRE(!write_keys || seg_stride == 0 || seg_stride == kSegEnds || (uint32_t)G <= seg_stride,
                  "dsr_sort_render: write_keys needs segments that hold every entry (seg_stride >= G)");
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_sort_render: bad sizes");
@@ -4086,7 +4100,7 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
   k_sort_render<K, L, NB, WP><<<grid, NT, lds, st>>>(G, H, W, gx, T, cams, geom, seg_start, seg_count, seg_stride, \
                                                      keys, scratch, id_bits, write_keys, clear_counts,             \
                                                      !(binning_layout & kLayoutRectBinning), out_color, final_T,   \
-                                                     n_contrib)
+                                                     n_contrib, seg_overflow)
   // n_contrib is optional (inference: LAST = false)
   const bool wide = (int64_t)V * T >= kWide;
   switch (ci * 2 + (n_contrib ? 1 : 0)) {

@@ -214,6 +214,9 @@ CUT_SORT_HINT = 4096  # LDS sort size for the written parts (larger ones sort th
 # evaluates no colour; each scatter pass lists the Gaussians that may emit and
 # dsr_project_survivors projects only those (~3 % of the (view, Gaussian) pairs at 12x512x960).
 DEFER_GEOM = os.environ.get("DSPLAT_DEFER_GEOM", "1") != "0"
+# ... and the written heads sorted + composited in one dsr_sort_render launch (flags for the
+# tail pass as dsr_render_fwd's) instead of dsr_bin_sort + dsr_render_fwd
+CUT_FUSED = os.environ.get("DSPLAT_CUT_FUSED", "1") != "0"
 LAYOUT_DEFER_GEOM = 32
 # Fixed-capacity binning with tile lists up to FUSED_MAX entries (the hint from earlier calls)
 # sorts and composites in one launch (dsr_sort_render); longer lists take dsr_bin_sort +
@@ -270,7 +273,7 @@ class RasterContext:
              "fused_sort_render": "FUSED_SORT_RENDER", "sort_render_hint": "SORT_RENDER_HINT",
              "inkernel_cameras": "INKERNEL_CAMERAS", "sort_prefix": "SORT_PREFIX", "cut_prefix": "CUT_PREFIX",
              "debug_keep_fast_lists": "DEBUG_KEEP_FAST_LISTS", "key_budget_bytes": "KEY_BUDGET_BYTES",
-             "seg_capacity": "SEG_CAPACITY", "defer_geom": "DEFER_GEOM"}
+             "seg_capacity": "SEG_CAPACITY", "defer_geom": "DEFER_GEOM", "cut_fused": "CUT_FUSED"}
 
     def __init__(self, **options):
         unknown = set(options) - set(self._OPTS)
@@ -612,6 +615,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         # list (None on the first call) decides whether this one builds the depth histogram
         cut_prefix = ctx.opt("cut_prefix")
         defer, surv, surv_n = False, None, None  # deferred geometry (set below when the cut is planned)
+        cut_fused = False
         prev = spec.get("two_phase_max")
         want_cut = cut_prefix > 0 and (prev is None or prev > 4 * cut_prefix)
         sb = lib.dsr_cut_superblock(H, W) if want_cut else 0
@@ -679,9 +683,14 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                   surv_n.data_ptr(), geom.data_ptr(), radii.data_ptr(), layout, st),
                            "dsr_project_survivors")
             tile_count, seg_count, stride = seg_count, cursor, SEG_ENDS
-            _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), seg_count.data_ptr(),
-                              stride, keys.data_ptr(), scratch.data_ptr(), CUT_SORT_HINT, None, 0, None, None, st),
-                       "dsr_bin_sort")
+            # no backward: the written heads are sorted and composited in one launch below
+            # (dsr_sort_render, flags as dsr_render_fwd); the keys stay unsorted in HBM unless a
+            # test asks for the lists (debug_keep_fast_lists)
+            cut_fused = bool(ctx.opt("cut_fused")) and not need_state
+            if not cut_fused:
+                _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), seg_count.data_ptr(),
+                                  stride, keys.data_ptr(), scratch.data_ptr(), CUT_SORT_HINT, None, 0, None, None,
+                                  st), "dsr_bin_sort")
             seg_sorted = None
         else:
             scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev) if maxc > lds_cap else None
@@ -704,7 +713,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(), None,
                           seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(),
                           int(bool(need_state) or snap is not None), int(fast),
-                          ctx.opt("sort_render_hint") or spec["max_count"], layout, *outs), "dsr_sort_render")
+                          ctx.opt("sort_render_hint") or spec["max_count"], layout, *outs[:3], None, st),
+                   "dsr_sort_render")
         state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, cams=cams)
         if fast:  # the counters are zero again once the launch above has run
             ctx.give_back_clean_counts(seg_count, dev, st)
@@ -721,9 +731,15 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         overflow = torch.zeros(V * T + 1, dtype=torch.int32, device=dev)  # + the any-flag word
     elif stride == SEG_ENDS:  # + any-flag + flags per (view, super-block)
         overflow = torch.zeros(V * T + 1 + V * nsb, dtype=torch.int32, device=dev)
-    _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
-                      _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(), _ptr(seg_sorted),
-                      _ptr(overflow), None, *outs), "dsr_render_fwd")
+    if cut_fused:  # n_contrib only from the tail's re-render: not exposed (state.n_contrib None)
+        _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
+                          seg_start.data_ptr(), seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(),
+                          int(bool(debug_lists)), 0, CUT_SORT_HINT, layout, color.data_ptr(), final_T.data_ptr(),
+                          None, overflow.data_ptr(), st), "dsr_sort_render(depth cut)")
+    else:
+        _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
+                          _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(), _ptr(seg_sorted),
+                          _ptr(overflow), None, *outs), "dsr_render_fwd")
     if overflow is not None:
         # tiles whose unsorted (or unwritten) tail would have blended: complete them, sort them
         # in full, render them again (every launch returns at once for unflagged tiles; no sync)
@@ -741,8 +757,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         _lib.check(lib.dsr_render_fwd(G, V, H, W, cams.data_ptr(), geom.data_ptr(), _ptr(seg_start),
                                       seg_count.data_ptr(), stride, keys.data_ptr(), None, None, overflow.data_ptr(),
                                       *outs), "dsr_render_fwd(overflow)")
-    state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, seg_sorted, overflow,
-                        tile_count if stride == SEG_ENDS else None, cams=cams)
+    state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, None if cut_fused else n_contrib,
+                        seg_sorted, overflow, tile_count if stride == SEG_ENDS else None, cams=cams)
     state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING) and stride != SEG_ENDS
     if stride == SEG_ENDS:  # the depth-cut plan (tools/cut_case.py statistics)
         state.cut_plan = (cut, cut_rec, lib.dsr_cut_superblock(H, W))

@@ -315,6 +315,7 @@ def test_config_d_shape_render_vs_oracle(gpu, monkeypatch):
     the written heads equal the heads of the oracle's lists, the image the stateful path's."""
     from my_depthsplat_amd import raster
     monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)  # no short-list hint from earlier tests
+    monkeypatch.setattr(raster, "DEBUG_KEEP_FAST_LISTS", True)  # the fused head sort writes its keys back
     sc = scene_inputs(h=448, w=768, n_ctx=6, n_tgt=2, seed=2000)
     st = settings_for(sc)
     means, shs, opac, cov6 = flat_inputs(sc)
@@ -352,6 +353,7 @@ def test_config_e_shape_render_vs_oracle(gpu, monkeypatch):
     render; the written heads equal the heads of the oracle's sorted lists."""
     from my_depthsplat_amd import raster
     monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)  # no short-list hint from earlier tests
+    monkeypatch.setattr(raster, "DEBUG_KEEP_FAST_LISTS", True)  # the fused head sort writes its keys back
     sc = scene_inputs(h=512, w=960, n_ctx=12, n_tgt=1, seed=3000)
     assert sc.gaussians.means.shape[1] == 12 * 512 * 960
     st = settings_for(sc)

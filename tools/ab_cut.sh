@@ -25,7 +25,7 @@ for round in 1 2; do
 import csv, sys
 rows = {r["Name"]: r for r in csv.DictReader(open(sys.argv[2]))}
 parts = []
-for k in ("k_preprocess_cut", "k_scatter_cut", "k_project_survivors", "k_sort_lds", "k_render_fwd", "k_sort_groups", "k_msd_split"):
+for k in ("k_preprocess_cut", "k_scatter_cut", "k_project_survivors", "k_sort_lds", "k_sort_render", "k_render_fwd", "k_sort_groups", "k_msd_split"):
     for name, r in rows.items():
         if k in name:
             parts.append(f"{k}={float(r['TotalDurationNs']) / 1e3 / 6:.1f}us/call x{int(r['Calls']) // 6}")
