@@ -557,6 +557,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     # from the previous call's sort + composite (two launches per forward), segments of bounded
     # capacity (keys + scratch: 16 B per (view, tile, capacity slot))
     debug_lists = ctx.opt("debug_keep_fast_lists")
+    cut_fused = False  # depth cut without a backward: heads sorted + composited by dsr_sort_render
     cap = G if debug_lists else ctx.seg_capacity(G)
     fast = (ctx.opt("fused_sort_render") and maxc_hint <= FUSED_MAX and ctx.opt("inkernel_cameras")
             and cam_in is not None and not need_state and zeroed_counts is None and T <= _HIST_LDS_MAX
@@ -615,7 +616,6 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         # list (None on the first call) decides whether this one builds the depth histogram
         cut_prefix = ctx.opt("cut_prefix")
         defer, surv, surv_n = False, None, None  # deferred geometry (set below when the cut is planned)
-        cut_fused = False
         prev = spec.get("two_phase_max")
         want_cut = cut_prefix > 0 and (prev is None or prev > 4 * cut_prefix)
         sb = lib.dsr_cut_superblock(H, W) if want_cut else 0
