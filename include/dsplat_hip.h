@@ -352,14 +352,17 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
  * projection of pixel (x,y) at depth[b,d,y,x] through K[b,j] and pose[b,j].
  *   ref [B,C,H,W]  tgt [B,J,C,H,W]  intr [B,J,3,3] (pixel units)  pose [B,J,4,4]
  *   depth [B,D,H,W] when depth_per_pixel else [B,D]   ->   cost [B,D,H,W]
- * C in {16, 32, 64, 128} (matrix cores): the reference pixels are grouped by the epipolar line
- * they lie on w.r.t. each source view (16 pixels of one line tap a thin band around ONE
- * target line); each group's correlations with its band's distinct target pixels are one
- * exact-f32 GEMM on v_mfma_f32_16x16x4_f32, finished by the 4-tap bilinear gather. Views are
- * summed in launch order (deterministic). Other C: a direct channel-last kernel.
+ * C in {16, 32, 64, 128} (matrix cores): small grids (B*H*W <= 32768, e.g. 2x64^2) run one
+ * band kernel: 16 reference pixels of a row x 64 depths per workgroup, correlated with the
+ * bounding box of their taps as one exact-f32 GEMM (v_mfma_f32_16x16x4_f32) straight from the
+ * [B,C,H,W] maps. Larger grids group the reference pixels by the epipolar line they lie on
+ * w.r.t. each source view (16 pixels of one line tap a thin band around ONE target line);
+ * each group's correlations with its band's distinct target pixels are one GEMM, finished by
+ * the 4-tap bilinear gather. Views are summed in launch order (deterministic). Other C: a
+ * direct channel-last kernel.
  * workspace: dcv_cost_volume_workspace_size bytes (channel-last copies of tgt and ref with a
- * zero padding row per image, and the epipolar groups), filled here and read by
- * dcv_cost_volume_bwd. */
+ * zero padding row per image, and the epipolar groups), filled here (or, after a band-kernel
+ * forward, by dcv_cost_volume_bwd itself) and read by dcv_cost_volume_bwd. */
 size_t dcv_cost_volume_workspace_size(int B, int J, int C, int H, int W);
 int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel,
                         const float* ref, const float* tgt, const float* intr, const float* pose,
@@ -368,12 +371,14 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
 
 /* Backward of dcv_cost_volume_fwd w.r.t. both feature maps (geometry gets no grad,
  * matching.py:46). dcost [B,D,H,W] -> dref [B,C,H,W] (overwritten), dtgt [B,J,C,H,W]
- * (overwritten). Needs the forward's workspace and dcv_cost_volume_bwd_workspace_size bytes
- * of scratch (channel-last gradient accumulators). Reference gradients are summed in a fixed
- * order; target gradients with float atomics (pixels shared between groups). */
+ * (overwritten). ref / tgt: the forward's inputs; workspace: the forward's (completed here
+ * when the forward ran the band kernel); dcv_cost_volume_bwd_workspace_size bytes of scratch
+ * (channel-last gradient accumulators). Reference gradients are summed in a fixed order;
+ * target gradients with float atomics (pixels shared between groups: the order of those adds,
+ * hence the last bits of dtgt, can change from run to run). */
 size_t dcv_cost_volume_bwd_workspace_size(int B, int J, int C, int H, int W);
 int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel,
-                        const float* ref, const void* workspace, const float* intr,
+                        const float* ref, const float* tgt, void* workspace, const float* intr,
                         const float* pose, const float* depth, float clamp_min_depth,
                         const float* dcost, float* dref, float* dtgt, void* bwd_workspace,
                         void* stream);

@@ -17,6 +17,9 @@
 
 #include "dsplat_common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace {
 
 constexpr int DG = 16;  // depth hypotheses per register group
@@ -847,6 +850,215 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
   }
 }
 
+// ---- forward on the matrix cores, band form (small grids: configs A / B) ---------------
+// Round-2 kernel, kept for shapes where one epipolar group per workgroup underfills the chip
+// (band_fwd below): one launch, no channel-last copies and no grouping pass.
+// One workgroup per (16 reference pixels of a row, 64 depth hypotheses): thread t owns pixel
+// t & 15 and depths (t >> 4) + 16 s, s < 4, and keeps those samples' positions in registers.
+// Per source view the workgroup takes the bounding box of every target pixel its samples tap
+// (a block min / max: no LDS atomics, no bitmap), computes the correlations of its 16
+// reference pixels with ALL box pixels as one exact-f32 GEMM on v_mfma_f32_16x16x4_f32
+// (A = the reference tile, loaded once into registers straight from [B,C,H,W]; B = target
+// columns loaded straight from [B,J,C,H,W], no channel-last copy), and finishes with the
+// 4-tap bilinear gather from LDS. A small-baseline epipolar band fills its box (a few tens
+// to a few hundred pixels at these scales); a box above kBandMax pixels is computed by direct
+// dot products from global memory instead (wide, scattered taps; rare).
+constexpr int BTP = 16;                       // reference pixels per workgroup
+constexpr int BDCH = 64;                      // depth hypotheses per workgroup
+constexpr int BSPT = BTP * BDCH / 256;        // samples per thread
+constexpr int kBandMax = 512;                 // box pixels whose correlations fit in LDS (33 KB:
+                                              // 4 workgroups per CU, all of config B's in one round)
+constexpr int kCorrStride = kBandMax + 1;     // odd row stride: the gather's lanes spread over banks
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+template <int NK>  // NK = C / 4 matrix-core steps
+__global__ __launch_bounds__(256) void k_cost_band(int J, int H, int W, int D, int depth_per_pixel,
+                                                   const float* __restrict__ ref, const float* __restrict__ tgt,
+                                                   const float* __restrict__ intr, const float* __restrict__ pose,
+                                                   const float* __restrict__ depth, float clampz,
+                                                   float* __restrict__ cost) {
+  constexpr int C = 4 * NK;
+  extern __shared__ __attribute__((aligned(16))) float cv_lds[];
+  float* s_corr = cv_lds;                                           // [BTP][kCorrStride]
+  int* s_box = reinterpret_cast<int*>(cv_lds + BTP * kCorrStride);  // [4 waves][4]
+  const int HW = H * W;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tpr = (W + BTP - 1) / BTP;
+  const int y = blockIdx.x / tpr, x0 = (blockIdx.x % tpr) * BTP;
+  const int b = blockIdx.y, d0 = blockIdx.z * BDCH;
+  const int i = tid & (BTP - 1), dl = tid >> 4;
+  const int px = x0 + i;
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  // A operand (v_mfma_f32_16x16x4f32: lane l holds A[l & 15][l >> 4]): channel 4 s + (l >> 4) of
+  // reference pixel x0 + (l & 15), for every step s — the whole 16 x C tile in NK registers
+  float a[NK];
+  {
+    const int ax = x0 + (lane & 15);
+    const float* rp = ref + ((size_t)b * C + (lane >> 4)) * HW + (size_t)y * W + ax;
+#pragma unroll
+    for (int s = 0; s < NK; ++s) a[s] = ax < W ? rp[(size_t)4 * s * HW] : 0.f;
+  }
+  float acc[BSPT];
+#pragma unroll
+  for (int s = 0; s < BSPT; ++s) acc[s] = 0.f;
+  for (int j = 0; j < J; ++j) {
+    Cam cam;
+    load_cam(intr + ((size_t)b * J + j) * 9, pose + ((size_t)b * J + j) * 16, cam);
+    // sample positions (reference operation order, as k_cost_mfma) and the taps' bounding box
+    float sx[BSPT], sy[BSPT];
+    int bx0 = 0x7fffffff, bx1 = -1, by0 = 0x7fffffff, by1 = -1;
+    {
+      const float fpx = (float)px, fpy = (float)y;
+      const float qx = cam.Kinv[0] * fpx + cam.Kinv[1] * fpy + cam.Kinv[2];
+      const float qy = cam.Kinv[3] * fpx + cam.Kinv[4] * fpy + cam.Kinv[5];
+      const float qz = cam.Kinv[6] * fpx + cam.Kinv[7] * fpy + cam.Kinv[8];
+      const float prx = cam.R[0] * qx + cam.R[1] * qy + cam.R[2] * qz;
+      const float pry = cam.R[3] * qx + cam.R[4] * qy + cam.R[5] * qz;
+      const float prz = cam.R[6] * qx + cam.R[7] * qy + cam.R[8] * qz;
+#pragma unroll
+      for (int s = 0; s < BSPT; ++s) {
+        const int d = d0 + dl + 16 * s;
+        sx[s] = __int_as_float(0x7fc00000);
+        sy[s] = 0.f;
+        if (d < D && px < W) {
+          const float dep = depth_per_pixel ? depth[((size_t)b * D + d) * HW + (size_t)y * W + px]
+                                            : depth[(size_t)b * D + d];
+          const float X = prx * dep + cam.t[0];
+          const float Y = pry * dep + cam.t[1];
+          const float Z = prz * dep + cam.t[2];
+          const float xx = cam.K[0] * X + cam.K[1] * Y + cam.K[2] * Z;
+          const float yy = cam.K[3] * X + cam.K[4] * Y + cam.K[5] * Z;
+          const float zz = fmaxf(cam.K[6] * X + cam.K[7] * Y + cam.K[8] * Z, clampz);
+          const float u = xx / zz, v = yy / zz;
+          const float gxn = 2 * u / (W - 1) - 1;
+          const float gyn = 2 * v / (H - 1) - 1;
+          const float ix = ((gxn + 1) / 2) * (W - 1);
+          const float iy = ((gyn + 1) / 2) * (H - 1);
+          if (ix > -2.f && ix < (float)W + 1.f && iy > -2.f && iy < (float)H + 1.f) {
+            sx[s] = ix;
+            sy[s] = iy;
+            const int tx = (int)floorf(ix), ty = (int)floorf(iy);
+            const int cx0 = max(tx, 0), cx1 = min(tx + 1, W - 1), cy0 = max(ty, 0), cy1 = min(ty + 1, H - 1);
+            if (cx0 <= cx1 && cy0 <= cy1) {
+              bx0 = min(bx0, cx0);
+              bx1 = max(bx1, cx1);
+              by0 = min(by0, cy0);
+              by1 = max(by1, cy1);
+            }
+          }
+        }
+      }
+    }
+    bx0 = wave_min_i(bx0);
+    by0 = wave_min_i(by0);
+    bx1 = wave_max_i(bx1);
+    by1 = wave_max_i(by1);
+    if (lane == 0) {
+      s_box[wv * 4] = bx0;
+      s_box[wv * 4 + 1] = bx1;
+      s_box[wv * 4 + 2] = by0;
+      s_box[wv * 4 + 3] = by1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bx0 = min(bx0, s_box[k * 4]);
+      bx1 = max(bx1, s_box[k * 4 + 1]);
+      by0 = min(by0, s_box[k * 4 + 2]);
+      by1 = max(by1, s_box[k * 4 + 3]);
+    }
+    const float* tg = tgt + ((size_t)b * J + j) * (size_t)C * HW;
+    if (bx1 >= bx0) {  // uniform: some sample taps the image
+      const int bw = bx1 - bx0 + 1, U = bw * (by1 - by0 + 1);
+      if (U <= kBandMax) {
+        // corr[16 x U] on the matrix cores: wave wv takes column blocks wv, wv + 4, ...
+        const int nblk = (U + 15) / 16;
+        for (int blk = wv; blk < nblk; blk += 4) {
+          const int u = blk * 16 + (lane & 15);
+          int q = -1;
+          if (u < U) {
+            const int r = u / bw;
+            q = (by0 + r) * W + bx0 + (u - r * bw);
+          }
+          float bv[NK];
+          const float* bp = tg + (size_t)(lane >> 4) * HW + (q < 0 ? 0 : q);
+#pragma unroll
+          for (int s = 0; s < NK; ++s) bv[s] = q >= 0 ? bp[(size_t)4 * s * HW] : 0.f;
+          // four independent accumulation chains (a dependent v_mfma_f32_16x16x4f32 waits ~40
+          // cycles for its accumulator), summed at the end
+          f32x4 c4[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) c4[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < NK; ++s) c4[s & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bv[s], c4[s & 3], 0, 0, 0);
+          c4[0] = (c4[0] + c4[1]) + (c4[2] + c4[3]);
+          // D[row][col]: col = lane & 15 (box pixel u), row = 4 (lane >> 4) + r (reference pixel)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s_corr[(4 * (lane >> 4) + r) * kCorrStride + u] = c4[0][r];
+        }
+        __syncthreads();
+        const float* crow = s_corr + i * kCorrStride;
+#pragma unroll
+        for (int s = 0; s < BSPT; ++s) {
+          if (!(sx[s] == sx[s])) continue;
+          const float fx0 = floorf(sx[s]), fy0 = floorf(sy[s]);
+          const int tx0 = (int)fx0, ty0 = (int)fy0;
+          const float wx0 = (float)(tx0 + 1) - sx[s], wx1 = sx[s] - fx0, wy0 = (float)(ty0 + 1) - sy[s],
+                      wy1 = sy[s] - fy0;
+          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
+          float sum = 0.f;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+            if (tx >= 0 && tx < W && ty >= 0 && ty < H) sum += wt[t] * crow[(ty - by0) * bw + (tx - bx0)];
+          }
+          acc[s] += sum;
+        }
+      } else {
+        // the box is too large for LDS: each tap's dot product over C straight from memory
+#pragma unroll
+        for (int s = 0; s < BSPT; ++s) {
+          if (!(sx[s] == sx[s])) continue;
+          const float fx0 = floorf(sx[s]), fy0 = floorf(sy[s]);
+          const int tx0 = (int)fx0, ty0 = (int)fy0;
+          const float wx0 = (float)(tx0 + 1) - sx[s], wx1 = sx[s] - fx0, wy0 = (float)(ty0 + 1) - sy[s],
+                      wy1 = sy[s] - fy0;
+          const float wt[4] = {wx0 * wy0, wx1 * wy0, wx0 * wy1, wx1 * wy1};
+          float sum = 0.f;
+          for (int t = 0; t < 4; ++t) {
+            const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+            if (!(tx >= 0 && tx < W && ty >= 0 && ty < H)) continue;
+            const float* rp = ref + (size_t)b * C * HW + (size_t)y * W + px;
+            const float* qp = tg + (size_t)ty * W + tx;
+            float dot = 0.f;
+            for (int c = 0; c < C; ++c) dot += rp[(size_t)c * HW] * qp[(size_t)c * HW];
+            sum += wt[t] * dot;
+          }
+          acc[s] += sum;
+        }
+      }
+    }
+    __syncthreads();  // s_corr / s_box reused by the next view
+  }
+#pragma unroll
+  for (int s = 0; s < BSPT; ++s) {
+    const int d = d0 + dl + 16 * s;
+    if (d < D && px < W) cost[((size_t)b * D + d) * HW + (size_t)y * W + px] = acc[s] * scale;
+  }
+}
+
+size_t cost_band_lds_bytes() { return (size_t)(BTP * kCorrStride + 16) * sizeof(float); }
+
 // Backward: one wave per (b, pixel); lanes over channels.
 //   dref[c,p]   += sum_{j,d} g(d) * warp_j[c,d,p]
 //   dtgt[q,c]   += g(d) * w_k * ref[c,p] for each tap (atomics into channel-last scratch)
@@ -993,6 +1205,43 @@ static bool epi_path(int C, int H, int W, bool bwd) {
   return C % 16 == 0 && C <= 128 && epi_lds_bytes(C, H, W, bwd) <= 160 * 1024;
 }
 
+// Small grids take the band kernel for the forward: one launch with no channel-last copies
+// and no grouping pass. The epipolar path's set-up is fixed cost (3 launches) and one
+// epipolar group per workgroup leaves a small grid's workgroups short of work (round 3: config A
+// 16.4 -> 27.5 us, config B scale 0 25.6 -> 38.5 us when every shape took it). Large grids
+// (config D's rig, diagonal epipolar lines whose row-segment boxes overflow kBandMax) keep
+// the epipolar groups. DSPLAT_CV_PATH=band / epi overrides the choice (A/B timing tools).
+constexpr long kBandMaxPixels = 32768;  // B * H * W
+static bool band_fwd(int B, int C, int H, int W) {
+  if (!(C == 16 || C == 32 || C == 64 || C == 128)) return false;
+  if (const char* f = getenv("DSPLAT_CV_PATH")) {
+    if (!strcmp(f, "band")) return true;
+    if (!strcmp(f, "epi")) return false;
+  }
+  return (long)B * H * W <= kBandMaxPixels;
+}
+
+// Channel-last copies (+ the epipolar groups when the epipolar kernels run): the forward's
+// set-up on the epipolar / generic paths, and the backward's when the forward took the band
+// kernel (which needs none of it).
+static int epi_setup(int B, int J, int C, int H, int W, const float* ref, const float* tgt, const float* intr,
+                     const float* pose, void* workspace, hipStream_t st) {
+  const int HW = H * W;
+  float* tgt_hwc = static_cast<float*>(workspace);
+  float* ref_hwc = tgt_hwc + (size_t)B * J * (HW + 1) * C;
+  int* groups = reinterpret_cast<int*>(ref_hwc + (size_t)B * (HW + 1) * C);
+  float* geom = reinterpret_cast<float*>(groups + (size_t)B * J * HW);
+  // a band pixel's C channels are one contiguous row for the GEMM's operands; row HW of each
+  // image is zero (the padding / out-of-image row)
+  k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc);
+  if (int e = dsplat::check_launch("k_to_hwc")) return e;
+  if (!epi_path(C, H, W, false)) return 0;
+  k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW + 1, ref, ref_hwc);
+  if (int e = dsplat::check_launch("k_to_hwc(ref)")) return e;
+  k_epi_groups<<<dim3(B, J), 1024, 0, st>>>(J, H, W, intr, pose, groups, geom);
+  return dsplat::check_launch("k_epi_groups");
+}
+
 int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref,
                         const float* tgt, const float* intr, const float* pose, const float* depth,
                         float clamp_min_depth, void* workspace, float* cost, void* stream) {
@@ -1000,33 +1249,38 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
   DSPLAT_REQUIRE(ref && tgt && intr && pose && depth && workspace && cost, "dcv_cost_volume_fwd: null pointer");
   hipStream_t st = (hipStream_t)stream;
   const int HW = H * W;
+  if (band_fwd(B, C, H, W)) {
+    const size_t lds = cost_band_lds_bytes();
+#define DCV_BAND(NK)                                                                                              \
+  do {                                                                                                            \
+    if (int e = dsplat::ensure_dyn_lds((const void*)k_cost_band<NK>, lds, "hipFuncSetAttribute(k_cost_band)"))    \
+      return e;                                                                                                   \
+    k_cost_band<NK><<<grid, 256, lds, st>>>(J, H, W, D, depth_per_pixel, ref, tgt, intr, pose, depth,            \
+                                            clamp_min_depth, cost);                                               \
+  } while (0)
+    const dim3 grid((unsigned)(((W + BTP - 1) / BTP) * H), (unsigned)B, (unsigned)((D + BDCH - 1) / BDCH));
+    switch (C) {
+      case 16: DCV_BAND(4); break;
+      case 32: DCV_BAND(8); break;
+      case 64: DCV_BAND(16); break;
+      default: DCV_BAND(32); break;
+    }
+#undef DCV_BAND
+    return dsplat::check_launch("k_cost_band");
+  }
+  if (int e = epi_setup(B, J, C, H, W, ref, tgt, intr, pose, workspace, st)) return e;
   float* tgt_hwc = static_cast<float*>(workspace);
   float* ref_hwc = tgt_hwc + (size_t)B * J * (HW + 1) * C;
   int* groups = reinterpret_cast<int*>(ref_hwc + (size_t)B * (HW + 1) * C);
   float* geom = reinterpret_cast<float*>(groups + (size_t)B * J * HW);
-  // channel-last copies: a band pixel's C channels are one contiguous row for the GEMM's
-  // operands; row HW of each image is zero (the padding / out-of-image row)
-  k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc);
-  if (int e = dsplat::check_launch("k_to_hwc")) return e;
   const float scale = 1.0f / (sqrtf((float)C) * (float)J);
   if (epi_path(C, H, W, false)) {
-    k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW + 1, ref, ref_hwc);
-    if (int e = dsplat::check_launch("k_to_hwc(ref)")) return e;
-    k_epi_groups<<<dim3(B, J), 1024, 0, st>>>(J, H, W, intr, pose, groups, geom);
-    if (int e = dsplat::check_launch("k_epi_groups")) return e;
     const size_t lds = epi_lds_bytes(C, H, W, false);
-    static size_t attr = 0;
-    if (lds > attr) {
-#define DCV_ATTR(NK, SPT)                                                                                    \
-  if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_cost_epi<NK, SPT>,                        \
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), \
-                                "hipFuncSetAttribute(k_cost_epi)"))                                         \
-    return e;
-      DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
-      DCV_ATTR(4, 8) DCV_ATTR(8, 8) DCV_ATTR(16, 8) DCV_ATTR(32, 8)
+#define DCV_ATTR(NK, SPT)                                                                                       \
+  if (int e = dsplat::ensure_dyn_lds((const void*)k_cost_epi<NK, SPT>, lds, "hipFuncSetAttribute(k_cost_epi)")) return e;
+    DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
+    DCV_ATTR(4, 8) DCV_ATTR(8, 8) DCV_ATTR(16, 8) DCV_ATTR(32, 8)
 #undef DCV_ATTR
-      attr = lds;
-    }
     const int ngroups = (HW + EG - 1) / EG;
     const int spt = D <= 32 ? 2 : 8;
     const dim3 grid(8u * (unsigned)((B * ngroups + 7) / 8), (unsigned)((D + 16 * spt - 1) / (16 * spt)));
@@ -1051,14 +1305,17 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
 }
 
 int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref,
-                        const void* workspace, const float* intr, const float* pose, const float* depth,
+                        const float* tgt, void* workspace, const float* intr, const float* pose, const float* depth,
                         float clamp_min_depth, const float* dcost, float* dref, float* dtgt, void* bwd_workspace,
                         void* stream) {
   DSPLAT_REQUIRE(B > 0 && J > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_cost_volume_bwd: bad sizes");
-  DSPLAT_REQUIRE(ref && workspace && intr && pose && depth && dcost && dref && dtgt && bwd_workspace,
+  DSPLAT_REQUIRE(ref && tgt && workspace && intr && pose && depth && dcost && dref && dtgt && bwd_workspace,
                  "dcv_cost_volume_bwd: null pointer");
   hipStream_t st = (hipStream_t)stream;
   const int HW = H * W;
+  // the band forward skipped the channel-last copies and the grouping: done here
+  if (band_fwd(B, C, H, W))
+    if (int e = epi_setup(B, J, C, H, W, ref, tgt, intr, pose, workspace, st)) return e;
   const float* tgt_hwc = static_cast<const float*>(workspace);
   const float* ref_hwc = tgt_hwc + (size_t)B * J * (HW + 1) * C;
   const int* groups = reinterpret_cast<const int*>(ref_hwc + (size_t)B * (HW + 1) * C);
@@ -1068,18 +1325,11 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
   if (int e = dsplat::zero_async(dtgt_hwc, (size_t)B * J * (HW + 1) * C * 4, st, "zero dtgt_hwc")) return e;
   if (epi_path(C, H, W, true) && epi_path(C, H, W, false)) {
     const size_t lds = epi_lds_bytes(C, H, W, true);
-    static size_t attr = 0;
-    if (lds > attr) {
-#define DCV_ATTR(NK, SPT)                                                                                    \
-  if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_cost_epi_bwd<NK, SPT>,                    \
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), \
-                                "hipFuncSetAttribute(k_cost_epi_bwd)"))                                     \
-    return e;
-      DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
-      DCV_ATTR(4, 8) DCV_ATTR(8, 8) DCV_ATTR(16, 8) DCV_ATTR(32, 8)
+#define DCV_ATTR(NK, SPT)                                                                                       \
+  if (int e = dsplat::ensure_dyn_lds((const void*)k_cost_epi_bwd<NK, SPT>, lds, "hipFuncSetAttribute(k_cost_epi_bwd)")) return e;
+    DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
+    DCV_ATTR(4, 8) DCV_ATTR(8, 8) DCV_ATTR(16, 8) DCV_ATTR(32, 8)
 #undef DCV_ATTR
-      attr = lds;
-    }
     const float scale = 1.0f / (sqrtf((float)C) * (float)J);
     const int ngroups = (HW + EG - 1) / EG, spt = D <= 32 ? 2 : 8;
     const dim3 grid(8u * (unsigned)((B * ngroups + 7) / 8));

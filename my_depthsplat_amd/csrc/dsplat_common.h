@@ -76,6 +76,11 @@ __device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t v) {
 __global__ void k_zero_u32(uint32_t* __restrict__ p, size_t n);
 int zero_async(void* p, size_t bytes, hipStream_t st, const char* what);
 
+// Opt kernel `fn` into `bytes` of dynamic LDS on the current device before its launch
+// (hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device). Remembered per (kernel,
+// device) under a mutex: safe from concurrent host threads driving different devices/streams.
+int ensure_dyn_lds(const void* fn, size_t bytes, const char* what);
+
 // Row-block staging through LDS: the rows of a [*, row] array owned by one block are one
 // contiguous span, so it moves as 16-byte vectors (coalesced) and each thread then reads /
 // writes its own row in LDS (odd row lengths are bank-conflict free). Per-thread rows of

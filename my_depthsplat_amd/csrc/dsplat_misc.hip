@@ -1,8 +1,16 @@
 // Error reporting and version for the libdsplat_hip.so C ABI (include/dsplat_hip.h).
 #include "dsplat_common.h"
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 namespace {
 thread_local char g_err[512] = "";
+// (kernel, device) -> the dynamic-LDS limit already opted into (hipFuncSetAttribute is a
+// per-device setting); guarded, so concurrent callers on different threads / devices are safe
+std::mutex g_attr_mu;
+std::map<std::pair<const void*, int>, size_t> g_attr;
 }
 
 namespace dsplat {
@@ -28,9 +36,21 @@ int zero_async(void* p, size_t bytes, hipStream_t st, const char* what) {
   k_zero_u32<<<blocks, 256, 0, st>>>(static_cast<uint32_t*>(p), n);
   return check_launch(what);
 }
+
+int ensure_dyn_lds(const void* fn, size_t bytes, const char* what) {
+  int dev = 0;
+  if (int e = check_hip(hipGetDevice(&dev), what)) return e;
+  std::lock_guard<std::mutex> lock(g_attr_mu);
+  size_t& cur = g_attr[{fn, dev}];
+  if (bytes <= cur) return 0;
+  if (int e = check_hip(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes), what))
+    return e;
+  cur = bytes;
+  return 0;
+}
 }  // namespace dsplat
 
 extern "C" {
 const char* dsplat_last_error(void) { return g_err; }
-int dsplat_abi_version(void) { return 12; }
+int dsplat_abi_version(void) { return 13; }
 }

@@ -17,6 +17,7 @@
 // rect, sort keys) keep the evaluation order of oracle/dsr_oracle.cpp (-ffp-contract=off).
 
 #include <type_traits>
+#include <utility>
 
 #include "dsplat_common.h"
 
@@ -3783,15 +3784,9 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, 
   const int deg = shs ? sh_degree : -1;
 #define DSR_PC(D, L)                                                                                         \
   do {                                                                                                       \
-    static bool attr = false;                                                                                \
-    if (!attr) {                                                                                             \
-      if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_preprocess_cut<D, kNTH, L>,           \
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize,          \
-                                                        kCutLdsWords * 4),                                   \
-                                    "hipFuncSetAttribute(k_preprocess_cut)"))                                \
-        return e;                                                                                            \
-      attr = true;                                                                                           \
-    }                                                                                                        \
+    if (int e = dsplat::ensure_dyn_lds((const void*)k_preprocess_cut<D, kNTH, L>, kCutLdsWords * 4,           \
+                                       "hipFuncSetAttribute(k_preprocess_cut)"))                             \
+      return e;                                                                                              \
     k_preprocess_cut<D, kNTH, L><<<xcd_grid(per_view, V), kNTH, lds, st>>>(                                  \
         G, V, H, W, gx, gy, M, means, shs, colors, opacities, cov6, cams, geom, radii, dzero, seg_count,      \
         depth_hist,                                                                                          \
@@ -3920,18 +3915,12 @@ int dsr_workspace_size(int G, int H, int W, int n_views, uint64_t key_budget, ds
 
 }  // extern "C"
 namespace {
-// dynamic LDS above 64 KiB must be opted into, once per kernel instantiation
+// dynamic LDS above 64 KiB must be opted into, per kernel instantiation and device
 template <int KM, int NTH_>
 int sort_lds_attr() {
-  static bool done = false;
-  if (done || sort_lds_bytes<KM, NTH_>() <= 65536) return 0;
-  if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds<KM, NTH_>,
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    (int)sort_lds_bytes<KM, NTH_>()),
-                                "hipFuncSetAttribute(k_sort_lds)"))
-    return e;
-  done = true;
-  return 0;
+  if (sort_lds_bytes<KM, NTH_>() <= 65536) return 0;
+  return dsplat::ensure_dyn_lds((const void*)k_sort_lds<KM, NTH_>, sort_lds_bytes<KM, NTH_>(),
+                                "hipFuncSetAttribute(k_sort_lds)");
 }
 }  // namespace
 extern "C" {
@@ -3958,30 +3947,13 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
   const int big_here = scratch != nullptr && !big_known;
   DSPLAT_REQUIRE(!big_known || workspace != nullptr,
                  "dsr_bin_sort: max_count %u > %u needs workspace (dsr_bin_sort_workspace_size)", max_count, kSortCap);
-  static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted into once
-  if (!attr_set) {
-    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds<32>,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)sort_lds_bytes<32>()),
-                                  "hipFuncSetAttribute(k_sort_lds)"))
-      return e;
-    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds<16>,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)sort_lds_bytes<16>()),
-                                  "hipFuncSetAttribute(k_sort_lds)"))
-      return e;
-    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_sort_lds<kSortCap / kSortNT, kSortNT>,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)sort_lds_bytes<kSortCap / kSortNT, kSortNT>()),
-                                  "hipFuncSetAttribute(k_sort_lds)"))
-      return e;
-    if (int e = dsplat::check_hip(hipFuncSetAttribute((const void*)k_msd_split<kSplitNT, kSplitKPT>,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)split_lds_bytes()),
-                                  "hipFuncSetAttribute(k_msd_split)"))
-      return e;
-    attr_set = true;
-  }
+  // dynamic LDS above 64 KiB must be opted into (per device; remembered by ensure_dyn_lds)
+  for (const auto& a : {std::make_pair((const void*)k_sort_lds<32>, sort_lds_bytes<32>()),
+                        std::make_pair((const void*)k_sort_lds<16>, sort_lds_bytes<16>()),
+                        std::make_pair((const void*)k_sort_lds<kSortCap / kSortNT, kSortNT>,
+                                       sort_lds_bytes<kSortCap / kSortNT, kSortNT>()),
+                        std::make_pair((const void*)k_msd_split<kSplitNT, kSplitKPT>, split_lds_bytes())})
+    if (int e = dsplat::ensure_dyn_lds(a.first, a.second, "hipFuncSetAttribute(k_sort_lds / k_msd_split)")) return e;
   uint32_t cap;
 #define DSR_SORT_LDS(KM, NTH_, FILT)                                                                        \
   do {                                                                                                      \
@@ -4074,19 +4046,11 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
   // -3 %; with n_contrib at 16 / 64 views: -5 / -6 %), loses on one scene's 768 tiles (+5 %)
   constexpr int kWide = 2048;  // (view, tile) segments from which the 5-wave kernels are used
   const void* k8w5[2] = {(const void*)k_sort_render<8, false, 12, 5>, (const void*)k_sort_render<8, true, 12, 5>};
-  static bool attr = false;
-  if (!attr) {
-    for (const Cls& c : cls)
-      for (const void* f : c.k)
-        if (int e = dsplat::check_hip(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds),
-                                      "hipFuncSetAttribute(k_sort_render)"))
-          return e;
-    for (const void* f : k8w5)
-      if (int e = dsplat::check_hip(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cls[0].lds),
-                                    "hipFuncSetAttribute(k_sort_render)"))
-        return e;
-    attr = true;
-  }
+  for (const Cls& c : cls)
+    for (const void* f : c.k)
+      if (int e = dsplat::ensure_dyn_lds(f, c.lds, "hipFuncSetAttribute(k_sort_render)")) return e;
+  for (const void* f : k8w5)
+    if (int e = dsplat::ensure_dyn_lds(f, cls[0].lds, "hipFuncSetAttribute(k_sort_render)")) return e;
   int ci = 0;
   while (ci < 2 && (max_count_hint == 0 || max_count_hint > cls[ci].cap)) ++ci;
   int id_bits = 0;

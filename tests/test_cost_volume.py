@@ -16,6 +16,16 @@ from oracle import cost_volume as ocv
 G = np.load(Path(__file__).parent / "golden" / "cost_volume.npz")
 T = lambda k: torch.from_numpy(G[k])  # noqa: E731
 TAGS = ["s0", "s1"]
+# forward kernels of dcv_cost_volume_fwd (C in {16, 32, 64, 128}): the band kernel (small grids,
+# B*H*W <= 32768) and the epipolar-group kernels (larger grids); DSPLAT_CV_PATH forces one, so
+# every shape below checks both (the backward completes the set-up after a band forward)
+PATHS = ["band", "epi"]
+
+
+@pytest.fixture(params=PATHS)
+def cv_path(request, monkeypatch):
+    monkeypatch.setenv("DSPLAT_CV_PATH", request.param)
+    return request.param
 
 
 def rel_close(a, b, tol):
@@ -56,7 +66,7 @@ def test_oracle_grads_match_reference(tag):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tag", TAGS)
-def test_hip_cost_volume_matches_reference(gpu, tag):
+def test_hip_cost_volume_matches_reference(gpu, cv_path, tag):
     from my_depthsplat_amd.matching import plane_sweep_cost_volume
     ref, tgt, K, pose, depth = [t.to(gpu) for t in case(tag)]
     per_image = tag == "s0"
@@ -90,7 +100,7 @@ def test_hip_warp_matches_reference(gpu, tag):
 
 
 @pytest.mark.gpu
-def test_hip_cost_volume_large_vs_oracle(gpu):
+def test_hip_cost_volume_large_vs_oracle(gpu, cv_path):
     """Config-B-like scale-0 shape (C=128, D=128, 64x64, 2 views) vs the oracle; out-of-view
     depths hit the zeros padding."""
     g = torch.Generator().manual_seed(11)
@@ -110,7 +120,7 @@ def test_hip_cost_volume_large_vs_oracle(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("spread", ["narrow", "wide"])
-def test_hip_cost_volume_rotated_views_vs_oracle(gpu, spread):
+def test_hip_cost_volume_rotated_views_vs_oracle(gpu, cv_path, spread):
     """Two source views with rotations and translations. narrow: per-image candidates
     (matrix-core path, a few hundred tapped pixels per tile); wide: random per-pixel depths
     scatter the taps over the image (more than the LDS tap budget -> direct fallback)."""
@@ -144,7 +154,7 @@ def test_hip_cost_volume_rotated_views_vs_oracle(gpu, spread):
 
 
 @pytest.mark.gpu
-def test_hip_cost_volume_config_a_shape_vs_oracle(gpu):
+def test_hip_cost_volume_config_a_shape_vs_oracle(gpu, cv_path):
     """BASELINE configs[0]'s cost-volume shape (2 views, C = D = 128, 32x32 features, the
     reference's linspace inverse-depth candidates, mv_unimatch.py:416-435): forward and both
     feature gradients vs the oracle (oracle/cost_volume.py, the reference's grid_sample
@@ -193,7 +203,7 @@ def _rig_case(per_pixel, C=32, H=28, W=48, D=64, seed=13):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("per_pixel", [False, True])
-def test_hip_cost_volume_circle_rig_vs_oracle(gpu, per_pixel):
+def test_hip_cost_volume_circle_rig_vs_oracle(gpu, cv_path, per_pixel):
     """Epipolar-group matrix-core path on the config-D rig geometry: forward and both feature
     gradients vs the oracle (oracle/cost_volume.py) within 1e-4; J = 2 source views summed in
     launch order, so two forward calls are bit-identical."""
