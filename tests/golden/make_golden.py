@@ -13,6 +13,9 @@ Missing third-party modules are replaced by tiny stubs written to a temp dir:
   diff_gaussian_rasterization   RECORDING stub: stores every GaussianRasterizationSettings
                             and the tensors handed to the rasterizer, returns zeros. This
                             pins the reference wrapper (cuda_splatting.py:46-264) exactly.
+  plyfile                   RECORDING stub: PlyElement.describe keeps the structured vertex
+                            array the reference builds, PlyData.write records it (no file
+                            format is written; the values pin ply_export.py:26-115).
 Reference packages are mounted as namespace packages (their __init__ chains import
 lightning / datasets and are skipped), following SURVEY.md Appendix A.
 """
@@ -85,6 +88,20 @@ class GaussianRasterizer(torch.nn.Module):
         s = self.raster_settings
         img = torch.zeros(3, s.image_height, s.image_width) + 0 * means3D.sum()
         return img, torch.zeros(means3D.shape[0], dtype=torch.int32)
+""",
+    "plyfile/__init__.py": """
+RECORD = []
+class PlyElement:
+    def __init__(self, data, name):
+        self.data, self.name = data, name
+    @staticmethod
+    def describe(data, name, **kw):
+        return PlyElement(data.copy(), name)
+class PlyData:
+    def __init__(self, elements, **kw):
+        self.elements = list(elements)
+    def write(self, path):
+        RECORD.append((str(path), [(e.name, e.data) for e in self.elements]))
 """,
 }
 
@@ -320,13 +337,68 @@ def gen_matching_tokens():
     np.savez_compressed(OUT / "matching_tokens.npz", **{k: t2n(v) for k, v in out.items()})
 
 
+def gen_ply():
+    """src/model/ply_export.py:26-115 on seeded inputs: export_ply with a non-identity c2w, and
+    save_gaussian_ply on a 2-view 20x20 context (the 8-pixel border trim, "h w spp v" order,
+    camera -> world rotations). The recorded vertex arrays are stored as float32 [N, 17]
+    (columns in construct_list_of_attributes(0) order)."""
+    import types as _t
+    from scipy.spatial.transform import Rotation
+    pe = importlib.import_module("src.model.ply_export")
+    rec = importlib.import_module("plyfile").RECORD
+    g = torch.Generator().manual_seed(21)
+    out = {}
+
+    def c2w_of(euler, t):
+        m = torch.eye(4)
+        m[:3, :3] = torch.from_numpy(Rotation.from_euler("xyz", euler).as_matrix()).float()
+        m[:3, 3] = torch.tensor(t)
+        return m
+
+    def unit_q(n):
+        q = torch.randn(n, 4, generator=g)
+        return q / q.norm(dim=-1, keepdim=True)
+
+    G = 64
+    ext = c2w_of([0.3, -0.2, 0.5], [0.1, 0.2, 0.3])
+    means = torch.randn(G, 3, generator=g)
+    scales = torch.rand(G, 3, generator=g) * 0.1 + 1e-3
+    rot = unit_q(G)
+    harm = torch.randn(G, 3, 9, generator=g)
+    opac = torch.rand(G, generator=g) * 0.98 + 0.01
+    rec.clear()
+    with tempfile.TemporaryDirectory() as td:
+        pe.export_ply(ext, means, scales, rot, harm, opac, Path(td) / "a.ply")
+    (_, els), = rec
+    (name, data), = els
+    assert name == "vertex"
+    out.update(export_ext=ext, export_means=means, export_scales=scales, export_rot=rot, export_harm=harm,
+               export_opac=opac, export_vertex=np.stack([data[f] for f in data.dtype.names], axis=1))
+    v, h, w = 2, 20, 20
+    N = v * h * w
+    exts = torch.stack([c2w_of([0.1, 0.4, -0.3], [0.0, 0.1, 0.2]), c2w_of([-0.2, 0.1, 0.25], [0.3, -0.1, 0.0])])
+    gs = _t.SimpleNamespace(means=torch.randn(1, N, 3, generator=g), harmonics=torch.randn(1, N, 3, 9, generator=g),
+                            opacities=torch.rand(1, N, generator=g) * 0.98 + 0.01)
+    dump = {"rotations": unit_q(N)[None], "scales": (torch.rand(1, N, 3, generator=g) * 0.1 + 1e-3)}
+    example = {"context": {"extrinsics": exts[None], "image": torch.rand(1, v, 3, h, w, generator=g)}}
+    rec.clear()
+    with tempfile.TemporaryDirectory() as td:
+        pe.save_gaussian_ply(gs, dump, example, Path(td) / "b.ply")
+    (_, els), = rec
+    (_, data), = els
+    out.update(save_means=gs.means, save_harm=gs.harmonics, save_opac=gs.opacities, save_rot=dump["rotations"],
+               save_scales=dump["scales"], save_ext=exts, save_hw=np.array([v, h, w]),
+               save_vertex=np.stack([data[f] for f in data.dtype.names], axis=1))
+    np.savez_compressed(OUT / "ply.npz", **{k: t2n(x) for k, x in out.items()})
+
+
 if __name__ == "__main__":
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     setup_imports()
     torch.set_default_dtype(torch.float32)
     only = sys.argv[1:]  # e.g. `make_golden.py matching` regenerates one fixture file
     for name, fn in (("cuda_splatting", gen_cuda_splatting), ("cost_volume", gen_cost_volume),
-                     ("adapter", gen_adapter), ("matching", gen_matching)):
+                     ("adapter", gen_adapter), ("matching", gen_matching), ("ply", gen_ply)):
         if not only or name in only:
             fn()
     if "matching_tokens" in only:  # separate: needs `python -O` (see gen_matching_tokens)

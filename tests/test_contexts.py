@@ -74,3 +74,60 @@ def test_two_decoders_interleaved_on_two_streams(gpu):
             assert torch.equal(o, solo[name][0]), name
     assert da.raster_ctx.hints["max_count"] == solo["a"][1]
     assert db.raster_ctx.hints["max_count"] == solo["b"][1]
+
+
+@pytest.mark.gpu
+def test_render_and_cost_volume_from_two_host_threads(gpu):
+    """SURVEY §8(b) concurrency clause: a decoder render and a plane-sweep cost volume issued
+    from two host threads at once, each on its own HIP stream, reproduce their solo outputs
+    bit for bit (the library keeps no unsynchronised global state: the dynamic-LDS opt-ins are
+    per (kernel, device) under a mutex, the raster state lives in each decoder's context)."""
+    import threading
+
+    from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
+    from my_depthsplat_amd.matching import plane_sweep_cost_volume
+    from my_depthsplat_amd.synthetic import make_scene
+    from test_cost_volume import _rig_case
+
+    sc = make_scene(batch=2, n_context=2, n_targets=3, height=256, width=256, seed=61, device=gpu)
+    ref, tgt, K, pose, depth = (t.to(gpu) for t in _rig_case(False, C=128, H=56, W=96, D=128, seed=62))
+    dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(gpu)
+
+    def render():
+        with torch.no_grad():
+            return dec(sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near, sc.far, sc.image_shape).color
+
+    def cost():
+        return plane_sweep_cost_volume(ref, tgt, K, pose, depth)
+
+    for _ in range(3):
+        solo_r = render()
+    solo_c = cost()
+    torch.cuda.synchronize()
+    solo_r, solo_c = solo_r.clone(), solo_c.clone()
+    start = threading.Barrier(2)
+    outs, errs = {"r": [], "c": []}, []
+
+    def worker(key, fn):
+        try:
+            s = torch.cuda.Stream(device=gpu)
+            start.wait()
+            with torch.cuda.stream(s):
+                for _ in range(6):
+                    outs[key].append(fn())
+            s.synchronize()
+        except Exception as e:  # surfaced below (a thread's exception would be lost)
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=("r", render)), threading.Thread(target=worker, args=("c", cost))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    assert len(outs["r"]) == 6 and len(outs["c"]) == 6
+    torch.cuda.synchronize()
+    for o in outs["r"]:
+        assert torch.equal(o, solo_r)
+    for o in outs["c"]:
+        assert torch.equal(o, solo_c)

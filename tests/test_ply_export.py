@@ -1,7 +1,8 @@
 """`.ply` export (drop-in for src/model/ply_export.py): header / attribute layout and the
 per-attribute transforms, checked against direct numpy / scipy restatements of
-ply_export.py:26-69 (the reference's `plyfile` writer is not installed: format pinned by
-the PLY spec and the reference's attribute list)."""
+ply_export.py:26-69, and the vertex arrays bit for bit against the reference's own
+(tests/golden/ply.npz: make_golden.py ran ply_export.py with a recording `plyfile` stub and
+real scipy). The byte layout of the file follows the PLY spec (plyfile itself is absent)."""
 import numpy as np
 import torch
 from scipy.spatial.transform import Rotation
@@ -62,3 +63,40 @@ def test_save_gaussian_ply_trims_borders(tmp_path):
     # identity cameras: positions pass through; first kept Gaussian = pixel (8, 8) of view 0
     first = gs.means[0].reshape(v, h, w, 3)[0, 8, 8].numpy()
     np.testing.assert_allclose(vals[0, 0:3], first, rtol=1e-6)
+
+
+def _golden():
+    from pathlib import Path
+    return np.load(Path(__file__).parent / "golden" / "ply.npz")
+
+
+def test_export_ply_matches_reference_fixture(tmp_path):
+    """tests/golden/ply.npz: the vertex array the REFERENCE's export_ply built
+    (src/model/ply_export.py:26-63, run by make_golden.py with a recording plyfile stub and
+    real scipy) for a non-identity c2w; reproduced bit for bit."""
+    G = _golden()
+    T = lambda k: torch.from_numpy(G[k])  # noqa: E731
+    path = tmp_path / "a.ply"
+    export_ply(T("export_ext"), T("export_means"), T("export_scales"), T("export_rot"), T("export_harm"),
+               T("export_opac"), path)
+    names, vals = read_vertex_ply(path)
+    assert names == construct_list_of_attributes(0)
+    np.testing.assert_array_equal(vals, G["export_vertex"])
+
+
+def test_save_gaussian_ply_matches_reference_fixture(tmp_path):
+    """save_gaussian_ply (ply_export.py:66-115) on a 2-view 20x20 context: the 8-pixel border
+    trim in the reference's "h w spp v" order (4 x 4 x 1 x 2 = 32 Gaussians), camera -> world
+    rotations, first-camera frame; equal to the reference-recorded vertex array bit for bit."""
+    import types
+    G = _golden()
+    T = lambda k: torch.from_numpy(G[k])  # noqa: E731
+    v, h, w = (int(x) for x in G["save_hw"])
+    gs = types.SimpleNamespace(means=T("save_means"), harmonics=T("save_harm"), opacities=T("save_opac"))
+    dump = {"rotations": T("save_rot"), "scales": T("save_scales")}
+    example = {"context": {"extrinsics": T("save_ext")[None], "image": torch.zeros(1, v, 3, h, w)}}
+    path = tmp_path / "b.ply"
+    save_gaussian_ply(gs, dump, example, path)
+    names, vals = read_vertex_ply(path)
+    assert vals.shape == G["save_vertex"].shape == (32, 17)
+    np.testing.assert_array_equal(vals, G["save_vertex"])
