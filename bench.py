@@ -63,6 +63,12 @@ def parse():
                         "recon12 (12-view 512x960 reconstruction, 100 views in chunks of 10), costvol (plane-sweep "
                         "cost volume, configs A / B shapes), train_d (config D data-parallel training step); '' = none")
     p.add_argument("--extra-steps", type=int, default=10)
+    p.add_argument("--recon-split", choices=["views", "scenes"], default="views",
+                   help="config-E leg over N ranks: 'views' splits the 100 target views of ONE scene over the ranks "
+                        "(Gaussians replicated, images all-gathered: per-scene latency, strong scaling); 'scenes': "
+                        "every rank reconstructs its own scene (weak scaling)")
+    p.add_argument("--skip-headline", action="store_true",
+                   help="run only the --extra legs (profiling passes of one leg's kernels)")
     p.add_argument("--selftest", action="store_true",
                    help="launcher self-test on the CPU: gloo ranks, a stub step instead of the renderer (no GPU)")
     return p.parse_args()
@@ -219,6 +225,15 @@ def main():
     from my_depthsplat_amd.synthetic import make_scene
 
     _lib.load()
+    if args.skip_headline:  # profiling passes of the secondary legs only
+        timed, max_over_ranks = make_timing(world, dev, backend)
+        extra = run_extras(args, dev, rank, world, timed, max_over_ranks)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "skip_headline": True, **dist_info(world, backend, ndev_used),
+                              **extra}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     H = W = args.size
     max_lanes = 1 if args.eager else int(os.environ.get("DSPLAT_BENCH_MAX_LANES", "4"))
     cal_batches = [int(x) for x in os.environ.get("DSPLAT_BENCH_BATCHES", "1,2,4,8,16").split(",")]
@@ -390,18 +405,7 @@ def main():
                 "valu_issue": pmc_valu(name, workload_tag, avg_ms)}
         if not args.no_cpu_baseline:
             psnr, cpu = cpu_leg(sc, out, args, H, W)
-    extra = {}
-    wanted = [e for e in args.extra.split(",") if e]
-    if "train" in wanted:
-        extra["train_config_c"] = train_leg(args, dev, rank, world, timed, max_over_ranks)
-    if "dl3dv" in wanted:
-        extra["render_config_d"] = dl3dv_leg(args, dev, rank, world, timed, max_over_ranks)
-    if "recon12" in wanted:
-        extra["recon_config_e"] = recon12_leg(args, dev, rank, world, timed, max_over_ranks)
-    if "costvol" in wanted:
-        extra["cost_volume"] = costvol_leg(args, dev, rank, world, max_over_ranks)
-    if "train_d" in wanted:
-        extra["train_config_d_dp"] = train_d_leg(args, dev, rank, world, timed, max_over_ranks)
+    extra = run_extras(args, dev, rank, world, timed, max_over_ranks)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -430,6 +434,22 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_extras(args, dev, rank, world, timed, max_over_ranks) -> dict:
+    extra = {}
+    wanted = [e for e in args.extra.split(",") if e]
+    if "train" in wanted:
+        extra["train_config_c"] = train_leg(args, dev, rank, world, timed, max_over_ranks)
+    if "dl3dv" in wanted:
+        extra["render_config_d"] = dl3dv_leg(args, dev, rank, world, timed, max_over_ranks)
+    if "recon12" in wanted:
+        extra["recon_config_e"] = recon12_leg(args, dev, rank, world, timed, max_over_ranks)
+    if "costvol" in wanted:
+        extra["cost_volume"] = costvol_leg(args, dev, rank, world, max_over_ranks)
+    if "train_d" in wanted:
+        extra["train_config_d_dp"] = train_d_leg(args, dev, rank, world, timed, max_over_ranks)
+    return extra
 
 
 def _pmc_file(workload):
@@ -477,6 +497,58 @@ def pmc_valu(kernel, workload, avg_ms):
             "source": f"profiles/pmc_traffic[_{workload}].json"}
 
 
+ADAPTER_FWD_BYTES_PER_PIXEL = 148 + 4 + 12 + 160   # head row + depth + image in; the Gaussian out
+ADAPTER_BWD_BYTES_PER_PIXEL = 148 + 4 + 160 + 148  # head row + depth + Gaussian grads in; dhead out
+
+
+def leg_kernel_bytes(name, st, *, G, V, S, HW, pixels=0, training=False):
+    """Algorithmic bytes of one launch of `name` in a secondary leg, from the
+    decoder context's last_stats() `st` (num_rendered; after a depth-cut forward the entries
+    written and the survivor records)."""
+    from my_depthsplat_amd import raster
+    if name == "k_adapter_fwd":
+        return ADAPTER_FWD_BYTES_PER_PIXEL * pixels
+    if name == "k_adapter_bwd":
+        return ADAPTER_BWD_BYTES_PER_PIXEL * pixels
+    N = st["num_rendered"]
+    if "written" in st:  # depth-cut forward (no backward): written heads, survivor records
+        return raster.algorithmic_bytes_cut(name, G=G, V=V, N_written=st["written"], HW=HW,
+                                            survivors=st.get("survivors", V * G), S=S)
+    b = raster.algorithmic_bytes(name, G=G, V=V, N=N, HW=HW, S=S)
+    if training and name == "k_project_emit":
+        b += 72 * V * G  # the backward's fixed-point rows zeroed in the same pass
+    if training and name == "k_sort_render":
+        b += 8 * N + 4 * V * HW  # sorted keys written back + n_contrib for the backward
+    return b
+
+
+def leg_roofline(step, n, bytes_of, workload):
+    """Roofline of a secondary leg's dominant kernel: HIP events around every named launch of
+    n eager steps (on the stream each is launched on), the kernel with the largest time per
+    step, its algorithmic bytes per launch (bytes_of(name)) over its average duration, the
+    committed PMC traffic / VALU issue of the same workload when profiles/ holds it."""
+    from my_depthsplat_amd import raster
+    probe = raster.KernelTimer()
+    raster.set_timer(probe)
+    try:
+        for _ in range(n):
+            step()
+    finally:
+        raster.set_timer(None)
+    summ = probe.summary()
+    per_step = {k: c / n * ms for k, (c, ms) in summ.items()}
+    name = max(per_step, key=per_step.get)
+    launches, avg_ms = summ[name]
+    alg = bytes_of(name)
+    ach = alg / (avg_ms * 1e-3) / 1e9
+    traffic, src = pmc_traffic(name, workload)
+    return {"bound": "hbm", "kernel": name, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": src,
+            "avg_ms": round(avg_ms, 5), "algorithmic_bytes_per_launch": int(alg), "launches_timed": launches,
+            "workload": workload, "valu_issue": pmc_valu(name, workload, avg_ms),
+            "per_step_ms_by_kernel": {k: round(v, 4) for k, v in sorted(per_step.items(), key=lambda kv: -kv[1])}}
+
+
 def train_leg(args, dev, rank, world, timed, max_over_ranks):
     """Config C (BASELINE.json configs[2]): 2-view 256x256, 16 scenes x 4 target views per
     step, Gaussians from the adapter (head outputs are the trainable leaf), rasterizer forward
@@ -518,10 +590,17 @@ def train_leg(args, dev, rank, world, timed, max_over_ranks):
         step()
     (el,) = max_over_ranks(timed(step, args.extra_steps))
     ms = 1e3 * el / args.extra_steps
+    roof = None
+    if rank == 0:
+        st = dec.raster_ctx.last_stats()
+        roof = leg_roofline(step, 3, lambda k: leg_kernel_bytes(k, st, G=V * H * W, V=B * v, S=B, HW=H * W,
+                                                                pixels=B * V * H * W, training=True),
+                            f"train_c_{V}v{H}x{W}b{B}x{v}")
+        roof["num_rendered_per_step"] = st["num_rendered"]
     return {"workload": "config C: 2-view 256x256, 16 scenes x 4 target views, adapter + raster fwd+bwd, "
                         "L1+MSE loss, SGD on head outputs (no encoder network: out of scope)",
             "ms_per_step": round(ms, 3), "views_per_s": round(B * v * world / (ms * 1e-3), 1), "steps": args.extra_steps,
-            "n_gpus": world}
+            "n_gpus": world, "roofline": roof}
 
 
 def dl3dv_leg(args, dev, rank, world, timed, max_over_ranks):
@@ -541,28 +620,47 @@ def dl3dv_leg(args, dev, rank, world, timed, max_over_ranks):
             return dec(sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near, sc.far, (H, W))
 
     for _ in range(2):
-        step()
+        out = step()
     (el,) = max_over_ranks(timed(step, args.extra_steps))
     ms = 1e3 * el / args.extra_steps
-    return {"workload": f"6-view {H}x{W} render, G={sc.gaussians.means.shape[1]}, {v} target views/scene, fp32",
-            "ms_per_step": round(ms, 3), "views_per_s": round(v * world / (ms * 1e-3), 1), "steps": args.extra_steps,
-            "n_gpus": world}
+    G = sc.gaussians.means.shape[1]
+    res = {"workload": f"6-view {H}x{W} render, G={G}, {v} target views/scene, fp32",
+           "ms_per_step": round(ms, 3), "views_per_s": round(v * world / (ms * 1e-3), 1), "steps": args.extra_steps,
+           "n_gpus": world}
+    if rank == 0:
+        out = step()
+        st = dec.raster_ctx.last_stats()
+        res["roofline"] = leg_roofline(step, 3, lambda k: leg_kernel_bytes(k, st, G=G, V=v, S=1, HW=H * W),
+                                       f"render_d_6v{H}x{W}x{v}")
+        res["roofline"].update(num_rendered_per_step=st["num_rendered"], written_per_step=st.get("written"),
+                               survivor_records_per_step=st.get("survivors"))
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_view_sample(sc, out, H, W, args.cpu_seconds)
+    return res
 
 
 def recon12_leg(args, dev, rank, world, timed, max_over_ranks):
     """BASELINE.json configs[4]: 12-view 512x960 feed-forward reconstruction (G = 5,898,240
     Gaussians from the fused adapter), then 100 target views rendered in chunks of 10
-    (render_chunk_size, README.md:198). One step = adapter + 10 decoder calls for one scene.
-    The reference's 0.6 s per scene on an A100 (README.md:105) also includes the encoder
-    network, which is out of scope here, so no ratio is reported. Per GPU; weak scaling."""
+    (render_chunk_size, README.md:198) and their PSNR against the target images (metrics.py:
+    12-19, as the reference test loop). One step = adapter + decoder calls + PSNR for one scene.
+    --recon-split views (default): the 100 views of ONE scene are split over the ranks, the
+    Gaussians replicated (each rank runs the adapter), the images all-gathered before the
+    PSNR (parallel.render_view_split): per-scene latency, strong scaling.
+    --recon-split scenes: each rank its own scene, weak scaling. The reference's 0.6 s per
+    scene on an A100 (README.md:105) also includes the encoder network, which is out of scope
+    here, so no ratio is reported."""
     import torch
 
     from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg, render_chunked
     from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg, gaussians_from_head
+    from my_depthsplat_amd.metrics import compute_psnr
+    from my_depthsplat_amd.parallel import render_view_split
     from my_depthsplat_amd.synthetic import context_cameras, target_cameras
 
     V, H, W, v, chunk = 12, 512, 960, 100, 10
-    g = torch.Generator(device=dev).manual_seed(99 + rank)
+    split_views = args.recon_split == "views"
+    g = torch.Generator(device=dev).manual_seed(99 + (0 if split_views else rank))
     adapter = GaussianAdapter(GaussianAdapterCfg(1e-10, 3.0, 2)).to(dev)
     head = torch.randn(1, V, H * W, 3 + adapter.d_in, generator=g, device=dev)
     depths = torch.rand(1, V, H * W, 1, 1, generator=g, device=dev) * 9 + 1
@@ -575,19 +673,41 @@ def recon12_leg(args, dev, rank, world, timed, max_over_ranks):
     far = torch.full((1, v), 100.0, device=dev)
     dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
 
+    gt = torch.rand(1, v, 3, H, W, generator=g, device=dev)
+    psnr = [None]
+
     def step():
         with torch.no_grad():
             gs = gaussians_from_head(head, depths, images, ctx, ctx_k, adapter)
-            return render_chunked(dec, gs, tgt, tgt_k, near, far, (H, W), chunk)  # model_wrapper.py:455-484
+            if split_views:
+                color = render_view_split(dec, gs, tgt, tgt_k, near, far, (H, W), chunk, rank, world)
+            else:
+                color = render_chunked(dec, gs, tgt, tgt_k, near, far, (H, W), chunk).color  # model_wrapper.py:455-484
+            psnr[0] = compute_psnr(gt[0], color[0])
+            return color
 
     step()
     steps = max(2, args.extra_steps // 2)
     (el,) = max_over_ranks(timed(step, steps))
     ms = 1e3 * el / steps
-    return {"workload": f"{V}-view {H}x{W} reconstruction, G={V * H * W}, adapter + {v} target views in chunks of "
-                        f"{chunk} (encoder network out of scope), fp32",
-            "ms_per_scene": round(ms, 2), "views_per_s": round(v * world / (ms * 1e-3), 1), "steps": steps,
-            "n_gpus": world, "reference": "0.6 s per scene end to end on an A100 incl. the encoder (README.md:105)"}
+    scenes = 1 if split_views else world
+    res = {"workload": f"{V}-view {H}x{W} reconstruction, G={V * H * W}, adapter + {v} target views in chunks of "
+                       f"{chunk} + PSNR (encoder network out of scope), fp32",
+           "split": ("views of one scene over the ranks (strong scaling), Gaussians replicated, images all-gathered"
+                     if split_views else "one scene per rank (weak scaling)"),
+           "ms_per_scene": round(ms / scenes, 2), "ms_per_step": round(ms, 2),
+           "views_per_s": round(v * scenes / (ms * 1e-3), 1), "steps": steps,
+           "n_gpus": world, "psnr_mean_db": round(float(psnr[0].mean()), 3),
+           "reference": "0.6 s per scene end to end on an A100 incl. the encoder (README.md:105)"}
+    if rank == 0 and world == 1:
+        # per-chunk kernels: the stats of the last chunk stand for every chunk (same scene)
+        st = dec.raster_ctx.last_stats()
+        res["roofline"] = leg_roofline(step, 1, lambda k: leg_kernel_bytes(k, st, G=V * H * W, V=chunk, S=1,
+                                                                           HW=H * W, pixels=V * H * W),
+                                       f"recon_e_{V}v{H}x{W}x{v}c{chunk}")
+        res["roofline"].update(num_rendered_per_chunk=st["num_rendered"], written_per_chunk=st.get("written"),
+                               survivor_records_per_chunk=st.get("survivors"))
+    return res
 
 
 def _costvol_case(tag, dev, rank):
@@ -808,6 +928,44 @@ def train_d_leg(args, dev, rank, world, timed, max_over_ranks):
             "backend": dist.get_backend() if dist.is_initialized() else None,
             "trainable_params": nparam, "allreduce_bucket_bytes": step.bucket_bytes,
             "allreduce_ms": round(1e3 * ar / 20, 4)}
+
+
+def cpu_view_sample(sc, out, H, W, seconds):
+    """The CPU oracle (oracle/dsr_oracle.cpp, OpenMP at the box's CPU share) on target views of
+    one scene of a secondary leg (north_star's 6-view 448x768 input): a bounded sample (at
+    least one view, about `seconds` of work), and the parity of the views rendered."""
+    import numpy as np
+
+    from my_depthsplat_amd.cuda_splatting import _cov6, camera_settings
+    from oracle import raster as orc
+    g = sc.gaussians
+    st = camera_settings(sc.target_extrinsics[0].cpu(), sc.target_intrinsics[0].cpu(), sc.near[0].cpu(),
+                         sc.far[0].cpu())
+    npst = {k: t.numpy() for k, t in st.items()}
+    means = g.means[0].cpu().numpy()
+    shs = g.harmonics[0].transpose(-1, -2).contiguous().cpu().numpy()
+    opac = g.opacities[0].cpu().numpy()
+    cov6 = _cov6(g.covariances[0]).contiguous().cpu().numpy()
+    deg = int(round(shs.shape[1] ** 0.5)) - 1
+    share, sysinfo = _cpu_share()
+    _set_omp_threads(share)
+    n_views = sc.target_extrinsics.shape[1]
+    n, t0, parity = 0, time.perf_counter(), []
+    while True:
+        i = n % n_views
+        o = orc.render_settings(means, shs, None, opac, cov6, npst, i, np.zeros(3, np.float32), H, W, deg)
+        ref, _, _ = o.image()
+        o.close()
+        n += 1
+        el = time.perf_counter() - t0
+        hip = out.color[0, i].float().cpu().numpy()
+        parity.append({"view": i, "l1": float(np.abs(hip - ref).mean()), "max_abs": float(np.abs(hip - ref).max())})
+        if el >= seconds or n >= 2 * n_views:
+            break
+    return {"value": round(n / el, 4), "unit": "views/s", "cores": share, "kind": "port",
+            "sample": f"{n} target view(s) of one {H}x{W} scene (G={means.shape[0]}) rendered by oracle/dsr_oracle.cpp "
+                      f"(OpenMP, {share} threads) in {el:.2f}s",
+            "parity_vs_gpu": parity, **sysinfo}
 
 
 def cpu_leg(sc, out, args, H, W):

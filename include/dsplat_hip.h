@@ -138,7 +138,13 @@ int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, in
  * first seg_capacity of them while seg_count goes on counting; dsr_sort_render (seg_stride =
  * seg_capacity) recognises such a segment (count > stride) and rebuilds its list from the
  * geometry records (the binning test is a function of one record), so images are identical
- * for every capacity — a capacity above the largest tile list only saves the rebuild. */
+ * for every capacity — a capacity above the largest tile list only saves the rebuild.
+ * extrinsics == NULL (camera-block mode): cams [V] is an INPUT holding the caller's camera
+ * blocks (dsr_build_cameras, or the reference wrapper's GaussianRasterizationSettings packed
+ * as dsr_camera); the other camera inputs are ignored and the same projection / binning
+ * kernel runs without its in-kernel camera set-up (exact binning unless
+ * DSR_LAYOUT_RECT_BINNING). With the wrapper's own matrices the tile lists equal the
+ * reference's bit for bit. */
 
 /* Exclusive scan of seg_count[V*T] -> seg_start[V*T+1], seg_cursor[V*T] (= seg_start),
  * totals[0] = N (num_rendered over all views), totals[1] = max entries in one tile,

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib
+from . import _lib, raster
 from .sh_rotation import _probe, wigner_d
 
 CAM_FLOATS = 104  # R[9] t[3] Kinv[9] D1[9] D2[25] D3[49] (include/dsplat_hip.h)
@@ -84,7 +84,7 @@ class _FusedAdapter(torch.autograd.Function):
         cov = torch.empty((B, G, 3, 3), dtype=torch.float32, device=dev)
         harm = torch.empty((B, G, 3, d_sh), dtype=torch.float32, device=dev)
         opac = torch.empty((B, G), dtype=torch.float32, device=dev)
-        _lib.check(lib.dga_adapter_fwd(B, V, H, W, d_sh, C, head.data_ptr(), depths.data_ptr(), images.data_ptr(),
+        _lib.check(raster._timed("k_adapter_fwd", lib.dga_adapter_fwd, B, V, H, W, d_sh, C, head.data_ptr(), depths.data_ptr(), images.data_ptr(),
                                        cams.data_ptr(), float(smin), float(smax), sh_mask.data_ptr(),
                                        means.data_ptr(), cov.data_ptr(), harm.data_ptr(), opac.data_ptr(),
                                        _lib.stream_of(dev)), "dga_adapter_fwd")
@@ -103,7 +103,7 @@ class _FusedAdapter(torch.autograd.Function):
         dhead = torch.empty_like(head)
         ddepth = torch.empty_like(depths) if ctx.needs_input_grad[1] else None
         p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-        _lib.check(lib.dga_adapter_bwd(B, V, H, W, d_sh, C, head.data_ptr(), depths.data_ptr(), cams.data_ptr(),
+        _lib.check(raster._timed("k_adapter_bwd", lib.dga_adapter_bwd, B, V, H, W, d_sh, C, head.data_ptr(), depths.data_ptr(), cams.data_ptr(),
                                        float(smin), float(smax), sh_mask.data_ptr(), p(dmeans), p(dcov), p(dharm),
                                        p(dopac), dhead.data_ptr(), p(ddepth), _lib.stream_of(head.device)),
                    "dga_adapter_bwd")

@@ -3715,8 +3715,16 @@ int dsr_project_bin_cameras(int S, int G, int V, int H, int W, int sh_degree, in
                             const float* bg, const int32_t* view_scene, int scale_invariant, dsr_camera* cams,
                             float* geom, int32_t* radii, int64_t* dgeom_zero, uint32_t* seg_count, uint64_t* keys,
                             uint32_t seg_capacity, int layout, void* stream) {
-  DSPLAT_REQUIRE(extrinsics && intrinsics && near && far && bg && view_scene,
-                 "dsr_project_bin_cameras: null camera input");
+  if (extrinsics == nullptr) {
+    // caller-supplied camera block: cams [V] is an input (e.g. the reference wrapper's own
+    // settings packed by the caller); the same kernel without its in-kernel camera set-up,
+    // binning exact unless DSR_LAYOUT_RECT_BINNING (as with the set-up)
+    const int lay = (layout & kLayoutRectBinning) ? (layout & ~kLayoutExactBinning) : (layout | kLayoutExactBinning);
+    return project_bin_impl("dsr_project_bin_cameras(camera block)", S, G, V, H, W, sh_degree, M, means, shs, colors,
+                            opacities, cov6, cams, nullptr, geom, radii, reinterpret_cast<long long*>(dgeom_zero),
+                            seg_count, keys, seg_capacity, lay, stream);
+  }
+  DSPLAT_REQUIRE(intrinsics && near && far && bg && view_scene, "dsr_project_bin_cameras: null camera input");
   const CamIn ci{extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant};
   return project_bin_impl("dsr_project_bin_cameras", S, G, V, H, W, sh_degree, M, means, shs, colors, opacities,
                           cov6, cams, &ci, geom, radii, reinterpret_cast<long long*>(dgeom_zero), seg_count, keys,

@@ -83,3 +83,39 @@ def reduce_max(value: float, device=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+@torch.no_grad()
+def gather_views(local: torch.Tensor, n_views: int, world: int) -> torch.Tensor:
+    """All-gather of per-rank view slices along dim 1 ([b, v_rank, ...] -> [b, n_views, ...] on
+    every rank; slices from shard(n_views, r, world), concatenated in rank order). Slices are
+    padded to the largest share (one all_gather of equal shapes); a gloo group moves CUDA
+    tensors through host memory (rehearsal of the RCCL path)."""
+    if world == 1:
+        return local
+    per = -(-n_views // world)
+    pad = local.new_zeros((local.shape[0], per, *local.shape[2:]))
+    pad[:, :local.shape[1]] = local
+    host = pad.is_cuda and dist.get_backend() == "gloo"
+    src = pad.cpu() if host else pad
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src)
+    out = torch.cat([p[:, :len(shard(n_views, r, world))] for r, p in enumerate(parts)], dim=1)
+    return out.to(local.device) if host else out
+
+
+@torch.no_grad()
+def render_view_split(decoder, gaussians, extrinsics, intrinsics, near, far, image_shape, chunk_size,
+                      rank: int, world: int, gather: bool = True) -> torch.Tensor:
+    """Strong scaling of ONE scene's render (pure rendering, configs B / E): the
+    v target views are split over the ranks (parallel.shard, contiguous), the Gaussians are
+    replicated read-only on every rank, each rank renders its share in chunks of chunk_size
+    (decoder.render_chunked, model_wrapper.py:455-484), then the images are all-gathered
+    (gather_views) -> color [b, v, 3, h, w] on every rank. No other exchange."""
+    from .decoder import render_chunked
+    v = extrinsics.shape[1]
+    mine = shard(v, rank, world)
+    sl = slice(mine.start, mine.stop)
+    local = render_chunked(decoder, gaussians, extrinsics[:, sl], intrinsics[:, sl], near[:, sl], far[:, sl],
+                           image_shape, chunk_size).color
+    return gather_views(local, v, world) if gather else local

@@ -122,6 +122,31 @@ def algorithmic_bytes(kernel: str, *, G: int, V: int, N: int, HW: int, T: int | 
         return 8 * N + 36 * V * G + 20 * V * HW
     if kernel == "k_sort_render":  # keys in (sorted copy stays in LDS: inference), records, RGB + T
         return 8 * N + 36 * V * G + 16 * V * HW  # (no n_contrib on the inference path)
+    if kernel == "k_render_bwd":   # keys, records, T + n_contrib + dL/dpixel in; 9 int64 sums per
+        return 8 * N + 36 * V * G + 20 * V * HW + 72 * V * G  # rendered (view, Gaussian) out
+    if kernel == "k_preprocess_bwd":  # params + per-view records and sums in; param grads out
+        return S * G * (148 + 148) + V * G * (48 + 72)
+    raise KeyError(kernel)
+
+
+def algorithmic_bytes_cut(kernel: str, *, G: int, V: int, N_written: int, HW: int, survivors: int,
+                          S: int = 1) -> int:
+    """Compulsory HBM bytes of one launch of the depth-cut kernels (deferred
+    geometry): the count pass reads 40 B of parameters per scene Gaussian (no SH: no colour)
+    and writes a radius + an 8-B rect record per (view, Gaussian); the scatter reads the rect
+    records and writes one key per written entry; the survivor projection reads the listed
+    Gaussians' 148 B and writes their 52-B record + radius; the fused sort + composite reads
+    the written keys, the survivors' 36-B compositing records, writes RGB + T."""
+    if kernel == "k_preprocess_cut":
+        return S * G * 40 + V * G * 12
+    if kernel == "k_scatter":
+        return V * G * 8 + 8 * N_written + 4 * survivors
+    if kernel == "k_project_survivors":
+        return survivors * (4 + 148 + 52)
+    if kernel == "k_sort_render":
+        return 8 * N_written + 36 * survivors + 16 * V * HW
+    if kernel == "k_bin_cutoff":
+        return V * 4 * 128 * 4
     raise KeyError(kernel)
 
 
@@ -339,7 +364,9 @@ class RasterContext:
             self._last["host_counts"] = (host, ev)
 
     def last_stats(self) -> dict:
-        """(num_rendered, max tile count) of this context's last forward (syncs)."""
+        """(num_rendered, max tile count) of this context's last forward (syncs); after a
+        depth-cut forward also the entries written (sorted + composited) and the (view,
+        Gaussian) records projected by the survivor passes."""
         c = self._last["counts"]
         if c is None:  # consumed on the device (inference fast path): the newest pinned copy
             hc = self._last.get("host_counts")
@@ -350,7 +377,14 @@ class RasterContext:
         n, m = int(c.sum()), int(c.max())
         if self.adapt_hints:
             self.hints["max_count"] = m
-        return {"num_rendered": n, "max_count": m}
+        out = {"num_rendered": n, "max_count": m}
+        cut = self._last.get("cut")
+        if cut is not None:
+            start, ends, surv_n = cut
+            out["written"] = int((ends.long() - start[:-1].long()).sum())
+            if surv_n is not None:
+                out["survivors"] = int(surv_n.long().sum())
+        return out
 
     # Counter buffers that are zero once the work of their last user is done:
     # dsr_sort_render(clear_counts=1) zeroes each counter as it consumes it, so the next
@@ -480,6 +514,19 @@ class CameraInputs:
         return self.extrinsics.shape[0]
 
 
+@dataclass
+class CameraBlock:
+    """A caller-built dsr_camera array [V, 44] float32 (pack_cameras of the reference wrapper's
+    GaussianRasterizationSettings, or build_cameras) for the inference fast path: the benched
+    kernels (dsr_project_bin_cameras in camera-block mode + dsr_sort_render) on exactly these
+    cameras instead of the ones they would set up in float from the render_cuda inputs."""
+    cams: torch.Tensor
+
+    @property
+    def V(self) -> int:
+        return self.cams.shape[0]
+
+
 def camera_inputs(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True) -> CameraInputs:
     dev = extrinsics.device
     _lib.require_gpu(extrinsics, intrinsics, near, far, bg)
@@ -537,6 +584,9 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     ctx: the caller's RasterContext (options + adaptive hints; default: the device's)."""
     lib = _lib.load()
     cam_in = cams if isinstance(cams, CameraInputs) else None
+    cam_blk = cams if isinstance(cams, CameraBlock) else None
+    if cam_blk is not None:
+        cams = cam_blk.cams
     _lib.require_gpu(means, feats, opacities, cov6, None if cam_in is not None else cams)
     S, G = means.shape[0], means.shape[1]
     M = (feats.shape[3] if layout & LAYOUT_SH_CHANNEL_MAJOR else feats.shape[2]) if use_sh else 0
@@ -559,8 +609,9 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     debug_lists = ctx.opt("debug_keep_fast_lists")
     cut_fused = False  # depth cut without a backward: heads sorted + composited by dsr_sort_render
     cap = G if debug_lists else ctx.seg_capacity(G)
-    fast = (ctx.opt("fused_sort_render") and maxc_hint <= FUSED_MAX and ctx.opt("inkernel_cameras")
-            and cam_in is not None and not need_state and zeroed_counts is None and T <= _HIST_LDS_MAX
+    fast = (ctx.opt("fused_sort_render") and maxc_hint <= FUSED_MAX
+            and ((ctx.opt("inkernel_cameras") and cam_in is not None) or cam_blk is not None)
+            and not need_state and zeroed_counts is None and T <= _HIST_LDS_MAX
             and V * T * cap < (1 << 32) and 16 * V * T * cap <= ctx.key_budget(dev))
     clean = ctx.take_clean_counts(V * T, dev, st) if fast else None
     fast = clean is not None
@@ -572,7 +623,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         layout |= LAYOUT_COUNTS_ZEROED
         if not ctx.opt("exact_binning"):
             layout |= LAYOUT_RECT_BINNING
-        cams = torch.empty((V, CAM_FLOATS), dtype=torch.float32, device=dev)
+        if cam_blk is None:  # written by the binning kernel's camera set-up
+            cams = torch.empty((V, CAM_FLOATS), dtype=torch.float32, device=dev)
     elif zeroed_counts is not None:  # zeroed by dsr_build_cameras (one launch fewer)
         assert zeroed_counts.numel() == V * T and zeroed_counts.dtype == torch.int32
         seg_count = zeroed_counts
@@ -590,10 +642,13 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         scratch = torch.empty(V * T * stride, dtype=torch.int64, device=dev)
         if fast:
             ci = cam_in
+            # camera-block mode: NULL render_cuda inputs, cams is the caller's (an input)
+            cin = (None,) * 6 + (0,) if ci is None else (
+                ci.extrinsics.data_ptr(), ci.intrinsics.data_ptr(), ci.near.data_ptr(), ci.far.data_ptr(),
+                ci.bg.data_ptr(), ci.view_scene.data_ptr(), int(ci.scale_invariant))
             _lib.check(_timed("k_project_emit", lib.dsr_project_bin_cameras,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-                ci.extrinsics.data_ptr(), ci.intrinsics.data_ptr(), ci.near.data_ptr(), ci.far.data_ptr(),
-                ci.bg.data_ptr(), ci.view_scene.data_ptr(), int(ci.scale_invariant), cams.data_ptr(),
+                *cin, cams.data_ptr(),
                 geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(), keys.data_ptr(), stride,
                 layout, st),
                 "dsr_project_bin_cameras")
@@ -725,6 +780,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         else:
             state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING)
         ctx._last["counts"] = None if fast else state.counts
+        ctx._last["cut"] = None
         return color, state
     overflow = None
     if seg_sorted is not None:
@@ -764,6 +820,9 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         state.cut_plan = (cut, cut_rec, lib.dsr_cut_superblock(H, W))
         state.geom_complete = surv is None
     ctx._last["counts"] = state.counts
+    # depth cut: per-segment ends and the survivor counters (small; bench.py's roofline of the
+    # cut kernels reads the entries written and the records projected from them)
+    ctx._last["cut"] = (seg_start, seg_count, surv_n) if stride == SEG_ENDS else None
     return color, state
 
 
@@ -830,7 +889,7 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
         dgeom_fx = torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev)
     gscale = torch.empty(GRAD_SCALE_BLOCKS, dtype=torch.float32, device=dev)
     _lib.check(lib.dsr_grad_scale(V, H, W, dcolor.data_ptr(), gscale.data_ptr(), st), "dsr_grad_scale")
-    _lib.check(lib.dsr_render_bwd(G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), _ptr(state.seg_start),
+    _lib.check(_timed("k_render_bwd", lib.dsr_render_bwd, G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), _ptr(state.seg_start),
                                   state.seg_count.data_ptr(), state.seg_stride, state.keys.data_ptr(),
                                   state.final_T.data_ptr(), state.n_contrib.data_ptr(), dcolor.data_ptr(),
                                   gscale.data_ptr(), dgeom_fx.data_ptr(), st), "dsr_render_bwd")
@@ -852,7 +911,7 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     dopac = torch.empty((S, G), dtype=torch.float32, device=dev)
     dcov6 = torch.empty_like(cov6, dtype=torch.float32)
     dmean2d = torch.empty((V, G, 3), dtype=torch.float32, device=dev) if want_mean2d else None
-    _lib.check(lib.dsr_preprocess_bwd(
+    _lib.check(_timed("k_preprocess_bwd", lib.dsr_preprocess_bwd,
         S, G, V, H, W, sh_degree if use_sh else -1, M, means.data_ptr(), feats.data_ptr() if use_sh else None,
         cov6.data_ptr(), cams.data_ptr(), state.geom.data_ptr(), dgeom_fx.data_ptr(), gscale.data_ptr(),
         idx.data_ptr(),
@@ -906,7 +965,7 @@ def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.T
     zeroed (build_cameras(zero_counts=...)). ctx: the caller's RasterContext (a decoder's own;
     default: the device's). Returns color [V,3,H,W] and radii [V,G] (int32)."""
     S = means.shape[0]
-    n_cams = cams.V if isinstance(cams, CameraInputs) else cams.shape[0]
+    n_cams = cams.V if isinstance(cams, (CameraInputs, CameraBlock)) else cams.shape[0]
     if len(view_scene) != n_cams:
         raise ValueError(f"view_scene has {len(view_scene)} entries for {n_cams} cameras")
     if any(not (0 <= s < S) for s in view_scene):
@@ -919,7 +978,8 @@ def rasterize_views(means: torch.Tensor, feats: torch.Tensor, opacities: torch.T
     f = lambda t: t.contiguous().float()  # noqa: E731
     layout = input_layout(feats, cov6, use_sh, channel_major_sh)
     return _RasterizeViews.apply(f(means), f(feats), f(opacities), f(cov6), means2d,
-                                 cams if isinstance(cams, CameraInputs) else cams.contiguous(),
+                                 cams if isinstance(cams, CameraInputs) else
+                                 CameraBlock(cams.cams.contiguous()) if isinstance(cams, CameraBlock) else cams.contiguous(),
                                  list(view_scene), use_sh, int(sh_degree), int(image_height), int(image_width),
                                  layout, zeroed_counts, ctx)
 

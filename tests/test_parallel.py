@@ -145,3 +145,53 @@ def test_training_step_gloo_world2_matches_full_batch():
     for a, b in zip(p0, p1):
         assert (a == b).all()
     assert abs((l0 + l1) / 2) > 0
+
+
+# ---------------------------------------------------------------- single-scene view split
+
+class _DenseDecoder:
+    """Decoder-signature stub over the dense torch renderer (returns DecoderOutput)."""
+
+    def __call__(self, gs, ext, K, near, far, image_shape, depth_mode=None):
+        from my_depthsplat_amd.decoder import DecoderOutput
+        return DecoderOutput(_dense_render(gs, ext, K, near, far, image_shape), None)
+
+
+def _split_scene():
+    from my_depthsplat_amd.synthetic import make_scene
+    return make_scene(batch=1, n_context=2, n_targets=7, height=12, width=20, seed=31, device="cpu")
+
+
+def _split_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from my_depthsplat_amd.parallel import render_view_split
+    sc = _split_scene()
+    color = render_view_split(_DenseDecoder(), sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near,
+                              sc.far, sc.image_shape, 2, rank, world)
+    q.put((rank, color.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_view_split_gloo_world2_matches_one_rank():
+    """One scene, 7 target views split 4 / 3 over 2 gloo ranks (Gaussians replicated), each rank
+    rendering its share in chunks of 2, then the all-gather: every rank ends with exactly the
+    images of the one-rank chunked render (render_chunked over all 7 views)."""
+    from my_depthsplat_amd.decoder import render_chunked
+    sc = _split_scene()
+    want = render_chunked(_DenseDecoder(), sc.gaussians, sc.target_extrinsics, sc.target_intrinsics, sc.near,
+                          sc.far, sc.image_shape, 2).color.numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, got in res:
+        assert got.shape == want.shape == (1, 7, 3, 12, 20)
+        assert (got == want).all()

@@ -27,7 +27,7 @@ import numpy as np
 import pytest
 import torch
 
-from raster_cases import flat_inputs, oracle_views, scene_inputs, settings_for
+from raster_cases import flat_inputs, oracle_views, packed_cams, scene_inputs, settings_for
 from test_fullsize_parity import _image_bars, _report, _segments
 
 pytestmark = pytest.mark.gpu
@@ -171,12 +171,13 @@ def test_config_d_training_backward_vs_oracle(gpu, monkeypatch):
     _check_grads("config_d_train", 0, got, acc)
 
 
-def test_product_entry_lists_vs_reference_settings(gpu, monkeypatch):
-    """Config B through the benched entry (cameras built in float inside the binning kernel)
-    with the reference's 3-sigma binning, against the oracle fed the reference wrapper's own
-    camera settings (torch: get_fov, get_projection_matrix, inverse; cuda_splatting.py:62-111).
-    Counts, over every (view, tile), the list entries that are not the same Gaussian at the
-    same position; DESIGN.md §3 states the bound asserted here. Images: north_star bars."""
+def _product_entry_list_diff(gpu, monkeypatch, camera_block):
+    """Config B through the benched entry with the reference's 3-sigma binning, against the
+    oracle fed the reference wrapper's own camera settings (torch: get_fov,
+    get_projection_matrix, inverse; cuda_splatting.py:62-111). camera_block=False: cameras
+    built in float inside the binning kernel; True: the same kernels in camera-block mode, fed
+    the wrapper's settings packed as dsr_camera. Counts, over every (view, tile), the list
+    entries that are not the same Gaussian at the same position. Images: north_star bars."""
     from my_depthsplat_amd import raster
     monkeypatch.setitem(raster.default_context(gpu).hints, "max_count", 2048)
     monkeypatch.setattr(raster.default_context(gpu), "adapt_hints", False)
@@ -184,8 +185,12 @@ def test_product_entry_lists_vs_reference_settings(gpu, monkeypatch):
     sc = scene_inputs(h=H, w=W, n_ctx=2, n_tgt=3, seed=1000)
     g = sc.gaussians
     gd = [t.to(gpu) for t in (g.means, g.covariances, g.harmonics, g.opacities)]
-    ci = raster.camera_inputs(sc.target_extrinsics[0].to(gpu), sc.target_intrinsics[0].to(gpu), sc.near[0].to(gpu),
-                              sc.far[0].to(gpu), torch.zeros(3, 3, device=gpu), [0] * 3, True)
+    st = settings_for(sc)
+    if camera_block:
+        ci = raster.CameraBlock(packed_cams(st, [0] * 3).to(gpu))
+    else:
+        ci = raster.camera_inputs(sc.target_extrinsics[0].to(gpu), sc.target_intrinsics[0].to(gpu),
+                                  sc.near[0].to(gpu), sc.far[0].to(gpu), torch.zeros(3, 3, device=gpu), [0] * 3, True)
     prev = (raster.EXACT_BINNING, raster.DEBUG_KEEP_FAST_LISTS)
     raster.EXACT_BINNING, raster.DEBUG_KEEP_FAST_LISTS = False, True
     try:
@@ -198,7 +203,6 @@ def test_product_entry_lists_vs_reference_settings(gpu, monkeypatch):
     T = (W // 16) * (H // 16)
     begin, end, keys = _segments(state, 3, T)
     col = color.cpu().numpy()
-    st = settings_for(sc)
     n_total = n_set = n_order = n_tiles_diff = 0
     for v, o in enumerate(oracle_views(sc, st)):
         okeys, ovals, ranges = o.binning()
@@ -217,15 +221,33 @@ def test_product_entry_lists_vs_reference_settings(gpu, monkeypatch):
             pos = {g_: k for k, g_ in enumerate(oids[np.isin(oids, common)])}
             n_order += len(a_) - _lis_len([pos[g_] for g_ in a_])  # entries out of the oracle's order
         oc, _, _ = o.image()
-        l1, mx, dp = _image_bars(col[v], oc, f"product entry view {v}")
-        _report(test="product_entry_vs_reference_settings", view=v, l1=l1, max_abs=mx, dpsnr=dp)
+        tag = "camera_block" if camera_block else "product_entry"
+        l1, mx, dp = _image_bars(col[v], oc, f"{tag} view {v}")
+        _report(test=f"{tag}_vs_reference_settings", view=v, l1=l1, max_abs=mx, dpsnr=dp)
+        if camera_block:  # same cameras, same projection chain: the same pixels as the oracle's lists
+            assert np.array_equal(state.radii[v].cpu().numpy(), o.geom()["radii"])
         o.close()
-    _report(test="product_entry_list_diff", entries=n_total, not_in_both=n_set, out_of_order=n_order,
-            tiles_differing=n_tiles_diff, tiles=3 * T)
-    # the in-kernel float cameras differ from the wrapper's torch matrices by a few
-    # ulps, which moves a Gaussian's 3-sigma rect across a tile edge or swaps two depths that
-    # differ by an ulp only rarely; the bound asserted is 1e-4 of the entries for each kind
+    _report(test=f"{'camera_block' if camera_block else 'product_entry'}_list_diff", entries=n_total,
+            not_in_both=n_set, out_of_order=n_order, tiles_differing=n_tiles_diff, tiles=3 * T)
+    return n_total, n_set, n_order, n_tiles_diff
+
+
+def test_product_entry_lists_vs_reference_settings(gpu, monkeypatch):
+    """In-kernel float cameras vs the wrapper's torch matrices. DESIGN.md §3: they differ by a
+    few ulps, which moves a Gaussian's 3-sigma rect across a tile edge or swaps two depths that
+    differ by an ulp only rarely; the bound asserted is 1e-4 of the entries for each kind."""
+    n_total, n_set, n_order, n_tiles_diff = _product_entry_list_diff(gpu, monkeypatch, camera_block=False)
     assert n_set <= 1e-4 * n_total and n_order <= 1e-4 * n_total, (n_set, n_order, n_total, n_tiles_diff)
+
+
+def test_camera_block_lists_bit_exact_vs_reference_settings(gpu, monkeypatch):
+    """north_star "tile/sort indices bit-exact" on the benched kernels: fed the reference
+    wrapper's own camera settings (camera-block mode of dsr_project_bin_cameras), every (view,
+    tile) list of config B (3 views, 2,324,029 entries with 3-sigma binning) equals the
+    oracle's list entry for entry: 0 entries in one list only, 0 out of order."""
+    n_total, n_set, n_order, n_tiles_diff = _product_entry_list_diff(gpu, monkeypatch, camera_block=True)
+    assert n_total > 2_000_000
+    assert n_set == 0 and n_order == 0 and n_tiles_diff == 0, (n_set, n_order, n_total, n_tiles_diff)
 
 
 def _lis_len(seq):
