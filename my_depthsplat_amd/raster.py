@@ -13,6 +13,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import warnings
 from dataclasses import dataclass
 
 import torch
@@ -139,7 +140,7 @@ def algorithmic_bytes_cut(kernel: str, *, G: int, V: int, N_written: int, HW: in
     the written keys, the survivors' 36-B compositing records, writes RGB + T."""
     if kernel == "k_preprocess_cut":
         return S * G * 40 + V * G * 12
-    if kernel == "k_scatter":
+    if kernel == "k_scatter_cut":
         return V * G * 8 + 8 * N_written + 4 * survivors
     if kernel == "k_project_survivors":
         return survivors * (4 + 148 + 52)
@@ -312,6 +313,7 @@ class RasterContext:
         self._auto_budget: dict = {}   # device index -> bytes
         self._clean_counts: dict = {}  # (device, n) -> (zeroed counters, last stream, event)
         self._graph_owned: list = []
+        self._warned_rebuild = False
 
     def opt(self, name: str):
         v = self.options.get(name)
@@ -344,24 +346,35 @@ class RasterContext:
             b = self._auto_budget[idx] = int(min(48 * (1 << 30), 0.4 * total, 0.5 * free))
         return b
 
-    def note_counts(self, counts: torch.Tensor) -> None:
+    def note_counts(self, counts: torch.Tensor, capacity: int | None = None) -> None:
         """Queue a non-blocking copy of the per-segment counts to pinned memory; completed
         copies from earlier calls update the LDS-sort size hint (their max). Never waits on
         the device, never adds a kernel (a device-side max would need same-address atomics
-        from every workgroup, which serialise)."""
+        from every workgroup, which serialise). capacity: the bounded segment capacity of that
+        call (inference fast path); tiles above it were rebuilt from the geometry records by
+        dsr_sort_render (exact, but one pass over the view's records per radix digit): counted
+        in last_stats()["rebuilt_tiles"], and warned about when the hints are frozen (the
+        capacity cannot grow to absorb them)."""
         if torch.cuda.is_current_stream_capturing():
             return  # inside a hipGraph capture: no host-side bookkeeping (hint stays fixed)
         while self._inflight and self._inflight[0][1].query():
-            host, _ = self._inflight.pop(0)
+            host, _, cap = self._inflight.pop(0)
+            m = int(host.max())
             if self.adapt_hints:
-                self.hints["max_count"] = int(host.max())
+                self.hints["max_count"] = m
+            elif cap is not None and m > cap and not self._warned_rebuild:
+                self._warned_rebuild = True
+                warnings.warn(f"{int((host > cap).sum())} tile list(s) of up to {m} entries exceeded the frozen "
+                              f"segment capacity {cap}: rebuilt from the geometry records (exact, slow); unfreeze "
+                              "the hints (adapt_hints) or set a larger seg_capacity", RuntimeWarning, stacklevel=3)
         if len(self._inflight) < 4:
             host = torch.empty(counts.shape, dtype=torch.int32, pin_memory=True)
             host.copy_(counts, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
-            self._inflight.append((host, ev))
+            self._inflight.append((host, ev, capacity))
             self._last["host_counts"] = (host, ev)
+            self._last["capacity"] = capacity
 
     def last_stats(self) -> dict:
         """(num_rendered, max tile count) of this context's last forward (syncs); after a
@@ -378,6 +391,9 @@ class RasterContext:
         if self.adapt_hints:
             self.hints["max_count"] = m
         out = {"num_rendered": n, "max_count": m}
+        cap = self._last.get("capacity")
+        if c is not None and cap is not None and self._last["counts"] is None:
+            out["rebuilt_tiles"] = int((c > cap).sum())  # bounded segments rebuilt by dsr_sort_render
         cut = self._last.get("cut")
         if cut is not None:
             start, ends, surv_n = cut
@@ -665,7 +681,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
             seg_sorted = _prefix_sort(lib, G, V, H, W, None, seg_count, stride, keys, scratch, maxc_hint, ws, st,
                                       lds_cap, ctx.opt("sort_prefix"))
-        ctx.note_counts(seg_count)
+        ctx.note_counts(seg_count, stride if fast and stride < G else None)
     else:
         # the depth cut pays when tile lists are long; the previous two-phase call's largest
         # list (None on the first call) decides whether this one builds the depth histogram
@@ -730,7 +746,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                 surv_n = torch.zeros(2 * ncnt.value, dtype=torch.int32, device=dev)
             proj = (S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                     cams.data_ptr())
-            _lib.check(_timed("k_scatter", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
+            _lib.check(_timed("k_scatter_cut", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
                               keys.data_ptr(), cut.data_ptr(), 0, None, _ptr(cut_rec), _ptr(surv), _ptr(surv_n), st),
                        "dsr_bin_scatter_cut")
             if defer:

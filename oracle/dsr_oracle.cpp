@@ -611,4 +611,29 @@ void orc_backward_f64(void* h, const float* dL_dpix, float* dmean2D, float* dcon
   backward_t<double>(*static_cast<State*>(h), dL_dpix, dmean2D, dconic, dopac, dcolor, dmean3D, dcov6, dsh);
 }
 
+// Gradient of the conic (inverse 2D covariance) w.r.t. cov2D = [[a, b], [b, c]] (b counted once:
+// dL/db is the derivative along the symmetric perturbation of both off-diagonal entries), in
+// double, from dconic as the render backward accumulates it (dL/dA, HALF the derivative w.r.t.
+// the conic's off-diagonal B, dL/dC). form 0: -S G S with S the exact inverse (the kernels' and
+// backward_t's form); form 1: the upstream computeCov2DCUDA formula through
+// denom2inv = 1 / (det^2 + 1e-7) [U]. out = (dL/da, dL/db, dL/dc). Test hook: pins that the
+// two forms agree (they differ by the 1e-7 regulariser only).
+void orc_conic_grad(double a, double b, double c, const double* dconic, int form, double* out) {
+  const double gA = dconic[0], gB = dconic[1], gC = dconic[2];
+  const double det = a * c - b * b;
+  if (form == 0) {
+    const double A = c / det, B = -b / det, C = a / det;
+    const double sg00 = A * gA + B * gB, sg01 = A * gB + B * gC, sg10 = B * gA + C * gB, sg11 = B * gB + C * gC;
+    out[0] = -(sg00 * A + sg01 * B);
+    out[1] = -2 * (sg00 * B + sg01 * C);
+    out[2] = -(sg10 * B + sg11 * C);
+    (void)sg10;
+    return;
+  }
+  const double denom2inv = 1.0 / (det * det + 0.0000001);
+  out[0] = denom2inv * (-c * c * gA + 2 * b * c * gB + (det - a * c) * gC);
+  out[2] = denom2inv * (-a * a * gC + 2 * a * b * gB + (det - a * c) * gA);
+  out[1] = denom2inv * 2 * (b * c * gA - (det + 2 * b * b) * gB + a * b * gC);
+}
+
 }  // extern "C"

@@ -33,6 +33,7 @@ def load():
         lib.orc_get_binning.argtypes = [c_void_p] * 4
         lib.orc_backward.argtypes = [c_void_p] * 9
         lib.orc_backward_f64.argtypes = [c_void_p] * 9
+        lib.orc_conic_grad.argtypes = [ctypes.c_double] * 3 + [c_void_p, c_int, c_void_p]
         _lib = lib
     return _lib
 
@@ -122,3 +123,12 @@ def render_settings(means, shs, colors, opacities, cov6, st: dict, i: int, bg, H
     c = np.asarray(cov6, np.float32) * np.float32(np.float32(s) * np.float32(s))
     return View(m, shs, colors, opacities, c, st["viewmatrix"][i], st["projmatrix"][i], st["campos"][i],
                 float(st["tanfovx"][i]), float(st["tanfovy"][i]), bg, H, W, sh_degree)
+
+
+def conic_grad(a: float, b: float, c: float, dconic, form: int) -> np.ndarray:
+    """dL/d(a, b, c) of cov2D from dL/dconic (render-backward convention), in double: form 0
+    the kernels' -S G S, form 1 upstream's denom2inv formula (orc_conic_grad)."""
+    d = np.ascontiguousarray(dconic, np.float64)
+    out = np.empty(3, np.float64)
+    load().orc_conic_grad(float(a), float(b), float(c), d.ctypes.data, int(form), out.ctypes.data)
+    return out

@@ -58,11 +58,18 @@ def test_bounded_capacity_images_equal_unbounded(gpu, case, capacity):
     stats = ctx.last_stats()
     if capacity <= 64:
         assert stats["max_count"] > capacity  # some tiles overflowed and were rebuilt
+    assert (stats["rebuilt_tiles"] > 0) == (stats["max_count"] > capacity), stats
     if case != "plain":
         assert stats["max_count"] > 2048, stats  # rebuilt lists span several LDS windows
     assert torch.equal(img, ref), float((img - ref).abs().max())
-    # a second call reuses the counters the rebuilt tiles zeroed
-    img2, _ = _render(sc, ctx, gpu, H, W)
+    # a second call reuses the counters the rebuilt tiles zeroed; with the hints frozen it
+    # warns (once) that the first call's tiles went through the slow rebuild
+    import warnings
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        img2, _ = _render(sc, ctx, gpu, H, W)
+    assert any("frozen segment capacity" in str(w.message) for w in rec) == (stats["rebuilt_tiles"] > 0), \
+        [str(w.message) for w in rec]
     assert torch.equal(img2, ref)
 
 

@@ -176,3 +176,39 @@ def test_forward_and_backward_vs_autograd(seed):
     chk(gr["dsh"], s.grad, "sh")
     chk(gr["dopacity"], o.grad, "opacity")
     chk(gr["dmean2D"][:, :2], off.grad, "means2D")
+
+
+@pytest.mark.parametrize("shape", ["regular", "needle", "tiny"])
+def test_conic_gradient_forms_agree(shape):
+    """The conic-inverse gradient of the kernels and of the oracle's backward (-S G S with the
+    stored conic) against upstream's computeCov2DCUDA formula through
+    denom2inv = 1 / (det^2 + 1e-7) [U], both in double (oracle orc_conic_grad), and both
+    against central differences of L = gA A + 2 gB B + gC C (the render backward's dconic
+    convention: gB is half the derivative w.r.t. the off-diagonal entry). regular: well
+    conditioned; needle: det(cov2D) ~ 4e-3 a c (the synthetic scenes' Gaussians); tiny: the
+    0.3 px dilation floor, where the 1e-7 regulariser matters most (~1e-5 relative)."""
+    from oracle.raster import conic_grad
+    rng = np.random.default_rng({"regular": 0, "needle": 1, "tiny": 2}[shape])
+    for _ in range(20):
+        if shape == "regular":
+            a, c = rng.uniform(0.5, 20, 2)
+            b = rng.uniform(-0.5, 0.5) * np.sqrt(a * c)
+        elif shape == "needle":
+            a, c = rng.uniform(50, 500, 2)
+            b = np.sqrt(a * c) * (1 - rng.uniform(1e-3, 5e-3)) * rng.choice([-1, 1])
+        else:
+            a, c = rng.uniform(0.0, 0.3, 2)
+            b = rng.uniform(-0.2, 0.2) * np.sqrt(a * c)
+        a, c = a + 0.3, c + 0.3
+        g = rng.normal(size=3)
+        f0, f1 = conic_grad(a, b, c, g, 0), conic_grad(a, b, c, g, 1)
+
+        def L(a_, b_, c_):
+            det = a_ * c_ - b_ * b_
+            return g[0] * c_ / det - 2 * g[1] * b_ / det + g[2] * a_ / det
+        h = 1e-6 * max(a, c)
+        fd = np.array([(L(a + h, b, c) - L(a - h, b, c)) / (2 * h), (L(a, b + h, c) - L(a, b - h, c)) / (2 * h),
+                       (L(a, b, c + h) - L(a, b, c - h)) / (2 * h)])
+        scale = np.abs(f0).max()
+        assert np.abs(f0 - f1).max() <= 2e-5 * scale, (shape, f0, f1)
+        assert np.abs(f0 - fd).max() <= 1e-5 * scale, (shape, f0, fd)

@@ -497,10 +497,49 @@ def test_depth_cut_large_rects(gpu, opacity, monkeypatch):
     lazy, lst, _ = hip_forward(sc, st, gpu, need_state=False)
     assert lst.seg_stride == raster.SEG_ENDS and not lst.geom_complete
     assert torch.equal(lazy.cpu(), full.cpu())
+    # the other no-backward variants of the cut: sort + render as two launches
+    # (dsr_bin_sort + dsr_render_fwd) instead of dsr_sort_render, and/or every record projected
+    # by the count pass instead of the survivor lists: the same images
+    for fused_, defer_ in ((False, True), (True, False), (False, False)):
+        monkeypatch.setattr(raster, "CUT_FUSED", fused_)
+        monkeypatch.setattr(raster, "DEFER_GEOM", defer_)
+        monkeypatch.setitem(raster.default_context(gpu).hints, "two_phase_max", None)
+        img, s2, _ = hip_forward(sc, st, gpu, need_state=False)
+        assert s2.seg_stride == raster.SEG_ENDS and s2.geom_complete == (not defer_)
+        assert torch.equal(img.cpu(), full.cpu()), (fused_, defer_)
     orcs = oracle_views(sc, st)
     _check_segments_vs_oracle(state, orcs, 2, 20 * 20)
     for o in orcs:
         o.close()
+
+
+@pytest.mark.parametrize("route", ["unfused_option", "hint_above_fused_max"])
+def test_fixed_capacity_unfused_state_forward(gpu, route):
+    """Regression (r3 68ffeda: an unbound variable crashed this path): the fixed-capacity
+    forward with a backward's state but WITHOUT the fused sort + composite — dsr_bin_sort +
+    dsr_render_fwd, taken when the context disables fusion or when the list-length hint is
+    above FUSED_MAX — gives the fused path's image, final T and n_contrib bit for bit."""
+    from my_depthsplat_amd import raster
+    sc = scene_inputs(h=96, w=128, n_ctx=2, n_tgt=2, seed=27)
+    st = settings_for(sc)
+    means, shs, opac, cov6 = (t.to(gpu) for t in flat_inputs(sc))
+    cams = packed_cams(st, [0, 0]).to(gpu)
+
+    def run(ctx):
+        color, state = raster.forward_raw(means, shs, True, 2, opac, cov6, cams, 2, 96, 128, ctx=ctx)
+        torch.cuda.synchronize()
+        return color.cpu(), state.final_T.cpu(), state.n_contrib.cpu(), state
+    ref = run(raster.RasterContext())
+    if route == "unfused_option":
+        ctx = raster.RasterContext(fused_sort_render=False)
+    else:
+        ctx = raster.RasterContext()
+        ctx.hints["max_count"] = raster.FUSED_MAX + 1
+        ctx.adapt_hints = False
+    got = run(ctx)
+    assert got[3].seg_stride > 0 and got[3].keys is not None  # the fixed-capacity layout
+    for a, b in zip(ref[:3], got[:3]):
+        assert torch.equal(a, b)
 
 
 def test_deferred_geometry_short_lists(gpu, monkeypatch):

@@ -16,14 +16,24 @@ def short(name):
     return m.group(1) if m else None
 
 
-def summarize(dirs):
+def summarize(dirs, idle_frac=0.1):
+    """Per kernel (short name) and counter, the average over its dispatches. Dispatches that
+    ran shorter than idle_frac x the longest dispatch of the same kernel in the same pass are
+    left out: launches that return at once (the depth cut's tail passes when no tile is
+    flagged) share the kernel's name but not its work, and bench.py times the working launch."""
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in dirs:
         f = next(Path(d).glob("*counter_collection.csv"))
-        for r in csv.DictReader(open(f)):
+        rows = [r for r in csv.DictReader(open(f)) if short(r["Kernel_Name"])]
+        longest = collections.defaultdict(float)
+        for r in rows:
+            dur = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+            longest[short(r["Kernel_Name"])] = max(longest[short(r["Kernel_Name"])], dur)
+        for r in rows:
             n = short(r["Kernel_Name"])
-            if n:
-                agg[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if float(r["End_Timestamp"]) - float(r["Start_Timestamp"]) < idle_frac * longest[n]:
+                continue
+            agg[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {n: {c: sum(v) / len(v) for c, v in dd.items()} for n, dd in agg.items()}
 
 
