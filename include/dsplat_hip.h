@@ -232,7 +232,13 @@ int dsr_project_survivors(int S, int G, int V, int H, int W, int sh_degree, int 
                           const float* means, const float* shs, const float* colors,
                           const float* opacities, const float* cov6, const dsr_camera* cams,
                           const uint32_t* survivors, const uint32_t* survivor_count, float* geom,
-                          int32_t* radii, int layout, void* stream);
+                          int32_t* radii, int64_t* dgeom_zero, uint8_t* row_live, int layout,
+                          void* stream);
+/* dgeom_zero / row_live (training with deferred geometry; both NULL for inference): the
+ * backward's accumulator rows of the projected (view, gaussian) pairs are zeroed here and
+ * row_live[v*G + g] (uint8, zeroed by the caller) set to 1 for them: the only rows
+ * dsr_render_bwd adds to and dsr_preprocess_bwd then reads (pass row_live to it). The
+ * count pass (dsr_preprocess_cut with DSR_LAYOUT_DEFER_GEOM) touches none of them. */
 
 /* Sort every segment by (depth, id) ascending — identical to upstream's stable radix
  * sort of (tile << 32 | depth) with emission-order ties (K4/K5). max_count sizes the LDS
@@ -331,14 +337,17 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
                    const float* dL_dpix, const float* grad_scale, int64_t* dgeom_fx, void* stream);
 
 /* dgeom_fx -> float dgeom [V,G,DSR_GEOM_STRIDE] (words 9..11 zero, rows of culled Gaussians
- * zero): the values the preprocess backward consumes, for callers that want them (tests,
- * diagnostics). */
+ * zero, and rows not marked in row_live when it is given): the values the preprocess backward
+ * consumes, for callers that want them (tests, diagnostics). */
 int dsr_dgeom_to_float(int G, int V, const float* geom, const int64_t* dgeom_fx, const float* grad_scale,
-                       float* dgeom, void* stream);
+                       const uint8_t* row_live, float* dgeom, void* stream);
 
 /* Preprocess backward (K8 + K9), reduced over all views of each scene without atomics.
  * dgeom_fx / grad_scale: as written by dsr_render_bwd / dsr_grad_scale.
  * scene_view_start [S+1], scene_views [V] list the views of each scene.
+ * row_live [V,G] uint8 or NULL: after a deferred-geometry forward (dsr_project_survivors with
+ * row_live), only the rows marked 1 are read (the others have no record and no zeroed
+ * accumulator); NULL: every row with radius > 0.
  * out (overwritten): dmeans [S,G,3], dshs [S,G,M,3] or NULL, dcolors [S,G,3] or NULL,
  * dopac [S,G], dcov6 [S,G,6]; dmean2D [V,G,3] optional (NULL to skip). `layout` as in
  * the forward; dshs / dcov6 are written in that layout (full covariance: upper triangle,
@@ -347,8 +356,8 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* cov6,
                        const dsr_camera* cams, const float* geom, const int64_t* dgeom_fx,
                        const float* grad_scale, const int32_t* scene_view_start, const int32_t* scene_views,
-                       float* dmeans, float* dshs, float* dcolors, float* dopac, float* dcov6,
-                       float* dmean2D, int layout, void* stream);
+                       const uint8_t* row_live, float* dmeans, float* dshs, float* dcolors, float* dopac,
+                       float* dcov6, float* dmean2D, int layout, void* stream);
 
 /* ---- plane-sweep cost volume -------------------------------------------------------
  * Fused warp_with_pose_depth_candidates (matching.py:24-90) + correlation

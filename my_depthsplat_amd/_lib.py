@@ -32,7 +32,8 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_bin_cutoff": (_I, [_I, _I, _I, _P, c_uint32, _P, _P]),
     "dsr_bin_scatter_cut": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P]),
     "dsr_survivor_layout": (_I, [_I, _I, _P, _P]),
-    "dsr_project_survivors": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "dsr_project_survivors": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I,
+                                   _P]),
     "dsr_bin_sort": (_I, [_I, _I, _I, _I, _P, _P, c_uint32, _P, _P, c_uint32, _P, c_uint32, _P, _P, _P]),
     "dsr_bin_sort_workspace_size": (ctypes.c_size_t, [_I, _I, _I, c_uint32]),
     "dsr_workspace_size": (_I, [_I, _I, _I, _I, ctypes.c_uint64, _P]),
@@ -44,9 +45,9 @@ SIGNATURES: dict[str, tuple] = {
                                      _P, _P, _P, _P, _P, c_uint32, _I, _P]),
     "dsr_grad_scale": (_I, [_I, _I, _I, _P, _P, _P]),
     "dsr_render_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P, _P, _P, _P]),
-    "dsr_dgeom_to_float": (_I, [_I, _I, _P, _P, _P, _P, _P]),
+    "dsr_dgeom_to_float": (_I, [_I, _I, _P, _P, _P, _P, _P, _P]),
     "dsr_preprocess_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                _P, _P, _P, _P, _P, _P, _I, _P]),
+                                _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "dcv_cost_volume_workspace_size": (ctypes.c_size_t, [_I, _I, _I, _I, _I]),
     "dcv_cost_volume_bwd_workspace_size": (ctypes.c_size_t, [_I, _I, _I, _I, _I]),
     "dcv_cost_volume_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P, _P]),

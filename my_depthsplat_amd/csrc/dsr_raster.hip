@@ -1271,7 +1271,8 @@ __global__ __launch_bounds__(NT) void k_project_survivors(int G, int V, int H, i
                                                           const uint32_t* __restrict__ surv,
                                                           const uint32_t* __restrict__ surv_count,
                                                           float* __restrict__ geom, int32_t* __restrict__ radii,
-                                                          int per_view, int layout) {
+                                                          long long* __restrict__ dzero,
+                                                          uint8_t* __restrict__ row_live, int per_view, int layout) {
   // workgroup (v, p) projects the slice the scatter's workgroup (v, p) listed
   const int v = blockIdx.x / per_view, p = blockIdx.x - v * per_view;
   const dsr_camera* cam = cams + v;
@@ -1286,7 +1287,9 @@ __global__ __launch_bounds__(NT) void k_project_survivors(int G, int V, int H, i
     float rec[GS];
     int x0, y0, x1, y1;
     const int r = project_gauss<DEG>(in, cam, focal, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
-    store_geom(geom, radii, (size_t)v * G + g, rec, r, nullptr);
+    const size_t vg = (size_t)v * G + g;
+    store_geom(geom, radii, vg, rec, r, dzero);  // (training: the backward's row zeroed here too)
+    if (row_live != nullptr && r > 0) row_live[vg] = 1u;  // the rows the backward reads
   }
 }
 
@@ -3308,6 +3311,7 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     const float* __restrict__ cov6, const dsr_camera* __restrict__ cams,
     const float* __restrict__ geom, const long long* __restrict__ dgeom, const float* __restrict__ gscale,
     const int32_t* __restrict__ scene_view_start, const int32_t* __restrict__ scene_views,
+    const uint8_t* __restrict__ row_live,
     float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
     float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D, int layout) {
   constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
@@ -3370,7 +3374,11 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
   for (int k = vb; k < ve; ++k) {
     const int v = scene_views[k];
     const size_t vg = (size_t)v * G + g;
-    const float4 rec2 = reinterpret_cast<const float4*>(geom + vg * GS)[2];  // depth, radius, clamp bits
+    // deferred geometry (depth cut): only the rows of the Gaussians some written list refers to
+    // have a record and a zeroed accumulator (row_live); the others are skipped unread
+    const bool live = row_live == nullptr || row_live[vg] != 0u;
+    const float4 rec2 = live ? reinterpret_cast<const float4*>(geom + vg * GS)[2]  // depth, radius, clamp bits
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
     const int radius = __float_as_int(rec2.z);
     if (radius <= 0) {
       if (dmean2D) {
@@ -3585,12 +3593,13 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
 // (rows of culled Gaussians: zero; their accumulator rows are never written or zeroed)
 __global__ __launch_bounds__(NT) void k_dgeom_to_float(size_t rows, const float* __restrict__ geom,
                                                        const long long* __restrict__ dq,
-                                                       const float* __restrict__ gscale, float* __restrict__ out) {
+                                                       const float* __restrict__ gscale,
+                                                       const uint8_t* __restrict__ row_live, float* __restrict__ out) {
   int k = 0;
   const float unit = grad_fx_exp(gscale, threadIdx.x & 63, k) ? ldexpf(1.f, k - DSR_GRAD_FRAC_BITS) : __builtin_nanf("");
   const size_t r = (size_t)blockIdx.x * NT + threadIdx.x;
   if (r >= rows) return;
-  const bool vis = __float_as_int(geom[r * GS + 10]) > 0;
+  const bool vis = (row_live == nullptr || row_live[r] != 0u) && __float_as_int(geom[r * GS + 10]) > 0;
 #pragma unroll
   for (int c = 0; c < GS; ++c) out[r * GS + c] = (c < 9 && vis) ? fx_to_float(dq[r * DSR_DGEOM_WORDS + c], unit) : 0.f;
 }
@@ -3859,7 +3868,8 @@ int dsr_survivor_layout(int G, int V, int64_t* slots, int* counters) {
 int dsr_project_survivors(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                           const float* shs, const float* colors, const float* opacities, const float* cov6,
                           const dsr_camera* cams, const uint32_t* survivors, const uint32_t* survivor_count,
-                          float* geom, int32_t* radii, int layout, void* stream) {
+                          float* geom, int32_t* radii, int64_t* dgeom_zero, uint8_t* row_live, int layout,
+                          void* stream) {
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_project_survivors: bad sizes S=%d G=%d V=%d H=%d W=%d", S, G, V, H, W);
   DSPLAT_REQUIRE((shs != nullptr) != (colors != nullptr), "dsr_project_survivors: exactly one of shs/colors must be given");
   DSPLAT_REQUIRE(shs == nullptr || (sh_degree >= 0 && sh_degree <= 3 && M >= (sh_degree + 1) * (sh_degree + 1)),
@@ -3874,7 +3884,9 @@ int dsr_project_survivors(int S, int G, int V, int H, int W, int sh_degree, int 
 #define DSR_PS(D)                                                                                            \
   k_project_survivors<D><<<(unsigned)(V * per_view), NT, 0, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, \
                                                                    opacities, cov6, cams, survivors,         \
-                                                                   survivor_count, geom, radii, per_view, layout)
+                                                                   survivor_count, geom, radii,              \
+                                                                   reinterpret_cast<long long*>(dgeom_zero), \
+                                                                   row_live, per_view, layout)
   switch (deg) {
     case -1: DSR_PS(-1); break;
     case 0: DSR_PS(0); break;
@@ -4123,20 +4135,20 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
   return dsplat::check_launch("k_render_bwd");
 }
 
-int dsr_dgeom_to_float(int G, int V, const float* geom, const int64_t* dgeom_fx, const float* grad_scale, float* dgeom,
-                       void* stream) {
+int dsr_dgeom_to_float(int G, int V, const float* geom, const int64_t* dgeom_fx, const float* grad_scale,
+                       const uint8_t* row_live, float* dgeom, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0, "dsr_dgeom_to_float: bad sizes");
   DSPLAT_REQUIRE(geom && dgeom_fx && grad_scale && dgeom, "dsr_dgeom_to_float: null pointer");
   const size_t rows = (size_t)G * V;
   k_dgeom_to_float<<<(unsigned)((rows + NT - 1) / NT), NT, 0, (hipStream_t)stream>>>(
-      rows, geom, reinterpret_cast<const long long*>(dgeom_fx), grad_scale, dgeom);
+      rows, geom, reinterpret_cast<const long long*>(dgeom_fx), grad_scale, row_live, dgeom);
   return dsplat::check_launch("k_dgeom_to_float");
 }
 
 int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, const float* means,
                        const float* shs, const float* cov6, const dsr_camera* cams, const float* geom,
                        const int64_t* dgeom_fx, const float* grad_scale, const int32_t* scene_view_start,
-                       const int32_t* scene_views,
+                       const int32_t* scene_views, const uint8_t* row_live,
                        float* dmeans, float* dshs, float* dcolors, float* dopac, float* dcov6, float* dmean2D,
                        int layout, void* stream) {
   DSPLAT_REQUIRE(S > 0 && G > 0 && V > 0 && H > 0 && W > 0, "dsr_preprocess_bwd: bad sizes");
@@ -4156,7 +4168,8 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
 #define DSR_PREB(D)                                                                                              \
   k_preprocess_bwd<D><<<grid, NT, lds, st>>>(G, H, W, M, means, shs, cov6, cams, geom, dgeom, grad_scale,          \
                                            scene_view_start,                                                     \
-                                           scene_views, dmeans, dshs, dcolors, dopac, dcov6, dmean2D, layout)
+                                           scene_views, row_live, dmeans, dshs, dcolors, dopac, dcov6, dmean2D,  \
+                                           layout)
   switch (deg) {
     case -1: DSR_PREB(-1); break;
     case 0: DSR_PREB(0); break;

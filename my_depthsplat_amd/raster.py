@@ -177,6 +177,9 @@ class RasterState:
     dgeom: torch.Tensor | None = None
     # depth-cut binning: (cut thresholds [V * super-blocks], compact records or None, super-block size)
     cut_plan: tuple | None = None
+    # deferred geometry with a backward: [V*G] uint8, 1 for the rows projected in full (whose
+    # records and accumulator rows exist); the preprocess backward reads only those
+    row_live: torch.Tensor | None = None
     # False when the depth cut deferred the geometry (no backward): only the records of the
     # Gaussians a scatter pass listed are written (every Gaussian some list entry refers to)
     geom_complete: bool = True
@@ -652,6 +655,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                              cam_in.view_scene, cam_in.scale_invariant,
                              zero_counts=None if layout & LAYOUT_COUNTS_ZEROED else seg_count)
         layout |= LAYOUT_COUNTS_ZEROED
+    surv = None      # depth cut, deferred geometry: the survivor lists of the scatter passes
+    row_live = None  # ... with a backward: the (view, Gaussian) rows projected in full (survivors)
     if fixed:
         keys = torch.empty(V * T * stride, dtype=torch.int64, device=dev)
         # scratch for segments above the LDS sort (their size is unknown before the sort)
@@ -696,10 +701,16 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             # 8 bytes per (view, Gaussian) for the scatter's pre-test instead of the 48-byte record
             cut_rec = torch.empty(V * G * 2, dtype=torch.int32, device=dev) \
                 if gx <= 255 and gy <= 255 else None
-            defer = bool(ctx.opt("defer_geom")) and not need_state and cut_rec is not None and dgeom_zero is None
+            # deferred geometry, with or without a backward: records (and, with a backward, the
+            # accumulator rows) only for the Gaussians the scatter passes list; row_live marks
+            # those rows for the preprocess backward (config D training: ~10 % of V x G)
+            defer = bool(ctx.opt("defer_geom")) and cut_rec is not None
+            if defer and need_state:
+                row_live = torch.zeros(V * G, dtype=torch.uint8, device=dev)
             _lib.check(_timed("k_preprocess_cut", lib.dsr_preprocess_cut,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(),
+                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), None if defer else _ptr(dgeom_zero),
+                seg_count.data_ptr(),
                 hist.data_ptr(), _ptr(cut_rec), layout | (LAYOUT_DEFER_GEOM if defer else 0), st),
                 "dsr_preprocess_cut")
         else:
@@ -729,7 +740,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             sb = 0
             if defer:  # the full scatter reads every record: project them all now
                 _project_all(lib, S, G, V, H, W, deg, M, means, shs_p, col_p, opacities, cov6, cams, geom, radii,
-                             layout, dev, st)
+                             layout, dev, st, dgeom_zero, row_live)
         if sb > 0:
             # depth cut: write only each tile's nearest entries (cursor ends at their end)
             scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev)  # only big segments touch it
@@ -751,8 +762,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                        "dsr_bin_scatter_cut")
             if defer:
                 _lib.check(_timed("k_project_survivors", lib.dsr_project_survivors, *proj, surv.data_ptr(),
-                                  surv_n.data_ptr(), geom.data_ptr(), radii.data_ptr(), layout, st),
-                           "dsr_project_survivors")
+                                  surv_n.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero),
+                                  _ptr(row_live), layout, st), "dsr_project_survivors")
             tile_count, seg_count, stride = seg_count, cursor, SEG_ENDS
             # no backward: the written heads are sorted and composited in one launch below
             # (dsr_sort_render, flags as dsr_render_fwd); the keys stay unsorted in HBM unless a
@@ -822,7 +833,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                                _ptr(tail_n), st), "dsr_bin_scatter_cut(tail)")
             if surv is not None:
                 _lib.check(lib.dsr_project_survivors(*proj, surv.data_ptr(), tail_n.data_ptr(), geom.data_ptr(),
-                                                     radii.data_ptr(), layout, st), "dsr_project_survivors(tail)")
+                                                     radii.data_ptr(), _ptr(dgeom_zero), _ptr(row_live), layout, st),
+                           "dsr_project_survivors(tail)")
         _lib.check(lib.dsr_bin_sort(G, V, H, W, _ptr(seg_start), seg_count.data_ptr(), stride, keys.data_ptr(),
                                     scratch.data_ptr(), 0, None, 0, _ptr(seg_sorted), overflow.data_ptr(), st),
                    "dsr_bin_sort(overflow)")
@@ -831,6 +843,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                                       *outs), "dsr_render_fwd(overflow)")
     state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, None if cut_fused else n_contrib,
                         seg_sorted, overflow, tile_count if stride == SEG_ENDS else None, cams=cams)
+    state.row_live = row_live
     state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING) and stride != SEG_ENDS
     if stride == SEG_ENDS:  # the depth-cut plan (tools/cut_case.py statistics)
         state.cut_plan = (cut, cut_rec, lib.dsr_cut_superblock(H, W))
@@ -842,7 +855,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     return color, state
 
 
-def _project_all(lib, S, G, V, H, W, deg, M, means, shs_p, col_p, opacities, cov6, cams, geom, radii, layout, dev, st):
+def _project_all(lib, S, G, V, H, W, deg, M, means, shs_p, col_p, opacities, cov6, cams, geom, radii, layout, dev, st,
+                 dgeom_zero=None, row_live=None):
     """Deferred geometry abandoned (the lists turned out short): every record, through the
     survivor projection with lists that hold every Gaussian (slice p of a view: the blocks p,
     p + per_view, ... that the scatter's workgroup p walks)."""
@@ -857,7 +871,8 @@ def _project_all(lib, S, G, V, H, W, deg, M, means, shs_p, col_p, opacities, cov
     n = n.repeat(V)
     _lib.check(lib.dsr_project_survivors(S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(),
                                          cov6.data_ptr(), cams.data_ptr(), ids.data_ptr(), n.data_ptr(),
-                                         geom.data_ptr(), radii.data_ptr(), layout, st), "dsr_project_survivors(all)")
+                                         geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), _ptr(row_live), layout,
+                                         st), "dsr_project_survivors(all)")
 
 
 def _prefix_sort(lib, G, V, H, W, seg_start, seg_count, stride, keys, scratch, max_count, ws, st, lds_cap,
@@ -913,7 +928,7 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     if want_dgeom:
         dgeom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
         _lib.check(lib.dsr_dgeom_to_float(G, V, state.geom.data_ptr(), dgeom_fx.data_ptr(), gscale.data_ptr(),
-                                          dgeom.data_ptr(), st), "dsr_dgeom_to_float")
+                                          _ptr(state.row_live), dgeom.data_ptr(), st), "dsr_dgeom_to_float")
     # views of each scene, in view order (fixed summation order -> deterministic reduce)
     order = sorted(range(V), key=lambda v: (view_scene[v], v))
     starts = [0] * (S + 1)
@@ -931,7 +946,7 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
         S, G, V, H, W, sh_degree if use_sh else -1, M, means.data_ptr(), feats.data_ptr() if use_sh else None,
         cov6.data_ptr(), cams.data_ptr(), state.geom.data_ptr(), dgeom_fx.data_ptr(), gscale.data_ptr(),
         idx.data_ptr(),
-        idx[S + 1:].data_ptr(), dmeans.data_ptr(), dfeat.data_ptr() if use_sh else None,
+        idx[S + 1:].data_ptr(), _ptr(state.row_live), dmeans.data_ptr(), dfeat.data_ptr() if use_sh else None,
         None if use_sh else dfeat.data_ptr(), dopac.data_ptr(), dcov6.data_ptr(),
         None if dmean2d is None else dmean2d.data_ptr(), layout, st), "dsr_preprocess_bwd")
     return dmeans, dfeat, dopac, dcov6, dmean2d, dgeom

@@ -702,7 +702,7 @@ def test_render_bwd_wide_grid_kernel(gpu):
                                       stream), "dsr_render_bwd")
         dgeom = torch.empty((n, G, raster.GEOM_STRIDE), device=gpu)
         _lib.check(lib.dsr_dgeom_to_float(G, n, st.geom.data_ptr(), dq.data_ptr(), gscale.data_ptr(),
-                                          dgeom.data_ptr(), stream), "dsr_dgeom_to_float")
+                                          None, dgeom.data_ptr(), stream), "dsr_dgeom_to_float")
         out[n] = (dq, dgeom)
     torch.cuda.synchronize()
     assert torch.equal(out[V][0][:3], out[3][0])  # the fixed-point sums, bit for bit
