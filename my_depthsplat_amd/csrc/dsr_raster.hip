@@ -1102,7 +1102,11 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
   __shared__ uint64_t s_k2[NW][64];
   const int T = gx * gy;
   if (tail && seg_overflow[(size_t)V * T] == 0u) return;  // no tile flagged (uniform)
-  const int v = blockIdx.x / per_view, p = blockIdx.x - v * per_view;
+  // one view's workgroups on one XCD (xcd_item): the 8-byte key stores to a tile's segment
+  // frontier then merge in that XCD's L2 before write-back (spread over the 8 XCDs, each
+  // frontier line came back as up to 8 partial writes: 3x the algorithmic bytes at config D)
+  int v, p;
+  if (!xcd_item(per_view, V, v, p)) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int sb = cut_superblock(gx, gy), sbl = __builtin_ctz((unsigned)sb);
   const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((gy + sb - 1) / sb);
@@ -1273,8 +1277,10 @@ __global__ __launch_bounds__(NT) void k_project_survivors(int G, int V, int H, i
                                                           float* __restrict__ geom, int32_t* __restrict__ radii,
                                                           long long* __restrict__ dzero,
                                                           uint8_t* __restrict__ row_live, int per_view, int layout) {
-  // workgroup (v, p) projects the slice the scatter's workgroup (v, p) listed
-  const int v = blockIdx.x / per_view, p = blockIdx.x - v * per_view;
+  // workgroup (v, p) projects the slice the scatter's workgroup (v, p) listed; a view's
+  // workgroups on one XCD (its 48-byte records are scattered over the view's rows)
+  int v, p;
+  if (!xcd_item(per_view, V, v, p)) return;
   const dsr_camera* cam = cams + v;
   const size_t slice = survivor_slice(G, V);
   const uint32_t n = min(surv_count[(size_t)v * per_view + p], (uint32_t)slice);
@@ -3850,7 +3856,7 @@ int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t*
   DSPLAT_REQUIRE(cut_superblock(gx, gy) > 0, "dsr_bin_scatter_cut: %dx%d tiles exceed the LDS histograms", gx, gy);
   constexpr int kNTH = kScatterCutNTH;
   const int per_view = scatter_cut_per_view(G, V);
-  k_scatter_cut<kNTH><<<(unsigned)(V * per_view), kNTH, 0, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor,
+  k_scatter_cut<kNTH><<<xcd_grid(per_view, V), kNTH, 0, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor,
                                                                                   keys, cut, tail, seg_overflow,
                                                                                   reinterpret_cast<const uint2*>(cut_rec),
                                                                                   per_view, survivors, survivor_count);
@@ -3882,7 +3888,7 @@ int dsr_project_survivors(int S, int G, int V, int H, int W, int sh_degree, int 
   const int deg = shs ? sh_degree : -1;
   hipStream_t st = (hipStream_t)stream;
 #define DSR_PS(D)                                                                                            \
-  k_project_survivors<D><<<(unsigned)(V * per_view), NT, 0, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, \
+  k_project_survivors<D><<<xcd_grid(per_view, V), NT, 0, st>>>(G, V, H, W, gx, gy, M, means, shs, colors, \
                                                                    opacities, cov6, cams, survivors,         \
                                                                    survivor_count, geom, radii,              \
                                                                    reinterpret_cast<long long*>(dgeom_zero), \

@@ -51,9 +51,13 @@ class GaussianHead(nn.Module):
         B, V, _, H, W = images.shape
         x = torch.cat([images, depths.reshape(B, V, 1, H, W)], 2).reshape(B * V, 4, H, W)
         x = F.avg_pool2d(x, self.down)
-        x = self.out(self.body(self.stem(x)))
-        x = F.pixel_shuffle(x, self.down)                       # [BV, d_out, H, W]
-        return x.reshape(B, V, self.d_out, H * W).transpose(2, 3).contiguous()
+        x = self.out(self.body(self.stem(x)))                   # [BV, d_out r^2, h, w], r = down
+        # pixel shuffle + "(b v) c h w -> b v (h w) c" as ONE permuted copy (a pixel_shuffle
+        # followed by the transpose moved the 1.2 GB head twice each way at config D):
+        # out[b, v, (hh r + i) W + ww r + j, c] = x[bv, c r^2 + i r + j, hh, ww]
+        r, h, w = self.down, H // self.down, W // self.down
+        x = x.view(B, V, self.d_out, r, r, h, w).permute(0, 1, 5, 3, 6, 4, 2)  # [B, V, h, i, w, j, c]
+        return x.reshape(B, V, H * W, self.d_out)
 
 
 @dataclass
