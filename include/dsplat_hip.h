@@ -87,6 +87,9 @@ int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, c
 #define DSR_LAYOUT_EXACT_BINNING 16    /* dsr_project_bin / dsr_preprocess_fwd / dsr_bin_scatter:
                                           exact alpha >= 1/255 tile test (as dsr_project_bin_cameras;
                                           the count and scatter calls of one forward must agree)    */
+#define DSR_LAYOUT_VIEWS_PER_SCENE(k) ((k) << 16)  /* dsr_project_bin_cameras: views grouped by
+                                          scene in order, k (< 256) per scene: whole scenes are placed
+                                          on one XCD (0 = no grouping: blocks x views)              */
 #define DSR_LAYOUT_DEFER_GEOM 32       /* dsr_preprocess_cut only: radii, counts, histogram and
                                           cut_rec, but no geometry record and no colour (see
                                           dsr_project_survivors); needs cut_rec, no dgeom_zero      */

@@ -121,6 +121,25 @@ __device__ __forceinline__ bool xcd_pair(int n_major, int n_minor, int& major, i
   return true;
 }
 
+// Scene-major variant for views grouped by scene (views_per_scene vps > 0: views s vps .. s vps
+// + vps - 1 render scene s): items ordered (scene, block, view of the scene), cut into the 8
+// per-XCD ranges. With S >= 8 scenes an XCD holds whole scenes: the views of a block still
+// share its inputs through one L2, and every tile segment of a scene's views receives its
+// keys from one XCD (frontier lines merge in one L2 instead of coming back as up to 8 partial
+// writes). vps = 0: xcd_pair(n_blocks, V).
+__device__ __forceinline__ bool xcd_scene_major(int n_blocks, int V, int vps, int& blk, int& v) {
+  if (vps <= 0) return xcd_pair(n_blocks, V, blk, v);
+  const int items = n_blocks * V;
+  const int per = (items + 7) >> 3;
+  const int item = (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
+  if ((int)(blockIdx.x >> 3) >= per || item >= items) return false;
+  const int per_scene = n_blocks * vps;
+  const int s = item / per_scene, r = item - s * per_scene;
+  blk = r / vps;
+  v = s * vps + (r - blk * vps);
+  return true;
+}
+
 struct WaveRects {
   uint32_t ex[64];    // exclusive scan of areas
   uint32_t org[64];   // x0 | y0 << 16
@@ -836,7 +855,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
   __shared__ uint32_t s_pairs[NT / 64][kPairCapW];
   __shared__ uint32_t s_ovf;
   int v, blk;
-  if (!xcd_pair((G + NT - 1) / NT, V, blk, v)) return;
+  // DSR_LAYOUT_VIEWS_PER_SCENE (scene-major XCD placement; same-box A/B at 16 scenes: -2 %)
+  if (!xcd_scene_major((G + NT - 1) / NT, V, (layout >> 16) & 0xFF, blk, v)) return;
   const dsr_camera* cam = cams + v;
   const int T = gx * gy;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;

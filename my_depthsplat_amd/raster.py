@@ -527,10 +527,24 @@ class CameraInputs:
     bg: torch.Tensor
     view_scene: torch.Tensor
     scale_invariant: bool
+    # views grouped by scene in order (view v renders scene v // views_per_scene), 0 otherwise:
+    # lets the binning kernel place whole scenes on one XCD
+    views_per_scene: int = 0
 
     @property
     def V(self) -> int:
         return self.extrinsics.shape[0]
+
+
+def views_per_scene(view_scene) -> int:
+    """k if view_scene == [0]*k + [1]*k + ... (the decoder's (b, v) flattening), else 0."""
+    vs = [int(x) for x in view_scene]
+    if not vs:
+        return 0
+    k = vs.count(0)
+    if k == 0 or len(vs) % k or any(s != i // k for i, s in enumerate(vs)):
+        return 0
+    return k if k < 256 else 0
 
 
 @dataclass
@@ -549,10 +563,12 @@ class CameraBlock:
 def camera_inputs(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True) -> CameraInputs:
     dev = extrinsics.device
     _lib.require_gpu(extrinsics, intrinsics, near, far, bg)
+    vps = 0 if isinstance(view_scene, torch.Tensor) else views_per_scene(view_scene)
     vs = view_scene.to(device=dev, dtype=torch.int32) if isinstance(view_scene, torch.Tensor) \
         else device_index(view_scene, dev)
     f = lambda t: t.detach().contiguous().float()  # noqa: E731
-    return CameraInputs(f(extrinsics), f(intrinsics), f(near), f(far), _dense_bg(bg), vs, bool(scale_invariant))
+    return CameraInputs(f(extrinsics), f(intrinsics), f(near), f(far), _dense_bg(bg), vs, bool(scale_invariant),
+                        vps)
 
 
 def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invariant=True,
@@ -667,11 +683,12 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             cin = (None,) * 6 + (0,) if ci is None else (
                 ci.extrinsics.data_ptr(), ci.intrinsics.data_ptr(), ci.near.data_ptr(), ci.far.data_ptr(),
                 ci.bg.data_ptr(), ci.view_scene.data_ptr(), int(ci.scale_invariant))
+            vps = ci.views_per_scene if ci is not None and S >= 8 else 0
             _lib.check(_timed("k_project_emit", lib.dsr_project_bin_cameras,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                 *cin, cams.data_ptr(),
                 geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero), seg_count.data_ptr(), keys.data_ptr(), stride,
-                layout, st),
+                layout | (vps << 16), st),
                 "dsr_project_bin_cameras")
         else:
             if ctx.opt("stateful_exact_binning"):
