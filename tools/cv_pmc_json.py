@@ -1,7 +1,7 @@
 """profiles/pmc_costvol.json from tools/prof_cv.sh output dirs (one per bench shape).
 
 usage: python tools/cv_pmc_json.py OUT SOURCE TAG=DIR [TAG=DIR ...]
-Per shape, the matrix-core kernel k_cost_epi: busy_frac = SQ_VALU_MFMA_BUSY_CYCLES /
+Per shape, the forward's matrix-core kernel (k_cost_band on small grids, else k_cost_epi): busy_frac = SQ_VALU_MFMA_BUSY_CYCLES /
 (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) (median over its dispatches), LDS bank conflicts per
 LDS instruction, and the HBM bytes of the channel-last copies (k_to_hwc)."""
 import csv
@@ -28,7 +28,8 @@ def main():
     for spec in specs:
         tag, d = spec.split("=", 1)
         sq, gr = rows(Path(d) / "pmc_sq"), rows(Path(d) / "pmc_grbm")
-        ks = sorted({k for _, k in sq if k.startswith("k_cost_epi")})
+        ks = sorted({k for _, k in sq if k.startswith("k_cost_band")}) or \
+            sorted({k for _, k in sq if k.startswith("k_cost_epi") and not k.startswith("k_cost_epi_bwd")})
         if not ks:
             continue
         k = ks[0]

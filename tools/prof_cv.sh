@@ -19,8 +19,8 @@ run pmc_grbm rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES --
 run fetch rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- python3 tools/cv_case.py $shape 5 "$@"
 run write rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- python3 tools/cv_case.py $shape 5 "$@"
 python3 tools/kstats.py $(find $out/stats -name '*kernel_stats.csv' | head -1) 8
-python3 tools/pmc_raw.py $out/pmc_sq k_cost_epi | head -4
-python3 tools/pmc_raw.py $out/pmc_grbm k_cost_epi | head -4
+python3 tools/pmc_raw.py $out/pmc_sq k_cost_ | head -4
+python3 tools/pmc_raw.py $out/pmc_grbm k_cost_ | head -4
 python3 tools/pmc_raw.py $out/fetch k_cost_epi | head -2
 python3 tools/pmc_raw.py $out/write k_cost_epi | head -2
 python3 tools/pmc_raw.py $out/fetch k_to_hwc | head -2
