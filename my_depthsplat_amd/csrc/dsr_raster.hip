@@ -2385,6 +2385,14 @@ __device__ __forceinline__ FallPoly fall_poly(float x, float y, float A, float B
 // ~2e-5 (terms of magnitude <= ~100), so "power <= 0" is tested as p2 <= kP2Max: every
 // positive-definite Gaussian still blends at its centre pixel (G = 2^p2 <= 1.00007 there).
 constexpr float kP2Max = 1e-4f;
+// Positive-definite scaled conic (p2 = A u^2 + B u v + C v^2 + ...: A < 0, 4 A C > B^2). For
+// such an entry the true p2 is <= 0 everywhere, so "power > 0" can only come from rounding
+// (of the polynomial form: needle Gaussians far from their centre) and the skip test is
+// alpha >= 1/255 alone. Only an indefinite conic (from a covariance that is not PSD: the +0.3
+// dilation makes every PSD input definite) keeps the p2 <= kP2Max test. Forward, backward
+// and the tail check evaluate this same expression on the same staged floats, so their
+// decisions agree.
+__device__ __forceinline__ bool conic_pd(float A, float B, float C) { return A < 0.f && 4.f * A * C > B * B; }
 __device__ __forceinline__ float fall_p2(const PixUV& p, float F, float D, float E, float A, float B, float C) {
   return fmaf(A, p.uu, fmaf(C, p.vv, fmaf(B, p.uv, fmaf(D, p.u, fmaf(E, p.v, F)))));
 }
@@ -2433,13 +2441,14 @@ __device__ __forceinline__ void pair_pad(WaveList* wl, int k) {  // opacity 0: a
 // as the stop flag (Tr < 0: stopped or outside the image, |Tr| the final T), so the chain
 // T -> test T -> stop -> T is vector compares and selects (VCC) only: no per-pixel lane mask
 // round-trips through SALU ops at every entry. Per entry, as the reference: skip
-// unless power <= 0 (p2 <= kP2Max) and alpha = min(.99, o G) >= 1/255; test T = T (1 - alpha); stop
+// unless power <= 0 (conic_pd, or p2 <= kP2Max) and alpha = min(.99, o G) >= 1/255 (PD: a
+// chunk whose entries all have definite conics tests alpha alone); test T = T (1 - alpha); stop
 // (without blending) when test T < 1e-4; else colour += rgb alpha T, T = test T, last =
 // position. A skipped entry gets alpha 0, which leaves T bit-identical (T * 1) and adds +0
 // colour; a stopped pixel fails the stop test at every later entry (T (1 - alpha) <= 0).
 // LAST: track the chunk index of the last blended entry (its list position, n_contrib, which
 // only a backward reads, is looked up once per chunk).
-template <bool LAST>
+template <bool LAST, bool PD>
 __device__ __forceinline__ void composite_pair(const PairRec& P, const PixUV2& pp, float& Tr, f2v& C01, float& C2,
                                                int& lastk, int k0) {
   const f2v p2 = fall_p2x2(pp, P);
@@ -2450,13 +2459,18 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, const PixUV2& p
   f2v alpha;
   alpha.x = fminf(0.99f, oG.x);
   alpha.y = fminf(0.99f, oG.y);
-  // ok <=> min(kP2Max - p2, alpha - 1/255) >= 0 (each difference has the exact sign of its
-  // comparison)
-  const f2v np2 = f2v{kP2Max, kP2Max} - p2;
-  const f2v over = alpha - f2v{1.0f / 255.0f, 1.0f / 255.0f};
   f2v a;
-  a.x = fminf(np2.x, over.x) >= 0.f ? alpha.x : 0.f;
-  a.y = fminf(np2.y, over.y) >= 0.f ? alpha.y : 0.f;
+  if (PD) {
+    a.x = alpha.x >= 1.0f / 255.0f ? alpha.x : 0.f;
+    a.y = alpha.y >= 1.0f / 255.0f ? alpha.y : 0.f;
+  } else {
+    // ok <=> min(kP2Max - p2, alpha - 1/255) >= 0 (each difference has the exact sign of its
+    // comparison); the power test only for an indefinite conic
+    const f2v np2 = f2v{kP2Max, kP2Max} - p2;
+    const f2v over = alpha - f2v{1.0f / 255.0f, 1.0f / 255.0f};
+    a.x = (conic_pd(P.A.x, P.B.x, P.C.x) ? over.x : fminf(np2.x, over.x)) >= 0.f ? alpha.x : 0.f;
+    a.y = (conic_pd(P.A.y, P.B.y, P.C.y) ? over.y : fminf(np2.y, over.y)) >= 0.f ? alpha.y : 0.f;
+  }
   const f2v om = f2v{1.f, 1.f} - a;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -2513,7 +2527,7 @@ __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* 
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const float alpha = fminf(0.99f, P.o[j] * __builtin_amdgcn_exp2f(p2[j]));
-        hit |= p2[j] <= kP2Max && alpha >= 1.0f / 255.0f;
+        hit |= (conic_pd(P.A[j], P.B[j], P.C[j]) || p2[j] <= kP2Max) && alpha >= 1.0f / 255.0f;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -2535,25 +2549,33 @@ __device__ __forceinline__ void composite_chunk(uint32_t base, uint32_t start, u
   const uint32_t e = base + lane;
   const bool mine = e < end && rect_hit(q, r, lx0, ly0, lx1, ly1);
   const uint64_t bal = __ballot(mine);
+  bool indef = false;  // an indefinite conic in the chunk: the loop with the power test
   if (mine) {
     const float4 sq = scaled_conic_q(q);  // (x, y, A, B)
-    pair_put(plist, __popcll(bal & lt), sq.x, sq.y, sq.z, -0.5f * kLog2e * r.x, sq.w, r.y, r.z, r.w, b,
-             e - start + 1u, fx0, fy0);
+    const float C = -0.5f * kLog2e * r.x;
+    indef = !conic_pd(sq.z, sq.w, C);
+    pair_put(plist, __popcll(bal & lt), sq.x, sq.y, sq.z, C, sq.w, r.y, r.z, r.w, b, e - start + 1u, fx0, fy0);
   }
   const int cnt = __popcll(bal);
   if (lane < 8) pair_pad(plist, cnt + lane);  // pad up to 8 entries (never blend)
   __builtin_amdgcn_wave_barrier();
   const PairRec* pl = plist->rec;
-  PairRec a0 = pl[0], a1 = pl[1];
   int lastk = -1;  // LAST: index of the chunk's last blended entry
-  for (int k = 0; k < cnt; k += 4) {
-    pl += 2;
-    const PairRec b0 = pl[0], b1 = pl[1];  // in bounds: pair k/2 + 3 <= (CH + 8) / 2 - 1
-    composite_pair<LAST>(a0, pp, Tr, C01, C2, lastk, k);
-    composite_pair<LAST>(a1, pp, Tr, C01, C2, lastk, k + 2);
-    if (!__any(Tr > 0.f)) break;
-    a0 = b0;
-    a1 = b1;
+  // four entries per step (the pads make pairs k/2, k/2 + 1 valid reads)
+  if (!__any(indef)) {
+    for (int k = 0; k < cnt; k += 4) {
+      const PairRec a0 = pl[k >> 1], a1 = pl[(k >> 1) + 1];
+      composite_pair<LAST, true>(a0, pp, Tr, C01, C2, lastk, k);
+      composite_pair<LAST, true>(a1, pp, Tr, C01, C2, lastk, k + 2);
+      if (!__any(Tr > 0.f)) break;
+    }
+  } else {
+    for (int k = 0; k < cnt; k += 4) {
+      const PairRec a0 = pl[k >> 1], a1 = pl[(k >> 1) + 1];
+      composite_pair<LAST, false>(a0, pp, Tr, C01, C2, lastk, k);
+      composite_pair<LAST, false>(a1, pp, Tr, C01, C2, lastk, k + 2);
+      if (!__any(Tr > 0.f)) break;
+    }
   }
   if (LAST && lastk >= 0) last = plist->pos[lastk];
   __builtin_amdgcn_wave_barrier();  // list reads of this chunk before the next chunk's writes
@@ -3107,7 +3129,7 @@ struct __align__(16) BwdRec {
   float4 r;   // B, opacity, red, green
   float4 s;   // blue, conic a, b, c
   float F, D, E;  // the forward's falloff polynomial of this wave's sub-tile (fall_poly)
-  uint32_t id, pos, pad[3];
+  uint32_t id, pos, pad[3];  // pad[0]: conic_pd of (A, B, C)
 };
 
 // K7: back-to-front gradient of the compositing (upstream renderCUDA backward semantics).
@@ -3207,6 +3229,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       d.E = f.E;
       d.id = id;
       d.pos = (uint32_t)p;
+      d.pad[0] = conic_pd(d.q.z, d.r.x, d.q.w) ? 1u : 0u;  // the forward's test on the same floats
     }
     const int cnt = __popcll(bal);
     __builtin_amdgcn_wave_barrier();
@@ -3226,7 +3249,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const float p2 = fall_p2(puv, cur.F, cur.D, cur.E, cur.q.z, cur.r.x, cur.q.w);
         const float Gs = __builtin_amdgcn_exp2f(p2);
         const float alpha = fminf(0.99f, cur.r.y * Gs);
-        const bool act = kk >= 0 && cur.pos < lastc && p2 <= kP2Max && alpha >= 1.0f / 255.0f;
+        const bool act = kk >= 0 && cur.pos < lastc && (cur.pad[0] != 0u || p2 <= kP2Max) && alpha >= 1.0f / 255.0f;
         any = any || act;
         if (act) {
           const float inv1ma = __builtin_amdgcn_rcpf(1.f - alpha);  // 1 ulp; the grads' tolerance is 2e-3
