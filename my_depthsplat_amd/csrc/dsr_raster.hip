@@ -2400,9 +2400,12 @@ __device__ __forceinline__ float fall_p2(const PixUV& p, float F, float D, float
 // as packed FP32 (v_pk_fma/mul) with no operand shuffling; per-element results are the same
 // IEEE operations as fall_p2 (the backward's decisions agree).
 struct __align__(16) PairRec {
-  f2v F, D, E, A, C, B, o;  // falloff fields of entries 0 and 1, interleaved (packed math)
+  f2v F, D, E, A, C, B;  // falloff fields of entries 0 and 1, interleaved (packed math); F holds
+                         // F + lo, lo = log2(opacity) (pair_put)
   f2v b;
-  f2v rg[2];                // (r, g) of entry j: one packed FMA into the pixel's (R, G)
+  f2v rg[2];             // (r, g) of entry j: one packed FMA into the pixel's (R, G)
+  f2v o;                 // lo (the power test of an indefinite conic only): last, so the common
+                         // loop reads the fields before it as whole 16-byte vectors
 };
 // A wave's staged chunk: up to CH kept entries + 8 pads as field-interleaved pairs (80 B: a
 // 20-word stride, so the 32 lanes' stores of one field hit 2-way at most), and beside them
@@ -2421,20 +2424,27 @@ __device__ __forceinline__ f2v fall_p2x2(const PixUV2& p, const PairRec& P) {
   const f2v t3 = __builtin_elementwise_fma(P.C, f2v{p.vv, p.vv}, t2);
   return __builtin_elementwise_fma(P.A, f2v{p.uu, p.uu}, t3);
 }
+// The opacity folded into the falloff: with lo = log2(o), exp2(p2 + lo) = o G, so a pixel's
+// o G is one v_exp of the polynomial whose constant term is F + lo (one multiply fewer per
+// (pixel, entry)); o = 0 gives lo = -inf, o G = 0. The backward stages F + lo with the same
+// two operations (fall_lo), so both evaluate the same alpha.
+__device__ __forceinline__ float fall_lo(float o) { return o > 0.f ? __builtin_amdgcn_logf(o) : -__builtin_inff(); }
 // stage one entry (centre x, y; scaled conic A, B, C) as element k of the wave's pair list
 __device__ __forceinline__ void pair_put(WaveList* wl, int k, float x, float y, float A, float C, float B, float o,
                                          float r, float g, float b, uint32_t pos, float fx0, float fy0) {
   PairRec& d = wl->rec[k >> 1];
   const int j = k & 1;
   const FallPoly f = fall_poly(x, y, A, B, C, fx0, fy0);
-  d.F[j] = f.F; d.D[j] = f.D; d.E[j] = f.E; d.A[j] = A; d.C[j] = C; d.B[j] = B; d.o[j] = o;
+  const float lo = fall_lo(o);
+  d.F[j] = f.F + lo; d.D[j] = f.D; d.E[j] = f.E; d.A[j] = A; d.C[j] = C; d.B[j] = B; d.o[j] = lo;
   d.rg[j] = f2v{r, g}; d.b[j] = b;
   wl->pos[k] = pos;
 }
 __device__ __forceinline__ void pair_pad(WaveList* wl, int k) {  // opacity 0: alpha 0, never blends
   PairRec& d = wl->rec[k >> 1];
   const int j = k & 1;
-  d.F[j] = 0.f; d.D[j] = 0.f; d.E[j] = 0.f; d.A[j] = 0.f; d.C[j] = 0.f; d.B[j] = 0.f; d.o[j] = 0.f;
+  constexpr float ninf = -__builtin_inff();
+  d.F[j] = ninf; d.D[j] = 0.f; d.E[j] = 0.f; d.A[j] = 0.f; d.C[j] = 0.f; d.B[j] = 0.f; d.o[j] = ninf;
   d.rg[j] = f2v{0.f, 0.f}; d.b[j] = 0.f;
 }
 // Front-to-back step over two entries. A pixel's state is its transmittance with the sign
@@ -2451,22 +2461,18 @@ __device__ __forceinline__ void pair_pad(WaveList* wl, int k) {  // opacity 0: a
 template <bool LAST, bool PD>
 __device__ __forceinline__ void composite_pair(const PairRec& P, const PixUV2& pp, float& Tr, f2v& C01, float& C2,
                                                int& lastk, int k0) {
-  const f2v p2 = fall_p2x2(pp, P);
-  f2v G;
-  G.x = __builtin_amdgcn_exp2f(p2.x);
-  G.y = __builtin_amdgcn_exp2f(p2.y);
-  const f2v oG = P.o * G;
+  const f2v p2o = fall_p2x2(pp, P);  // p2 + lo
   f2v alpha;
-  alpha.x = fminf(0.99f, oG.x);
-  alpha.y = fminf(0.99f, oG.y);
+  alpha.x = fminf(0.99f, __builtin_amdgcn_exp2f(p2o.x));
+  alpha.y = fminf(0.99f, __builtin_amdgcn_exp2f(p2o.y));
   f2v a;
   if (PD) {
     a.x = alpha.x >= 1.0f / 255.0f ? alpha.x : 0.f;
     a.y = alpha.y >= 1.0f / 255.0f ? alpha.y : 0.f;
   } else {
-    // ok <=> min(kP2Max - p2, alpha - 1/255) >= 0 (each difference has the exact sign of its
-    // comparison); the power test only for an indefinite conic
-    const f2v np2 = f2v{kP2Max, kP2Max} - p2;
+    // ok <=> min(thr - p2o, alpha - 1/255) >= 0 with thr = kP2Max + lo (each difference has
+    // the exact sign of its comparison); the power test only for an indefinite conic
+    const f2v np2 = (f2v{kP2Max, kP2Max} + P.o) - p2o;
     const f2v over = alpha - f2v{1.0f / 255.0f, 1.0f / 255.0f};
     a.x = (conic_pd(P.A.x, P.B.x, P.C.x) ? over.x : fminf(np2.x, over.x)) >= 0.f ? alpha.x : 0.f;
     a.y = (conic_pd(P.A.y, P.B.y, P.C.y) ? over.y : fminf(np2.y, over.y)) >= 0.f ? alpha.y : 0.f;
@@ -2523,11 +2529,11 @@ __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* 
     bool hit = false;
     for (int k = 0; k < cnt; k += 2) {
       const PairRec& P = plist->rec[k >> 1];
-      const f2v p2 = fall_p2x2(pp, P);
+      const f2v p2o = fall_p2x2(pp, P);  // p2 + lo (pair_put)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float alpha = fminf(0.99f, P.o[j] * __builtin_amdgcn_exp2f(p2[j]));
-        hit |= (conic_pd(P.A[j], P.B[j], P.C[j]) || p2[j] <= kP2Max) && alpha >= 1.0f / 255.0f;
+        const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2o[j]));
+        hit |= (conic_pd(P.A[j], P.B[j], P.C[j]) || p2o[j] <= kP2Max + P.o[j]) && alpha >= 1.0f / 255.0f;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -3129,7 +3135,7 @@ struct __align__(16) BwdRec {
   float4 r;   // B, opacity, red, green
   float4 s;   // blue, conic a, b, c
   float F, D, E;  // the forward's falloff polynomial of this wave's sub-tile (fall_poly)
-  uint32_t id, pos, pad[3];  // pad[0]: conic_pd of (A, B, C)
+  uint32_t id, pos, pad[3];  // pad[0]: power-test threshold (float); pad[1]: 1 / o (float)
 };
 
 // K7: back-to-front gradient of the compositing (upstream renderCUDA backward semantics).
@@ -3224,12 +3230,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       d.r = make_float4(sq.w, r.y, r.z, r.w);
       d.s = make_float4(bl, q.z, q.w, r.x);
       const FallPoly f = fall_poly(sq.x, sq.y, sq.z, sq.w, d.q.w, fx0, fy0);
-      d.F = f.F;
+      const float lo = fall_lo(r.y);
+      d.F = f.F + lo;  // as pair_put: the forward's o G = exp2(p2 + lo)
       d.D = f.D;
       d.E = f.E;
       d.id = id;
       d.pos = (uint32_t)p;
-      d.pad[0] = conic_pd(d.q.z, d.r.x, d.q.w) ? 1u : 0u;  // the forward's test on the same floats
+      // the forward's power test on the same floats: p2o <= thr (definite conic: always)
+      d.pad[0] = __float_as_uint(conic_pd(d.q.z, d.r.x, d.q.w) ? __builtin_inff() : kP2Max + lo);
+      d.pad[1] = __float_as_uint(r.y > 0.f ? __builtin_amdgcn_rcpf(r.y) : 0.f);  // 1 / o (dL/do)
     }
     const int cnt = __popcll(bal);
     __builtin_amdgcn_wave_barrier();
@@ -3245,11 +3254,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
         for (int c = 0; c < 9; ++c) g[j][c] = 0.f;
         const float dx = cur.q.x - pfx, dy = cur.q.y - pfy;
-        // same falloff sequence as k_render_fwd (decisions must agree with the forward)
-        const float p2 = fall_p2(puv, cur.F, cur.D, cur.E, cur.q.z, cur.r.x, cur.q.w);
-        const float Gs = __builtin_amdgcn_exp2f(p2);
-        const float alpha = fminf(0.99f, cur.r.y * Gs);
-        const bool act = kk >= 0 && cur.pos < lastc && (cur.pad[0] != 0u || p2 <= kP2Max) && alpha >= 1.0f / 255.0f;
+        // same falloff sequence as k_render_fwd (decisions must agree with the forward):
+        // p2o = p2 + lo, o G = exp2(p2o)
+        const float p2o = fall_p2(puv, cur.F, cur.D, cur.E, cur.q.z, cur.r.x, cur.q.w);
+        const float oG = __builtin_amdgcn_exp2f(p2o);
+        const float alpha = fminf(0.99f, oG);
+        const bool act = kk >= 0 && cur.pos < lastc && p2o <= __uint_as_float(cur.pad[0]) && alpha >= 1.0f / 255.0f;
         any = any || act;
         if (act) {
           const float inv1ma = __builtin_amdgcn_rcpf(1.f - alpha);  // 1 ulp; the grads' tolerance is 2e-3
@@ -3271,10 +3281,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           dL_dalpha *= Tr;
           last_alpha = alpha;
           dL_dalpha += (-Tfin * inv1ma) * bg_dot;
-          // per pixel only the factors that vary over the pixels: with h = G dL/dalpha the
-          // entry's sums are S(h dx), S(h dy), S(h dx^2), S(h dx dy), S(h dy^2), S(h); the
-          // conic, opacity and ndc factors multiply the sums once per entry (finish_grads)
-          const float h = Gs * dL_dalpha;
+          // per pixel only the factors that vary over the pixels: with h = o G dL/dalpha the entry's sums are S(h dx), S(h dy), S(h dx^2), S(h dx dy),
+          // S(h dy^2), S(h) = o S(G dL/dalpha); the conic and ndc factors (and 1 / o for
+          // dL/do) multiply the sums once per entry
+          const float h = oG * dL_dalpha;
           const float hx = h * dx, hy = h * dy;
           g[j][0] = hx;
           g[j][1] = hy;
@@ -3292,18 +3302,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           const int row = lane >> 4;
           const int kk = k - ((row & 1) * 2 + (row >> 1));
           if (kk >= 0) {
-            // dL/dmean2D = o S(h dG/dd) (ndc scale), dL/dconic = -o/2 S(h d d^T), dL/do = S(h)
-            // (upstream renderCUDA backward, its per-pixel products regrouped)
+            // dL/dmean2D = S(o G dL/dalpha dG/dd / G) (ndc scale), dL/dconic = -1/2 S(h d d^T),
+            // dL/do = S(h) / o (upstream renderCUDA backward, its per-pixel products regrouped)
             const float4 cs = list[kk].s;  // (blue, conic a, b, c)
-            const float o = list[kk].r.y;
             float* a9 = acc + kk * 9;
-            a9[0] = -o * (cs.y * R[0] + cs.z * R[1]) * ddelx_dx;
-            a9[1] = -o * (cs.w * R[1] + cs.z * R[0]) * ddely_dy;
-            a9[2] = -0.5f * o * R[2];
-            a9[3] = -0.5f * o * R[3];
-            a9[4] = -0.5f * o * R[4];
+            a9[0] = -(cs.y * R[0] + cs.z * R[1]) * ddelx_dx;
+            a9[1] = -(cs.w * R[1] + cs.z * R[0]) * ddely_dy;
+            a9[2] = -0.5f * R[2];
+            a9[3] = -0.5f * R[3];
+            a9[4] = -0.5f * R[4];
+            a9[5] = R[5] * __uint_as_float(list[kk].pad[1]);
 #pragma unroll
-            for (int c = 5; c < 9; ++c) a9[c] = R[c];
+            for (int c = 6; c < 9; ++c) a9[c] = R[c];
           }
         }
       } else if ((lane & 15) == 15) {
