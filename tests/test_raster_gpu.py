@@ -1047,3 +1047,41 @@ def test_stateful_exact_binning(gpu, layout, case, monkeypatch):
         if a is None:
             continue
         assert torch.equal(a, b_), (case, layout, name, float((a - b_).abs().max()))
+
+
+@pytest.mark.parametrize("opacity", [0.012, 0.5])
+def test_inference_long_lists_camera_block_vs_stateful(gpu, opacity, monkeypatch):
+    """Tiles of > 512 entries through the inference fast path (k_project_emit in camera-block
+    mode + the fused k_sort_render without n_contrib) against the stateful exact-binning
+    forward fed the same camera block (k_sort_render with n_contrib and sorted keys written
+    back): large faint Gaussians whose pixels never saturate (opacity 0.012: T stays ~0.3, every
+    walk runs to the end of its list) or saturate early (0.5). Bit-identical images, and the
+    oracle within the usual bar."""
+    from my_depthsplat_amd import raster
+    sc = scene_inputs(h=32, w=32, seed=41, n_ctx=2)
+    g = sc.gaussians
+    g.covariances = g.covariances * 100.0
+    g.opacities = torch.full_like(g.opacities, opacity)
+    st = settings_for(sc)
+    monkeypatch.setattr(raster, "STATEFUL_EXACT_BINNING", True)
+    color_ref, state, cams = hip_forward(sc, st, gpu)
+    B, v = sc.target_extrinsics.shape[:2]
+    h, w = sc.image_shape
+    gx, gy = raster.tiles(h, w)
+    b0, e0, _ = _segments(state, B * v, gx * gy)
+    lens = e0 - b0
+    assert 512 < lens.max() <= 2048  # G = 2 x 32 x 32: every list fits the smallest LDS class
+    ncon = state.n_contrib.cpu().numpy()
+    if opacity < 0.02:
+        assert ncon.max() > 512  # walks run past the first 512 entries
+    means, shs, opac, cov6 = flat_inputs(sc)
+    with torch.no_grad():
+        color, _ = raster.forward_raw(means.to(gpu), shs.to(gpu), True, 2, opac.to(gpu), cov6.to(gpu),
+                                      raster.CameraBlock(cams), B * v, h, w,
+                                      raster.input_layout(shs, cov6, True, False), need_state=False)
+    torch.cuda.synchronize()
+    assert torch.equal(color, color_ref)
+    for i, o in enumerate(oracle_views(sc, st)):
+        oc, _, _ = o.image()
+        assert float(np.abs(color[i].cpu().numpy() - oc).mean()) < 1e-4
+        o.close()
