@@ -468,6 +468,16 @@ int dga_adapter_backward(int BV, int H, int W, int S, int d_sh, int C, const flo
                          const float* dscales, const float* drotations, float* draw,
                          float* dcoordinates, float* ddepths, void* stream);
 
+/* Head glue: the conv head's output x [BV, C*r*r, h, w] (C channels per pixel at r x r
+ * sub-pixels, pixel-shuffled) to per-pixel rows [BV, (h*r)*(w*r), C] — the layout
+ * dga_adapter_fwd reads — in one LDS-tiled pass:
+ *   rows[bv][(hh*r + i)*(w*r) + ww*r + j][c] = x[bv][c*r*r + i*r + j][hh][ww]
+ * (torch: x.view(BV, C, r, r, h, w).permute(0, 4, 2, 5, 3, 1); with r = 1 the einops
+ * rearrange of the head output, encoder_depthsplat.py:224-233). dga_head_rows_bwd writes the
+ * inverse (dx from drows). Requires 16 * r * (C + 1) * 4 <= 64 KiB. */
+int dga_head_rows(int BV, int C, int r, int h, int w, const float* x, float* rows, void* stream);
+int dga_head_rows_bwd(int BV, int C, int r, int h, int w, const float* drows, float* dx, void* stream);
+
 /* ---- loss / metric (the step after the rasterizer) ------------------------------------
  * One pass over n_images images of n_per_image floats: loss[0] = w_l1 mean|p - t| +
  * w_mse mean (p - t)^2 (loss_mse.py:33-44), grad (optional) = dloss/dp, psnr (optional)

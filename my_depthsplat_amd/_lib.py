@@ -56,6 +56,8 @@ SIGNATURES: dict[str, tuple] = {
     "dcv_warp_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, _P, _P]),
     "dcv_warp_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, _P, _P]),
     "dga_adapter_cameras": (_I, [_I, _P, _P, _I, _P, _P, _P]),
+    "dga_head_rows": (_I, [_I, _I, _I, _I, _I, _P, _P, _P]),
+    "dga_head_rows_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P]),
     "dga_adapter_fwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, c_float, _P, _P, _P, _P, _P, _P]),
     "dga_adapter_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, c_float, c_float, _P, _P, _P, _P, _P, _P, _P,
                              _P]),

@@ -535,6 +535,52 @@ int launch_bwd(const AdIn& a, const float* dmeans, const float* dcovs, const flo
     case 9: return CALL(9);      \
     default: return CALL(16);    \
   }
+
+// ---- head rows: pixel shuffle + "(b v) c h w -> b v (h w) c" in one LDS-tiled pass ---------
+// rows[bv][(hh r + i) W + ww r + j][c] = x[bv][c r^2 + i r + j][hh][ww] (W = w r): the head's
+// conv output [BV, C r^2, h, w] to the per-pixel rows the adapter reads (encoder_depthsplat.py
+// rearranges its head output the same way), and the inverse for the backward. One workgroup
+// per (bv, output row hh r + i, kRowTile columns ww): the C r x kRowTile input block is read as
+// kRowTile-float runs, transposed through LDS, and written as one contiguous run of
+// kRowTile r C floats (a strided torch permute of the 1.2 GB config-D head moved ~1 TB/s).
+constexpr int kRowTile = 16;
+__global__ __launch_bounds__(256) void k_head_rows(int C, int r, int h, int w, float* __restrict__ x,
+                                                   float* __restrict__ rows, int inverse) {
+  extern __shared__ float s_tile[];  // [kRowTile r][C] (+1 pad per r C row group)
+  const int bv = blockIdx.z, hr = blockIdx.y, hh = hr / r, i = hr - hh * r;
+  const int ww0 = blockIdx.x * kRowTile, nw = min(kRowTile, w - ww0);
+  const int W = w * r, CR = C * r, stride = C + 1;  // odd row stride: the transposed accesses spread over banks
+  const size_t plane = (size_t)h * w;
+  float* xb = x + ((size_t)bv * C * r * r + (size_t)i * r) * plane + (size_t)hh * w + ww0;
+  const size_t rbase = ((size_t)bv * h * r * W + (size_t)hr * W + (size_t)ww0 * r) * C;
+  const int n_in = CR * kRowTile, n_out = nw * r * C;
+  if (!inverse) {
+    for (int e = threadIdx.x; e < n_in; e += 256) {
+      const int q = e / kRowTile, k = e - q * kRowTile;  // q = c r + j
+      if (k >= nw) continue;
+      const int c = q / r, j = q - c * r;
+      s_tile[(k * r + j) * stride + c] = xb[((size_t)c * r * r + j) * plane + k];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < n_out; e += 256) {
+      const int p = e / C, c = e - p * C;
+      rows[rbase + e] = s_tile[p * stride + c];
+    }
+  } else {
+    for (int e = threadIdx.x; e < n_out; e += 256) {
+      const int p = e / C, c = e - p * C;
+      s_tile[p * stride + c] = rows[rbase + e];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < n_in; e += 256) {
+      const int q = e / kRowTile, k = e - q * kRowTile;
+      if (k >= nw) continue;
+      const int c = q / r, j = q - c * r;
+      xb[((size_t)c * r * r + j) * plane + k] = s_tile[(k * r + j) * stride + c];
+    }
+  }
+}
+size_t head_rows_lds(int C, int r) { return sizeof(float) * (size_t)kRowTile * r * (C + 1); }
 }  // namespace
 
 extern "C" {
@@ -614,6 +660,26 @@ int dga_adapter_backward(int BV, int H, int W, int S, int d_sh, int C, const flo
   launch_bwd<NS, false>(a, dmeans, dcovariances, dharmonics, nullptr, dscales, drotations, draw, ddepths, dcoordinates, st)
   DGA_DISPATCH(d_sh, DGA_B)
 #undef DGA_B
+}
+
+int dga_head_rows(int BV, int C, int r, int h, int w, const float* x, float* rows, void* stream) {
+  DSPLAT_REQUIRE(BV > 0 && C > 0 && r > 0 && h > 0 && w > 0, "dga_head_rows: bad sizes");
+  DSPLAT_REQUIRE(x && rows, "dga_head_rows: null pointer");
+  const size_t lds = head_rows_lds(C, r);
+  DSPLAT_REQUIRE(lds <= 64 * 1024, "dga_head_rows: %d channels x %d exceed the LDS tile", C, r);
+  k_head_rows<<<dim3((w + kRowTile - 1) / kRowTile, h * r, BV), 256, lds, (hipStream_t)stream>>>(
+      C, r, h, w, const_cast<float*>(x), rows, 0);  // x is only read (inverse = 0)
+  return dsplat::check_launch("k_head_rows");
+}
+
+int dga_head_rows_bwd(int BV, int C, int r, int h, int w, const float* drows, float* dx, void* stream) {
+  DSPLAT_REQUIRE(BV > 0 && C > 0 && r > 0 && h > 0 && w > 0, "dga_head_rows_bwd: bad sizes");
+  DSPLAT_REQUIRE(drows && dx, "dga_head_rows_bwd: null pointer");
+  const size_t lds = head_rows_lds(C, r);
+  DSPLAT_REQUIRE(lds <= 64 * 1024, "dga_head_rows_bwd: %d channels x %d exceed the LDS tile", C, r);
+  k_head_rows<<<dim3((w + kRowTile - 1) / kRowTile, h * r, BV), 256, lds, (hipStream_t)stream>>>(
+      C, r, h, w, dx, const_cast<float*>(drows), 1);  // drows is only read (inverse = 1)
+  return dsplat::check_launch("k_head_rows(bwd)");
 }
 
 }  // extern "C"

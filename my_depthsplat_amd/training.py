@@ -31,6 +31,45 @@ from torch import nn
 from .parallel import allreduce_gradients, shard
 
 
+class _HeadRows(torch.autograd.Function):
+    """x [BV, C r^2, h, w] (contiguous fp32 on the GPU) -> rows [BV, (h r)(w r), C] through
+    dga_head_rows (one LDS-tiled pass each way; include/dsplat_hip.h)."""
+
+    @staticmethod
+    def forward(ctx, x, C: int, r: int):
+        from . import _lib
+        lib = _lib.load()
+        _lib.require_gpu(x)
+        x = x.contiguous()
+        BV, _, h, w = x.shape
+        rows = torch.empty((BV, h * r * w * r, C), dtype=torch.float32, device=x.device)
+        _lib.check(lib.dga_head_rows(BV, C, r, h, w, x.data_ptr(), rows.data_ptr(), _lib.stream_of(x.device)),
+                   "dga_head_rows")
+        ctx.dims = (BV, C, r, h, w)
+        return rows
+
+    @staticmethod
+    def backward(ctx, drows):
+        from . import _lib
+        BV, C, r, h, w = ctx.dims
+        drows = drows.contiguous()
+        dx = torch.empty((BV, C * r * r, h, w), dtype=torch.float32, device=drows.device)
+        _lib.check(_lib.load().dga_head_rows_bwd(BV, C, r, h, w, drows.data_ptr(), dx.data_ptr(),
+                                                 _lib.stream_of(drows.device)), "dga_head_rows_bwd")
+        return dx, None, None
+
+
+def head_rows(x: torch.Tensor, C: int, r: int) -> torch.Tensor:
+    """[BV, C r^2, h, w] -> [BV, (h r)(w r), C]: pixel shuffle + "(b v) c h w -> b v (h w) c"
+    (encoder_depthsplat.py:224-233 rearranges its head output this way; r = 1 is exactly that).
+    GPU tensors: one HIP pass (dga_head_rows); CPU tensors (the gloo tests): the same
+    permutation in torch."""
+    if x.is_cuda:
+        return _HeadRows.apply(x.float(), C, r)
+    BV, _, h, w = x.shape
+    return x.view(BV, C, r, r, h, w).permute(0, 4, 2, 5, 3, 1).reshape(BV, h * r * w * r, C)
+
+
 class GaussianHead(nn.Module):
     """Trainable stand-in for the Gaussian regressor + head: context image + depth ->
     per-pixel head channels [B, V, H*W, d_out] (d_out = 1 opacity + 2 offsets + adapter.d_in).
@@ -52,12 +91,9 @@ class GaussianHead(nn.Module):
         x = torch.cat([images, depths.reshape(B, V, 1, H, W)], 2).reshape(B * V, 4, H, W)
         x = F.avg_pool2d(x, self.down)
         x = self.out(self.body(self.stem(x)))                   # [BV, d_out r^2, h, w], r = down
-        # pixel shuffle + "(b v) c h w -> b v (h w) c" as ONE permuted copy (a pixel_shuffle
-        # followed by the transpose moved the 1.2 GB head twice each way at config D):
+        # pixel shuffle + "(b v) c h w -> b v (h w) c" in one pass (head_rows):
         # out[b, v, (hh r + i) W + ww r + j, c] = x[bv, c r^2 + i r + j, hh, ww]
-        r, h, w = self.down, H // self.down, W // self.down
-        x = x.view(B, V, self.d_out, r, r, h, w).permute(0, 1, 5, 3, 6, 4, 2)  # [B, V, h, i, w, j, c]
-        return x.reshape(B, V, H * W, self.d_out)
+        return head_rows(x, self.d_out, self.down).view(B, V, H * W, self.d_out)
 
 
 @dataclass

@@ -193,3 +193,23 @@ def test_reference_signature_camera_grads_and_broadcast(gpu):
     b = adapter.forward_torch(e1, k, coords, dep, opac, raw, (8, 12), input_images=images)
     torch.testing.assert_close(a.means, b.means, rtol=2e-5, atol=2e-5)
     torch.testing.assert_close(a.harmonics, b.harmonics, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("BV,C,r,h,w", [(3, 37, 8, 7, 12), (2, 5, 1, 9, 33), (1, 38, 4, 5, 20)])
+def test_head_rows_matches_torch_permute(gpu, BV, C, r, h, w):
+    """dga_head_rows (the head glue's pixel shuffle + "(b v) c h w -> b v (h w) c" in one
+    LDS-tiled pass, encoder_depthsplat.py:224-233 at r = 1) and its backward: bit-identical to
+    the torch permutation and to its autograd gradient, on tiles that do not divide w."""
+    from my_depthsplat_amd.training import head_rows
+    gen = torch.Generator().manual_seed(BV * 100 + C)
+    x = torch.randn(BV, C * r * r, h, w, generator=gen).to(gpu).requires_grad_(True)
+    rows = head_rows(x, C, r)
+    x_ref = x.detach().clone().requires_grad_(True)
+    ref = x_ref.view(BV, C, r, r, h, w).permute(0, 4, 2, 5, 3, 1).reshape(BV, h * r * w * r, C)
+    torch.cuda.synchronize()
+    assert rows.shape == ref.shape and torch.equal(rows, ref)
+    g = torch.randn(rows.shape, generator=gen).to(gpu)
+    rows.backward(g)
+    ref.backward(g)
+    torch.cuda.synchronize()
+    assert torch.equal(x.grad, x_ref.grad)
