@@ -118,6 +118,44 @@ __global__ __launch_bounds__(256) void k_to_hwc(int C, int HW, int rows, const f
   }
 }
 
+// The same transpose with 16-byte accesses (C % 4 == 0, HW % 4 == 0): each thread reads 4
+// consecutive pixels of one channel and writes 4 consecutive channels of one pixel (the
+// 4-byte version moved ~4.2 TB/s at config D's 24 x 2 x 128 x 5376 floats).
+__global__ __launch_bounds__(256) void k_to_hwc4(int C, int HW, int rows, const float* __restrict__ src,
+                                                 float* __restrict__ dst) {
+  __shared__ float tile[64][65];
+  const int bj = blockIdx.z;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const float* s = src + (size_t)bj * C * HW;
+  float* d = dst + (size_t)bj * rows * C;
+  if (blockIdx.x == 0 && (int)threadIdx.x < 64 && c0 + (int)threadIdx.x < C)
+    for (int p = HW; p < rows; ++p) d[(size_t)p * C + c0 + threadIdx.x] = 0.f;
+  const int q = threadIdx.x & 15, rr = threadIdx.x >> 4;  // 16 float4 per 64-float run, 16 runs per pass
+  float4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = c0 + rr + 16 * k, p = p0 + 4 * q;
+    v[k] = (c < C && p < HW) ? *reinterpret_cast<const float4*>(s + (size_t)c * HW + p) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float* t = &tile[rr + 16 * k][4 * q];
+    t[0] = v[k].x;
+    t[1] = v[k].y;
+    t[2] = v[k].z;
+    t[3] = v[k].w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = p0 + rr + 16 * k, c = c0 + 4 * q;
+    if (p < HW && c < C)
+      *reinterpret_cast<float4*>(d + (size_t)p * C + c) =
+          make_float4(tile[4 * q][rr + 16 * k], tile[4 * q + 1][rr + 16 * k], tile[4 * q + 2][rr + 16 * k],
+                      tile[4 * q + 3][rr + 16 * k]);
+  }
+}
+
 // [n][rows][C] (the first HW rows) -> [n][C][HW]
 __global__ __launch_bounds__(256) void k_to_chw(int C, int HW, int rows, const float* __restrict__ src,
                                                 float* __restrict__ dst) {
@@ -135,6 +173,40 @@ __global__ __launch_bounds__(256) void k_to_chw(int C, int HW, int rows, const f
   for (int r = ty; r < 64; r += 4) {
     const int c = c0 + r, p = p0 + tx;
     if (c < C && p < HW) d[(size_t)c * HW + p] = tile[tx][r];
+  }
+}
+
+// k_to_chw with 16-byte accesses (C % 4 == 0, HW % 4 == 0).
+__global__ __launch_bounds__(256) void k_to_chw4(int C, int HW, int rows, const float* __restrict__ src,
+                                                 float* __restrict__ dst) {
+  __shared__ float tile[64][65];
+  const int bj = blockIdx.z;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const float* s = src + (size_t)bj * rows * C;
+  float* d = dst + (size_t)bj * C * HW;
+  const int q = threadIdx.x & 15, rr = threadIdx.x >> 4;
+  float4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = p0 + rr + 16 * k, c = c0 + 4 * q;
+    v[k] = (p < HW && c < C) ? *reinterpret_cast<const float4*>(s + (size_t)p * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float* t = &tile[rr + 16 * k][4 * q];  // tile[p - p0][c - c0]
+    t[0] = v[k].x;
+    t[1] = v[k].y;
+    t[2] = v[k].z;
+    t[3] = v[k].w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = c0 + rr + 16 * k, p = p0 + 4 * q;
+    if (c < C && p < HW)
+      *reinterpret_cast<float4*>(d + (size_t)c * HW + p) =
+          make_float4(tile[4 * q][rr + 16 * k], tile[4 * q + 1][rr + 16 * k], tile[4 * q + 2][rr + 16 * k],
+                      tile[4 * q + 3][rr + 16 * k]);
   }
 }
 
@@ -1221,6 +1293,8 @@ static bool band_fwd(int B, int C, int H, int W) {
   return (long)B * H * W <= kBandMaxPixels;
 }
 
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
 // Channel-last copies (+ the epipolar groups when the epipolar kernels run): the forward's
 // set-up on the epipolar / generic paths, and the backward's when the forward took the band
 // kernel (which needs none of it).
@@ -1233,10 +1307,11 @@ static int epi_setup(int B, int J, int C, int H, int W, const float* ref, const 
   float* geom = reinterpret_cast<float*>(groups + (size_t)B * J * HW);
   // a band pixel's C channels are one contiguous row for the GEMM's operands; row HW of each
   // image is zero (the padding / out-of-image row)
-  k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc);
+  const bool v4 = C % 4 == 0 && HW % 4 == 0 && aligned16(tgt) && aligned16(ref) && aligned16(workspace);
+  (v4 ? k_to_hwc4 : k_to_hwc)<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc);
   if (int e = dsplat::check_launch("k_to_hwc")) return e;
   if (!epi_path(C, H, W, false)) return 0;
-  k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW + 1, ref, ref_hwc);
+  (v4 ? k_to_hwc4 : k_to_hwc)<<<dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW + 1, ref, ref_hwc);
   if (int e = dsplat::check_launch("k_to_hwc(ref)")) return e;
   k_epi_groups<<<dim3(B, J), 1024, 0, st>>>(J, H, W, intr, pose, groups, geom);
   return dsplat::check_launch("k_epi_groups");
@@ -1346,14 +1421,16 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
 #undef DCV_EPIB
       if (int e = dsplat::check_launch("k_cost_epi_bwd")) return e;
     }
-    k_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW, dref_hwc, dref);
+    (C % 4 == 0 && HW % 4 == 0 && aligned16(dref) && aligned16(bwd_workspace) ? k_to_chw4 : k_to_chw)<<<
+        dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW, dref_hwc, dref);
     if (int e = dsplat::check_launch("k_to_chw(dref)")) return e;
   } else {
     k_cost_bwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
                                                      depth, clamp_min_depth, dcost, dref, dtgt_hwc);
     if (int e = dsplat::check_launch("k_cost_bwd")) return e;
   }
-  k_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_hwc, dtgt);
+  (C % 4 == 0 && HW % 4 == 0 && aligned16(dtgt) && aligned16(bwd_workspace) ? k_to_chw4 : k_to_chw)<<<
+      dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_hwc, dtgt);
   return dsplat::check_launch("k_to_chw");
 }
 
