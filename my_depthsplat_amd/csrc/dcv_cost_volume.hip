@@ -121,10 +121,17 @@ __global__ __launch_bounds__(256) void k_to_hwc(int C, int HW, int rows, const f
 // The same transpose with 16-byte accesses (C % 4 == 0, HW % 4 == 0): each thread reads 4
 // consecutive pixels of one channel and writes 4 consecutive channels of one pixel (the
 // 4-byte version moved ~4.2 TB/s at config D's 24 x 2 x 128 x 5376 floats).
+// Two copies in one launch: planes z < nz1 from (src, dst), the rest from (src2, dst2).
 __global__ __launch_bounds__(256) void k_to_hwc4(int C, int HW, int rows, const float* __restrict__ src,
-                                                 float* __restrict__ dst) {
+                                                 float* __restrict__ dst, int nz1, const float* __restrict__ src2,
+                                                 float* __restrict__ dst2) {
   __shared__ float tile[64][65];
-  const int bj = blockIdx.z;
+  int bj = blockIdx.z;
+  if (bj >= nz1) {
+    bj -= nz1;
+    src = src2;
+    dst = dst2;
+  }
   const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
   const float* s = src + (size_t)bj * C * HW;
   float* d = dst + (size_t)bj * rows * C;
@@ -1308,11 +1315,20 @@ static int epi_setup(int B, int J, int C, int H, int W, const float* ref, const 
   // a band pixel's C channels are one contiguous row for the GEMM's operands; row HW of each
   // image is zero (the padding / out-of-image row)
   const bool v4 = C % 4 == 0 && HW % 4 == 0 && aligned16(tgt) && aligned16(ref) && aligned16(workspace);
-  (v4 ? k_to_hwc4 : k_to_hwc)<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc);
-  if (int e = dsplat::check_launch("k_to_hwc")) return e;
-  if (!epi_path(C, H, W, false)) return 0;
-  (v4 ? k_to_hwc4 : k_to_hwc)<<<dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW + 1, ref, ref_hwc);
-  if (int e = dsplat::check_launch("k_to_hwc(ref)")) return e;
+  const bool epi = epi_path(C, H, W, false);
+  if (v4) {  // tgt (and, for the epipolar kernels, ref) in one launch
+    k_to_hwc4<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J + (epi ? B : 0)), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc,
+                                                                                       B * J, ref, ref_hwc);
+    if (int e = dsplat::check_launch("k_to_hwc4")) return e;
+  } else {
+    k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc);
+    if (int e = dsplat::check_launch("k_to_hwc")) return e;
+    if (epi) {
+      k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW + 1, ref, ref_hwc);
+      if (int e = dsplat::check_launch("k_to_hwc(ref)")) return e;
+    }
+  }
+  if (!epi) return 0;
   k_epi_groups<<<dim3(B, J), 1024, 0, st>>>(J, H, W, intr, pose, groups, geom);
   return dsplat::check_launch("k_epi_groups");
 }
