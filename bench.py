@@ -235,7 +235,9 @@ def main():
             dist.destroy_process_group()
         return
     H = W = args.size
-    max_lanes = 1 if args.eager else int(os.environ.get("DSPLAT_BENCH_MAX_LANES", "4"))
+    # up to 8 captures in flight (16-scene batches, same box: 4 / 6 / 8 lanes 91.3 / 92.4 / 92.7 K
+    # views/s, tools/ab_lanes.sh; ~1.5 GB of keys and records per lane)
+    max_lanes = 1 if args.eager else int(os.environ.get("DSPLAT_BENCH_MAX_LANES", "8"))
     cal_batches = [int(x) for x in os.environ.get("DSPLAT_BENCH_BATCHES", "1,2,4,8,16").split(",")]
     batches = [args.batch] if args.batch else (cal_batches if args.launch == "auto" and not args.eager else [1])
     dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
@@ -256,7 +258,7 @@ def main():
     timed, max_over_ranks = make_timing(world, dev, backend)
 
     # launch mode: the whole decoder call of a B-scene batch replayed as ONE hipGraph per step,
-    # or launched eagerly; "hipgraphN" (N = 2..4): N captures, one per lane (own scenes, own
+    # or launched eagerly; "hipgraphN" (N = 2..8): N captures, one per lane (own scenes, own
     # buffers), replayed in turn on N HIP streams so consecutive batches overlap — one batch's
     # compositing tail shares the chip with the next one's binning. B scenes per launch pair
     # fill the chip's workgroup slots several times over, so tiles of different scenes balance
