@@ -474,7 +474,8 @@ int dga_adapter_backward(int BV, int H, int W, int S, int d_sh, int C, const flo
  *   rows[bv][(hh*r + i)*(w*r) + ww*r + j][c] = x[bv][c*r*r + i*r + j][hh][ww]
  * (torch: x.view(BV, C, r, r, h, w).permute(0, 4, 2, 5, 3, 1); with r = 1 the einops
  * rearrange of the head output, encoder_depthsplat.py:224-233). dga_head_rows_bwd writes the
- * inverse (dx from drows). Requires 16 * r * (C + 1) * 4 <= 64 KiB. */
+ * inverse (dx from drows). Requires 16 * r * (C + 1) * 4 <= 64 KiB (32-column tiles when
+ * 32 * r * (C + 1) * 4 fits). */
 int dga_head_rows(int BV, int C, int r, int h, int w, const float* x, float* rows, void* stream);
 int dga_head_rows_bwd(int BV, int C, int r, int h, int w, const float* drows, float* dx, void* stream);
 

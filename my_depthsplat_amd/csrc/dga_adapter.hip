@@ -543,7 +543,7 @@ int launch_bwd(const AdIn& a, const float* dmeans, const float* dcovs, const flo
 // per (bv, output row hh r + i, kRowTile columns ww): the C r x kRowTile input block is read as
 // kRowTile-float runs, transposed through LDS, and written as one contiguous run of
 // kRowTile r C floats (a strided torch permute of the 1.2 GB config-D head moved ~1 TB/s).
-constexpr int kRowTile = 16;
+template <int kRowTile>  // columns ww per workgroup: 32 = whole 128-byte lines when the tile fits
 __global__ __launch_bounds__(256) void k_head_rows(int C, int r, int h, int w, float* __restrict__ x,
                                                    float* __restrict__ rows, int inverse) {
   extern __shared__ float s_tile[];  // [kRowTile r][C] (+1 pad per r C row group)
@@ -580,7 +580,17 @@ __global__ __launch_bounds__(256) void k_head_rows(int C, int r, int h, int w, f
     }
   }
 }
-size_t head_rows_lds(int C, int r) { return sizeof(float) * (size_t)kRowTile * r * (C + 1); }
+size_t head_rows_lds(int tile, int C, int r) { return sizeof(float) * (size_t)tile * r * (C + 1); }
+int head_rows_launch(int BV, int C, int r, int h, int w, float* x, float* rows, int inverse, hipStream_t st) {
+  const int tile = head_rows_lds(32, C, r) <= 64 * 1024 ? 32 : 16;
+  const size_t lds = head_rows_lds(tile, C, r);
+  DSPLAT_REQUIRE(lds <= 64 * 1024, "dga_head_rows: %d channels x %d exceed the LDS tile", C, r);
+  if (tile == 32)
+    k_head_rows<32><<<dim3((w + 31) / 32, h * r, BV), 256, lds, st>>>(C, r, h, w, x, rows, inverse);
+  else
+    k_head_rows<16><<<dim3((w + 15) / 16, h * r, BV), 256, lds, st>>>(C, r, h, w, x, rows, inverse);
+  return dsplat::check_launch("k_head_rows");
+}
 }  // namespace
 
 extern "C" {
@@ -665,21 +675,13 @@ int dga_adapter_backward(int BV, int H, int W, int S, int d_sh, int C, const flo
 int dga_head_rows(int BV, int C, int r, int h, int w, const float* x, float* rows, void* stream) {
   DSPLAT_REQUIRE(BV > 0 && C > 0 && r > 0 && h > 0 && w > 0, "dga_head_rows: bad sizes");
   DSPLAT_REQUIRE(x && rows, "dga_head_rows: null pointer");
-  const size_t lds = head_rows_lds(C, r);
-  DSPLAT_REQUIRE(lds <= 64 * 1024, "dga_head_rows: %d channels x %d exceed the LDS tile", C, r);
-  k_head_rows<<<dim3((w + kRowTile - 1) / kRowTile, h * r, BV), 256, lds, (hipStream_t)stream>>>(
-      C, r, h, w, const_cast<float*>(x), rows, 0);  // x is only read (inverse = 0)
-  return dsplat::check_launch("k_head_rows");
+  return head_rows_launch(BV, C, r, h, w, const_cast<float*>(x), rows, 0, (hipStream_t)stream);  // x only read
 }
 
 int dga_head_rows_bwd(int BV, int C, int r, int h, int w, const float* drows, float* dx, void* stream) {
   DSPLAT_REQUIRE(BV > 0 && C > 0 && r > 0 && h > 0 && w > 0, "dga_head_rows_bwd: bad sizes");
   DSPLAT_REQUIRE(drows && dx, "dga_head_rows_bwd: null pointer");
-  const size_t lds = head_rows_lds(C, r);
-  DSPLAT_REQUIRE(lds <= 64 * 1024, "dga_head_rows_bwd: %d channels x %d exceed the LDS tile", C, r);
-  k_head_rows<<<dim3((w + kRowTile - 1) / kRowTile, h * r, BV), 256, lds, (hipStream_t)stream>>>(
-      C, r, h, w, dx, const_cast<float*>(drows), 1);  // drows is only read (inverse = 1)
-  return dsplat::check_launch("k_head_rows(bwd)");
+  return head_rows_launch(BV, C, r, h, w, dx, const_cast<float*>(drows), 1, (hipStream_t)stream);  // drows only read
 }
 
 }  // extern "C"
