@@ -2,6 +2,7 @@
 declares; the ctypes signature table matches the header's parameter counts."""
 from __future__ import annotations
 
+import ctypes
 import re
 import subprocess
 from pathlib import Path
@@ -74,3 +75,19 @@ def test_cpu_tensors_fail_loudly():
         raster.rasterize_views(torch.zeros(1, 4, 3), torch.zeros(1, 4, 1, 3), torch.zeros(1, 4),
                                torch.zeros(1, 4, 6), cams, [0], use_sh=True, sh_degree=0, image_height=8,
                                image_width=8)
+
+
+def test_head_rows_validation_without_gpu():
+    """dga_head_rows / _bwd reject bad sizes, null pointers and tiles above the LDS budget
+    before any HIP call (GPU-less host)."""
+    from my_depthsplat_amd import _lib
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("extension not built")
+    lib = _lib.load()
+    assert lib.dga_head_rows(0, 37, 8, 7, 12, None, None, None) == 1
+    assert b"bad sizes" in lib.dsplat_last_error()
+    assert lib.dga_head_rows(1, 37, 8, 7, 12, None, None, None) == 1
+    assert b"null pointer" in lib.dsplat_last_error()
+    x = ctypes.create_string_buffer(16)
+    assert lib.dga_head_rows_bwd(1, 1000, 8, 2, 2, x, x, None) == 1  # 16 * 8 * 1001 * 4 B > 64 KiB
+    assert b"LDS tile" in lib.dsplat_last_error()
