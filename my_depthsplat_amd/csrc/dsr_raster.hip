@@ -322,7 +322,8 @@ __device__ __forceinline__ float sh_eval(const float* sh, int ch, float x, float
 // what cuda_splatting.py:114,122's triu gather hands the rasterizer.
 constexpr int kLayoutShChannelMajor = DSR_LAYOUT_SH_CHANNEL_MAJOR, kLayoutCovFull = DSR_LAYOUT_COV_FULL,
               kLayoutCountsZeroed = DSR_LAYOUT_COUNTS_ZEROED, kLayoutRectBinning = DSR_LAYOUT_RECT_BINNING,
-              kLayoutExactBinning = DSR_LAYOUT_EXACT_BINNING, kLayoutDeferGeom = DSR_LAYOUT_DEFER_GEOM;
+              kLayoutExactBinning = DSR_LAYOUT_EXACT_BINNING, kLayoutDeferGeom = DSR_LAYOUT_DEFER_GEOM,
+              kLayoutConsumeDgeom = DSR_LAYOUT_CONSUME_DGEOM;
 __device__ __forceinline__ float load_cov(const float* cov, size_t sg, int k, int layout) {
   if (layout & kLayoutCovFull) {
     constexpr int idx[6] = {0, 1, 2, 4, 5, 8};
@@ -3368,7 +3369,7 @@ template <int DEG>
 __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     int G, int H, int W, int M, const float* __restrict__ means, const float* __restrict__ shs,
     const float* __restrict__ cov6, const dsr_camera* __restrict__ cams,
-    const float* __restrict__ geom, const long long* __restrict__ dgeom, const float* __restrict__ gscale,
+    const float* __restrict__ geom, long long* __restrict__ dgeom, const float* __restrict__ gscale,
     const int32_t* __restrict__ scene_view_start, const int32_t* __restrict__ scene_views,
     const uint8_t* __restrict__ row_live,
     float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
@@ -3595,6 +3596,17 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     dm0 += e0 * gsc;
     dm1 += e1 * gsc;
     dm2 += e2 * gsc;
+  }
+  if (layout & kLayoutConsumeDgeom) {
+    // leave the accumulator zero for the next forward: the block's rows of every view of the
+    // scene (contiguous, 72 B each; rows never added to are zero already) once all lanes read
+    __syncthreads();
+    const int zb = scene_view_start[s], ze = scene_view_start[s + 1];
+    const int nw = nrows * DSR_DGEOM_WORDS;
+    for (int k = zb; k < ze; ++k) {
+      long long* z = dgeom + ((size_t)scene_views[k] * G + g0) * DSR_DGEOM_WORDS;
+      for (int i = tid; i < nw; i += NT) z[i] = 0;
+    }
   }
   // outputs: coalesced through LDS
   if (valid) {
@@ -4218,7 +4230,8 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   DSPLAT_REQUIRE(means && cov6 && cams && geom && dgeom_fx && grad_scale && scene_view_start && scene_views && dmeans &&
                      dopac && dcov6,
                  "dsr_preprocess_bwd: null pointer");
-  const long long* dgeom = reinterpret_cast<const long long*>(dgeom_fx);
+  // DSR_LAYOUT_CONSUME_DGEOM: the rows read are zeroed (the header documents the write)
+  long long* dgeom = reinterpret_cast<long long*>(const_cast<int64_t*>(dgeom_fx));
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((G + NT - 1) / NT, S);
   const int deg = shs ? sh_degree : -1;

@@ -175,6 +175,8 @@ class RasterState:
     pruned_lists: bool = False
     # the backward's int64 gradient accumulator, its rendered rows zeroed by the forward
     dgeom: torch.Tensor | None = None
+    dgeom_filled: bool = False   # dgeom zeroed in full by this forward (not only its rendered rows)
+    dgeom_pool: object = None    # RasterContext that takes dgeom back, all zero, after the backward
     # depth-cut binning: (cut thresholds [V * super-blocks], compact records or None, super-block size)
     cut_plan: tuple | None = None
     # deferred geometry with a backward: [V*G] uint8, 1 for the rows projected in full (whose
@@ -272,6 +274,9 @@ LAYOUT_RECT_BINNING = 8
 # entries. Off: the reference's lists exactly (the oracle list tests switch it off).
 STATEFUL_EXACT_BINNING = os.environ.get("DSPLAT_STATEFUL_EXACT_BINNING", "1") != "0"
 LAYOUT_EXACT_BINNING = 16
+# The backward's accumulator handed, all zero, from one differentiable forward to the next of
+# the same shape (RasterContext.take_clean_dgeom) instead of a fill per forward
+REUSE_DGEOM = os.environ.get("DSPLAT_REUSE_DGEOM", "0") != "0"
 # Test hook (tests/test_fullsize_parity.py): the fast path also snapshots its per-tile counts
 # and writes its sorted keys back, so its lists can be compared with the oracle's. It adds a
 # copy and the key stores; the product never sets it.
@@ -293,7 +298,8 @@ class RasterContext:
       debug_keep_fast_lists, key_budget_bytes (None and no module override: automatic,
       min(48 GiB, 40 % of the device, half of its memory free when first asked)),
       seg_capacity (inference fast path: entries per (view, tile) segment; None = from the
-      hints, see SEG_CAPACITY), defer_geom (depth cut without a backward: see DEFER_GEOM).
+      hints, see SEG_CAPACITY), defer_geom (depth cut without a backward: see DEFER_GEOM),
+      reuse_dgeom (REUSE_DGEOM).
     hints: max_count (largest tile list seen: picks the fused sort's LDS class),
       two_phase_max (largest list of the last two-phase call: plans the depth cut).
     adapt_hints False freezes the hints (tests pin a class)."""
@@ -302,7 +308,8 @@ class RasterContext:
              "fused_sort_render": "FUSED_SORT_RENDER", "sort_render_hint": "SORT_RENDER_HINT",
              "inkernel_cameras": "INKERNEL_CAMERAS", "sort_prefix": "SORT_PREFIX", "cut_prefix": "CUT_PREFIX",
              "debug_keep_fast_lists": "DEBUG_KEEP_FAST_LISTS", "key_budget_bytes": "KEY_BUDGET_BYTES",
-             "seg_capacity": "SEG_CAPACITY", "defer_geom": "DEFER_GEOM", "cut_fused": "CUT_FUSED"}
+             "seg_capacity": "SEG_CAPACITY", "defer_geom": "DEFER_GEOM", "cut_fused": "CUT_FUSED",
+             "reuse_dgeom": "REUSE_DGEOM"}
 
     def __init__(self, **options):
         unknown = set(options) - set(self._OPTS)
@@ -315,6 +322,7 @@ class RasterContext:
         self._last: dict = {"counts": None, "host_counts": None}
         self._auto_budget: dict = {}   # device index -> bytes
         self._clean_counts: dict = {}  # (device, n) -> (zeroed counters, last stream, event)
+        self._clean_dgeom: dict = {}   # (device, V, G) -> (all-zero backward accumulator, stream, event)
         self._graph_owned: list = []
         self._warned_rebuild = False
 
@@ -436,6 +444,31 @@ class RasterContext:
         if len(self._clean_counts) > 64:
             self._clean_counts.clear()
         self._clean_counts[(str(dev), t.numel())] = (t, int(stream), ev)
+
+
+    # The backward's fixed-point accumulator [V, G, DGEOM_WORDS] (72 B per (view, Gaussian)):
+    # dsr_preprocess_bwd with LAYOUT_CONSUME_DGEOM zeroes every row it reads, and those are all
+    # the rows dsr_render_bwd added to, so a buffer that was all zero before its forward is all
+    # zero again after its backward and the next forward of the same shape takes it without a
+    # fill (config C: a 604 MB memset per step). Not used inside a graph capture.
+    def take_clean_dgeom(self, V: int, G: int, dev, stream) -> tuple[torch.Tensor, bool]:
+        key = (str(dev), V, G)
+        ent = self._clean_dgeom.get(key)
+        if ent is not None and self.opt("reuse_dgeom") and not torch.cuda.is_current_stream_capturing():
+            t, last_stream, ev = ent
+            if last_stream == int(stream) or ev.query():
+                del self._clean_dgeom[key]
+                return t, True
+        return torch.empty((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev), False
+
+    def give_back_clean_dgeom(self, t: torch.Tensor, stream) -> None:
+        if torch.cuda.is_current_stream_capturing():
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+        if len(self._clean_dgeom) > 4:
+            self._clean_dgeom.clear()
+        self._clean_dgeom[(str(t.device), t.shape[0], t.shape[1])] = (t, int(stream), ev)
 
 
 _default_contexts: dict = {}
@@ -595,6 +628,7 @@ def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invar
 LAYOUT_SH_CHANNEL_MAJOR = 1  # feats [S,G,3,M] (Gaussians.harmonics) instead of [S,G,M,3]
 LAYOUT_COV_FULL = 2          # covariance [S,G,3,3] instead of cov6 [S,G,6]
 LAYOUT_COUNTS_ZEROED = 4     # seg_count handed in already zeroed
+LAYOUT_CONSUME_DGEOM = 64    # dsr_preprocess_bwd zeroes the accumulator rows it reads
 
 
 def input_layout(feats, cov6, use_sh, channel_major_sh):
@@ -605,7 +639,8 @@ def input_layout(feats, cov6, use_sh, channel_major_sh):
 
 
 def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0, zeroed_counts=None,
-                need_state=True, dgeom_zero: torch.Tensor | None = None, ctx: RasterContext | None = None):
+                need_state=True, dgeom_zero: torch.Tensor | None = None, ctx: RasterContext | None = None,
+                dgeom_clean: bool = False):
     """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh; [S,G,3,M] with
     LAYOUT_SH_CHANNEL_MAJOR) or [S,G,3]; opacities [S,G]; cov6 [S,G,6] (or [S,G,3,3] with
     LAYOUT_COV_FULL); cams [V,44]. Returns (color [V,3,H,W], RasterState).
@@ -615,7 +650,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     kernel (no scan, no second pass over the geometry, no host sync); otherwise the
     two-phase path counts, scans (one 8-byte read-back of N), scatters.
     dgeom_zero: the backward's [V, G, DGEOM_WORDS] int64 accumulator, whose rendered rows
-    the projection kernel zeroes as it writes their records (no separate fill pass).
+    the projection kernel zeroes as it writes their records (no separate fill pass);
+    dgeom_clean: it is all zero already (RasterContext.take_clean_dgeom), no fill needed.
     ctx: the caller's RasterContext (options + adaptive hints; default: the device's)."""
     lib = _lib.load()
     cam_in = cams if isinstance(cams, CameraInputs) else None
@@ -636,6 +672,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     col_p = None if use_sh else feats.data_ptr()
     geom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
     radii = torch.empty((V, G), dtype=torch.int32, device=dev)
+    dgeom_filled = False
     lds_cap = lib.dsr_sort_lds_capacity()
     maxc_hint = spec["max_count"] or lds_cap
     # eager inference fast path: cameras set up inside the binning kernel, counters taken zeroed
@@ -698,9 +735,10 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             # 3.06 ms, same-box A/B); the depth-cut path below keeps the in-kernel zeroing of the
             # few rows it projects in full
             dz = dgeom_zero
-            if dz is not None:
+            if dz is not None and not dgeom_clean:
                 dz.zero_()
-                dz = None
+            dgeom_filled = dz is not None
+            dz = None
             _lib.check(_timed("k_project_emit", lib.dsr_project_bin,
                 S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                 cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dz), seg_count.data_ptr(),
@@ -822,7 +860,8 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                           int(bool(need_state) or snap is not None), int(fast),
                           ctx.opt("sort_render_hint") or spec["max_count"], layout, *outs[:3], None, st),
                    "dsr_sort_render")
-        state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, cams=cams)
+        state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, cams=cams,
+                            dgeom_filled=dgeom_filled)
         if fast:  # the counters are zero again once the launch above has run
             ctx.give_back_clean_counts(seg_count, dev, st)
             # consumed (no backward in this mode); with exact binning n_contrib counts positions
@@ -869,6 +908,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, None if cut_fused else n_contrib,
                         seg_sorted, overflow, tile_count if stride == SEG_ENDS else None, cams=cams)
     state.row_live = row_live
+    state.dgeom_filled = dgeom_filled
     state.pruned_lists = bool(layout & LAYOUT_EXACT_BINNING) and stride != SEG_ENDS
     if stride == SEG_ENDS:  # the depth-cut plan (tools/cut_case.py statistics)
         state.cut_plan = (cut, cut_rec, lib.dsr_cut_superblock(H, W))
@@ -939,8 +979,10 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     dev = means.device
     st = _lib.stream_of(dev)
     dcolor = dcolor.contiguous().float()
+    pool = None
     if state.dgeom is not None:  # rendered rows zeroed by the forward's projection kernel
         dgeom_fx, state.dgeom = state.dgeom, None
+        pool, state.dgeom_pool = state.dgeom_pool, None
     else:
         dgeom_fx = torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev)
     gscale = torch.empty(GRAD_SCALE_BLOCKS, dtype=torch.float32, device=dev)
@@ -973,7 +1015,10 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
         idx.data_ptr(),
         idx[S + 1:].data_ptr(), _ptr(state.row_live), dmeans.data_ptr(), dfeat.data_ptr() if use_sh else None,
         None if use_sh else dfeat.data_ptr(), dopac.data_ptr(), dcov6.data_ptr(),
-        None if dmean2d is None else dmean2d.data_ptr(), layout, st), "dsr_preprocess_bwd")
+        None if dmean2d is None else dmean2d.data_ptr(), layout | (LAYOUT_CONSUME_DGEOM if pool else 0), st),
+        "dsr_preprocess_bwd")
+    if pool is not None:  # all zero again once the launch above has run
+        pool.give_back_clean_dgeom(dgeom_fx, st)
     return dmeans, dfeat, dopac, dcov6, dmean2d, dgeom
 
 
@@ -984,11 +1029,14 @@ class _RasterizeViews(torch.autograd.Function):
         V = len(view_scene)
         need = any(ctx.needs_input_grad[:5])
         # the backward's accumulator: its rendered rows are zeroed by the projection kernel
-        dgeom = torch.empty((V, means.shape[1], DGEOM_WORDS), dtype=torch.int64, device=means.device) \
-            if need else None
+        rc = rctx or default_context(means.device)
+        dgeom, clean = rc.take_clean_dgeom(V, means.shape[1], means.device, _lib.stream_of(means.device)) \
+            if need else (None, False)
         color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout,
-                                   zeroed_counts, need_state=need, dgeom_zero=dgeom, ctx=rctx)
+                                   zeroed_counts, need_state=need, dgeom_zero=dgeom, ctx=rc, dgeom_clean=clean)
         state.dgeom = dgeom
+        # all zero outside the rows the backward reads: the pool's buffer, or the full fill
+        state.dgeom_pool = rc if rc.opt("reuse_dgeom") and (clean or state.dgeom_filled) else None
         ctx.save_for_backward(means, feats, opacities, cov6, state.cams)
         ctx.state = state
         ctx.meta = (view_scene, use_sh, sh_degree, None if means2d is None else means2d.shape, layout)

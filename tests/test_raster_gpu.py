@@ -785,6 +785,43 @@ def test_reference_layout_gradients(gpu):
     assert float(a[2][..., 1, 0].abs().max()) == 0.0  # lower triangle gets no gradient
 
 
+def test_dgeom_pool_reuse_is_bit_identical(gpu):
+    """The backward's accumulator handed from one step to the next (dsr_preprocess_bwd with
+    LAYOUT_CONSUME_DGEOM zeroes what it reads; no fill in the next forward): gradients equal a
+    fresh context's bit for bit, across scenes, and the pooled buffer is all zero between steps."""
+    from my_depthsplat_amd import raster
+    from my_depthsplat_amd.cuda_splatting import _cov6
+    from my_depthsplat_amd.synthetic import make_scene
+    H, W = 48, 64
+    scenes = [make_scene(batch=1, n_context=2, n_targets=2, height=H, width=W, seed=s, device=gpu) for s in (21, 22)]
+    gp = torch.Generator(device=gpu).manual_seed(6)
+    dcol = torch.randn(2, 3, H, W, device=gpu, generator=gp)
+
+    def grads(sc, ctx):
+        g = sc.gaussians
+        m = g.means.clone().requires_grad_(True)
+        h = g.harmonics.clone().requires_grad_(True)
+        o = g.opacities.clone().requires_grad_(True)
+        c = _cov6(g.covariances).clone().requires_grad_(True)
+        cams = raster.build_cameras(sc.target_extrinsics[0], sc.target_intrinsics[0], sc.near[0], sc.far[0],
+                                    torch.zeros(2, 3, device=gpu), [0, 0], True)
+        img, _ = raster.rasterize_views(m, h.transpose(-1, -2), o, c, cams, [0, 0], use_sh=True, sh_degree=2,
+                                        image_height=H, image_width=W, ctx=ctx)
+        (img * dcol).sum().backward()
+        return m.grad, h.grad, o.grad, c.grad
+
+    ref = [grads(sc, raster.RasterContext(reuse_dgeom=False)) for sc in scenes]
+    ctx = raster.RasterContext(reuse_dgeom=True)
+    for i in (0, 1, 0, 1):
+        got = grads(scenes[i], ctx)
+        for x, y in zip(got, ref[i]):
+            assert torch.equal(x, y)
+        pooled = list(ctx._clean_dgeom.values())
+        assert len(pooled) == 1
+        torch.cuda.synchronize()
+        assert int(pooled[0][0].count_nonzero()) == 0
+
+
 def test_graph_capture_replay_matches_eager(gpu):
     """The sync-free forward captured into a hipGraph: replays equal eager calls, and
     replays pick up new data written into the captured input buffers."""
