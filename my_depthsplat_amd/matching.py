@@ -69,21 +69,27 @@ def warp_with_pose_depth_candidates(feature1, intrinsics, pose, depth, clamp_min
                        float(clamp_min_depth))
 
 
+def _cost_volume_fwd(ref, tgt, intrinsics, pose, depth, per_pixel, clamp):
+    lib = _lib.load()
+    B, J, C, H, W = tgt.shape
+    D = depth.shape[1]
+    dev = ref.device
+    # channel-last copies of the features + the epipolar pixel groups (the backward reuses
+    # them; after a band-kernel forward the backward makes them)
+    ws = torch.empty(lib.dcv_cost_volume_workspace_size(B, J, C, H, W), dtype=torch.uint8, device=dev)
+    cost = torch.empty((B, D, H, W), dtype=torch.float32, device=dev)
+    _lib.check(lib.dcv_cost_volume_fwd(B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), tgt.data_ptr(),
+                                       intrinsics.data_ptr(), pose.data_ptr(), depth.data_ptr(), clamp,
+                                       ws.data_ptr(), cost.data_ptr(), _lib.stream_of(dev)), "dcv_cost_volume_fwd")
+    return cost, ws
+
+
 class _CostVolume(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ref, tgt, intrinsics, pose, depth, per_pixel, clamp):
-        lib = _lib.load()
         B, J, C, H, W = tgt.shape
         D = depth.shape[1]
-        dev = ref.device
-        st = _lib.stream_of(dev)
-        # channel-last copies of the features + the epipolar pixel groups (the backward reuses
-        # them; after a band-kernel forward the backward makes them)
-        ws = torch.empty(lib.dcv_cost_volume_workspace_size(B, J, C, H, W), dtype=torch.uint8, device=dev)
-        cost = torch.empty((B, D, H, W), dtype=torch.float32, device=dev)
-        _lib.check(lib.dcv_cost_volume_fwd(B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), tgt.data_ptr(),
-                                           intrinsics.data_ptr(), pose.data_ptr(), depth.data_ptr(), clamp,
-                                           ws.data_ptr(), cost.data_ptr(), st), "dcv_cost_volume_fwd")
+        cost, ws = _cost_volume_fwd(ref, tgt, intrinsics, pose, depth, per_pixel, clamp)
         ctx.save_for_backward(ref, tgt, ws, intrinsics, pose, depth)
         ctx.meta = (B, J, C, H, W, D, per_pixel, clamp)
         return cost
@@ -122,8 +128,13 @@ def plane_sweep_cost_volume(ref: torch.Tensor, tgt: torch.Tensor, intrinsics: to
         raise ValueError("depth must be [B, D] or [B, D, H, W]")
     _lib.require_gpu(ref, tgt, intrinsics, pose, depth)
     per_pixel = depth.dim() == 4
-    return _CostVolume.apply(_f(ref), _f(tgt), _f(intrinsics).detach(), _f(pose).detach(), _f(depth).detach(),
-                             per_pixel, float(clamp_min_depth))
+    args = (_f(ref), _f(tgt), _f(intrinsics).detach(), _f(pose).detach(), _f(depth).detach(), per_pixel,
+            float(clamp_min_depth))
+    if torch.is_grad_enabled() and (args[0].requires_grad or args[1].requires_grad):
+        return _CostVolume.apply(*args)
+    # nothing to differentiate: the launch without the autograd node (its set-up is ~5 us of host
+    # time, a third of a 32x32 call)
+    return _cost_volume_fwd(*args)[0]
 
 
 def batch_features_camera_parameters(features, intrinsics, extrinsics, nn_matrix=None, no_batch=False):
