@@ -542,8 +542,8 @@ def leg_kernel_bytes(name, st, *, G, V, S, HW, pixels=0, training=False):
         return raster.algorithmic_bytes_cut(name, G=G, V=V, N_written=st["written"], HW=HW,
                                             survivors=st.get("survivors", V * G), S=S)
     b = raster.algorithmic_bytes(name, G=G, V=V, N=N, HW=HW, S=S)
-    if training and name == "k_project_emit":
-        b += 72 * V * G  # the backward's fixed-point rows zeroed in the same pass
+    # (training: the backward's fixed-point rows are zeroed by a separate streaming fill on the
+    # fixed-capacity path, not by k_project_emit: no extra bytes here)
     if training and name == "k_sort_render":
         b += 8 * N + 4 * V * HW  # sorted keys written back + n_contrib for the backward
     return b

@@ -93,10 +93,6 @@ int dsr_build_cameras(int V, const float* extrinsics, const float* intrinsics, c
 #define DSR_LAYOUT_DEFER_GEOM 32       /* dsr_preprocess_cut only: radii, counts, histogram and
                                           cut_rec, but no geometry record and no colour (see
                                           dsr_project_survivors); needs cut_rec, no dgeom_zero      */
-#define DSR_LAYOUT_CONSUME_DGEOM 64    /* dsr_preprocess_bwd only: every dgeom_fx row it reads is
-                                          zeroed after the read (with the rest of its block of rows), so an accumulator that was all zero
-                                          before the forward is all zero again (reusable without a
-                                          fill); dgeom_fx is written despite its const             */
 int dsr_preprocess_fwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* means, const float* shs, const float* colors,
                        const float* opacities, const float* cov6, const dsr_camera* cams,

@@ -322,8 +322,7 @@ __device__ __forceinline__ float sh_eval(const float* sh, int ch, float x, float
 // what cuda_splatting.py:114,122's triu gather hands the rasterizer.
 constexpr int kLayoutShChannelMajor = DSR_LAYOUT_SH_CHANNEL_MAJOR, kLayoutCovFull = DSR_LAYOUT_COV_FULL,
               kLayoutCountsZeroed = DSR_LAYOUT_COUNTS_ZEROED, kLayoutRectBinning = DSR_LAYOUT_RECT_BINNING,
-              kLayoutExactBinning = DSR_LAYOUT_EXACT_BINNING, kLayoutDeferGeom = DSR_LAYOUT_DEFER_GEOM,
-              kLayoutConsumeDgeom = DSR_LAYOUT_CONSUME_DGEOM;
+              kLayoutExactBinning = DSR_LAYOUT_EXACT_BINNING, kLayoutDeferGeom = DSR_LAYOUT_DEFER_GEOM;
 __device__ __forceinline__ float load_cov(const float* cov, size_t sg, int k, int layout) {
   if (layout & kLayoutCovFull) {
     constexpr int idx[6] = {0, 1, 2, 4, 5, 8};
@@ -2502,15 +2501,15 @@ __device__ __forceinline__ void composite_pair(const PairRec& P, const PixUV2& p
 // one does.
 __device__ bool tail_reaches_live(const float* __restrict__ gv, const uint64_t* __restrict__ keys, uint32_t b,
                                   uint32_t e, float fx0, float fy0, const PixUV2& pp, bool alive, WaveList* plist,
-                                  uint64_t lt, int lane) {
-  uint32_t nid = b + lane < e ? (uint32_t)keys[b + lane] : 0xffffffffu;
+                                  uint64_t lt, int lane, uint32_t gmax) {
+  uint32_t nid = b + lane < e ? min((uint32_t)keys[b + lane], gmax) : 0xffffffffu;
   for (uint32_t base = b; base < e; base += 64) {
     const uint64_t live = __ballot(alive);
     if (!live) break;
     float lx0, ly0, lx1, ly1;
     live_rect(live, fx0, fy0, lx0, ly0, lx1, ly1);
     const uint32_t id = nid;
-    nid = base + 64 + lane < e ? (uint32_t)keys[base + 64 + lane] : 0xffffffffu;
+    nid = base + 64 + lane < e ? min((uint32_t)keys[base + 64 + lane], gmax) : 0xffffffffu;
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f), r = q;
     if (id != 0xffffffffu) {
       const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
@@ -2755,13 +2754,14 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
   float Tr = 1.0f, C2 = 0.f;
   bool alive = inside;
   uint32_t last = 0;
-  composite_tile<true>([&](uint32_t e) { return (uint32_t)keys[e]; }, start, end, gv, fx0, fy0, pp, lane, lt, plist,
+  const uint32_t gmax = (uint32_t)G - 1u;  // ids are clamped: a corrupt key reads a valid record, never faults
+  composite_tile<true>([&](uint32_t e) { return min((uint32_t)keys[e], gmax); }, start, end, gv, fx0, fy0, pp, lane, lt, plist,
                        Tr, C01, C2, last, alive);
   bool void_tile = false;  // wave-uniform
   if (absent_tail)
     void_tile = __any(alive);  // a pixel still live at the end of the written part: the rest may blend
   else if (end < tail_end)
-    void_tile = tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pp, alive, plist, lt, lane);
+    void_tile = tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pp, alive, plist, lt, lane, gmax);
   if (void_tile && lane == 0) {  // the tile's output is void: completed, sorted and re-rendered by the caller
     seg_overflow[seg] = 1u;
     seg_overflow[(size_t)gridDim.z * T] = 1u;  // any-flag
@@ -2929,8 +2929,8 @@ __device__ __attribute__((noinline)) void render_rebuilt(int G, int gx, int gy, 
     __syncthreads();
     if (n > 1) count_sort<KMAX, NT, NBL>(tmp, n, A, id_bits, cnt, wsum, flag);
     uint32_t wl = 0;
-    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)A[padi<KMAX>(i)]; }, 0u, n, gv, fx0, fy0, pp, lane, lt,
-                         plist, Tr, C01, C2, wl, alive);
+    composite_tile<LAST>([&](uint32_t i) { return min((uint32_t)A[padi<KMAX>(i)], (uint32_t)G - 1u); }, 0u, n, gv, fx0,
+                         fy0, pp, lane, lt, plist, Tr, C01, C2, wl, alive);
     if (LAST && wl) last = base + wl;
     const bool more = __syncthreads_or(alive);
     if (!more || hi == ~0ull) break;
@@ -3014,12 +3014,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   float Tr = 1.0f, C2 = 0.f;
   bool alive = inside;
   uint32_t last = 0;
+  // Gaussian ids come from LDS (or HBM) slots the sort filled; they are clamped to the view's
+  // range so that a slot the sort did not write (a broken variant: r04 "noscat" read garbage
+  // ids and faulted with hipErrorIllegalAddress) reads a valid record instead of faulting
+  const uint32_t gmax = (uint32_t)G - 1u;
   if (in_lds)
-    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)A[padi<KMAX>(i)]; }, 0u, n, gv, (float)sx0, (float)sy0, pp,
-                         lane, lt, plist, Tr, C01, C2, last, alive);
+    composite_tile<LAST>([&](uint32_t i) { return min((uint32_t)A[padi<KMAX>(i)], gmax); }, 0u, n, gv, (float)sx0,
+                         (float)sy0, pp, lane, lt, plist, Tr, C01, C2, last, alive);
   else
-    composite_tile<LAST>([&](uint32_t i) { return (uint32_t)keys[i]; }, b, e, gv, (float)sx0, (float)sy0, pp, lane, lt,
-                         plist, Tr, C01, C2, last, alive);
+    composite_tile<LAST>([&](uint32_t i) { return min((uint32_t)keys[i], gmax); }, b, e, gv, (float)sx0, (float)sy0, pp,
+                         lane, lt, plist, Tr, C01, C2, last, alive);
   if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
   // depth cut (seg_overflow given, DSR_SEG_ENDS): a pixel of this wave still live at the end
   // of the written part while the tile has omitted entries -> flag the tile, the any-flag and
@@ -3210,7 +3214,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const int nch = (int)((nproc + BCH - 1) / BCH);
   auto id_at = [&](int c) -> uint32_t {  // unconditional key read (clamped), id 0 past the range
     const int pos = (int)nproc - (c + 1) * BCH + lane;
-    const uint32_t k = (uint32_t)keys[start + (uint32_t)min(max(pos, 0), max((int)nproc - 1, 0))];
+    const uint32_t k = min((uint32_t)keys[start + (uint32_t)min(max(pos, 0), max((int)nproc - 1, 0))], (uint32_t)G - 1u);
     return (pos >= 0 && c < nch) ? k : 0u;
   };
   auto chunk = [&](int ch, uint32_t id, float4 q, float4 r, float bl) {
@@ -3239,7 +3243,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       d.pos = (uint32_t)p;
       // the forward's power test on the same floats: p2o <= thr (definite conic: always)
       d.pad[0] = __float_as_uint(conic_pd(d.q.z, d.r.x, d.q.w) ? __builtin_inff() : kP2Max + lo);
-      d.pad[1] = __float_as_uint(r.y > 0.f ? __builtin_amdgcn_rcpf(r.y) : 0.f);  // 1 / o (dL/do)
+      // 1 / o for dL/do = S(h) / o; a subnormal o would give rcp = inf and 0 * inf = NaN (such an
+      // entry never blends, S(h) = 0): its dL/do is 0, as the reference's S(G dL/dalpha) gives
+      d.pad[1] = __float_as_uint(r.y >= 1.17549435e-38f ? __builtin_amdgcn_rcpf(r.y) : 0.f);
     }
     const int cnt = __popcll(bal);
     __builtin_amdgcn_wave_barrier();
@@ -3369,7 +3375,7 @@ template <int DEG>
 __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     int G, int H, int W, int M, const float* __restrict__ means, const float* __restrict__ shs,
     const float* __restrict__ cov6, const dsr_camera* __restrict__ cams,
-    const float* __restrict__ geom, long long* __restrict__ dgeom, const float* __restrict__ gscale,
+    const float* __restrict__ geom, const long long* __restrict__ dgeom, const float* __restrict__ gscale,
     const int32_t* __restrict__ scene_view_start, const int32_t* __restrict__ scene_views,
     const uint8_t* __restrict__ row_live,
     float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
@@ -3596,17 +3602,6 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     dm0 += e0 * gsc;
     dm1 += e1 * gsc;
     dm2 += e2 * gsc;
-  }
-  if (layout & kLayoutConsumeDgeom) {
-    // leave the accumulator zero for the next forward: the block's rows of every view of the
-    // scene (contiguous, 72 B each; rows never added to are zero already) once all lanes read
-    __syncthreads();
-    const int zb = scene_view_start[s], ze = scene_view_start[s + 1];
-    const int nw = nrows * DSR_DGEOM_WORDS;
-    for (int k = zb; k < ze; ++k) {
-      long long* z = dgeom + ((size_t)scene_views[k] * G + g0) * DSR_DGEOM_WORDS;
-      for (int i = tid; i < nw; i += NT) z[i] = 0;
-    }
   }
   // outputs: coalesced through LDS
   if (valid) {
@@ -4230,8 +4225,7 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   DSPLAT_REQUIRE(means && cov6 && cams && geom && dgeom_fx && grad_scale && scene_view_start && scene_views && dmeans &&
                      dopac && dcov6,
                  "dsr_preprocess_bwd: null pointer");
-  // DSR_LAYOUT_CONSUME_DGEOM: the rows read are zeroed (the header documents the write)
-  long long* dgeom = reinterpret_cast<long long*>(const_cast<int64_t*>(dgeom_fx));
+  const long long* dgeom = reinterpret_cast<const long long*>(dgeom_fx);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((G + NT - 1) / NT, S);
   const int deg = shs ? sh_degree : -1;

@@ -176,7 +176,6 @@ class RasterState:
     # the backward's int64 gradient accumulator, its rendered rows zeroed by the forward
     dgeom: torch.Tensor | None = None
     dgeom_filled: bool = False   # dgeom zeroed in full by this forward (not only its rendered rows)
-    dgeom_pool: object = None    # RasterContext that takes dgeom back, all zero, after the backward
     # depth-cut binning: (cut thresholds [V * super-blocks], compact records or None, super-block size)
     cut_plan: tuple | None = None
     # deferred geometry with a backward: [V*G] uint8, 1 for the rows projected in full (whose
@@ -241,30 +240,30 @@ SORT_PREFIX = int(os.environ.get("DSPLAT_SORT_PREFIX", "4096"))
 # not all saturate within them get the rest appended, sorted and rendered again. 0 = off.
 CUT_PREFIX = int(os.environ.get("DSPLAT_CUT_PREFIX", "2048"))
 CUT_SORT_HINT = 4096  # LDS sort size for the written parts (larger ones sort through HBM)
-# Depth cut without a backward (need_state False): the preprocess writes no geometry record and
-# evaluates no colour; each scatter pass lists the Gaussians that may emit and
-# dsr_project_survivors projects only those (~3 % of the (view, Gaussian) pairs at 12x512x960).
-DEFER_GEOM = os.environ.get("DSPLAT_DEFER_GEOM", "1") != "0"
-# ... and the written heads sorted + composited in one dsr_sort_render launch (flags for the
-# tail pass as dsr_render_fwd's) instead of dsr_bin_sort + dsr_render_fwd
-CUT_FUSED = os.environ.get("DSPLAT_CUT_FUSED", "1") != "0"
+# Depth cut (need_state False or True): the count pass writes no geometry record and evaluates
+# no colour; each scatter pass lists the Gaussians that may emit and dsr_project_survivors
+# projects only those (~3 % of the (view, Gaussian) pairs at 12x512x960). Off only where the
+# compact 8-byte pre-test records cannot address the grid (more than 255 tiles a side) and in
+# the test that keeps the full-record kernel covered. Without a backward the written heads are
+# sorted and composited by one dsr_sort_render launch (flags for the tail pass as
+# dsr_render_fwd's).
+DEFER_GEOM = True
 LAYOUT_DEFER_GEOM = 32
 # Fixed-capacity binning with tile lists up to FUSED_MAX entries (the hint from earlier calls)
 # sorts and composites in one launch (dsr_sort_render); longer lists take dsr_bin_sort +
 # dsr_render_fwd (MSD split, prefix sort). Either is exact for any list length.
-FUSED_SORT_RENDER = os.environ.get("DSPLAT_FUSED_SORT_RENDER", "1") != "0"
+FUSED_SORT_RENDER = True
 FUSED_MAX = 4096
 # dsr_sort_render's LDS class comes from the largest count of earlier calls (the context's
-# hints); a nonzero
-# override pins it (tests: every class on the same lists)
+# hints); a nonzero override pins it (tests: every class on the same lists)
 SORT_RENDER_HINT = 0
-# inference fast path (cameras inside the binning kernel, self-zeroing counters); env
-# DSPLAT_INKERNEL_CAMERAS=0 keeps the separate camera launch (experiments)
-INKERNEL_CAMERAS = os.environ.get("DSPLAT_INKERNEL_CAMERAS", "1") != "0"
+# inference fast path: cameras inside the binning kernel, self-zeroing counters (False: the
+# separate camera launch of the stateful path)
+INKERNEL_CAMERAS = True
 # Binning of the inference fast path: exact (a (Gaussian, tile) pair is kept only when the
 # alpha >= 1/255 ellipse reaches the tile; same images, shorter lists) or the reference's
 # 3-sigma rects (DSR_LAYOUT_RECT_BINNING; bench.py reports both throughputs).
-EXACT_BINNING = os.environ.get("DSPLAT_EXACT_BINNING", "1") != "0"
+EXACT_BINNING = True
 LAYOUT_RECT_BINNING = 8
 # The same exact test on the stateful (training) path, in the fixed-capacity and plain
 # two-phase layouts (DSR_LAYOUT_EXACT_BINNING; the depth-cut layout keeps 3-sigma rects): the
@@ -272,11 +271,8 @@ LAYOUT_RECT_BINNING = 8
 # per-pixel alpha test at every pixel of their tile, so images and gradients are unchanged
 # (tests/test_raster_gpu.py) while the sort, the forward and the backward walk about half the
 # entries. Off: the reference's lists exactly (the oracle list tests switch it off).
-STATEFUL_EXACT_BINNING = os.environ.get("DSPLAT_STATEFUL_EXACT_BINNING", "1") != "0"
+STATEFUL_EXACT_BINNING = True
 LAYOUT_EXACT_BINNING = 16
-# The backward's accumulator handed, all zero, from one differentiable forward to the next of
-# the same shape (RasterContext.take_clean_dgeom) instead of a fill per forward
-REUSE_DGEOM = os.environ.get("DSPLAT_REUSE_DGEOM", "0") != "0"
 # Test hook (tests/test_fullsize_parity.py): the fast path also snapshots its per-tile counts
 # and writes its sorted keys back, so its lists can be compared with the oracle's. It adds a
 # copy and the key stores; the product never sets it.
@@ -298,8 +294,7 @@ class RasterContext:
       debug_keep_fast_lists, key_budget_bytes (None and no module override: automatic,
       min(48 GiB, 40 % of the device, half of its memory free when first asked)),
       seg_capacity (inference fast path: entries per (view, tile) segment; None = from the
-      hints, see SEG_CAPACITY), defer_geom (depth cut without a backward: see DEFER_GEOM),
-      reuse_dgeom (REUSE_DGEOM).
+      hints, see SEG_CAPACITY), defer_geom (depth cut: see DEFER_GEOM).
     hints: max_count (largest tile list seen: picks the fused sort's LDS class),
       two_phase_max (largest list of the last two-phase call: plans the depth cut).
     adapt_hints False freezes the hints (tests pin a class)."""
@@ -308,8 +303,7 @@ class RasterContext:
              "fused_sort_render": "FUSED_SORT_RENDER", "sort_render_hint": "SORT_RENDER_HINT",
              "inkernel_cameras": "INKERNEL_CAMERAS", "sort_prefix": "SORT_PREFIX", "cut_prefix": "CUT_PREFIX",
              "debug_keep_fast_lists": "DEBUG_KEEP_FAST_LISTS", "key_budget_bytes": "KEY_BUDGET_BYTES",
-             "seg_capacity": "SEG_CAPACITY", "defer_geom": "DEFER_GEOM", "cut_fused": "CUT_FUSED",
-             "reuse_dgeom": "REUSE_DGEOM"}
+             "seg_capacity": "SEG_CAPACITY", "defer_geom": "DEFER_GEOM"}
 
     def __init__(self, **options):
         unknown = set(options) - set(self._OPTS)
@@ -322,7 +316,6 @@ class RasterContext:
         self._last: dict = {"counts": None, "host_counts": None}
         self._auto_budget: dict = {}   # device index -> bytes
         self._clean_counts: dict = {}  # (device, n) -> (zeroed counters, last stream, event)
-        self._clean_dgeom: dict = {}   # (device, V, G) -> (all-zero backward accumulator, stream, event)
         self._graph_owned: list = []
         self._warned_rebuild = False
 
@@ -444,31 +437,6 @@ class RasterContext:
         if len(self._clean_counts) > 64:
             self._clean_counts.clear()
         self._clean_counts[(str(dev), t.numel())] = (t, int(stream), ev)
-
-
-    # The backward's fixed-point accumulator [V, G, DGEOM_WORDS] (72 B per (view, Gaussian)):
-    # dsr_preprocess_bwd with LAYOUT_CONSUME_DGEOM zeroes every row it reads, and those are all
-    # the rows dsr_render_bwd added to, so a buffer that was all zero before its forward is all
-    # zero again after its backward and the next forward of the same shape takes it without a
-    # fill (config C: a 604 MB memset per step). Not used inside a graph capture.
-    def take_clean_dgeom(self, V: int, G: int, dev, stream) -> tuple[torch.Tensor, bool]:
-        key = (str(dev), V, G)
-        ent = self._clean_dgeom.get(key)
-        if ent is not None and self.opt("reuse_dgeom") and not torch.cuda.is_current_stream_capturing():
-            t, last_stream, ev = ent
-            if last_stream == int(stream) or ev.query():
-                del self._clean_dgeom[key]
-                return t, True
-        return torch.empty((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev), False
-
-    def give_back_clean_dgeom(self, t: torch.Tensor, stream) -> None:
-        if torch.cuda.is_current_stream_capturing():
-            return
-        ev = torch.cuda.Event()
-        ev.record()
-        if len(self._clean_dgeom) > 4:
-            self._clean_dgeom.clear()
-        self._clean_dgeom[(str(t.device), t.shape[0], t.shape[1])] = (t, int(stream), ev)
 
 
 _default_contexts: dict = {}
@@ -628,7 +596,6 @@ def build_cameras(extrinsics, intrinsics, near, far, bg, view_scene, scale_invar
 LAYOUT_SH_CHANNEL_MAJOR = 1  # feats [S,G,3,M] (Gaussians.harmonics) instead of [S,G,M,3]
 LAYOUT_COV_FULL = 2          # covariance [S,G,3,3] instead of cov6 [S,G,6]
 LAYOUT_COUNTS_ZEROED = 4     # seg_count handed in already zeroed
-LAYOUT_CONSUME_DGEOM = 64    # dsr_preprocess_bwd zeroes the accumulator rows it reads
 
 
 def input_layout(feats, cov6, use_sh, channel_major_sh):
@@ -639,8 +606,7 @@ def input_layout(feats, cov6, use_sh, channel_major_sh):
 
 
 def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout=0, zeroed_counts=None,
-                need_state=True, dgeom_zero: torch.Tensor | None = None, ctx: RasterContext | None = None,
-                dgeom_clean: bool = False):
+                need_state=True, dgeom_zero: torch.Tensor | None = None, ctx: RasterContext | None = None):
     """Run the forward kernels. means [S,G,3]; feats [S,G,M,3] (use_sh; [S,G,3,M] with
     LAYOUT_SH_CHANNEL_MAJOR) or [S,G,3]; opacities [S,G]; cov6 [S,G,6] (or [S,G,3,3] with
     LAYOUT_COV_FULL); cams [V,44]. Returns (color [V,3,H,W], RasterState).
@@ -650,8 +616,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     kernel (no scan, no second pass over the geometry, no host sync); otherwise the
     two-phase path counts, scans (one 8-byte read-back of N), scatters.
     dgeom_zero: the backward's [V, G, DGEOM_WORDS] int64 accumulator, whose rendered rows
-    the projection kernel zeroes as it writes their records (no separate fill pass);
-    dgeom_clean: it is all zero already (RasterContext.take_clean_dgeom), no fill needed.
+    the projection kernel zeroes as it writes their records (no separate fill pass).
     ctx: the caller's RasterContext (options + adaptive hints; default: the device's)."""
     lib = _lib.load()
     cam_in = cams if isinstance(cams, CameraInputs) else None
@@ -735,7 +700,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             # 3.06 ms, same-box A/B); the depth-cut path below keeps the in-kernel zeroing of the
             # few rows it projects in full
             dz = dgeom_zero
-            if dz is not None and not dgeom_clean:
+            if dz is not None:
                 dz.zero_()
             dgeom_filled = dz is not None
             dz = None
@@ -831,7 +796,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             # no backward: the written heads are sorted and composited in one launch below
             # (dsr_sort_render, flags as dsr_render_fwd); the keys stay unsorted in HBM unless a
             # test asks for the lists (debug_keep_fast_lists)
-            cut_fused = bool(ctx.opt("cut_fused")) and not need_state
+            cut_fused = not need_state
             if not cut_fused:
                 _lib.check(_timed("k_sort", lib.dsr_bin_sort, G, V, H, W, seg_start.data_ptr(), seg_count.data_ptr(),
                                   stride, keys.data_ptr(), scratch.data_ptr(), CUT_SORT_HINT, None, 0, None, None,
@@ -979,10 +944,8 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     dev = means.device
     st = _lib.stream_of(dev)
     dcolor = dcolor.contiguous().float()
-    pool = None
     if state.dgeom is not None:  # rendered rows zeroed by the forward's projection kernel
         dgeom_fx, state.dgeom = state.dgeom, None
-        pool, state.dgeom_pool = state.dgeom_pool, None
     else:
         dgeom_fx = torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev)
     gscale = torch.empty(GRAD_SCALE_BLOCKS, dtype=torch.float32, device=dev)
@@ -1015,10 +978,8 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
         idx.data_ptr(),
         idx[S + 1:].data_ptr(), _ptr(state.row_live), dmeans.data_ptr(), dfeat.data_ptr() if use_sh else None,
         None if use_sh else dfeat.data_ptr(), dopac.data_ptr(), dcov6.data_ptr(),
-        None if dmean2d is None else dmean2d.data_ptr(), layout | (LAYOUT_CONSUME_DGEOM if pool else 0), st),
+        None if dmean2d is None else dmean2d.data_ptr(), layout, st),
         "dsr_preprocess_bwd")
-    if pool is not None:  # all zero again once the launch above has run
-        pool.give_back_clean_dgeom(dgeom_fx, st)
     return dmeans, dfeat, dopac, dcov6, dmean2d, dgeom
 
 
@@ -1030,13 +991,11 @@ class _RasterizeViews(torch.autograd.Function):
         need = any(ctx.needs_input_grad[:5])
         # the backward's accumulator: its rendered rows are zeroed by the projection kernel
         rc = rctx or default_context(means.device)
-        dgeom, clean = rc.take_clean_dgeom(V, means.shape[1], means.device, _lib.stream_of(means.device)) \
-            if need else (None, False)
+        dgeom = torch.empty((V, means.shape[1], DGEOM_WORDS), dtype=torch.int64, device=means.device) \
+            if need else None
         color, state = forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W, layout,
-                                   zeroed_counts, need_state=need, dgeom_zero=dgeom, ctx=rc, dgeom_clean=clean)
+                                   zeroed_counts, need_state=need, dgeom_zero=dgeom, ctx=rc)
         state.dgeom = dgeom
-        # all zero outside the rows the backward reads: the pool's buffer, or the full fill
-        state.dgeom_pool = rc if rc.opt("reuse_dgeom") and (clean or state.dgeom_filled) else None
         ctx.save_for_backward(means, feats, opacities, cov6, state.cams)
         ctx.state = state
         ctx.meta = (view_scene, use_sh, sh_degree, None if means2d is None else means2d.shape, layout)

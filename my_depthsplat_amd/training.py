@@ -38,6 +38,10 @@ class _HeadRows(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, C: int, r: int):
         from . import _lib
+        # the kernel indexes raw pointers by these sizes: a mismatched caller must not reach it
+        if x.dim() != 4 or x.dtype != torch.float32 or x.shape[1] != C * r * r:
+            raise ValueError(f"head_rows: x must be float32 [BV, C r^2 = {C * r * r}, h, w], got "
+                             f"{x.dtype} {tuple(x.shape)}")
         lib = _lib.load()
         _lib.require_gpu(x)
         x = x.contiguous()
@@ -52,7 +56,9 @@ class _HeadRows(torch.autograd.Function):
     def backward(ctx, drows):
         from . import _lib
         BV, C, r, h, w = ctx.dims
-        drows = drows.contiguous()
+        if tuple(drows.shape) != (BV, h * r * w * r, C):
+            raise ValueError(f"head_rows backward: gradient {tuple(drows.shape)} != {(BV, h * r * w * r, C)}")
+        drows = drows.contiguous().float()
         dx = torch.empty((BV, C * r * r, h, w), dtype=torch.float32, device=drows.device)
         _lib.check(_lib.load().dga_head_rows_bwd(BV, C, r, h, w, drows.data_ptr(), dx.data_ptr(),
                                                  _lib.stream_of(drows.device)), "dga_head_rows_bwd")

@@ -53,7 +53,7 @@ def test_load_without_gpu_and_error_channel():
     if not _lib.LIB_PATH.exists():
         pytest.skip("extension not built")
     lib = _lib.load()
-    assert lib.dsplat_abi_version() == 14
+    assert lib.dsplat_abi_version() == 15
     assert lib.dsr_sort_lds_capacity() >= 256
     # argument validation happens before any HIP call -> works on a GPU-less host
     rc = lib.dsr_render_fwd(0, 1, 8, 8, None, None, None, None, 0, None, None, None, None, None, None, None, None)
@@ -91,3 +91,14 @@ def test_head_rows_validation_without_gpu():
     x = ctypes.create_string_buffer(16)
     assert lib.dga_head_rows_bwd(1, 1000, 8, 2, 2, x, x, None) == 1  # 16 * 8 * 1001 * 4 B > 64 KiB
     assert b"LDS tile" in lib.dsplat_last_error()
+
+
+def test_head_rows_rejects_mismatched_shapes_without_gpu():
+    """the head-rows autograd function checks x against (C, r) before any pointer
+    reaches the kernel (wrong channel count, rank or dtype raise ValueError, on any device)."""
+    import pytest
+    import torch
+    from my_depthsplat_amd.training import _HeadRows
+    for x in (torch.zeros(2, 5, 3, 3), torch.zeros(8, 3, 3), torch.zeros(2, 8, 3, 3, dtype=torch.float64)):
+        with pytest.raises(ValueError):
+            _HeadRows.apply(x, 2, 2)
