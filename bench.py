@@ -750,6 +750,8 @@ def _costvol_case(tag, dev, rank):
     from my_depthsplat_amd.matching import depth_candidates
     from my_depthsplat_amd.synthetic import context_cameras
     g = torch.Generator(device=dev).manual_seed(5 + rank)
+    rand_prior = tag.endswith("_rand")
+    tag = tag.removesuffix("_rand")
     if tag in ("config_a_32x32", "config_b_scale0_64x64"):
         BV, J, C, Hc, Wc, D = {"config_a_32x32": (2, 1, 128, 32, 32, 128),
                                "config_b_scale0_64x64": (2, 1, 128, 64, 64, 128)}[tag]
@@ -771,8 +773,15 @@ def _costvol_case(tag, dev, rank):
         K = torch.tensor([[Wc * 1.0, 0, Wc / 2], [0, Hc * 1.0, Hc / 2], [0, 0, 1]], device=dev).expand(BV, J, 3, 3)
         inv_min = torch.full((BV,), 1 / 100.0, device=dev)
         inv_max = torch.full((BV,), 1 / 0.5, device=dev)
-        if scale1:  # per-pixel window around the previous scale's (upsampled) inverse depth
+        if scale1 and rand_prior:  # round-4 form: the prior independent per pixel (worst case for bands)
             prior = inv_min.view(-1, 1, 1, 1) + torch.rand(BV, 1, Hc, Wc, generator=g, device=dev) * 0.5
+        elif scale1:  # per-pixel window around the previous scale's inverse depth, upsampled x2
+            # bilinearly from the scale-0 grid (mv_unimatch.py:436-461 upsamples the coarser
+            # prediction the same way)
+            lo = torch.rand(BV, 1, Hc // 2, Wc // 2, generator=g, device=dev) * 0.5
+            prior = inv_min.view(-1, 1, 1, 1) + torch.nn.functional.interpolate(lo, scale_factor=2, mode="bilinear",
+                                                                                align_corners=True)
+        if scale1:
             depth = 1.0 / depth_candidates(inv_min, inv_max, 128, 1, prior)
         else:
             depth = (1.0 / torch.linspace(1 / 0.5, 1 / 100.0, D, device=dev)).expand(BV, D)
@@ -797,7 +806,8 @@ def costvol_leg(args, dev, rank, world, max_over_ranks):
     from my_depthsplat_amd.matching import plane_sweep_cost_volume
 
     res = {}
-    for tag in ("config_a_32x32", "config_b_scale0_64x64", "config_d_scale0_56x96", "config_d_scale1_112x192"):
+    for tag in ("config_a_32x32", "config_b_scale0_64x64", "config_d_scale0_56x96", "config_d_scale1_112x192",
+                "config_d_scale1_112x192_rand"):
         ref, tgt, K, pose, depth, (BV, J, C, Hc, Wc, D) = _costvol_case(tag, dev, rank)
 
         def call():

@@ -376,26 +376,37 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
  * [B,C,H,W] maps. Larger grids group the reference pixels by the epipolar line they lie on
  * w.r.t. each source view (16 pixels of one line tap a thin band around ONE target line);
  * each group's correlations with its band's distinct target pixels are one GEMM, finished by
- * the 4-tap bilinear gather. Views are summed in launch order (deterministic). Other C: a
- * direct channel-last kernel.
+ * the 4-tap bilinear gather; the band's bitmap and list cover only the bounding box of the
+ * group's taps. Views are summed in launch order (deterministic). Other C: a direct
+ * channel-last kernel.
+ * path: dcv_cost_volume_path(...) for this shape (0 band, 1 epipolar groups, 2 direct; env
+ * DSPLAT_CV_PATH=band / epi overrides it there, for timing tools only). The caller passes the
+ * SAME value to the forward and to the backward (which must know what the forward left in the
+ * workspace); a path the shape cannot take is an error.
  * workspace: dcv_cost_volume_workspace_size bytes (channel-last copies of tgt and ref with a
  * zero padding row per image, and the epipolar groups), filled here (or, after a band-kernel
  * forward, by dcv_cost_volume_bwd itself) and read by dcv_cost_volume_bwd. */
+#define DCV_PATH_BAND 0
+#define DCV_PATH_EPI 1
+#define DCV_PATH_DIRECT 2
+int dcv_cost_volume_path(int B, int J, int C, int H, int W);
 size_t dcv_cost_volume_workspace_size(int B, int J, int C, int H, int W);
-int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel,
+int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, int path,
                         const float* ref, const float* tgt, const float* intr, const float* pose,
                         const float* depth, float clamp_min_depth, void* workspace, float* cost,
                         void* stream);
 
 /* Backward of dcv_cost_volume_fwd w.r.t. both feature maps (geometry gets no grad,
  * matching.py:46). dcost [B,D,H,W] -> dref [B,C,H,W] (overwritten), dtgt [B,J,C,H,W]
- * (overwritten). ref / tgt: the forward's inputs; workspace: the forward's (completed here
- * when the forward ran the band kernel); dcv_cost_volume_bwd_workspace_size bytes of scratch
- * (channel-last gradient accumulators). Reference gradients are summed in a fixed order;
- * target gradients with float atomics (pixels shared between groups: the order of those adds,
- * hence the last bits of dtgt, can change from run to run). */
+ * (overwritten). fwd_path: the forward's path argument; ref / tgt: the forward's inputs;
+ * workspace: the forward's (completed here when the forward ran the band kernel);
+ * dcv_cost_volume_bwd_workspace_size bytes of scratch (channel-last gradient accumulators).
+ * On the matrix-core paths both gradients are bit-identical run to run: reference gradients
+ * are summed in a fixed order, the shared sums (the gradient weights in LDS, the target
+ * gradients in HBM) in integer fixed point (units from the largest |dcost| and |ref|). The
+ * direct kernel (C not a multiple of 16) adds target gradients with float atomics. */
 size_t dcv_cost_volume_bwd_workspace_size(int B, int J, int C, int H, int W);
-int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel,
+int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, int fwd_path,
                         const float* ref, const float* tgt, void* workspace, const float* intr,
                         const float* pose, const float* depth, float clamp_min_depth,
                         const float* dcost, float* dref, float* dtgt, void* bwd_workspace,

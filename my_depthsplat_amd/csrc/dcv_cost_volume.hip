@@ -343,15 +343,27 @@ __device__ __forceinline__ int epi_bucket(const EpiKey& k, float px, float py) {
 // to source coordinates). Finite epipole: lines are buckets of the angle about e, 1 / dmax
 // radians wide (dmax: farthest pixel from e), so neighbouring buckets are <= 1 px apart
 // anywhere in the image; epipole far outside the image (sideways baseline): parallel lines,
-// 1-px buckets of the offset across them; no baseline: rows. Order inside a bucket is the
-// arrival order of an LDS atomic (results do not depend on it: each output is computed
-// from its own correlations, whichever group holds its pixel).
+// 1-px buckets of the offset across them; no baseline: rows. Inside a line (round 5) the
+// pixels are ordered by where their middle depth candidate lands along the target line: each
+// line's key range is cut into ceil(n / 16) segments (about one 16-pixel group each), the
+// pixels are counting-sorted by (line, segment) and, inside a segment, by pixel id. With
+// per-pixel candidate windows (scale > 0) a group's 16 pixels then tap nearby stretches of the
+// line and its band is their windows' union, not the whole line. The order is a function of
+// the inputs only (never of atomic arrival), so the groups, and with them the backward's MFMA
+// blocking and bits, are the same in every run. (Results of the forward do not depend on the
+// grouping at all: each output is computed from its own correlations.)
 // Also writes geom[b, j] = {M = K R K^-1 (row-major), K t} (double, rounded once): the
 // projection of reference pixel p at depth d is M [px, py, 1] d + K t (see epi_ray).
-__global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, const float* __restrict__ intr,
-                                                     const float* __restrict__ pose, int* __restrict__ groups,
+constexpr int kEpiKeyMaxPixels = 24576;  // larger images (pixel id in 15 bits, keys in registers): lines only
+__global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, int D, int depth_per_pixel,
+                                                     const float* __restrict__ intr, const float* __restrict__ pose,
+                                                     const float* __restrict__ depth, int* __restrict__ groups,
                                                      float* __restrict__ geom) {
-  __shared__ uint32_t hist[kEpiBuckets];
+  __shared__ uint32_t hist[kEpiBuckets];  // line counts, then segment-bin counters
+  __shared__ uint32_t bst[kEpiBuckets];   // first segment bin of each line
+  __shared__ uint32_t lmin[kEpiBuckets];  // per line: key minimum (orderable bits), then the bins' starts
+  __shared__ uint32_t lmax[kEpiBuckets];  // per line: key maximum
+  __shared__ float s_geom[12];
   __shared__ uint32_t wsum[16];
   const int b = blockIdx.x, j = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int HW = H * W;
@@ -382,6 +394,7 @@ __global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, const 
         v = k[rr * 3 + 0] * tx + k[rr * 3 + 1] * ty + k[rr * 3 + 2] * tz;
       }
       geom[bj * 12 + tid] = (float)v;
+      s_geom[tid] = (float)v;
     }
     const double cx = -(P[0] * tx + P[4] * ty + P[8] * tz);
     const double cy = -(P[1] * tx + P[5] * ty + P[9] * tz);
@@ -422,17 +435,49 @@ __global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, const 
       key.inv = (float)key.nb / fmaxf(hi - lo + 1.f, 1.f);
     }
   }
-  for (int i = tid; i < kEpiBuckets; i += 1024) hist[i] = 0u;
-  __syncthreads();
-  for (int p = tid; p < HW; p += 1024) atomicAdd(&hist[epi_bucket(key, (float)(p % W), (float)(p / W))], 1u);
-  __syncthreads();
-  // exclusive scan of the buckets (8 per thread)
-  {
+  int* out = groups + bj * HW;
+  // each pixel's sort key: where its middle candidate lands, projected on the direction of its
+  // own near-to-far step (canonically oriented: x > 0, or y > 0 on vertical lines), so the
+  // pixels of one target line, whose directions agree to a fraction of a degree, order along it
+  const float* dp = depth + (size_t)b * D * (depth_per_pixel ? HW : 1);
+  const int dm = D / 2, d1 = D > 1 ? D - 1 : 0;
+  auto target = [&](int p, float d, float& u, float& v) {
+    const float px = (float)(p % W), py = (float)(p / W);
+    const float x = fmaf(fmaf(s_geom[0], px, fmaf(s_geom[1], py, s_geom[2])), d, s_geom[9]);
+    const float y = fmaf(fmaf(s_geom[3], px, fmaf(s_geom[4], py, s_geom[5])), d, s_geom[10]);
+    const float z = fmaxf(fmaf(fmaf(s_geom[6], px, fmaf(s_geom[7], py, s_geom[8])), d, s_geom[11]), 1e-3f);
+    u = x / z;
+    v = y / z;
+  };
+  auto sort_key = [&](int p) -> float {
+    const float dmid = depth_per_pixel ? dp[(size_t)dm * HW + p] : dp[dm];
+    const float dfar = depth_per_pixel ? dp[(size_t)d1 * HW + p] : dp[d1];
+    float u0, v0, u1, v1;
+    target(p, dmid, u0, v0);
+    target(p, dfar, u1, v1);
+    float dx = u1 - u0, dy = v1 - v0;
+    const float l = sqrtf(dx * dx + dy * dy);
+    if (l > 1e-6f && l < 3.0e38f) {
+      dx /= l;
+      dy /= l;
+    } else {
+      dx = 1.f;
+      dy = 0.f;
+    }
+    if (dx < -1e-3f || (!(dx > 1e-3f) && dy < 0.f)) {
+      dx = -dx;
+      dy = -dy;
+    }
+    const float kv = fmaf(u0, dx, v0 * dy);
+    return (kv == kv && fabsf(kv) < 1e30f) ? kv : 1e30f;  // NaN / inf: last
+  };
+  // exclusive scan of 8192 words in place (8 per thread); returns the total
+  auto scan8k = [&](uint32_t* a, uint32_t* copy) -> uint32_t {
     constexpr int PT = kEpiBuckets / 1024;
     uint32_t v[PT], tot = 0;
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
-      v[i] = hist[tid * PT + i];
+      v[i] = a[tid * PT + i];
       tot += v[i];
     }
     const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
@@ -440,15 +485,111 @@ __global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, const 
     __syncthreads();
     uint32_t off = incl - tot;
     for (int k = 0; k < wv; ++k) off += wsum[k];
+    uint32_t total = 0;
+    for (int k = 0; k < 16; ++k) total += wsum[k];
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
-      hist[tid * PT + i] = off;
+      a[tid * PT + i] = off;
+      if (copy) copy[tid * PT + i] = off;
       off += v[i];
     }
+    __syncthreads();
+    return total;
+  };
+  // orderable bits of a float (monotone as unsigned)
+  auto obits = [](float f) -> uint32_t {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  };
+  auto ofloat = [](uint32_t o) -> float { return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o); };
+  // 1) per line: count, key min / max (the keys are kept in registers)
+  constexpr int PER = kEpiKeyMaxPixels / 1024;
+  const bool sorted = HW <= kEpiKeyMaxPixels;  // uniform
+  for (int i = tid; i < kEpiBuckets; i += 1024) {
+    hist[i] = 0u;
+    lmin[i] = 0xFFFFFFFFu;
+    lmax[i] = 0u;
   }
   __syncthreads();
-  int* out = groups + bj * HW;
-  for (int p = tid; p < HW; p += 1024) out[atomicAdd(&hist[epi_bucket(key, (float)(p % W), (float)(p / W))], 1u)] = p;
+  if (!sorted) {  // large images: lines only, arrival order inside them
+    for (int p = tid; p < HW; p += 1024) atomicAdd(&hist[epi_bucket(key, (float)(p % W), (float)(p / W))], 1u);
+    __syncthreads();
+    scan8k(hist, nullptr);
+    for (int p = tid; p < HW; p += 1024) out[atomicAdd(&hist[epi_bucket(key, (float)(p % W), (float)(p / W))], 1u)] = p;
+    return;
+  }
+  // (the line of pixel p is recomputed where needed instead of kept: registers)
+  auto line_of = [&](int p) { return epi_bucket(key, (float)(p % W), (float)(p / W)); };
+  float kv[PER];
+#pragma unroll
+  for (int t = 0; t < PER; ++t) kv[t] = tid + 1024 * t < HW ? sort_key(tid + 1024 * t) : 0.f;
+#pragma unroll
+  for (int t = 0; t < PER; ++t)
+    if (tid + 1024 * t < HW) {
+      const int l = line_of(tid + 1024 * t);
+      atomicAdd(&hist[l], 1u);
+      atomicMin(&lmin[l], obits(kv[t]));
+      atomicMax(&lmax[l], obits(kv[t]));
+    }
+  __syncthreads();
+  // 2) each line cut into ceil(n / 16) segments of its key range (about one 16-pixel group per
+  //    segment); segment bins numbered line by line: bst[line] = the line's first bin
+  for (int i = tid; i < kEpiBuckets; i += 1024) bst[i] = (hist[i] + 15u) / 16u;
+  __syncthreads();
+  const uint32_t nbins = scan8k(bst, nullptr);
+  if (nbins > (uint32_t)kEpiBuckets) {  // (more bins than counters: lines only, as above; uniform)
+    scan8k(hist, nullptr);
+#pragma unroll
+    for (int t = 0; t < PER; ++t)
+      if (tid + 1024 * t < HW) out[atomicAdd(&hist[line_of(tid + 1024 * t)], 1u)] = tid + 1024 * t;
+    return;
+  }
+  int bin[PER];
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    bin[t] = 0;
+    if (tid + 1024 * t < HW) {
+      const int l = line_of(tid + 1024 * t);
+      const uint32_t nseg = (hist[l] + 15u) / 16u;
+      const float lo = ofloat(lmin[l]), hi = ofloat(lmax[l]);
+      const float f = hi > lo ? (kv[t] - lo) / (hi - lo) : 0.f;
+      bin[t] = (int)bst[l] + min((int)nseg - 1, max(0, (int)(f * (float)nseg)));
+    }
+  }
+  __syncthreads();  // hist / bst reads above before they are reused
+  // 3) counting sort by bin (pixel and bin packed into one word: bin << 15 | p)
+  for (int i = tid; i < kEpiBuckets; i += 1024) hist[i] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < PER; ++t)
+    if (tid + 1024 * t < HW) atomicAdd(&hist[bin[t]], 1u);
+  __syncthreads();
+  scan8k(hist, lmin);  // lmin: the bins' starts (hist: their ends after the scatter)
+#pragma unroll
+  for (int t = 0; t < PER; ++t)
+    if (tid + 1024 * t < HW) out[atomicAdd(&hist[bin[t]], 1u)] = (bin[t] << 15) | (tid + 1024 * t);
+  __syncthreads();
+  // 4) inside each bin (~16 pixels) the pixels in id order, so the groups never depend on the
+  //    scatter's arrival order (the backward's MFMA blocking, hence its bits, are the same
+  //    every run)
+  int pv[PER], rk[PER];
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    const int pos = tid + 1024 * t;
+    rk[t] = -1;
+    if (pos < HW) {
+      const int v = out[pos], bn = v >> 15, pp = v & 0x7FFF;
+      const int st = (int)lmin[bn], en = (int)hist[bn];
+      int r = 0;
+      for (int q = st; q < en; ++q) r += (out[q] & 0x7FFF) < pp ? 1 : 0;
+      pv[t] = pp;
+      rk[t] = st + r;
+    }
+  }
+  __syncthreads();  // every read of out[] above before the writes below
+#pragma unroll
+  for (int t = 0; t < PER; ++t)
+    if (rk[t] >= 0) out[rk[t]] = pv[t];
 }
 
 // Shared set-up of the forward and backward group kernels: the workgroup's (b, group) with
@@ -477,7 +618,7 @@ struct EpiLds {
   int* list;        // [kEUMax] image pixel of each band position of the current pass (-1: outside)
   float* corr;      // [EG][kECorr] correlations (forward) / gradient weights (backward)
   float* dacc;      // [EG][C + 4] reference gradients (backward)
-  uint32_t* misc;   // [16]
+  uint32_t* misc;   // [32]: scan partials, totals, the band box
 };
 __host__ __device__ constexpr int epi_words(int H, int W) { return ((W + 2) * (H + 2) + 31) / 32 + 1; }
 __device__ __forceinline__ EpiLds epi_lds(float* p, int C, int NWx, bool bwd) {
@@ -501,7 +642,7 @@ __device__ __forceinline__ EpiLds epi_lds(float* p, int C, int NWx, bool bwd) {
   return L;
 }
 size_t epi_lds_bytes(int C, int H, int W, bool bwd) {
-  return sizeof(float) * ((size_t)EG * (C + 4) * (bwd ? 2 : 1) + EG * kECorr + kEUMax + 4 * epi_words(H, W) + 1 + 16);
+  return sizeof(float) * ((size_t)EG * (C + 4) * (bwd ? 2 : 1) + EG * kECorr + kEUMax + 4 * epi_words(H, W) + 1 + 32);
 }
 
 // The group's reference tile [EG][C] into LDS from the channel-last copy (rows of 16-byte
@@ -542,8 +683,9 @@ __device__ __forceinline__ EpiRay epi_ray(const float* __restrict__ gm, float px
   return r;
 }
 // Sample position (grid_sample's unnormalised coordinates = the projected pixel, align_corners
-// = True); the extended-grid index of its top-left tap, or -1 when no tap is inside the image.
-// 1 / z is the hardware reciprocal (1 ulp; the parity bar is 1e-4).
+// = True) and its top-left tap (tx0, ty0) in [-1, W - 1] x [-1, H - 1] packed as
+// (ty0 + 1) << 16 | (tx0 + 1), or -1 when no tap is inside the image. 1 / z is the hardware
+// reciprocal (1 ulp; the parity bar is 1e-4).
 __device__ __forceinline__ int epi_sample(const EpiRay& ry, float dep, float clampz, int H, int W, float& ix,
                                           float& iy) {
   const float xx = fmaf(ry.ax, dep, ry.bx), yy = fmaf(ry.ay, dep, ry.by);
@@ -552,19 +694,76 @@ __device__ __forceinline__ int epi_sample(const EpiRay& ry, float dep, float cla
   ix = xx * rz;
   iy = yy * rz;
   if (!(ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H)) return -1;  // also NaN
-  const int tx0 = (int)floorf(ix), ty0 = (int)floorf(iy);  // in [-1, W - 1] x [-1, H - 1]
-  return ty0 * (W + 2) + tx0 + (W + 3);
+  const int tx0 = (int)floorf(ix), ty0 = (int)floorf(iy);
+  return ((ty0 + 1) << 16) | (tx0 + 1);
 }
 
-// Front half shared by the forward and the backward, in three steps:
-//   epi_depths  the samples' depth candidates (global loads, issued early: their latency runs
-//               under the reference tile load in the forward);
-//   epi_taps    the samples' top-left taps into the base bitmap (LDS atomics; base must have
-//               been cleared before the last barrier);
-//   epi_band    after a barrier: the tapped set (base | shifted copies) of each thread's own
-//               contiguous run of words, its popcount prefix (wave scans) and the non-zero
-//               words; returns U (band positions). Two barriers.
-// es[s]: extended index of sample s's top-left tap (-1: zero sample).
+// The band box (round 5): the bitmap, its word pass and the band list cover only the bounding
+// box of the group's top-left taps (+1 column and row for the other three taps), not the whole
+// (W + 2) x (H + 2) extended image: at config-D scale 1 a group's 16 x 32 per-pixel samples tap a
+// few short segments (tens to a few hundred positions) while the image has 22 K, and the
+// per-word band set-up was the workgroup's largest fixed cost. Local index of top-left tap
+// (tx0, ty0): (ty0 - y0) wb + (tx0 - x0); taps e, e + 1, e + wb, e + wb + 1.
+struct EpiBox {
+  int x0, y0, wb, nw;  // box origin (extended-grid coordinates, i.e. + 1), row width, bitmap words
+};
+// Block-wide box of the packed taps es[] (all threads; one barrier). Empty box: nw = 0.
+template <int SPT>
+__device__ __forceinline__ EpiBox epi_box(const EpiLds& L, const int (&es)[SPT]) {
+  int mnx = 1 << 30, mny = 1 << 30, mxx = -1, mxy = -1;
+#pragma unroll
+  for (int s = 0; s < SPT; ++s)
+    if (es[s] >= 0) {
+      const int x = es[s] & 0xFFFF, y = es[s] >> 16;
+      mnx = min(mnx, x);
+      mny = min(mny, y);
+      mxx = max(mxx, x);
+      mxy = max(mxy, y);
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mnx = min(mnx, __shfl_xor(mnx, off, 64));
+    mny = min(mny, __shfl_xor(mny, off, 64));
+    mxx = max(mxx, __shfl_xor(mxx, off, 64));
+    mxy = max(mxy, __shfl_xor(mxy, off, 64));
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    L.misc[16 + 4 * wv] = (uint32_t)mnx;
+    L.misc[17 + 4 * wv] = (uint32_t)mny;
+    L.misc[18 + 4 * wv] = (uint32_t)mxx;
+    L.misc[19 + 4 * wv] = (uint32_t)mxy;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    mnx = min(mnx, (int)L.misc[16 + 4 * k]);
+    mny = min(mny, (int)L.misc[17 + 4 * k]);
+    mxx = max(mxx, (int)L.misc[18 + 4 * k]);
+    mxy = max(mxy, (int)L.misc[19 + 4 * k]);
+  }
+  EpiBox bx;
+  bx.x0 = mnx;
+  bx.y0 = mny;
+  bx.wb = mxx - mnx + 2;
+  bx.nw = mxx < 0 ? 0 : ((mxx - mnx + 2) * (mxy - mny + 2) + 31) / 32 + 1;
+  return bx;
+}
+__device__ __forceinline__ int epi_local(const EpiBox& bx, int es) {
+  return es < 0 ? -1 : ((es >> 16) - bx.y0) * bx.wb + ((es & 0xFFFF) - bx.x0);
+}
+
+// Front half shared by the forward and the backward:
+//   epi_depths   the samples' depth candidates (global loads, issued early: their latency runs
+//                under the reference tile load in the forward);
+//   epi_taps     the samples' packed top-left taps (registers);
+//   epi_box      (one barrier) their bounding box;
+//   epi_mark     the taps into the box's base bitmap (LDS atomics; the bitmap's words must be
+//                zero: cleared before the box's barrier);
+//   epi_band     after a barrier: the tapped set (base | shifted copies) of each thread's own
+//                contiguous run of words, its popcount prefix (wave scans) and the non-zero
+//                words; returns U (band positions). Two barriers.
+// es[s]: local index of sample s's top-left tap (-1: zero sample).
 template <int SPT>
 __device__ __forceinline__ void epi_depths(int HW, int D, int depth_per_pixel, int b, int d0, int pix,
                                            const float* __restrict__ depth, float (&dep)[SPT]) {
@@ -575,7 +774,7 @@ __device__ __forceinline__ void epi_depths(int HW, int D, int depth_per_pixel, i
   for (int s = 0; s < SPT; ++s) dep[s] = dp[(uint32_t)(min(d0 + dl + 16 * s, D - 1) * dstride + pc)];
 }
 template <int SPT>
-__device__ __forceinline__ void epi_taps(const EpiLds& L, int H, int W, int D, int d0, int pix, const EpiRay& ry,
+__device__ __forceinline__ void epi_taps(int H, int W, int D, int d0, int pix, const EpiRay& ry,
                                          const float (&dep)[SPT], float clampz, float (&sx)[SPT], float (&sy)[SPT],
                                          int (&es)[SPT]) {
   const int dl = threadIdx.x >> 4;
@@ -584,13 +783,20 @@ __device__ __forceinline__ void epi_taps(const EpiLds& L, int H, int W, int D, i
     const int d = d0 + dl + 16 * s;
     es[s] = epi_sample(ry, dep[s], clampz, H, W, sx[s], sy[s]);
     if (pix < 0 || d >= D) es[s] = -1;
+  }
+}
+template <int SPT>
+__device__ __forceinline__ void epi_mark(const EpiLds& L, const EpiBox& bx, int (&es)[SPT]) {
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) {
+    es[s] = epi_local(bx, es[s]);
     if (es[s] >= 0) atomicOr(&L.base[es[s] >> 5], 1u << (es[s] & 31));
   }
 }
-__device__ __forceinline__ int epi_band(const EpiLds& L, int H, int W) {
+__device__ __forceinline__ int epi_band(const EpiLds& L, const EpiBox& bx) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int Wx = W + 2, NWx = epi_words(H, W);
-  // tapped = base | base << 1 | base << Wx | base << (Wx + 1) (bit shifts across the words)
+  const int wb = bx.wb, NWx = bx.nw;
+  // tapped = base | base << 1 | base << wb | base << (wb + 1) (bit shifts across the words)
   auto shl = [&](int w, int sft) -> uint32_t {
     const int wo = sft >> 5, bo = sft & 31;
     const uint32_t lo = w - wo >= 0 ? L.base[w - wo] : 0u;
@@ -604,7 +810,7 @@ __device__ __forceinline__ int epi_band(const EpiLds& L, int H, int W) {
   const int w0 = tid * per, w1 = min(NWx, w0 + per);
   uint32_t tot = 0, nz = 0;
   for (int w = w0; w < w1; ++w) {
-    const uint32_t bits = shl(w, 0) | shl(w, 1) | shl(w, Wx) | shl(w, Wx + 1);
+    const uint32_t bits = shl(w, 0) | shl(w, 1) | shl(w, wb) | shl(w, wb + 1);
     L.wb[w].x = bits;
     const uint32_t c = __popc(bits);
     tot += c;
@@ -634,21 +840,26 @@ __device__ __forceinline__ int epi_band(const EpiLds& L, int H, int W) {
   __syncthreads();
   return (int)L.misc[4];
 }
-__device__ __forceinline__ void epi_clear_base(const EpiLds& L, int H, int W) {
-  for (int w = threadIdx.x, NWx = epi_words(H, W); w < NWx; w += 256) L.base[w] = 0u;
+// clear the words of a box (or, before the first one, of the whole extended image)
+__device__ __forceinline__ void epi_clear_words(const EpiLds& L, int nw) {
+  for (int w = threadIdx.x; w < nw; w += 256) L.base[w] = 0u;
 }
-// the three steps with their own clear + barrier (the backward's per-depth-chunk loop)
+// the steps for one depth chunk with their own barriers (the backward's per-chunk loop); the
+// base words of the previous chunk's box (nw_prev, the whole image before the first) are
+// cleared before the box barrier
 template <int SPT>
 __device__ __forceinline__ int epi_front(const EpiLds& L, int H, int W, int HW, int D, int depth_per_pixel, int b,
                                          int d0, int pix, const EpiRay& ry, const float* __restrict__ depth,
-                                         float clampz, float (&sx)[SPT], float (&sy)[SPT], int (&es)[SPT]) {
+                                         float clampz, float (&sx)[SPT], float (&sy)[SPT], int (&es)[SPT],
+                                         EpiBox& bx, int nw_prev) {
   float dep[SPT];
   epi_depths<SPT>(HW, D, depth_per_pixel, b, d0, pix, depth, dep);
-  epi_clear_base(L, H, W);
+  epi_taps<SPT>(H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
+  epi_clear_words(L, nw_prev);
+  bx = epi_box<SPT>(L, es);
+  epi_mark<SPT>(L, bx, es);
   __syncthreads();
-  epi_taps<SPT>(L, H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
-  __syncthreads();
-  return epi_band(L, H, W);
+  return bx.nw ? epi_band(L, bx) : 0;
 }
 
 // list[] = the target row of band ranks [r0, r0 + n): the image pixel, or HW (the all-zero
@@ -656,10 +867,10 @@ __device__ __forceinline__ int epi_front(const EpiLds& L, int H, int W, int HW, 
 // [n, round_up(n, kEPad)) past the band. 32 lanes per non-zero word, one bit each.
 constexpr int kEPad = 32;
 __device__ __forceinline__ int epi_padded(int n) { return (n + kEPad - 1) / kEPad * kEPad; }
-__device__ __forceinline__ void epi_list(const EpiLds& L, int H, int W, int r0, int n) {
-  const int Wx = W + 2, nnz = (int)L.misc[5], bit = threadIdx.x & 31, HW = H * W;
+__device__ __forceinline__ void epi_list(const EpiLds& L, int H, int W, const EpiBox& bx, int r0, int n) {
+  const int wb = bx.wb, nnz = (int)L.misc[5], bit = threadIdx.x & 31, HW = H * W;
   if ((int)threadIdx.x < epi_padded(n) - n) L.list[n + threadIdx.x] = HW;
-  const float rWx = 1.0f / (float)Wx;
+  const float rwb = 1.0f / (float)wb;
   for (int k = threadIdx.x >> 5; k < nnz; k += 8) {
     const int w = L.nzw[k];
     const uint2 wv2 = L.wb[w];
@@ -668,15 +879,15 @@ __device__ __forceinline__ void epi_list(const EpiLds& L, int H, int W, int r0, 
     const int r = (int)(wv2.y + __popc(bits & ((1u << bit) - 1u)));
     if (r < r0 || r >= r0 + n) continue;
     const int e = w * 32 + bit;
-    int ye = (int)((float)e * rWx), xe = e - ye * Wx;  // the float quotient is within 1 of e / Wx
+    int ye = (int)((float)e * rwb), xe = e - ye * wb;  // the float quotient is within 1 of e / wb
     if (xe < 0) {
       --ye;
-      xe += Wx;
-    } else if (xe >= Wx) {
+      xe += wb;
+    } else if (xe >= wb) {
       ++ye;
-      xe -= Wx;
+      xe -= wb;
     }
-    const int x = xe - 1, y = ye - 1;
+    const int x = bx.x0 + xe - 1, y = bx.y0 + ye - 1;  // box origin is in extended (+1) coordinates
     L.list[r - r0] = (x >= 0 && x < W && y >= 0 && y < H) ? y * W + x : HW;
   }
 }
@@ -697,7 +908,7 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
                                                   float clampz, float scale, float* __restrict__ cost) {
   constexpr int C = 4 * NK;
   extern __shared__ __attribute__((aligned(16))) float cv_lds[];
-  const int HW = H * W, ngroups = (HW + EG - 1) / EG, Wx = W + 2;
+  const int HW = H * W, ngroups = (HW + EG - 1) / EG;
   int b, g;
   if (!epi_item(B, ngroups, b, g)) return;
   const EpiLds L = epi_lds(cv_lds, C, epi_words(H, W), false);
@@ -706,10 +917,10 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
   const size_t bj = (size_t)b * J + j;
   __shared__ int s_gid[EG];
   if (tid < EG) s_gid[tid] = g * EG + tid < HW ? groups[bj * HW + g * EG + tid] : -1;
-  epi_clear_base(L, H, W);
+  epi_clear_words(L, epi_words(H, W));
   __syncthreads();
   // depth loads, then the reference tile's loads, all in flight together; the taps go into the
-  // base bitmap while the tile's LDS stores drain, and one barrier covers both
+  // base bitmap of their box while the tile's LDS stores drain, and one barrier covers both
   const int pix = s_gid[i];  // -1: past the last pixel
   float dep[SPT];
   epi_depths<SPT>(HW, D, depth_per_pixel, b, d0, pix, depth, dep);
@@ -717,9 +928,12 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
   const EpiRay ry = epi_ray(geom + bj * 12, pix >= 0 ? (float)(pix % W) : 0.f, pix >= 0 ? (float)(pix / W) : 0.f);
   float sx[SPT], sy[SPT];
   int es[SPT];
-  epi_taps<SPT>(L, H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
+  epi_taps<SPT>(H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
+  const EpiBox bx = epi_box<SPT>(L, es);
+  epi_mark<SPT>(L, bx, es);
   __syncthreads();
-  const int U = epi_band(L, H, W);
+  const int U = bx.nw ? epi_band(L, bx) : 0;
+  const int Wx = bx.wb;
   // per sample: sum over its taps of grid_sample's weight x correlation, taps in a fixed order
   // (a band of more than kEUMax positions takes several passes, each adding its taps)
   float* cb = cost + (size_t)b * D * HW;  // this scene's cost volume (< 2^32 elements)
@@ -735,7 +949,7 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
   const float* tg = tgt_hwc + bj * (size_t)(HW + 1) * C;
   for (int r0 = 0; r0 < U; r0 += kEUMax) {
     const int n = min(kEUMax, U - r0);
-    epi_list(L, H, W, r0, n);
+    epi_list(L, H, W, bx, r0, n);
     __syncthreads();
     // corr[16 x n] = aref[16 x C] . tgt[n x C]^T; per 16-channel step lane l feeds channels
     // cb + 4 (l >> 4) + s to MFMA s (A and B permuted alike). The C / 16 row loads of a
@@ -809,12 +1023,68 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
   }
 }
 
+// Deterministic sums of the backward (round 5). Float atomics make a sum depend on the order in
+// which the adds arrive, so the gradients differed run to run in the last bits. Both sums that
+// several writers share are now integer (fixed point), whose result does not depend on order:
+//   * G[p][u] (LDS): each add is dcost * scale * w rounded to units of 2^(kg - 23), kg the
+//     exponent of the largest |dcost * scale| of the workgroup's depth chunk; an element takes at
+//     most 16 SPT <= 128 adds of <= 2^23 units, so int32 never overflows;
+//   * dtgt (HBM): each workgroup's MFMA partial G^T aref (a fixed-order float) rounded to units
+//     of 2^(kt - 40), 2^kt bounding one partial (16 x 16 SPT x max|dcost scale| x max|ref|, from
+//     the per-block maxima of k_cv_absmax, the same in every workgroup), added as int64: 2^23
+//     partials of the bound fit. k_fx_to_chw converts the sum back to float while transposing.
+// dref needs none of this: each element has one writer (its pixel's group, views in launch order).
+constexpr int kCvMaxBlocks = 256;
+__global__ __launch_bounds__(256) void k_cv_absmax(size_t n1, const float* __restrict__ a1, size_t n2,
+                                                   const float* __restrict__ a2, float* __restrict__ out) {
+  float m1 = 0.f, m2 = 0.f;
+  const size_t stride = (size_t)256 * gridDim.x;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n1; i += stride) m1 = fmaxf(m1, fabsf(a1[i]));
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += stride) m2 = fmaxf(m2, fabsf(a2[i]));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
+    m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
+  }
+  __shared__ float s1[4], s2[4];
+  if ((threadIdx.x & 63) == 0) {
+    s1[threadIdx.x >> 6] = m1;
+    s2[threadIdx.x >> 6] = m2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[blockIdx.x] = fmaxf(fmaxf(s1[0], s1[1]), fmaxf(s1[2], s1[3]));
+    out[kCvMaxBlocks + blockIdx.x] = fmaxf(fmaxf(s2[0], s2[1]), fmaxf(s2[2], s2[3]));
+  }
+}
+// the dtgt unit 2^(kt - 40) from the per-block maxima (every caller reads the same values; a
+// non-finite maximum gives a unit of 0: the sums stay 0 and the conversion yields NaN below)
+__device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, float scale, int spt) {
+  const int lane = threadIdx.x & 63;
+  float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < kCvMaxBlocks / 64; ++k) {
+    m1 = fmaxf(m1, bm[k * 64 + lane]);
+    m2 = fmaxf(m2, bm[kCvMaxBlocks + k * 64 + lane]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
+    m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
+  }
+  const float bound = 256.f * (float)spt * m1 * scale * m2;
+  if (!(bound <= 3.0e38f)) return 0.f;
+  int e = 0;
+  frexpf(bound, &e);  // bound < 2^e
+  return ldexpf(1.f, max(e, -80) - 40);
+}
+
 // Backward, view j (grid.x as the forward; depth chunks looped inside): per group the gradient
-// weights G[p][u] = sum over its samples' taps of dcost * scale * w (LDS), then
+// weights G[p][u] = sum over its samples' taps of dcost * scale * w (LDS, fixed point), then
 // dref[p] += G[p, :] . tgt[band]  (MFMA, K = band) and dtgt[band] += G^T . aref  (MFMA,
-// K = 16 pixels; global float atomics: target pixels are shared between groups, so their
-// gradients arrive in any order). dref_hwc [B][HW][C] is written (view 0) or added to (views
-// after it, in launch order): each pixel is in exactly one group per view.
+// K = 16 pixels; target pixels are shared between groups: int64 fixed-point atomics).
+// dref_hwc [B][HW][C] is written (view 0) or added to (views after it, in launch order): each
+// pixel is in exactly one group per view. cvmax: k_cv_absmax's per-block maxima (dcost, ref).
 template <int NK, int SPT>
 __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
                                                       int accumulate, const float* __restrict__ ref_hwc,
@@ -822,17 +1092,21 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
                                                       const int* __restrict__ groups, const float* __restrict__ geom,
                                                       const float* __restrict__ depth,
                                                       float clampz, float scale, const float* __restrict__ dcost,
-                                                      float* __restrict__ dref_hwc, float* __restrict__ dtgt_hwc) {
+                                                      const float* __restrict__ cvmax,
+                                                      float* __restrict__ dref_hwc, long long* __restrict__ dtgt_fx) {
   constexpr int C = 4 * NK;
   extern __shared__ __attribute__((aligned(16))) float cv_lds[];
-  const int HW = H * W, ngroups = (HW + EG - 1) / EG, Wx = W + 2;
+  const int HW = H * W, ngroups = (HW + EG - 1) / EG;
   int b, g;
   if (!epi_item(B, ngroups, b, g)) return;
   const EpiLds L = epi_lds(cv_lds, C, epi_words(H, W), true);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int i = tid & (EG - 1), dl = tid >> 4;
   const size_t bj = (size_t)b * J + j;
+  const float unit_t = cv_dtgt_unit(cvmax, scale, SPT);
+  const float unit_t_inv = unit_t > 0.f ? 1.f / unit_t : 0.f;  // exact: a power of 2
   __shared__ int s_gid[EG];
+  __shared__ float s_gmax[4];
   if (tid < EG) s_gid[tid] = g * EG + tid < HW ? groups[bj * HW + g * EG + tid] : -1;
   for (int k = tid; k < EG * (C + 4); k += 256) L.dacc[k] = 0.f;
   __syncthreads();
@@ -840,7 +1114,9 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
   const int pix = s_gid[i];
   const EpiRay ry = epi_ray(geom + bj * 12, pix >= 0 ? (float)(pix % W) : 0.f, pix >= 0 ? (float)(pix / W) : 0.f);
   const float* tg = tgt_hwc + bj * (size_t)(HW + 1) * C;
-  float* dtg = dtgt_hwc + bj * (size_t)(HW + 1) * C;
+  long long* dtg = dtgt_fx + bj * (size_t)(HW + 1) * C;
+  int* gi = reinterpret_cast<int*>(L.corr);  // G in fixed point
+  int nw_prev = epi_words(H, W);
   for (int d0 = 0; d0 < D; d0 += 16 * SPT) {  // depth chunks in turn: dacc is this workgroup's alone
     float gs[SPT];
     {
@@ -850,14 +1126,31 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
     }
     float sx[SPT], sy[SPT];
     int es[SPT];
-    const int U = epi_front<SPT>(L, H, W, HW, D, depth_per_pixel, b, d0, pix, ry, depth, clampz, sx, sy, es);
+    EpiBox bx;
+    const int U = epi_front<SPT>(L, H, W, HW, D, depth_per_pixel, b, d0, pix, ry, depth, clampz, sx, sy, es, bx,
+                                 nw_prev);
+    nw_prev = bx.nw;
+    const int Wx = bx.wb;
+    // the chunk's fixed-point unit: 2^(kg - 23), |dcost scale| <= 2^kg over its samples
+    float gm = 0.f;
 #pragma unroll
-    for (int s = 0; s < SPT; ++s) gs[s] = es[s] >= 0 ? gs[s] * scale : 0.f;
+    for (int s = 0; s < SPT; ++s) {
+      gs[s] = es[s] >= 0 ? gs[s] * scale : 0.f;
+      gm = fmaxf(gm, fabsf(gs[s]));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) gm = fmaxf(gm, __shfl_xor(gm, off, 64));
+    if (lane == 0) s_gmax[wv] = gm;
     for (int r0 = 0; r0 < U; r0 += kEUMax) {
       const int n = min(kEUMax, U - r0), np = epi_padded(n);
-      for (int k = tid; k < EG * np; k += 256) L.corr[(k & (EG - 1)) * kECorr + (k >> 4)] = 0.f;
-      epi_list(L, H, W, r0, n);
+      for (int k = tid; k < EG * np; k += 256) gi[(k & (EG - 1)) * kECorr + (k >> 4)] = 0;
+      epi_list(L, H, W, bx, r0, n);
       __syncthreads();
+      gm = fmaxf(fmaxf(s_gmax[0], s_gmax[1]), fmaxf(s_gmax[2], s_gmax[3]));
+      int ke = 0;
+      frexpf(gm, &ke);
+      const float unit_g = (gm > 0.f && gm <= 3.0e38f) ? ldexpf(1.f, max(ke, -100) - 23) : 0.f;
+      const float unit_g_inv = unit_g > 0.f ? 1.f / unit_g : 0.f;
 #pragma unroll
       for (int s = 0; s < SPT; ++s) {
         if (gs[s] == 0.f) continue;
@@ -867,11 +1160,12 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
         const float fx0 = floorf(x), fy0 = floorf(y);
         const float wx0 = (fx0 + 1.f) - x, wx1 = x - fx0, wy0 = (fy0 + 1.f) - y, wy1 = y - fy0;
         const int ra = epi_rank(L, e) - r0, rb = epi_rank(L, e + Wx) - r0;
-        float* grow = L.corr + i * kECorr;
-        if (ra >= 0 && ra < n) atomicAdd(&grow[ra], gs[s] * (wx0 * wy0));
-        if (ra + 1 >= 0 && ra + 1 < n) atomicAdd(&grow[ra + 1], gs[s] * (wx1 * wy0));
-        if (rb >= 0 && rb < n) atomicAdd(&grow[rb], gs[s] * (wx0 * wy1));
-        if (rb + 1 >= 0 && rb + 1 < n) atomicAdd(&grow[rb + 1], gs[s] * (wx1 * wy1));
+        int* grow = gi + i * kECorr;
+        const float gu = gs[s] * unit_g_inv;
+        if (ra >= 0 && ra < n) atomicAdd(&grow[ra], (int)rintf(gu * (wx0 * wy0)));
+        if (ra + 1 >= 0 && ra + 1 < n) atomicAdd(&grow[ra + 1], (int)rintf(gu * (wx1 * wy0)));
+        if (rb >= 0 && rb < n) atomicAdd(&grow[rb], (int)rintf(gu * (wx0 * wy1)));
+        if (rb + 1 >= 0 && rb + 1 < n) atomicAdd(&grow[rb + 1], (int)rintf(gu * (wx1 * wy1)));
       }
       __syncthreads();
       // dref[16 x C] += G[16 x np] . tgt[np x C]: wave wv owns channel blocks wv, wv + 4, ...
@@ -886,7 +1180,7 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
           for (int t = 0; t < kEPad / 4; ++t) {
             const int u = u0 + 4 * t + (lane >> 4);
             bv[t] = tcol[(size_t)L.list[u] * C];
-            av[t] = L.corr[(lane & 15) * kECorr + u];
+            av[t] = (float)gi[(lane & 15) * kECorr + u] * unit_g;
           }
 #pragma unroll
           for (int t = 0; t < kEPad / 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], acc, 0, 0, 0);
@@ -902,17 +1196,23 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
 #pragma unroll
         for (int k0 = 0; k0 < EG; k0 += 4) {
           const int u = ub * 16 + (lane & 15), p = k0 + (lane >> 4);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(L.corr[p * kECorr + u], L.aref[p * (C + 4) + cbk * 16 + (lane & 15)],
-                                                     acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[p * kECorr + u] * unit_g,
+                                                     L.aref[p * (C + 4) + cbk * 16 + (lane & 15)], acc, 0, 0, 0);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = L.list[ub * 16 + 4 * (lane >> 4) + r];
-          if (q < HW && acc[r] != 0.f) atomicAdd(&dtg[(size_t)q * C + cbk * 16 + (lane & 15)], acc[r]);
+          if (q < HW && acc[r] != 0.f) {
+            const long long v = (long long)rintf(fminf(fmaxf(acc[r] * unit_t_inv, -4.0e18f), 4.0e18f));
+            if (v != 0ll)
+              atomicAdd(reinterpret_cast<unsigned long long*>(&dtg[(size_t)q * C + cbk * 16 + (lane & 15)]),
+                        (unsigned long long)v);
+          }
         }
       }
       __syncthreads();  // corr / list / dacc rows reused by the next pass
     }
+    if (U == 0) __syncthreads();  // s_gmax of this chunk read by every wave before the next writes it
   }
   // the group's reference-gradient rows, channel-last (16-byte vectors)
   for (int k = tid; k < EG * C / 4; k += 256) {
@@ -926,6 +1226,33 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
     } else {
       *o = v;
     }
+  }
+}
+
+// [n][rows][C] int64 fixed point (the first HW rows) -> [n][C][HW] float, times the unit of
+// k_cost_epi_bwd (cv_dtgt_unit, recomputed from the same maxima)
+__global__ __launch_bounds__(256) void k_fx_to_chw(int C, int HW, int rows, const long long* __restrict__ src,
+                                                   const float* __restrict__ cvmax, float scale, int spt,
+                                                   float* __restrict__ dst) {
+  __shared__ float tile[64][65];
+  const float unit = cv_dtgt_unit(cvmax, scale, spt);
+  const bool ok = unit > 0.f;
+  const int bj = blockIdx.z;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const long long* s = src + (size_t)bj * rows * C;
+  float* d = dst + (size_t)bj * C * HW;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int p = p0 + r, c = c0 + tx;
+    const long long q = (p < HW && c < C) ? s[(size_t)p * C + c] : 0ll;
+    const int hi = (int)(q >> 32);
+    const unsigned lo = (unsigned)(q & 0xffffffffll);
+    tile[r][tx] = ok ? fmaf((float)hi, 4294967296.0f * unit, (float)lo * unit) : __builtin_nanf("");
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, p = p0 + tx;
+    if (c < C && p < HW) d[(size_t)c * HW + p] = tile[tx][r];
   }
 }
 
@@ -1274,10 +1601,12 @@ size_t dcv_cost_volume_workspace_size(int B, int J, int C, int H, int W) {
   return ((size_t)B * J * rows * C + (size_t)B * rows * C + (size_t)B * J * 12) * sizeof(float) +
          (size_t)B * J * H * W * sizeof(int32_t);
 }
-// backward workspace: dtgt_hwc [B][J][HW + 1][C] | dref_hwc [B][HW][C]
+// backward workspace: dtgt [B][J][HW + 1][C] (int64 fixed point on the matrix-core path, float
+// on the direct one) | dref_hwc [B][HW][C] float | per-block maxima of |dcost| and |ref|
 size_t dcv_cost_volume_bwd_workspace_size(int B, int J, int C, int H, int W) {
   if (B <= 0 || J <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
-  return ((size_t)B * J * ((size_t)H * W + 1) * C + (size_t)B * H * W * C) * sizeof(float);
+  return (size_t)B * J * ((size_t)H * W + 1) * C * sizeof(long long) + (size_t)B * H * W * C * sizeof(float) +
+         2 * kCvMaxBlocks * sizeof(float);
 }
 
 static bool epi_path(int C, int H, int W, bool bwd) {
@@ -1289,24 +1618,19 @@ static bool epi_path(int C, int H, int W, bool bwd) {
 // epipolar group per workgroup leaves a small grid's workgroups short of work (round 3: config A
 // 16.4 -> 27.5 us, config B scale 0 25.6 -> 38.5 us when every shape took it). Large grids
 // (config D's rig, diagonal epipolar lines whose row-segment boxes overflow kBandMax) keep
-// the epipolar groups. DSPLAT_CV_PATH=band / epi overrides the choice (A/B timing tools).
+// the epipolar groups. DSPLAT_CV_PATH=band / epi overrides the choice (A/B timing tools); the
+// caller asks once per forward and hands the answer to both calls (the backward
+// used to re-read the variable and could disagree with its forward).
 constexpr long kBandMaxPixels = 32768;  // B * H * W
-static bool band_fwd(int B, int C, int H, int W) {
-  if (!(C == 16 || C == 32 || C == 64 || C == 128)) return false;
-  if (const char* f = getenv("DSPLAT_CV_PATH")) {
-    if (!strcmp(f, "band")) return true;
-    if (!strcmp(f, "epi")) return false;
-  }
-  return (long)B * H * W <= kBandMaxPixels;
-}
+static bool band_ok(int C) { return C == 16 || C == 32 || C == 64 || C == 128; }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // Channel-last copies (+ the epipolar groups when the epipolar kernels run): the forward's
 // set-up on the epipolar / generic paths, and the backward's when the forward took the band
 // kernel (which needs none of it).
-static int epi_setup(int B, int J, int C, int H, int W, const float* ref, const float* tgt, const float* intr,
-                     const float* pose, void* workspace, hipStream_t st) {
+static int epi_setup(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref, const float* tgt,
+                     const float* intr, const float* pose, const float* depth, void* workspace, hipStream_t st) {
   const int HW = H * W;
   float* tgt_hwc = static_cast<float*>(workspace);
   float* ref_hwc = tgt_hwc + (size_t)B * J * (HW + 1) * C;
@@ -1329,18 +1653,34 @@ static int epi_setup(int B, int J, int C, int H, int W, const float* ref, const 
     }
   }
   if (!epi) return 0;
-  k_epi_groups<<<dim3(B, J), 1024, 0, st>>>(J, H, W, intr, pose, groups, geom);
+  k_epi_groups<<<dim3(B, J), 1024, 0, st>>>(J, H, W, D, depth_per_pixel, intr, pose, depth, groups, geom);
   return dsplat::check_launch("k_epi_groups");
 }
 
-int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref,
+int dcv_cost_volume_path(int B, int J, int C, int H, int W) {
+  if (B <= 0 || J <= 0 || C <= 0 || H <= 1 || W <= 1) return -1;
+  if (const char* f = getenv("DSPLAT_CV_PATH")) {
+    if (!strcmp(f, "band") && band_ok(C)) return DCV_PATH_BAND;
+    if (!strcmp(f, "epi") && epi_path(C, H, W, false)) return DCV_PATH_EPI;
+  }
+  if (band_ok(C) && (long)B * H * W <= kBandMaxPixels) return DCV_PATH_BAND;
+  return epi_path(C, H, W, false) ? DCV_PATH_EPI : DCV_PATH_DIRECT;
+}
+
+static bool path_ok(int path, int C, int H, int W) {
+  return path == DCV_PATH_DIRECT || (path == DCV_PATH_BAND && band_ok(C)) ||
+         (path == DCV_PATH_EPI && epi_path(C, H, W, false));
+}
+
+int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, int path, const float* ref,
                         const float* tgt, const float* intr, const float* pose, const float* depth,
                         float clamp_min_depth, void* workspace, float* cost, void* stream) {
   DSPLAT_REQUIRE(B > 0 && J > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_cost_volume_fwd: bad sizes B=%d J=%d C=%d H=%d W=%d D=%d", B, J, C, H, W, D);
   DSPLAT_REQUIRE(ref && tgt && intr && pose && depth && workspace && cost, "dcv_cost_volume_fwd: null pointer");
+  DSPLAT_REQUIRE(path_ok(path, C, H, W), "dcv_cost_volume_fwd: path %d not available for C=%d H=%d W=%d", path, C, H, W);
   hipStream_t st = (hipStream_t)stream;
   const int HW = H * W;
-  if (band_fwd(B, C, H, W)) {
+  if (path == DCV_PATH_BAND) {
     const size_t lds = cost_band_lds_bytes();
 #define DCV_BAND(NK)                                                                                              \
   do {                                                                                                            \
@@ -1359,13 +1699,13 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
 #undef DCV_BAND
     return dsplat::check_launch("k_cost_band");
   }
-  if (int e = epi_setup(B, J, C, H, W, ref, tgt, intr, pose, workspace, st)) return e;
+  if (int e = epi_setup(B, J, C, H, W, D, depth_per_pixel, ref, tgt, intr, pose, depth, workspace, st)) return e;
   float* tgt_hwc = static_cast<float*>(workspace);
   float* ref_hwc = tgt_hwc + (size_t)B * J * (HW + 1) * C;
   int* groups = reinterpret_cast<int*>(ref_hwc + (size_t)B * (HW + 1) * C);
   float* geom = reinterpret_cast<float*>(groups + (size_t)B * J * HW);
   const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-  if (epi_path(C, H, W, false)) {
+  if (path == DCV_PATH_EPI) {
     const size_t lds = epi_lds_bytes(C, H, W, false);
 #define DCV_ATTR(NK, SPT)                                                                                       \
   if (int e = dsplat::ensure_dyn_lds((const void*)k_cost_epi<NK, SPT>, lds, "hipFuncSetAttribute(k_cost_epi)")) return e;
@@ -1395,39 +1735,47 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
   return dsplat::check_launch("k_cost_fwd");
 }
 
-int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref,
+int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, int fwd_path, const float* ref,
                         const float* tgt, void* workspace, const float* intr, const float* pose, const float* depth,
                         float clamp_min_depth, const float* dcost, float* dref, float* dtgt, void* bwd_workspace,
                         void* stream) {
   DSPLAT_REQUIRE(B > 0 && J > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_cost_volume_bwd: bad sizes");
   DSPLAT_REQUIRE(ref && tgt && workspace && intr && pose && depth && dcost && dref && dtgt && bwd_workspace,
                  "dcv_cost_volume_bwd: null pointer");
+  DSPLAT_REQUIRE(path_ok(fwd_path, C, H, W), "dcv_cost_volume_bwd: forward path %d not available for C=%d H=%d W=%d",
+                 fwd_path, C, H, W);
   hipStream_t st = (hipStream_t)stream;
   const int HW = H * W;
   // the band forward skipped the channel-last copies and the grouping: done here
-  if (band_fwd(B, C, H, W))
-    if (int e = epi_setup(B, J, C, H, W, ref, tgt, intr, pose, workspace, st)) return e;
+  if (fwd_path == DCV_PATH_BAND)
+    if (int e = epi_setup(B, J, C, H, W, D, depth_per_pixel, ref, tgt, intr, pose, depth, workspace, st)) return e;
   const float* tgt_hwc = static_cast<const float*>(workspace);
   const float* ref_hwc = tgt_hwc + (size_t)B * J * (HW + 1) * C;
   const int* groups = reinterpret_cast<const int*>(ref_hwc + (size_t)B * (HW + 1) * C);
   const float* geom = reinterpret_cast<const float*>(groups + (size_t)B * J * HW);
-  float* dtgt_hwc = static_cast<float*>(bwd_workspace);
-  float* dref_hwc = dtgt_hwc + (size_t)B * J * (HW + 1) * C;
-  if (int e = dsplat::zero_async(dtgt_hwc, (size_t)B * J * (HW + 1) * C * 4, st, "zero dtgt_hwc")) return e;
-  if (epi_path(C, H, W, true) && epi_path(C, H, W, false)) {
+  const size_t ntg = (size_t)B * J * (HW + 1) * C;
+  long long* dtgt_fx = static_cast<long long*>(bwd_workspace);
+  float* dref_hwc = reinterpret_cast<float*>(dtgt_fx + ntg);
+  float* cvmax = dref_hwc + (size_t)B * HW * C;
+  const bool epi = epi_path(C, H, W, true) && epi_path(C, H, W, false);
+  if (int e = dsplat::zero_async(dtgt_fx, ntg * (epi ? sizeof(long long) : sizeof(float)), st, "zero dtgt")) return e;
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  const int spt = D <= 32 ? 2 : 8;
+  if (epi) {
+    k_cv_absmax<<<kCvMaxBlocks, 256, 0, st>>>((size_t)B * D * HW, dcost, (size_t)B * C * HW, ref, cvmax);
+    if (int e = dsplat::check_launch("k_cv_absmax")) return e;
     const size_t lds = epi_lds_bytes(C, H, W, true);
 #define DCV_ATTR(NK, SPT)                                                                                       \
   if (int e = dsplat::ensure_dyn_lds((const void*)k_cost_epi_bwd<NK, SPT>, lds, "hipFuncSetAttribute(k_cost_epi_bwd)")) return e;
     DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
     DCV_ATTR(4, 8) DCV_ATTR(8, 8) DCV_ATTR(16, 8) DCV_ATTR(32, 8)
 #undef DCV_ATTR
-    const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-    const int ngroups = (HW + EG - 1) / EG, spt = D <= 32 ? 2 : 8;
+    const int ngroups = (HW + EG - 1) / EG;
     const dim3 grid(8u * (unsigned)((B * ngroups + 7) / 8));
     for (int j = 0; j < J; ++j) {
 #define DCV_EPIB(NK)                                                                                           \
   (spt == 2 ? k_cost_epi_bwd<NK, 2> : k_cost_epi_bwd<NK, 8>)<<<grid, 256, lds, st>>>(B, j, J, H, W, D, depth_per_pixel, j > 0, ref_hwc, tgt_hwc, groups, \
-                                             geom, depth, clamp_min_depth, scale, dcost, dref_hwc, dtgt_hwc)
+                                             geom, depth, clamp_min_depth, scale, dcost, cvmax, dref_hwc, dtgt_fx)
       switch (C) {
         case 16: DCV_EPIB(4); break;
         case 32: DCV_EPIB(8); break;
@@ -1440,11 +1788,14 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
     (C % 4 == 0 && HW % 4 == 0 && aligned16(dref) && aligned16(bwd_workspace) ? k_to_chw4 : k_to_chw)<<<
         dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW, dref_hwc, dref);
     if (int e = dsplat::check_launch("k_to_chw(dref)")) return e;
-  } else {
-    k_cost_bwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
-                                                     depth, clamp_min_depth, dcost, dref, dtgt_hwc);
-    if (int e = dsplat::check_launch("k_cost_bwd")) return e;
+    k_fx_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_fx, cvmax, scale, spt,
+                                                                          dtgt);
+    return dsplat::check_launch("k_fx_to_chw");
   }
+  float* dtgt_hwc = reinterpret_cast<float*>(dtgt_fx);
+  k_cost_bwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
+                                                   depth, clamp_min_depth, dcost, dref, dtgt_hwc);
+  if (int e = dsplat::check_launch("k_cost_bwd")) return e;
   (C % 4 == 0 && HW % 4 == 0 && aligned16(dtgt) && aligned16(bwd_workspace) ? k_to_chw4 : k_to_chw)<<<
       dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_hwc, dtgt);
   return dsplat::check_launch("k_to_chw");

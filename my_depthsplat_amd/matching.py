@@ -74,14 +74,16 @@ def _cost_volume_fwd(ref, tgt, intrinsics, pose, depth, per_pixel, clamp):
     B, J, C, H, W = tgt.shape
     D = depth.shape[1]
     dev = ref.device
+    # the kernel path, chosen once: the backward is handed the same one (include/dsplat_hip.h)
+    path = lib.dcv_cost_volume_path(B, J, C, H, W)
     # channel-last copies of the features + the epipolar pixel groups (the backward reuses
     # them; after a band-kernel forward the backward makes them)
     ws = torch.empty(lib.dcv_cost_volume_workspace_size(B, J, C, H, W), dtype=torch.uint8, device=dev)
     cost = torch.empty((B, D, H, W), dtype=torch.float32, device=dev)
-    _lib.check(lib.dcv_cost_volume_fwd(B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), tgt.data_ptr(),
+    _lib.check(lib.dcv_cost_volume_fwd(B, J, C, H, W, D, int(per_pixel), path, ref.data_ptr(), tgt.data_ptr(),
                                        intrinsics.data_ptr(), pose.data_ptr(), depth.data_ptr(), clamp,
                                        ws.data_ptr(), cost.data_ptr(), _lib.stream_of(dev)), "dcv_cost_volume_fwd")
-    return cost, ws
+    return cost, ws, path
 
 
 class _CostVolume(torch.autograd.Function):
@@ -89,15 +91,15 @@ class _CostVolume(torch.autograd.Function):
     def forward(ctx, ref, tgt, intrinsics, pose, depth, per_pixel, clamp):
         B, J, C, H, W = tgt.shape
         D = depth.shape[1]
-        cost, ws = _cost_volume_fwd(ref, tgt, intrinsics, pose, depth, per_pixel, clamp)
+        cost, ws, path = _cost_volume_fwd(ref, tgt, intrinsics, pose, depth, per_pixel, clamp)
         ctx.save_for_backward(ref, tgt, ws, intrinsics, pose, depth)
-        ctx.meta = (B, J, C, H, W, D, per_pixel, clamp)
+        ctx.meta = (B, J, C, H, W, D, per_pixel, clamp, path)
         return cost
 
     @staticmethod
     def backward(ctx, dcost):
         ref, tgt, ws, intrinsics, pose, depth = ctx.saved_tensors
-        B, J, C, H, W, D, per_pixel, clamp = ctx.meta
+        B, J, C, H, W, D, per_pixel, clamp, path = ctx.meta
         dev = ref.device
         dcost = _f(dcost)
         dref = torch.empty_like(ref)
@@ -105,7 +107,7 @@ class _CostVolume(torch.autograd.Function):
         lib = _lib.load()
         scratch = torch.empty(lib.dcv_cost_volume_bwd_workspace_size(B, J, C, H, W), dtype=torch.uint8, device=dev)
         _lib.check(lib.dcv_cost_volume_bwd(
-            B, J, C, H, W, D, int(per_pixel), ref.data_ptr(), tgt.data_ptr(), ws.data_ptr(), intrinsics.data_ptr(),
+            B, J, C, H, W, D, int(per_pixel), path, ref.data_ptr(), tgt.data_ptr(), ws.data_ptr(), intrinsics.data_ptr(),
             pose.data_ptr(), depth.data_ptr(), clamp, dcost.data_ptr(), dref.data_ptr(), dtgt.data_ptr(),
             scratch.data_ptr(), _lib.stream_of(dev)), "dcv_cost_volume_bwd")
         return dref, dtgt, None, None, None, None, None

@@ -27,7 +27,7 @@ cost = torch.zeros(BV * D * HW + BV * ngroups * 8, dtype=torch.float32, device=d
 pp = int(depth.dim() == 4)
 st = _lib.stream_of(dev)
 for _ in range(5):
-    assert lib.dcv_cost_volume_fwd(BV, 1, C, H, W, D, pp, ref.data_ptr(), tgt.data_ptr(), K.data_ptr(), pose.data_ptr(),
+    assert lib.dcv_cost_volume_fwd(BV, 1, C, H, W, D, pp, 1, ref.data_ptr(), tgt.data_ptr(), K.data_ptr(), pose.data_ptr(),
                                    depth.data_ptr(), 1e-3, ws.data_ptr(), cost.data_ptr(), st) == 0
 torch.cuda.synchronize()
 r = cost[BV * D * HW:].view(torch.int32).cpu().numpy().astype(np.int64).reshape(-1, 8) & 0xFFFFFFFF
