@@ -301,9 +301,9 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
  * results are identical for any hint. */
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                     const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
-                    uint64_t* scratch, int write_keys, int clear_counts, uint32_t max_count_hint,
-                    int binning_layout, float* out_color, float* final_T, uint32_t* n_contrib,
-                    uint32_t* seg_overflow, void* stream);
+                    uint64_t* scratch, uint64_t* spill_keys, int write_keys, int clear_counts,
+                    uint32_t max_count_hint, int binning_layout, float* out_color, float* final_T,
+                    uint32_t* n_contrib, uint32_t* seg_overflow, void* stream);
 /* seg_overflow (NULL: none; DSR_SEG_ENDS layout only): the depth cut's flags, written exactly
  * as dsr_render_fwd writes them (tile, any-flag, super-block), so this launch can replace
  * dsr_bin_sort + dsr_render_fwd for the written heads when no backward needs sorted keys. */
@@ -313,7 +313,13 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
  * segment with seg_count[s] > seg_stride is rebuilt by its workgroup from the view's geometry
  * records with the binning test of `binning_layout` (the layout bits of the binning call:
  * DSR_LAYOUT_RECT_BINNING = 3-sigma rects, else the exact test) and composited in depth
- * windows of the LDS capacity (slow, exact). write_keys requires seg_stride >= G. */
+ * windows of the LDS capacity (slow, exact). With write_keys, the sorted keys of a segment
+ * with seg_count[s] <= seg_stride go back to `keys`; those of a rebuilt segment go to
+ * spill_keys [V*T, G] (its slots s*G + position, written up to the window in which every pixel
+ * of the tile stopped — all that dsr_render_bwd reads). spill_keys (NULL: not stored) needs
+ * write_keys and the fixed-capacity layout; pass the same pointer to dsr_render_bwd, which
+ * reads a segment with seg_count[s] > seg_stride from there. (round 5: bounded segments for
+ * forwards with a backward, no host check between forward and backward) */
 
 /* ---- rasterizer backward -----------------------------------------------------------
  * Deterministic: every per-Gaussian gradient is a sum over (tile, sub-tile wave) partials,
@@ -336,8 +342,9 @@ int dsr_grad_scale(int V, int H, int W, const float* dL_dpix, float* grad_scale,
  * upstream dL_dmean2D), [2..4] dL/dconic, [5] dL/dopacity, [6..8] dL/drgb. */
 int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride,
-                   const uint64_t* keys, const float* final_T, const uint32_t* n_contrib,
-                   const float* dL_dpix, const float* grad_scale, int64_t* dgeom_fx, void* stream);
+                   const uint64_t* keys, const uint64_t* spill_keys, const float* final_T,
+                   const uint32_t* n_contrib, const float* dL_dpix, const float* grad_scale, int64_t* dgeom_fx,
+                   void* stream);
 
 /* dgeom_fx -> float dgeom [V,G,DSR_GEOM_STRIDE] (words 9..11 zero, rows of culled Gaussians
  * zero, and rows not marked in row_live when it is given): the values the preprocess backward

@@ -39,12 +39,12 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_workspace_size": (_I, [_I, _I, _I, _I, ctypes.c_uint64, _P]),
     "dsr_sort_lds_capacity": (c_uint32, []),
     "dsr_render_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "dsr_sort_render": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _I, _I, c_uint32, _I, _P, _P, _P, _P,
-                            _P]),
+    "dsr_sort_render": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _I, _I, c_uint32, _I, _P, _P, _P,
+                            _P, _P]),
     "dsr_project_bin_cameras": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P,
                                      _P, _P, _P, _P, _P, c_uint32, _I, _P]),
     "dsr_grad_scale": (_I, [_I, _I, _I, _P, _P, _P]),
-    "dsr_render_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P, _P, _P, _P]),
+    "dsr_render_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dsr_dgeom_to_float": (_I, [_I, _I, _P, _P, _P, _P, _P, _P]),
     "dsr_preprocess_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                 _P, _P, _P, _P, _P, _P, _P, _I, _P]),

@@ -2886,12 +2886,14 @@ __device__ __forceinline__ void hist_select(const uint32_t* hist, uint32_t r, ui
 // descent once half a window is certain) — each window sorted in LDS (count_sort) and
 // composited before the next, until every pixel has stopped or the list is exhausted.
 // Entries are blended in exactly the full list's order, so the image equals the unbounded
-// layout's. LAST: n_contrib positions count from the list's start.
+// layout's. LAST: n_contrib positions count from the list's start. spill (non-NULL): each
+// window's sorted keys are stored at their list positions there — every position below the
+// tile's last blended one, which is all the backward reads.
 template <int KMAX, bool LAST, int NBL>
 __device__ __attribute__((noinline)) void render_rebuilt(int G, int gx, int gy, int tx, int ty, bool exact, const float* __restrict__ gv,
                                uint64_t* A, uint16_t* cnt, uint32_t* wsum, uint32_t* flag, int id_bits, float fx0,
                                float fy0, const PixUV2& pp, int lane, uint64_t lt, WaveList* plist, float& Tr, f2v& C01,
-                               float& C2, uint32_t& last, bool& alive) {
+                               float& C2, uint32_t& last, bool& alive, uint64_t* __restrict__ spill) {
   constexpr uint32_t capl = NT * KMAX;
   constexpr int kNB = 2048;  // 11-bit digits
   static_assert((NT * KMAX + NT) * 2 >= kNB, "digit histogram fits the key array");
@@ -2959,6 +2961,8 @@ __device__ __attribute__((noinline)) void render_rebuilt(int G, int gx, int gy, 
     }
     __syncthreads();
     if (n > 1) count_sort<KMAX, NT, NBL>(tmp, n, A, id_bits, cnt, wsum, flag);
+    if (spill)  // the window's sorted keys at their list positions, for the backward
+      for (uint32_t i = tid; i < n; i += NT) spill[base + i] = A[padi<KMAX>(i)];
     uint32_t wl = 0;
     composite_tile<LAST>([&](uint32_t i) { return min((uint32_t)A[padi<KMAX>(i)], (uint32_t)G - 1u); }, 0u, n, gv, fx0,
                          fy0, pp, lane, lt, plist, Tr, C01, C2, wl, alive);
@@ -2974,8 +2978,8 @@ template <int KMAX, bool LAST, int NBL, int WPE>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_sort_render(
     int G, int H, int W, int gx, int T, const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
     const uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_count, uint32_t stride,
-    uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, int id_bits, int write_keys, int clear_counts,
-    int exact_rebuild, float* __restrict__ out, float* __restrict__ finalT, uint32_t* __restrict__ ncontrib,
+    uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch, uint64_t* __restrict__ spill_keys, int id_bits,
+    int write_keys, int clear_counts, int exact_rebuild, float* __restrict__ out, float* __restrict__ finalT, uint32_t* __restrict__ ncontrib,
     uint32_t* __restrict__ seg_overflow) {
   constexpr uint32_t cap = NT * KMAX;
   constexpr uint32_t padded = cap + cap / KMAX;
@@ -3005,7 +3009,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                                     reinterpret_cast<uint32_t*>(s_keys + padded) + sort_render_aux_words<NBL>() + 16,
                                     id_bits, (float)sx0, (float)sy0, pp, lane, dsplat::lanemask_lt(lane),
                                     reinterpret_cast<WaveList*>(reinterpret_cast<uint32_t*>(s_keys + padded)) + w, Tr,
-                                    C01, C2, last, alive);
+                                    C01, C2, last, alive, spill_keys ? spill_keys + (size_t)seg * G : nullptr);
     if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
     if (clear_counts && tid == 0) seg_count[seg] = 0u;
     return;
@@ -3191,6 +3195,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                                                    const uint32_t* __restrict__ seg_start,
                                                    const uint32_t* __restrict__ seg_count, uint32_t stride,
                                                    const uint64_t* __restrict__ keys,
+                                                   const uint64_t* __restrict__ spill_keys,
                                                    const float* __restrict__ finalT,
                                                    const uint32_t* __restrict__ ncontrib,
                                                    const float* __restrict__ dpix,
@@ -3208,6 +3213,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const int seg = v * T + ty * gx + tx;
   uint32_t start, end;
   seg_bounds(seg_start, seg_count, stride, seg, start, end);
+  // a bounded segment that overflowed: dsr_sort_render stored its rebuilt list in the spill
+  // area (G slots per segment) instead
+  const bool spilled = spill_keys != nullptr && stride != 0u && stride != kSegEnds && end - start > stride;
+  const uint64_t* __restrict__ kseg = spilled ? spill_keys + (size_t)seg * G : keys + start;
   const size_t HW = (size_t)H * W;
   const size_t pix = (size_t)py * W + px;
   const float pfx = (float)px, pfy = (float)py;
@@ -3245,7 +3254,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const int nch = (int)((nproc + BCH - 1) / BCH);
   auto id_at = [&](int c) -> uint32_t {  // unconditional key read (clamped), id 0 past the range
     const int pos = (int)nproc - (c + 1) * BCH + lane;
-    const uint32_t k = min((uint32_t)keys[start + (uint32_t)min(max(pos, 0), max((int)nproc - 1, 0))], (uint32_t)G - 1u);
+    const uint32_t k = min((uint32_t)kseg[(uint32_t)min(max(pos, 0), max((int)nproc - 1, 0))], (uint32_t)G - 1u);
     return (pos >= 0 && c < nch) ? k : 0u;
   };
   auto chunk = [&](int ch, uint32_t id, float4 q, float4 r, float bl) {
@@ -4130,14 +4139,16 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
 
 int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                     const uint32_t* seg_start, uint32_t* seg_count, uint32_t seg_stride, uint64_t* keys,
-                    uint64_t* scratch, int write_keys, int clear_counts, uint32_t max_count_hint,
-                    int binning_layout, float* out_color, float* final_T, uint32_t* n_contrib,
-                    uint32_t* seg_overflow, void* stream) {
+                    uint64_t* scratch, uint64_t* spill_keys, int write_keys, int clear_counts,
+                    uint32_t max_count_hint, int binning_layout, float* out_color, float* final_T,
+                    uint32_t* n_contrib, uint32_t* seg_overflow, void* stream) {
   DSPLAT_REQUIRE(!clear_counts || seg_stride > 0, "dsr_sort_render: clear_counts needs the fixed-capacity layout");
   DSPLAT_REQUIRE(seg_overflow == nullptr || (seg_stride == kSegEnds && seg_start != nullptr),
                  "dsr_sort_render: seg_overflow needs the DSR_SEG_ENDS layout (depth cut)");
-  DSPLAT_REQUIRE(!write_keys || seg_stride == 0 || seg_stride == kSegEnds || (uint32_t)G <= seg_stride,
-                 "dsr_sort_render: write_keys needs segments that hold every entry (seg_stride >= G)");
+  // write_keys with bounded segments (seg_stride < G): a tile whose count exceeds the stride is
+  // rebuilt; its sorted list goes to spill_keys (G slots per segment) when given
+  DSPLAT_REQUIRE(spill_keys == nullptr || (write_keys && seg_stride != 0u && seg_stride != kSegEnds),
+                 "dsr_sort_render: spill_keys needs write_keys and the fixed-capacity layout");
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_sort_render: bad sizes");
   DSPLAT_REQUIRE(cams && geom && keys && scratch && seg_ptrs_ok(seg_start, seg_count, seg_stride) && out_color &&
                      final_T,
@@ -4179,7 +4190,7 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
   hipStream_t st = (hipStream_t)stream;
 #define DSR_SR_LAUNCH(K, L, NB, WP)                                                                          \
   k_sort_render<K, L, NB, WP><<<grid, NT, lds, st>>>(G, H, W, gx, T, cams, geom, seg_start, seg_count, seg_stride, \
-                                                     keys, scratch, id_bits, write_keys, clear_counts,             \
+                                                     keys, scratch, spill_keys, id_bits, write_keys, clear_counts, \
                                                      !(binning_layout & kLayoutRectBinning), out_color, final_T,   \
                                                      n_contrib, seg_overflow)
   // n_contrib is optional (inference: LAST = false)
@@ -4216,19 +4227,21 @@ int dsr_grad_scale(int V, int H, int W, const float* dL_dpix, float* grad_scale,
 
 int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const float* geom,
                    const uint32_t* seg_start, const uint32_t* seg_count, uint32_t seg_stride, const uint64_t* keys,
-                   const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, const float* grad_scale,
-                   int64_t* dgeom_fx, void* stream) {
+                   const uint64_t* spill_keys, const float* final_T, const uint32_t* n_contrib,
+                   const float* dL_dpix, const float* grad_scale, int64_t* dgeom_fx, void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_render_bwd: bad sizes");
   DSPLAT_REQUIRE(cams && geom && seg_ptrs_ok(seg_start, seg_count, seg_stride) && final_T && n_contrib &&
                      dL_dpix && grad_scale && dgeom_fx,
                  "dsr_render_bwd: null pointer");
+  DSPLAT_REQUIRE(spill_keys == nullptr || (seg_stride != 0u && seg_stride != kSegEnds),
+                 "dsr_render_bwd: spill_keys needs the fixed-capacity layout");
   long long* dgeom = reinterpret_cast<long long*>(dgeom_fx);
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
   constexpr int64_t kWideBwd = 8192;  // (view, tile) segments from which WPE = 5 pays
   auto kern = (int64_t)V * gx * gy >= kWideBwd ? k_render_bwd<5> : k_render_bwd<1>;
   kern<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count, seg_stride, keys,
-                                             final_T, n_contrib, dL_dpix, grad_scale, dgeom);
+                                             spill_keys, final_T, n_contrib, dL_dpix, grad_scale, dgeom);
   return dsplat::check_launch("k_render_bwd");
 }
 

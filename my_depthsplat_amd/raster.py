@@ -176,6 +176,9 @@ class RasterState:
     # the backward's int64 gradient accumulator, its rendered rows zeroed by the forward
     dgeom: torch.Tensor | None = None
     dgeom_filled: bool = False   # dgeom zeroed in full by this forward (not only its rendered rows)
+    # bounded segments with a backward: the rebuilt tiles' sorted lists ([V*T, G] slots; read by
+    # dsr_render_bwd for segments with seg_count > seg_stride)
+    spill: torch.Tensor | None = None
     # depth-cut binning: (cut thresholds [V * super-blocks], compact records or None, super-block size)
     cut_plan: tuple | None = None
     # deferred geometry with a backward: [V*G] uint8, 1 for the rows projected in full (whose
@@ -273,6 +276,8 @@ LAYOUT_RECT_BINNING = 8
 # entries. Off: the reference's lists exactly (the oracle list tests switch it off).
 STATEFUL_EXACT_BINNING = True
 LAYOUT_EXACT_BINNING = 16
+# Forwards with a backward use bounded fixed-capacity segments too (forward_raw, round 5)
+BOUNDED_TRAIN_SEGMENTS = True
 # Test hook (tests/test_fullsize_parity.py): the fast path also snapshots its per-tile counts
 # and writes its sorted keys back, so its lists can be compared with the oracle's. It adds a
 # copy and the key stores; the product never sets it.
@@ -303,7 +308,8 @@ class RasterContext:
              "fused_sort_render": "FUSED_SORT_RENDER", "sort_render_hint": "SORT_RENDER_HINT",
              "inkernel_cameras": "INKERNEL_CAMERAS", "sort_prefix": "SORT_PREFIX", "cut_prefix": "CUT_PREFIX",
              "debug_keep_fast_lists": "DEBUG_KEEP_FAST_LISTS", "key_budget_bytes": "KEY_BUDGET_BYTES",
-             "seg_capacity": "SEG_CAPACITY", "defer_geom": "DEFER_GEOM"}
+             "seg_capacity": "SEG_CAPACITY", "defer_geom": "DEFER_GEOM",
+             "bounded_train_segments": "BOUNDED_TRAIN_SEGMENTS"}
 
     def __init__(self, **options):
         unknown = set(options) - set(self._OPTS)
@@ -654,7 +660,15 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     fast = clean is not None
     fixed = fast or bool(workspace(G, H, W, V, dev, ctx).fixed_capacity)
     fused = fixed and ctx.opt("fused_sort_render") and maxc_hint <= FUSED_MAX
-    stride = cap if fast else G
+    # training with bounded segments (round 5): the fixed-capacity layout with the same adaptive
+    # capacity as the inference fast path instead of G slots per (view, tile) — config C's keys
+    # then span 1 GB instead of 17 GB (the scattered key stores and the sort's reads touched a
+    # new page per segment). A tile above the capacity is rendered exactly (rebuilt by
+    # dsr_sort_render), which stores its sorted list in the spill area ([V*T, G] slots, touched
+    # only by such tiles) where dsr_render_bwd reads it: no host check between the passes.
+    bounded = (not fast and fused and need_state and not debug_lists and ctx.opt("bounded_train_segments")
+               and cap < G and T <= _HIST_LDS_MAX and V * T * cap < (1 << 32))
+    stride = cap if (fast or bounded) else G
     if fast:
         seg_count = clean
         layout |= LAYOUT_COUNTS_ZEROED
@@ -679,6 +693,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         keys = torch.empty(V * T * stride, dtype=torch.int64, device=dev)
         # scratch for segments above the LDS sort (their size is unknown before the sort)
         scratch = torch.empty(V * T * stride, dtype=torch.int64, device=dev)
+        spill = torch.empty(V * T * G, dtype=torch.int64, device=dev) if bounded else None
         if fast:
             ci = cam_in
             # camera-block mode: NULL render_cuda inputs, cams is the caller's (an input)
@@ -704,17 +719,25 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                 dz.zero_()
             dgeom_filled = dz is not None
             dz = None
-            _lib.check(_timed("k_project_emit", lib.dsr_project_bin,
-                S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-                cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dz), seg_count.data_ptr(),
-                keys.data_ptr(), layout, st), "dsr_project_bin")
+            if bounded:  # camera-block mode: the same kernel with a segment capacity
+                if not layout & LAYOUT_EXACT_BINNING:  # (dsr_sort_render rebuilds with the same test)
+                    layout |= LAYOUT_RECT_BINNING
+                _lib.check(_timed("k_project_emit", lib.dsr_project_bin_cameras,
+                    S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+                    *((None,) * 6 + (0,)), cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), None,
+                    seg_count.data_ptr(), keys.data_ptr(), stride, layout, st), "dsr_project_bin_cameras(bounded)")
+            else:
+                _lib.check(_timed("k_project_emit", lib.dsr_project_bin,
+                    S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+                    cams.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dz), seg_count.data_ptr(),
+                    keys.data_ptr(), layout, st), "dsr_project_bin")
         seg_start = None
         seg_sorted = None
         if not fused:
             ws = _sort_workspace(lib, V, H, W, maxc_hint, dev)
             seg_sorted = _prefix_sort(lib, G, V, H, W, None, seg_count, stride, keys, scratch, maxc_hint, ws, st,
                                       lds_cap, ctx.opt("sort_prefix"))
-        ctx.note_counts(seg_count, stride if fast and stride < G else None)
+        ctx.note_counts(seg_count, stride if (fast or bounded) and stride < G else None)
     else:
         # the depth cut pays when tile lists are long; the previous two-phase call's largest
         # list (None on the first call) decides whether this one builds the depth histogram
@@ -821,12 +844,13 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     if fused:  # sort + composite in one launch; sorted keys kept only when a backward needs them
         snap = seg_count.clone() if (fast and debug_lists) else None
         _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(), None,
-                          seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(),
+                          seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(), _ptr(spill),
                           int(bool(need_state) or snap is not None), int(fast),
                           ctx.opt("sort_render_hint") or spec["max_count"], layout, *outs[:3], None, st),
                    "dsr_sort_render")
         state = RasterState(geom, radii, seg_start, seg_count, stride, keys, final_T, n_contrib, cams=cams,
                             dgeom_filled=dgeom_filled)
+        state.spill = spill
         if fast:  # the counters are zero again once the launch above has run
             ctx.give_back_clean_counts(seg_count, dev, st)
             # consumed (no backward in this mode); with exact binning n_contrib counts positions
@@ -846,7 +870,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
     if cut_fused:  # n_contrib only from the tail's re-render: not exposed (state.n_contrib None)
         _lib.check(_timed("k_sort_render", lib.dsr_sort_render, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
                           seg_start.data_ptr(), seg_count.data_ptr(), stride, keys.data_ptr(), scratch.data_ptr(),
-                          int(bool(debug_lists)), 0, CUT_SORT_HINT, layout, color.data_ptr(), final_T.data_ptr(),
+                          None, int(bool(debug_lists)), 0, CUT_SORT_HINT, layout, color.data_ptr(), final_T.data_ptr(),
                           None, overflow.data_ptr(), st), "dsr_sort_render(depth cut)")
     else:
         _lib.check(_timed("k_render_fwd", lib.dsr_render_fwd, G, V, H, W, cams.data_ptr(), geom.data_ptr(),
@@ -952,7 +976,7 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     _lib.check(lib.dsr_grad_scale(V, H, W, dcolor.data_ptr(), gscale.data_ptr(), st), "dsr_grad_scale")
     _lib.check(_timed("k_render_bwd", lib.dsr_render_bwd, G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), _ptr(state.seg_start),
                                   state.seg_count.data_ptr(), state.seg_stride, state.keys.data_ptr(),
-                                  state.final_T.data_ptr(), state.n_contrib.data_ptr(), dcolor.data_ptr(),
+                                  _ptr(state.spill), state.final_T.data_ptr(), state.n_contrib.data_ptr(), dcolor.data_ptr(),
                                   gscale.data_ptr(), dgeom_fx.data_ptr(), st), "dsr_render_bwd")
     dgeom = None
     if want_dgeom:

@@ -45,7 +45,8 @@ def hip_forward(sc, st, gpu, use_sh=True, bg=(0.0, 0.0, 0.0), need_state=True):
 
 def _segments(state, V, T):
     """(begin [V*T], end [V*T], keys): the written, sorted part of each segment, whichever
-    layout the forward used (fixed capacity, prefix, or depth-cut ends)."""
+    layout the forward used (fixed capacity, prefix, depth-cut ends, or bounded segments
+    with a spill area: see _spilled)."""
     keys = state.keys.cpu().numpy().view(np.uint64)
     if state.seg_stride == 0:
         start = state.seg_start.cpu().numpy().astype(np.int64)
@@ -56,7 +57,50 @@ def _segments(state, V, T):
     cnt = state.seg_count.cpu().numpy().astype(np.int64)
     assert cnt.shape[0] == V * T
     begin = np.arange(V * T, dtype=np.int64) * state.seg_stride
-    return begin, begin + cnt, keys
+    end = begin + cnt
+    sp = _spilled(state, V, T)
+    if sp is not None and sp.any():
+        # a rebuilt segment's list is in the spill area ([V*T, G] slots), written at least up
+        # to the tile's last blended position (what the backward reads): that prefix
+        G = state.spill.numel() // (V * T)
+        spill = state.spill.view(V * T, G)[torch.from_numpy(np.nonzero(sp)[0]).to(state.spill.device)]
+        spill = spill.cpu().numpy().view(np.uint64)
+        lim = _tile_max_ncontrib(state, V, T)
+        base = len(keys)
+        keys = np.concatenate([keys, spill.reshape(-1)])
+        for j, sg in enumerate(np.nonzero(sp)[0]):
+            begin[sg] = base + j * G
+            end[sg] = begin[sg] + min(int(lim[sg]), int(cnt[sg]))
+    return begin, end, keys
+
+
+def _spilled(state, V, T):
+    """Bounded segments (training, round 5) that overflowed and were rebuilt: [V*T] bool, or
+    None when the state has no spill area. Their _segments part is a prefix of the list."""
+    if getattr(state, "spill", None) is None:
+        return None
+    return state.seg_count.cpu().numpy().astype(np.int64) > state.seg_stride
+
+
+def _tile_max_ncontrib(state, V, T):
+    """Per (view, tile): the largest n_contrib (last blended list position) of its pixels."""
+    from my_depthsplat_amd import raster
+    nc = state.n_contrib.cpu().numpy().astype(np.int64)
+    H, W = nc.shape[1:]
+    gx, gy = raster.tiles(H, W)
+    assert gx * gy == T
+    pad = np.zeros((V, gy * raster.TILE, gx * raster.TILE), np.int64)
+    pad[:, :H, :W] = nc
+    return pad.reshape(V, gy, raster.TILE, gx, raster.TILE).max(axis=(2, 4)).reshape(V * T)
+
+
+def _fused_ctx(**options):
+    """A RasterContext whose first call already takes the fused sort + composite (a fresh
+    context's size hint is the LDS capacity, above FUSED_MAX): hint pinned at 2048 keys."""
+    ctx = raster_mod().RasterContext(**options)
+    ctx.hints["max_count"] = 2048
+    ctx.adapt_hints = False
+    return ctx
 
 
 def raster_mod():
@@ -195,13 +239,15 @@ def _check_segments_vs_oracle(state, orcs, V, T):
     the sorted prefix exactly and the unordered tail as a set."""
     begin, end, keys = _segments(state, V, T)
     srt = None if state.seg_sorted is None else state.seg_sorted.cpu().numpy()
+    spilled = _spilled(state, V, T)
     for v, o in enumerate(orcs):
         okeys, ovals, ranges = o.binning()
         for t in range(T):
             s = v * T + t
             hk = (keys[begin[s]:end[s]] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
             ob, oe = ranges[t]
-            if state.seg_stride == raster_mod().SEG_ENDS:  # depth cut: the head of the sorted list
+            if state.seg_stride == raster_mod().SEG_ENDS or (spilled is not None and spilled[s]):
+                # depth cut / rebuilt bounded segment: the head of the sorted list
                 assert len(hk) <= oe - ob
                 np.testing.assert_array_equal(hk, ovals[ob:ob + len(hk)])
                 continue
@@ -694,7 +740,7 @@ def test_render_bwd_wide_grid_kernel(gpu):
     for n in (V, 3):
         dq = torch.zeros((n, G, raster.DGEOM_WORDS), dtype=torch.int64, device=gpu)
         _lib.check(lib.dsr_render_bwd(G, n, H, W, cams.data_ptr(), st.geom.data_ptr(), sp, st.seg_count.data_ptr(),
-                                      st.seg_stride, st.keys.data_ptr(), st.final_T.data_ptr(),
+                                      st.seg_stride, st.keys.data_ptr(), None, st.final_T.data_ptr(),
                                       st.n_contrib.data_ptr(), dpix.data_ptr(), gscale.data_ptr(), dq.data_ptr(),
                                       stream), "dsr_render_bwd")
         dgeom = torch.empty((n, G, raster.GEOM_STRIDE), device=gpu)
@@ -1059,9 +1105,16 @@ def test_stateful_exact_binning(gpu, layout, case, monkeypatch):
     # order, the tail unordered): compare as sets, and the sorted parts for order
     p0 = None if s0.seg_sorted is None else s0.seg_sorted.cpu().numpy()
     p1 = None if s1.seg_sorted is None else s1.seg_sorted.cpu().numpy()
+    # bounded segments (the product's training layout) that overflowed keep the sorted list up
+    # to the tile's last blended entry: where either run has one, compare those prefixes (the
+    # deepest last-blended Gaussian is the same in both lists)
+    sp0, sp1 = _spilled(s0, B * v, T), _spilled(s1, B * v, T)
+    lim0, lim1 = _tile_max_ncontrib(s0, B * v, T), _tile_max_ncontrib(s1, B * v, T)
     for sg in range(B * v * T):
         ref = k0[b0[sg]:e0[sg]]
         sub = k1[b1[sg]:e1[sg]]
+        if (sp0 is not None and sp0[sg]) or (sp1 is not None and sp1[sg]):
+            ref, sub = ref[:lim0[sg]], sub[:lim1[sg]]
         assert np.isin(sub, ref).all(), sg
         n_sorted = len(sub) if p1 is None else int(p1[sg])
         assert np.all(sub[1:n_sorted] > sub[:n_sorted - 1]), sg  # keys are distinct
@@ -1110,3 +1163,91 @@ def test_inference_long_lists_camera_block_vs_stateful(gpu, opacity, monkeypatch
         oc, _, _ = o.image()
         assert float(np.abs(color[i].cpu().numpy() - oc).mean()) < 1e-4
         o.close()
+
+
+def test_bounded_training_segments_match_unbounded(gpu):
+    """Round 5: forwards with a backward use bounded fixed-capacity segments (RasterContext
+    seg_capacity, like the inference fast path). Images, final T and gradients equal the
+    G-slot layout's bit for bit — also with a capacity far below the longest tile list, where
+    the forward renders the overflowing tiles exactly (rebuilt, their sorted lists stored in
+    the spill area) and the backward reads those lists from there."""
+    from my_depthsplat_amd import raster
+    from my_depthsplat_amd.cuda_splatting import _cov6
+    from my_depthsplat_amd.synthetic import make_scene
+    H, W = 64, 96
+    sc = make_scene(batch=2, n_context=2, n_targets=2, height=H, width=W, seed=31, device=gpu)
+    dcol = torch.randn(4, 3, H, W, device=gpu, generator=torch.Generator(device=gpu).manual_seed(2))
+
+    def run(ctx):
+        g = sc.gaussians
+        m = g.means.clone().requires_grad_(True)
+        h = g.harmonics.clone().requires_grad_(True)
+        o = g.opacities.clone().requires_grad_(True)
+        c = _cov6(g.covariances).clone().requires_grad_(True)
+        cams = raster.build_cameras(sc.target_extrinsics.flatten(0, 1), sc.target_intrinsics.flatten(0, 1),
+                                    sc.near.flatten(), sc.far.flatten(), torch.zeros(4, 3, device=gpu),
+                                    [0, 0, 1, 1], True)
+        img, _ = raster.rasterize_views(m, h.transpose(-1, -2), o, c, cams, [0, 0, 1, 1], use_sh=True, sh_degree=2,
+                                        image_height=H, image_width=W, ctx=ctx)
+        (img * dcol).sum().backward()
+        torch.cuda.synchronize()
+        return img.detach(), m.grad, h.grad, o.grad, c.grad
+
+    ref = run(_fused_ctx(bounded_train_segments=False))
+    for cap in (4096, 64):  # 64: every busy tile overflows (rebuilt, spilled)
+        got = run(_fused_ctx(seg_capacity=cap))
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b), cap
+
+
+@pytest.mark.parametrize("cap", [4096, 256, 64])
+def test_bounded_training_spill_lists(gpu, cap):
+    """Bounded training segments, state level: forward_raw + backward_raw with a capacity that
+    some tiles (4096) or every tile (256, 64) exceeds, against the G-slot layout on
+    large Gaussians. Images, final T, n_contrib and every gradient bit-identical; a segment
+    within the capacity holds its full sorted list, a rebuilt one's list in the spill area
+    equals the G-slot list up to the tile's last blended entry (all dsr_render_bwd reads)."""
+    from my_depthsplat_amd import raster
+    sc = scene_inputs(h=64, w=96, seed=31, n_tgt=2, batch=2)
+    sc.gaussians.covariances = sc.gaussians.covariances * 30.0
+    st = settings_for(sc)
+    means, shs, opac, cov6 = (t.to(gpu) for t in flat_inputs(sc))
+    B, v = sc.target_extrinsics.shape[:2]
+    V, G = B * v, means.shape[1]
+    vs = [i // v for i in range(V)]
+    cams = packed_cams(st, vs).to(gpu)
+    h, w = sc.image_shape
+    gx, gy = raster.tiles(h, w)
+    T = gx * gy
+    dpix = torch.randn(V, 3, h, w, generator=torch.Generator().manual_seed(9)).to(gpu)
+
+    def run(ctx):
+        color, state = raster.forward_raw(means, shs, True, 2, opac, cov6, cams, V, h, w, need_state=True, ctx=ctx)
+        grads = raster.backward_raw(means, shs, True, 2, opac, cov6, cams, vs, state, dpix, want_mean2d=True)
+        torch.cuda.synchronize()
+        return color, state, grads
+
+    c0, s0, g0 = run(_fused_ctx(bounded_train_segments=False))
+    assert s0.spill is None and s0.seg_stride == G
+    c1, s1, g1 = run(_fused_ctx(seg_capacity=cap))
+    assert s1.spill is not None and s1.seg_stride == cap
+    assert torch.equal(c1, c0) and torch.equal(s1.final_T, s0.final_T) and torch.equal(s1.n_contrib, s0.n_contrib)
+    sp = _spilled(s1, V, T)
+    cnt = s0.seg_count.cpu().numpy().astype(np.int64)
+    assert np.array_equal(sp, cnt > cap)
+    assert sp.any()
+    if cap == 4096:
+        assert not sp.all()
+    b0, e0, k0 = _segments(s0, V, T)
+    b1, e1, k1 = _segments(s1, V, T)
+    lim = _tile_max_ncontrib(s0, V, T)
+    for sg in range(V * T):
+        ref, got = k0[b0[sg]:e0[sg]], k1[b1[sg]:e1[sg]]
+        if sp[sg]:
+            assert len(got) == min(int(lim[sg]), len(ref)), sg
+            np.testing.assert_array_equal(got, ref[:len(got)])
+        else:
+            np.testing.assert_array_equal(got, ref)
+    for a, b_, name in zip(g1, g0, ("means", "shs", "opacity", "cov6", "mean2d")):
+        if a is not None:
+            assert torch.equal(a, b_), (cap, name)

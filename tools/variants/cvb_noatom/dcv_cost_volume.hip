@@ -1224,8 +1224,7 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
           if (q < HW && acc[r] != 0.f) {
             const long long v = (long long)rintf(fminf(fmaxf(acc[r] * unit_t_inv, -4.0e18f), 4.0e18f));
             if (v != 0ll)
-              atomicAdd(reinterpret_cast<unsigned long long*>(&dtg[(size_t)q * C + cbk * 16 + (lane & 15)]),
-                        (unsigned long long)v);
+              asm volatile("" :: "v"(v));
           }
         }
       }

@@ -1179,12 +1179,12 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
         const float fx0 = floorf(x), fy0 = floorf(y);
         const float wx0 = (fx0 + 1.f) - x, wx1 = x - fx0, wy0 = (fy0 + 1.f) - y, wy1 = y - fy0;
         const int ra = epi_rank(L, e) - r0, rb = epi_rank(L, e + Wx) - r0;
-        int* grow = gi + i * kECorr;
-        const float gu = gs[s] * unit_g_inv;
-        if (ra >= 0 && ra < n) atomicAdd(&grow[ra], (int)rintf(gu * (wx0 * wy0)));
-        if (ra + 1 >= 0 && ra + 1 < n) atomicAdd(&grow[ra + 1], (int)rintf(gu * (wx1 * wy0)));
-        if (rb >= 0 && rb < n) atomicAdd(&grow[rb], (int)rintf(gu * (wx0 * wy1)));
-        if (rb + 1 >= 0 && rb + 1 < n) atomicAdd(&grow[rb + 1], (int)rintf(gu * (wx1 * wy1)));
+        float* growf = reinterpret_cast<float*>(gi) + i * kECorr;
+        const float gu = gs[s];
+        if (ra >= 0 && ra < n) atomicAdd(&growf[ra], gu * (wx0 * wy0));
+        if (ra + 1 >= 0 && ra + 1 < n) atomicAdd(&growf[ra + 1], gu * (wx1 * wy0));
+        if (rb >= 0 && rb < n) atomicAdd(&growf[rb], gu * (wx0 * wy1));
+        if (rb + 1 >= 0 && rb + 1 < n) atomicAdd(&growf[rb + 1], gu * (wx1 * wy1));
       }
       __syncthreads();
       // dref[16 x C] += G[16 x np] . tgt[np x C]: wave wv owns channel blocks wv, wv + 4, ...
@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
           for (int t = 0; t < kEPad / 4; ++t) {
             const int u = u0 + 4 * t + (lane >> 4);
             bv[t] = tcol[(size_t)L.list[u] * C];
-            av[t] = (float)gi[(lane & 15) * kECorr + u] * unit_g;
+            av[t] = reinterpret_cast<const float*>(gi)[(lane & 15) * kECorr + u];
           }
 #pragma unroll
           for (int t = 0; t < kEPad / 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], acc, 0, 0, 0);
@@ -1215,7 +1215,7 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
 #pragma unroll
         for (int k0 = 0; k0 < EG; k0 += 4) {
           const int u = ub * 16 + (lane & 15), p = k0 + (lane >> 4);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[p * kECorr + u] * unit_g,
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(reinterpret_cast<const float*>(gi)[p * kECorr + u],
                                                      L.aref[p * (C + 4) + cbk * 16 + (lane & 15)], acc, 0, 0, 0);
         }
 #pragma unroll
