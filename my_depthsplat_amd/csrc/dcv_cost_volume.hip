@@ -19,6 +19,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 namespace {
 
@@ -616,19 +617,16 @@ struct EpiLds {
   uint2* wb;        // [NWx] {tapped positions, exclusive popcount prefix} per word
   int* nzw;         // [NWx] the non-zero words of bm, ascending
   int* list;        // [kEUMax] image pixel of each band position of the current pass (-1: outside)
-  float* corr;      // [EG][kECorr] correlations (forward) / gradient weights (backward)
-  float* dacc;      // [EG][C + 4] reference gradients (backward)
+  float* corr;      // [EG][kECorr] correlations (forward) / [EGW][kECorrB] gradient weights (backward)
   uint32_t* misc;   // [32]: scan partials, totals, the band box
 };
 __host__ __device__ constexpr int epi_words(int H, int W) { return ((W + 2) * (H + 2) + 31) / 32 + 1; }
-__device__ __forceinline__ EpiLds epi_lds(float* p, int C, int NWx, bool bwd) {
+__device__ __forceinline__ EpiLds epi_lds(float* p, int C, int NWx) {
   EpiLds L;
   L.aref = p;
   p += EG * (C + 4);
   L.corr = p;
   p += EG * kECorr;
-  L.dacc = p;
-  p += bwd ? EG * (C + 4) : 0;
   L.list = reinterpret_cast<int*>(p);
   p += kEUMax;
   L.base = reinterpret_cast<uint32_t*>(p);
@@ -641,16 +639,16 @@ __device__ __forceinline__ EpiLds epi_lds(float* p, int C, int NWx, bool bwd) {
   L.misc = reinterpret_cast<uint32_t*>(p);
   return L;
 }
-size_t epi_lds_bytes(int C, int H, int W, bool bwd) {
-  return sizeof(float) * ((size_t)EG * (C + 4) * (bwd ? 2 : 1) + EG * kECorr + kEUMax + 4 * epi_words(H, W) + 1 + 32);
+size_t epi_lds_bytes(int C, int H, int W) {
+  return sizeof(float) * ((size_t)EG * (C + 4) + EG * kECorr + kEUMax + 4 * epi_words(H, W) + 1 + 32);
 }
 
 // The group's reference tile [EG][C] into LDS from the channel-last copy (rows of 16-byte
 // vectors; a past-the-end pixel reads the zero row HW), loads issued together.
-template <int NK>
+template <int NK, int ROWS = EG>
 __device__ __forceinline__ void epi_aref(const EpiLds& L, int HW, int b, const int* gids,
                                          const float* __restrict__ ref_hwc) {
-  constexpr int C = 4 * NK, N4 = EG * C / 4, IT = (N4 + 255) / 256;
+  constexpr int C = 4 * NK, N4 = ROWS * C / 4, IT = (N4 + 255) / 256;
   float4 v[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -764,23 +762,27 @@ __device__ __forceinline__ int epi_local(const EpiBox& bx, int es) {
 //                contiguous run of words, its popcount prefix (wave scans) and the non-zero
 //                words; returns U (band positions). Two barriers.
 // es[s]: local index of sample s's top-left tap (-1: zero sample).
-template <int SPT>
+// PXB: log2 of the pixels per depth slot (4: 16-pixel groups, thread t has pixel t & 15 and
+// depths d0 + (t >> 4) + 16 s; 6: the backward's 64-pixel groups, depths d0 + (t >> 6) + 4 s)
+template <int SPT, int PXB = 4>
 __device__ __forceinline__ void epi_depths(int HW, int D, int depth_per_pixel, int b, int d0, int pix,
                                            const float* __restrict__ depth, float (&dep)[SPT]) {
-  const int dl = threadIdx.x >> 4;
+  constexpr int DST = 256 >> PXB;
+  const int dl = threadIdx.x >> PXB;
   const float* dp = depth + (size_t)b * D * (depth_per_pixel ? HW : 1);
   const int dstride = depth_per_pixel ? HW : 1, pc = depth_per_pixel ? max(pix, 0) : 0;
 #pragma unroll
-  for (int s = 0; s < SPT; ++s) dep[s] = dp[(uint32_t)(min(d0 + dl + 16 * s, D - 1) * dstride + pc)];
+  for (int s = 0; s < SPT; ++s) dep[s] = dp[(uint32_t)(min(d0 + dl + DST * s, D - 1) * dstride + pc)];
 }
-template <int SPT>
+template <int SPT, int PXB = 4>
 __device__ __forceinline__ void epi_taps(int H, int W, int D, int d0, int pix, const EpiRay& ry,
                                          const float (&dep)[SPT], float clampz, float (&sx)[SPT], float (&sy)[SPT],
                                          int (&es)[SPT]) {
-  const int dl = threadIdx.x >> 4;
+  constexpr int DST = 256 >> PXB;
+  const int dl = threadIdx.x >> PXB;
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
-    const int d = d0 + dl + 16 * s;
+    const int d = d0 + dl + DST * s;
     es[s] = epi_sample(ry, dep[s], clampz, H, W, sx[s], sy[s]);
     if (pix < 0 || d >= D) es[s] = -1;
   }
@@ -847,14 +849,14 @@ __device__ __forceinline__ void epi_clear_words(const EpiLds& L, int nw) {
 // the steps for one depth chunk with their own barriers (the backward's per-chunk loop); the
 // base words of the previous chunk's box (nw_prev, the whole image before the first) are
 // cleared before the box barrier
-template <int SPT>
+template <int SPT, int PXB>
 __device__ __forceinline__ int epi_front(const EpiLds& L, int H, int W, int HW, int D, int depth_per_pixel, int b,
                                          int d0, int pix, const EpiRay& ry, const float* __restrict__ depth,
                                          float clampz, float (&sx)[SPT], float (&sy)[SPT], int (&es)[SPT],
                                          EpiBox& bx, int nw_prev) {
   float dep[SPT];
-  epi_depths<SPT>(HW, D, depth_per_pixel, b, d0, pix, depth, dep);
-  epi_taps<SPT>(H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
+  epi_depths<SPT, PXB>(HW, D, depth_per_pixel, b, d0, pix, depth, dep);
+  epi_taps<SPT, PXB>(H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
   epi_clear_words(L, nw_prev);
   bx = epi_box<SPT>(L, es);
   epi_mark<SPT>(L, bx, es);
@@ -911,7 +913,7 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
   const int HW = H * W, ngroups = (HW + EG - 1) / EG;
   int b, g;
   if (!epi_item(B, ngroups, b, g)) return;
-  const EpiLds L = epi_lds(cv_lds, C, epi_words(H, W), false);
+  const EpiLds L = epi_lds(cv_lds, C, epi_words(H, W));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int i = tid & (EG - 1), dl = tid >> 4, d0 = blockIdx.y * 16 * SPT;
   const size_t bj = (size_t)b * J + j;
@@ -1028,9 +1030,11 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
 // several writers share are now integer (fixed point), whose result does not depend on order:
 //   * G[p][u] (LDS): each add is dcost * scale * w rounded to units of 2^(kg - 23), kg the
 //     exponent of the largest |dcost * scale| of the workgroup's depth chunk; an element takes at
-//     most 16 SPT <= 128 adds of <= 2^23 units, so int32 never overflows;
+//     most (256 >> PXB) SPT <= 128 adds of <= 2^23 units (one per sample of its pixel in the
+//     chunk), so int32 never overflows;
 //   * dtgt (HBM): each workgroup's MFMA partial G^T aref (a fixed-order float) rounded to units
-//     of 2^(kt - 40), 2^kt bounding one partial (16 x 16 SPT x max|dcost scale| x max|ref|, from
+//     of 2^(kt - 40), 2^kt bounding one partial (2^PXB pixels x (256 >> PXB) SPT samples each =
+//     256 SPT x max|dcost scale| x max|ref|, from
 //     the per-block maxima of k_cv_absmax, the same in every workgroup), added as int64: 2^23
 //     partials of the bound fit. k_fx_to_chw converts the sum back to float while transposing.
 // dref needs none of this: each element has one writer (its pixel's group, views in launch order).
@@ -1098,14 +1102,50 @@ __device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, floa
   return ldexpf(1.f, max(e, -80) - 40);
 }
 
-// Backward, view j (grid.x as the forward; depth chunks looped inside): per group the gradient
-// weights G[p][u] = sum over its samples' taps of dcost * scale * w (LDS, fixed point), then
-// dref[p] += G[p, :] . tgt[band]  (MFMA, K = band) and dtgt[band] += G^T . aref  (MFMA,
-// K = 16 pixels; target pixels are shared between groups: int64 fixed-point atomics).
+// Backward, view j, on groups of 2^PXB reference pixels (round 5): 16 (a group of
+// k_epi_groups' order), or 32 / 64 = 2 / 4 consecutive groups (neighbours along one epipolar
+// line, whose target bands overlap), depth chunks of (256 >> PXB) x SPT looped inside. Thread t
+// has pixel t & (2^PXB - 1) and depths d0 + (t >> PXB) + (256 >> PXB) s. Per chunk the gradient
+// weights G[p][u] = sum over p's samples' taps of dcost * scale * w (LDS, fixed point) over the
+// union band of the workgroup's pixels, then
+//   dref[p] += G[p, :] . tgt[band]   (MFMA, K = band; registers across passes and chunks)
+//   dtgt[band] += G^T . aref         (MFMA, K = 2^PXB pixels; int64 fixed-point atomics).
+// The dtgt atomics were the backward's largest cost (same-box A/B with them removed: config D
+// scale 0 fwd + bwd 2.23 -> 1.34 ms, profiles/r05j_ab_cvbwd_atomics.log); a wider group issues
+// them once per union position instead of once per group and position, at the price of GEMM
+// work over the union band and fewer workgroups (bwd_pxb picks the width per shape).
 // dref_hwc [B][HW][C] is written (view 0) or added to (views after it, in launch order): each
 // pixel is in exactly one group per view. cvmax: k_cv_absmax's per-block maxima (dcost, ref).
-template <int NK, int SPT>
-__global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
+constexpr int kEGWMax = 64;             // widest backward group
+template <int PXB>
+constexpr int bwd_band() { return PXB == 6 ? 128 : 256; }  // band positions per pass (LDS)
+static_assert(bwd_band<4>() <= kEUMax && bwd_band<6>() <= kEUMax, "the band list holds a pass");
+template <int PXB>
+__device__ __forceinline__ EpiLds epi_lds_wide(float* p, int C, int NWx) {
+  constexpr int EGW = 1 << PXB, kECorrB = bwd_band<PXB>() + 1;
+  EpiLds L;
+  L.aref = p;
+  p += EGW * (C + 4);
+  L.corr = p;
+  p += EGW * kECorrB;
+  L.list = reinterpret_cast<int*>(p);
+  p += kEUMax;
+  L.base = reinterpret_cast<uint32_t*>(p);
+  p += NWx;
+  p += (NWx & 1);
+  L.wb = reinterpret_cast<uint2*>(p);
+  p += 2 * NWx;
+  L.nzw = reinterpret_cast<int*>(p);
+  p += NWx;
+  L.misc = reinterpret_cast<uint32_t*>(p);
+  return L;
+}
+size_t epi_lds_bytes_wide(int pxb, int C, int H, int W) {
+  const size_t egw = (size_t)1 << pxb, corr = (pxb == 6 ? 128 : 256) + 1;
+  return sizeof(float) * (egw * (C + 4) + egw * corr + kEUMax + 4 * epi_words(H, W) + 1 + 32);
+}
+template <int NK, int PXB, int SPT>
+__global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
                                                       int accumulate, const float* __restrict__ ref_hwc,
                                                       const float* __restrict__ tgt_hwc,
                                                       const int* __restrict__ groups, const float* __restrict__ geom,
@@ -1113,44 +1153,51 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
                                                       float clampz, float scale, const float* __restrict__ dcost,
                                                       const float* __restrict__ cvmax,
                                                       float* __restrict__ dref_hwc, long long* __restrict__ dtgt_fx) {
-  constexpr int C = 4 * NK;
+  constexpr int C = 4 * NK, NCB = (C / 16 + 3) / 4;  // channel blocks per wave (dref)
+  constexpr int EGW = 1 << PXB, MB = EGW / 16, DSL = 256 >> PXB;  // pixels, row blocks, depth slots
+  constexpr int kEUMaxB = bwd_band<PXB>(), kECorrB = kEUMaxB + 1;
   extern __shared__ __attribute__((aligned(16))) float cv_lds[];
-  const int HW = H * W, ngroups = (HW + EG - 1) / EG;
+  const int HW = H * W, ngw = (HW + EGW - 1) / EGW;
   int b, g;
-  if (!epi_item(B, ngroups, b, g)) return;
-  const EpiLds L = epi_lds(cv_lds, C, epi_words(H, W), true);
+  if (!epi_item(B, ngw, b, g)) return;
+  const EpiLds L = epi_lds_wide<PXB>(cv_lds, C, epi_words(H, W));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int i = tid & (EG - 1), dl = tid >> 4;
   const size_t bj = (size_t)b * J + j;
   const float unit_t = cv_dtgt_unit(cvmax, scale, SPT);
   const float unit_t_inv = unit_t > 0.f ? 1.f / unit_t : 0.f;  // exact: a power of 2
-  __shared__ int s_gid[EG];
+  __shared__ int s_gid[kEGWMax];
   __shared__ float s_gmax[4];
-  if (tid < EG) s_gid[tid] = g * EG + tid < HW ? groups[bj * HW + g * EG + tid] : -1;
-  for (int k = tid; k < EG * (C + 4); k += 256) L.dacc[k] = 0.f;
+  if (tid < EGW) s_gid[tid] = g * EGW + tid < HW ? groups[bj * HW + g * EGW + tid] : -1;
   __syncthreads();
-  epi_aref<NK>(L, HW, b, s_gid, ref_hwc);
+  epi_aref<NK, EGW>(L, HW, b, s_gid, ref_hwc);
+  const int i = tid & (EGW - 1), dl = tid >> PXB;
   const int pix = s_gid[i];
   const EpiRay ry = epi_ray(geom + bj * 12, pix >= 0 ? (float)(pix % W) : 0.f, pix >= 0 ? (float)(pix / W) : 0.f);
   const float* tg = tgt_hwc + bj * (size_t)(HW + 1) * C;
   long long* dtg = dtgt_fx + bj * (size_t)(HW + 1) * C;
-  int* gi = reinterpret_cast<int*>(L.corr);  // G in fixed point
+  int* gi = reinterpret_cast<int*>(L.corr);  // G in fixed point, [EGW][kECorrB]
+  f32x4 dacc[NCB][MB];
+#pragma unroll
+  for (int q = 0; q < NCB; ++q)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) dacc[q][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
   int nw_prev = epi_words(H, W);
-  for (int d0 = 0; d0 < D; d0 += 16 * SPT) {  // depth chunks in turn: dacc is this workgroup's alone
+  for (int d0 = 0; d0 < D; d0 += DSL * SPT) {  // depth chunks in turn
     float gs[SPT];
     {
       const float* gp = dcost + (size_t)b * D * HW;
 #pragma unroll
-      for (int s = 0; s < SPT; ++s) gs[s] = gp[(uint32_t)(min(d0 + dl + 16 * s, D - 1) * HW + max(pix, 0))];
+      for (int s = 0; s < SPT; ++s) gs[s] = gp[(uint32_t)(min(d0 + dl + DSL * s, D - 1) * HW + max(pix, 0))];
     }
     float sx[SPT], sy[SPT];
     int es[SPT];
     EpiBox bx;
-    const int U = epi_front<SPT>(L, H, W, HW, D, depth_per_pixel, b, d0, pix, ry, depth, clampz, sx, sy, es, bx,
-                                 nw_prev);
+    const int U = epi_front<SPT, PXB>(L, H, W, HW, D, depth_per_pixel, b, d0, pix, ry, depth, clampz, sx, sy, es, bx,
+                                      nw_prev);
     nw_prev = bx.nw;
     const int Wx = bx.wb;
-    // the chunk's fixed-point unit: 2^(kg - 23), |dcost scale| <= 2^kg over its samples
+    // the chunk's fixed-point unit: 2^(kg - 23), |dcost scale| <= 2^kg over its samples; an
+    // element of G takes at most DSL SPT <= 128 adds of <= 2^23 units
     float gm = 0.f;
 #pragma unroll
     for (int s = 0; s < SPT; ++s) {
@@ -1160,9 +1207,9 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) gm = fmaxf(gm, __shfl_xor(gm, off, 64));
     if (lane == 0) s_gmax[wv] = gm;
-    for (int r0 = 0; r0 < U; r0 += kEUMax) {
-      const int n = min(kEUMax, U - r0), np = epi_padded(n);
-      for (int k = tid; k < EG * np; k += 256) gi[(k & (EG - 1)) * kECorr + (k >> 4)] = 0;
+    for (int r0 = 0; r0 < U; r0 += kEUMaxB) {
+      const int n = min(kEUMaxB, U - r0), np = epi_padded(n);
+      for (int k = tid; k < EGW * np; k += 256) gi[(k & (EGW - 1)) * kECorrB + (k >> PXB)] = 0;
       epi_list(L, H, W, bx, r0, n);
       __syncthreads();
       gm = fmaxf(fmaxf(s_gmax[0], s_gmax[1]), fmaxf(s_gmax[2], s_gmax[3]));
@@ -1170,6 +1217,7 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
       frexpf(gm, &ke);
       const float unit_g = (gm > 0.f && gm <= 3.0e38f) ? ldexpf(1.f, max(ke, -100) - 23) : 0.f;
       const float unit_g_inv = unit_g > 0.f ? 1.f / unit_g : 0.f;
+      int* grow = gi + i * kECorrB;
 #pragma unroll
       for (int s = 0; s < SPT; ++s) {
         if (gs[s] == 0.f) continue;
@@ -1179,7 +1227,6 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
         const float fx0 = floorf(x), fy0 = floorf(y);
         const float wx0 = (fx0 + 1.f) - x, wx1 = x - fx0, wy0 = (fy0 + 1.f) - y, wy1 = y - fy0;
         const int ra = epi_rank(L, e) - r0, rb = epi_rank(L, e + Wx) - r0;
-        int* grow = gi + i * kECorr;
         const float gu = gs[s] * unit_g_inv;
         if (ra >= 0 && ra < n) atomicAdd(&grow[ra], (int)rintf(gu * (wx0 * wy0)));
         if (ra + 1 >= 0 && ra + 1 < n) atomicAdd(&grow[ra + 1], (int)rintf(gu * (wx1 * wy0)));
@@ -1187,35 +1234,36 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
         if (rb + 1 >= 0 && rb + 1 < n) atomicAdd(&grow[rb + 1], (int)rintf(gu * (wx1 * wy1)));
       }
       __syncthreads();
-      // dref[16 x C] += G[16 x np] . tgt[np x C]: wave wv owns channel blocks wv, wv + 4, ...
-      // (one writer per element: a fixed summation order); 32 band positions (8 MFMAs) per
-      // batch of loads
-      for (int cbk = wv; cbk < C / 16; cbk += 4) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      // dref[EGW x C] += G[EGW x np] . tgt[np x C]: wave wv owns channel blocks wv, wv + 4, ...
+      // for all MB row blocks (one target load feeds MB MFMAs); 32 band positions per batch
+#pragma unroll
+      for (int q = 0; q < NCB; ++q) {
+        const int cbk = wv + 4 * q;
+        if (cbk >= C / 16) break;  // wave-uniform
         const float* tcol = tg + cbk * 16 + (lane & 15);
         for (int u0 = 0; u0 < np; u0 += kEPad) {
-          float av[kEPad / 4], bv[kEPad / 4];
+          float bv[kEPad / 4];
+#pragma unroll
+          for (int t = 0; t < kEPad / 4; ++t) bv[t] = tcol[(size_t)L.list[u0 + 4 * t + (lane >> 4)] * C];
 #pragma unroll
           for (int t = 0; t < kEPad / 4; ++t) {
             const int u = u0 + 4 * t + (lane >> 4);
-            bv[t] = tcol[(size_t)L.list[u] * C];
-            av[t] = (float)gi[(lane & 15) * kECorr + u] * unit_g;
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb)
+              dacc[q][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[(mb * 16 + (lane & 15)) * kECorrB + u] * unit_g,
+                                                                 bv[t], dacc[q][mb], 0, 0, 0);
           }
-#pragma unroll
-          for (int t = 0; t < kEPad / 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], acc, 0, 0, 0);
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) L.dacc[(4 * (lane >> 4) + r) * (C + 4) + cbk * 16 + (lane & 15)] += acc[r];
       }
-      // dtgt[n x C] += G^T[n x 16] . aref[16 x C]: (band block, channel block) pairs over the waves
+      // dtgt[n x C] += G^T[n x EGW] . aref[EGW x C]: (band block, channel block) pairs over the waves
       const int nub = np / 16;
       for (int pr = wv; pr < nub * (C / 16); pr += 4) {
         const int ub = pr / (C / 16), cbk = pr - ub * (C / 16);
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k0 = 0; k0 < EG; k0 += 4) {
+        for (int k0 = 0; k0 < EGW; k0 += 4) {
           const int u = ub * 16 + (lane & 15), p = k0 + (lane >> 4);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[p * kECorr + u] * unit_g,
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[p * kECorrB + u] * unit_g,
                                                      L.aref[p * (C + 4) + cbk * 16 + (lane & 15)], acc, 0, 0, 0);
         }
 #pragma unroll
@@ -1229,22 +1277,25 @@ __global__ __launch_bounds__(256, 3) void k_cost_epi_bwd(int B, int j, int J, in
           }
         }
       }
-      __syncthreads();  // corr / list / dacc rows reused by the next pass
+      __syncthreads();  // G / list reused by the next pass
     }
     if (U == 0) __syncthreads();  // s_gmax of this chunk read by every wave before the next writes it
   }
-  // the group's reference-gradient rows, channel-last (16-byte vectors)
-  for (int k = tid; k < EG * C / 4; k += 256) {
-    const int r = k / (C / 4), c4 = k - r * (C / 4), p = s_gid[r];
-    if (p < 0) continue;
-    const float4 v = *reinterpret_cast<const float4*>(L.dacc + r * (C + 4) + 4 * c4);
-    float4* o = reinterpret_cast<float4*>(dref_hwc + ((size_t)b * HW + p) * C + 4 * c4);
-    if (accumulate) {
-      const float4 o0 = *o;
-      *o = make_float4(o0.x + v.x, o0.y + v.y, o0.z + v.z, o0.w + v.w);
-    } else {
-      *o = v;
-    }
+  // the group's reference-gradient rows, channel-last: dacc[q][mb][r] is row
+  // 16 mb + 4 (lane >> 4) + r, channel 16 (wv + 4 q) + (lane & 15)
+#pragma unroll
+  for (int q = 0; q < NCB; ++q) {
+    const int cbk = wv + 4 * q;
+    if (cbk >= C / 16) break;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = s_gid[mb * 16 + 4 * (lane >> 4) + r];
+        if (p < 0) continue;
+        float* o = dref_hwc + ((size_t)b * HW + p) * C + cbk * 16 + (lane & 15);
+        *o = accumulate ? *o + dacc[q][mb][r] : dacc[q][mb][r];
+      }
   }
 }
 
@@ -1628,8 +1679,22 @@ size_t dcv_cost_volume_bwd_workspace_size(int B, int J, int C, int H, int W) {
          2 * kCvMaxBlocks * sizeof(float);
 }
 
+// backward group width (log2 pixels) and samples per thread (depth chunk = (256 >> pxb) spt)
+struct BwdShape {
+  int pxb, spt;
+};
+// Same-box A/B (profiles/r05n_ab_cvbwd_width.log, fwd + bwd ms, widths 16 / 32 / 64):
+// config D scale 1 (per-pixel candidates, D = 32) 3.38 / 3.15 / 3.00; scale 0 (per-image,
+// D = 128: every group's band is a long stretch of its line, the union grows almost as fast as
+// the pixels) 2.25 / 2.18 / 2.79; config B (512 groups: a wide group underfills the chip) best
+// at 16.
+static BwdShape bwd_shape(int B, int H, int W, int D, int depth_per_pixel) {
+  const int64_t groups16 = (int64_t)B * ((H * W + 15) / 16);
+  if (groups16 < 4096) return {4, D <= 32 ? 2 : 8};
+  return {depth_per_pixel ? 6 : 5, 8};
+}
 static bool epi_path(int C, int H, int W, bool bwd) {
-  return C % 16 == 0 && C <= 128 && epi_lds_bytes(C, H, W, bwd) <= 160 * 1024;
+  return C % 16 == 0 && C <= 128 && (bwd ? epi_lds_bytes_wide(6, C, H, W) : epi_lds_bytes(C, H, W)) <= 160 * 1024;
 }
 
 // Small grids take the band kernel for the forward: one launch with no channel-last copies
@@ -1725,7 +1790,7 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
   float* geom = reinterpret_cast<float*>(groups + (size_t)B * J * HW);
   const float scale = 1.0f / (sqrtf((float)C) * (float)J);
   if (path == DCV_PATH_EPI) {
-    const size_t lds = epi_lds_bytes(C, H, W, false);
+    const size_t lds = epi_lds_bytes(C, H, W);
 #define DCV_ATTR(NK, SPT)                                                                                       \
   if (int e = dsplat::ensure_dyn_lds((const void*)k_cost_epi<NK, SPT>, lds, "hipFuncSetAttribute(k_cost_epi)")) return e;
     DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
@@ -1779,36 +1844,39 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
   const bool epi = epi_path(C, H, W, true) && epi_path(C, H, W, false);
   if (int e = dsplat::zero_async(dtgt_fx, ntg * (epi ? sizeof(long long) : sizeof(float)), st, "zero dtgt")) return e;
   const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-  const int spt = D <= 32 ? 2 : 8;
   if (epi) {
     k_cv_absmax<<<kCvMaxBlocks, 256, 0, st>>>((size_t)B * D * HW, dcost, (size_t)B * C * HW, ref, cvmax);
     if (int e = dsplat::check_launch("k_cv_absmax")) return e;
-    const size_t lds = epi_lds_bytes(C, H, W, true);
-#define DCV_ATTR(NK, SPT)                                                                                       \
-  if (int e = dsplat::ensure_dyn_lds((const void*)k_cost_epi_bwd<NK, SPT>, lds, "hipFuncSetAttribute(k_cost_epi_bwd)")) return e;
-    DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
-    DCV_ATTR(4, 8) DCV_ATTR(8, 8) DCV_ATTR(16, 8) DCV_ATTR(32, 8)
-#undef DCV_ATTR
-    const int ngroups = (HW + EG - 1) / EG;
-    const dim3 grid(8u * (unsigned)((B * ngroups + 7) / 8));
+    const BwdShape bs = bwd_shape(B, H, W, D, depth_per_pixel);
+    const size_t lds = epi_lds_bytes_wide(bs.pxb, C, H, W);
+    const int ngw = (HW + (1 << bs.pxb) - 1) >> bs.pxb;
+    const dim3 grid(8u * (unsigned)((B * ngw + 7) / 8));
+    // one instance per (C, width, samples per thread)
+    auto kern = [&](auto nk) -> const void* {
+      constexpr int NK = decltype(nk)::value;
+      if (bs.pxb == 6) return (const void*)k_cost_epi_bwd<NK, 6, 8>;
+      if (bs.pxb == 5) return (const void*)k_cost_epi_bwd<NK, 5, 8>;
+      return bs.spt == 2 ? (const void*)k_cost_epi_bwd<NK, 4, 2> : (const void*)k_cost_epi_bwd<NK, 4, 8>;
+    };
+    const void* f = C == 16 ? kern(std::integral_constant<int, 4>{})
+                  : C == 32 ? kern(std::integral_constant<int, 8>{})
+                  : C == 64 ? kern(std::integral_constant<int, 16>{})
+                            : kern(std::integral_constant<int, 32>{});
+    if (int e = dsplat::ensure_dyn_lds(f, lds, "hipFuncSetAttribute(k_cost_epi_bwd)")) return e;
     for (int j = 0; j < J; ++j) {
-#define DCV_EPIB(NK)                                                                                           \
-  (spt == 2 ? k_cost_epi_bwd<NK, 2> : k_cost_epi_bwd<NK, 8>)<<<grid, 256, lds, st>>>(B, j, J, H, W, D, depth_per_pixel, j > 0, ref_hwc, tgt_hwc, groups, \
-                                             geom, depth, clamp_min_depth, scale, dcost, cvmax, dref_hwc, dtgt_fx)
-      switch (C) {
-        case 16: DCV_EPIB(4); break;
-        case 32: DCV_EPIB(8); break;
-        case 64: DCV_EPIB(16); break;
-        default: DCV_EPIB(32); break;
-      }
-#undef DCV_EPIB
-      if (int e = dsplat::check_launch("k_cost_epi_bwd")) return e;
+      int a_j = j, a_acc = j > 0;
+      int a_B = B, a_J = J, a_H = H, a_W = W, a_D = D, a_dpp = depth_per_pixel;
+      float a_clamp = clamp_min_depth, a_scale = scale;
+      void* args[] = {&a_B, &a_j, &a_J, &a_H, &a_W, &a_D, &a_dpp, &a_acc, (void*)&ref_hwc, (void*)&tgt_hwc,
+                      (void*)&groups, (void*)&geom, (void*)&depth, &a_clamp, &a_scale, (void*)&dcost, (void*)&cvmax,
+                      (void*)&dref_hwc, (void*)&dtgt_fx};
+      if (int e = dsplat::check_hip(hipLaunchKernel(f, grid, dim3(256), args, lds, st), "k_cost_epi_bwd")) return e;
     }
     (C % 4 == 0 && HW % 4 == 0 && aligned16(dref) && aligned16(bwd_workspace) ? k_to_chw4 : k_to_chw)<<<
         dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW, dref_hwc, dref);
     if (int e = dsplat::check_launch("k_to_chw(dref)")) return e;
-    k_fx_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_fx, cvmax, scale, spt,
-                                                                          dtgt);
+    k_fx_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_fx, cvmax, scale,
+                                                                          bs.spt, dtgt);
     return dsplat::check_launch("k_fx_to_chw");
   }
   float* dtgt_hwc = reinterpret_cast<float*>(dtgt_fx);
