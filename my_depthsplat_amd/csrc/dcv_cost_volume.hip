@@ -355,15 +355,22 @@ __device__ __forceinline__ int epi_bucket(const EpiKey& k, float px, float py) {
 // grouping at all: each output is computed from its own correlations.)
 // Also writes geom[b, j] = {M = K R K^-1 (row-major), K t} (double, rounded once): the
 // projection of reference pixel p at depth d is M [px, py, 1] d + K t (see epi_ray).
-constexpr int kEpiKeyMaxPixels = 24576;  // larger images (pixel id in 15 bits, keys in registers): lines only
+// larger images (pixel id in 15 bits, keys in registers, the scattered pixels staged in LDS
+// with the two line tables: 160 KB): lines only
+constexpr int kEpiPool = 3 * kEpiBuckets - 32;
+constexpr int kEpiKeyMaxPixels = kEpiPool;
 __global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, int D, int depth_per_pixel,
                                                      const float* __restrict__ intr, const float* __restrict__ pose,
                                                      const float* __restrict__ depth, int* __restrict__ groups,
                                                      float* __restrict__ geom) {
   __shared__ uint32_t hist[kEpiBuckets];  // line counts, then segment-bin counters
-  __shared__ uint32_t bst[kEpiBuckets];   // first segment bin of each line
   __shared__ uint32_t lmin[kEpiBuckets];  // per line: key minimum (orderable bits), then the bins' starts
-  __shared__ uint32_t lmax[kEpiBuckets];  // per line: key maximum
+  // bst (first segment bin of each line) and lmax (per line: key maximum), then the pixels
+  // scattered by bin (read back by the in-bin ranking: LDS instead of a global round trip per
+  // comparison, which made this kernel 204 us at config D scale 1)
+  __shared__ uint32_t pool[kEpiPool];
+  uint32_t* const bst = pool;
+  uint32_t* const lmax = pool + kEpiBuckets;
   __shared__ float s_geom[12];
   __shared__ uint32_t wsum[16];
   const int b = blockIdx.x, j = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -504,7 +511,7 @@ __global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, int D,
   };
   auto ofloat = [](uint32_t o) -> float { return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o); };
   // 1) per line: count, key min / max (the keys are kept in registers)
-  constexpr int PER = kEpiKeyMaxPixels / 1024;
+  constexpr int PER = (kEpiKeyMaxPixels + 1023) / 1024;
   const bool sorted = HW <= kEpiKeyMaxPixels;  // uniform
   for (int i = tid; i < kEpiBuckets; i += 1024) {
     hist[i] = 0u;
@@ -568,29 +575,22 @@ __global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, int D,
   scan8k(hist, lmin);  // lmin: the bins' starts (hist: their ends after the scatter)
 #pragma unroll
   for (int t = 0; t < PER; ++t)
-    if (tid + 1024 * t < HW) out[atomicAdd(&hist[bin[t]], 1u)] = (bin[t] << 15) | (tid + 1024 * t);
+    if (tid + 1024 * t < HW) pool[atomicAdd(&hist[bin[t]], 1u)] = (bin[t] << 15) | (tid + 1024 * t);
   __syncthreads();
   // 4) inside each bin (~16 pixels) the pixels in id order, so the groups never depend on the
   //    scatter's arrival order (the backward's MFMA blocking, hence its bits, are the same
   //    every run)
-  int pv[PER], rk[PER];
-#pragma unroll
+#pragma unroll 4
   for (int t = 0; t < PER; ++t) {
     const int pos = tid + 1024 * t;
-    rk[t] = -1;
     if (pos < HW) {
-      const int v = out[pos], bn = v >> 15, pp = v & 0x7FFF;
+      const int v = (int)pool[pos], bn = v >> 15, pp = v & 0x7FFF;
       const int st = (int)lmin[bn], en = (int)hist[bn];
       int r = 0;
-      for (int q = st; q < en; ++q) r += (out[q] & 0x7FFF) < pp ? 1 : 0;
-      pv[t] = pp;
-      rk[t] = st + r;
+      for (int q = st; q < en; ++q) r += (int)(pool[q] & 0x7FFFu) < pp ? 1 : 0;
+      out[st + r] = pp;
     }
   }
-  __syncthreads();  // every read of out[] above before the writes below
-#pragma unroll
-  for (int t = 0; t < PER; ++t)
-    if (rk[t] >= 0) out[rk[t]] = pv[t];
 }
 
 // Shared set-up of the forward and backward group kernels: the workgroup's (b, group) with

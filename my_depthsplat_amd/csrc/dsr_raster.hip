@@ -1385,6 +1385,7 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
   for (int k = tid; k < gxp * gyp + nsb * kCutBuckets; k += NTH) s_mem[k] = 0u;
   __syncthreads();
   const dsr_camera* cam = cams + v;
+  const float2 focal = focal_of(cam, H, W);  // (two IEEE divisions, not re-done per block)
   const int nblk = (G + NTH - 1) / NTH;
   WaveRects& wr = s_wr[w];
   for (int blk = p; blk < nblk; blk += per_view) {  // round-robin blocks (see k_scatter_cut)
@@ -1397,8 +1398,7 @@ __global__ __launch_bounds__(NTH) void k_preprocess_cut(int G, int V, int H, int
       float rec[GS];
       // LAZY (deferred geometry): no colour, no record; dsr_project_survivors writes the
       // records of the Gaussians the depth-cut scatter keeps (a few % of them)
-      r = project_gauss<DEG, !LAZY>(in, cam, focal_of(cam, H, W), H, W, gx, gy, M, shs, colors, layout, rec, x0, y0,
-                                    x1, y1);
+      r = project_gauss<DEG, !LAZY>(in, cam, focal, H, W, gx, gy, M, shs, colors, layout, rec, x0, y0, x1, y1);
       if constexpr (LAZY)
         radii[(size_t)v * G + g] = r;
       else
