@@ -617,32 +617,10 @@ struct EpiLds {
   uint2* wb;        // [NWx] {tapped positions, exclusive popcount prefix} per word
   int* nzw;         // [NWx] the non-zero words of bm, ascending
   int* list;        // [kEUMax] image pixel of each band position of the current pass (-1: outside)
-  float* corr;      // [EG][kECorr] correlations (forward) / [EGW][kECorrB] gradient weights (backward)
+  float* corr;      // [2^PXB][band + 1] correlations (forward) / gradient weights (backward)
   uint32_t* misc;   // [32]: scan partials, totals, the band box
 };
 __host__ __device__ constexpr int epi_words(int H, int W) { return ((W + 2) * (H + 2) + 31) / 32 + 1; }
-__device__ __forceinline__ EpiLds epi_lds(float* p, int C, int NWx) {
-  EpiLds L;
-  L.aref = p;
-  p += EG * (C + 4);
-  L.corr = p;
-  p += EG * kECorr;
-  L.list = reinterpret_cast<int*>(p);
-  p += kEUMax;
-  L.base = reinterpret_cast<uint32_t*>(p);
-  p += NWx;
-  p += (NWx & 1);  // 8-byte alignment of wb (base and list above hold whole 4-byte words)
-  L.wb = reinterpret_cast<uint2*>(p);
-  p += 2 * NWx;
-  L.nzw = reinterpret_cast<int*>(p);
-  p += NWx;
-  L.misc = reinterpret_cast<uint32_t*>(p);
-  return L;
-}
-size_t epi_lds_bytes(int C, int H, int W) {
-  return sizeof(float) * ((size_t)EG * (C + 4) + EG * kECorr + kEUMax + 4 * epi_words(H, W) + 1 + 32);
-}
-
 // The group's reference tile [EG][C] into LDS from the channel-last copy (rows of 16-byte
 // vectors; a past-the-end pixel reads the zero row HW), loads issued together.
 template <int NK, int ROWS = EG>
@@ -898,46 +876,85 @@ __device__ __forceinline__ int epi_rank(const EpiLds& L, int e) {
   return (int)(w.y + __popc(w.x & ((1u << (e & 31)) - 1u)));
 }
 
-// Forward, view j: grid.x = 8 * ceil(B * ngroups / 8) (XCD-contiguous), grid.y = D chunks of
-// 16 * SPT. Writes (accumulate = 0) or adds (accumulate = 1: views after the first, launched in
-// view order, so the sum over views is deterministic) scale * sum_taps w * corr.
-// ref_hwc [B][HW + 1][C], tgt_hwc [B][J][HW + 1][C]: channel-last copies, row HW zero.
-template <int NK, int SPT>
-__global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
-                                                  int accumulate, const float* __restrict__ ref_hwc,
-                                                  const float* __restrict__ tgt_hwc, const int* __restrict__ groups,
-                                                  const float* __restrict__ geom, const float* __restrict__ depth,
-                                                  float clampz, float scale, float* __restrict__ cost) {
-  constexpr int C = 4 * NK;
+// Workgroups of 2^PXB reference pixels (round 5): 16 (one group of k_epi_groups' order) or
+// 32 / 64 (2 / 4 consecutive groups: neighbours along one epipolar line, whose target bands
+// overlap), their samples' bands merged into one. The band set-up (bitmap, box, word pass,
+// list), the target rows' loads and the barriers are then paid once per 2^PXB pixels; the
+// GEMM covers the union band.
+constexpr int kEGWMax = 64;             // widest backward group
+template <int PXB>
+constexpr int bwd_band() { return PXB == 6 ? 128 : 256; }  // band positions per pass (LDS)
+static_assert(bwd_band<4>() <= kEUMax && bwd_band<6>() <= kEUMax, "the band list holds a pass");
+template <int PXB>
+__device__ __forceinline__ EpiLds epi_lds_wide(float* p, int C, int NWx) {
+  constexpr int EGW = 1 << PXB, kECorrB = bwd_band<PXB>() + 1;
+  EpiLds L;
+  L.aref = p;
+  p += EGW * (C + 4);
+  L.corr = p;
+  p += EGW * kECorrB;
+  L.list = reinterpret_cast<int*>(p);
+  p += kEUMax;
+  L.base = reinterpret_cast<uint32_t*>(p);
+  p += NWx;
+  p += (NWx & 1);
+  L.wb = reinterpret_cast<uint2*>(p);
+  p += 2 * NWx;
+  L.nzw = reinterpret_cast<int*>(p);
+  p += NWx;
+  L.misc = reinterpret_cast<uint32_t*>(p);
+  return L;
+}
+size_t epi_lds_bytes_wide(int pxb, int C, int H, int W) {
+  const size_t egw = (size_t)1 << pxb, corr = (pxb == 6 ? 128 : 256) + 1;
+  return sizeof(float) * (egw * (C + 4) + egw * corr + kEUMax + 4 * epi_words(H, W) + 1 + 32);
+}
+// Forward, view j: grid.x = 8 * ceil(B * ngroups / 8) (XCD-contiguous, ngroups of 2^PXB
+// pixels), grid.y = D chunks of (256 >> PXB) * SPT. Thread t has pixel t & (2^PXB - 1) and
+// depths d0 + (t >> PXB) + (256 >> PXB) s. Writes (accumulate = 0) or adds (accumulate = 1:
+// views after the first, launched in view order, so the sum over views is deterministic)
+// scale * sum_taps w * corr. ref_hwc [B][HW + 1][C], tgt_hwc [B][J][HW + 1][C]: channel-last
+// copies, row HW zero.
+template <int NK, int SPT, int PXB>
+__global__ __launch_bounds__(256, PXB == 4 ? 4 : 2) void k_cost_epi(int B, int j, int J, int H, int W, int D,
+                                                                  int depth_per_pixel, int accumulate,
+                                                                  const float* __restrict__ ref_hwc,
+                                                                  const float* __restrict__ tgt_hwc,
+                                                                  const int* __restrict__ groups,
+                                                                  const float* __restrict__ geom,
+                                                                  const float* __restrict__ depth, float clampz,
+                                                                  float scale, float* __restrict__ cost) {
+  constexpr int C = 4 * NK, EGW = 1 << PXB, MB = EGW / 16, DSL = 256 >> PXB;
+  constexpr int kEU = bwd_band<PXB>(), kEC = kEU + 1;
   extern __shared__ __attribute__((aligned(16))) float cv_lds[];
-  const int HW = H * W, ngroups = (HW + EG - 1) / EG;
+  const int HW = H * W, ngw = (HW + EGW - 1) / EGW;
   int b, g;
-  if (!epi_item(B, ngroups, b, g)) return;
-  const EpiLds L = epi_lds(cv_lds, C, epi_words(H, W));
+  if (!epi_item(B, ngw, b, g)) return;
+  const EpiLds L = epi_lds_wide<PXB>(cv_lds, C, epi_words(H, W));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int i = tid & (EG - 1), dl = tid >> 4, d0 = blockIdx.y * 16 * SPT;
+  const int i = tid & (EGW - 1), dl = tid >> PXB, d0 = blockIdx.y * DSL * SPT;
   const size_t bj = (size_t)b * J + j;
-  __shared__ int s_gid[EG];
-  if (tid < EG) s_gid[tid] = g * EG + tid < HW ? groups[bj * HW + g * EG + tid] : -1;
+  __shared__ int s_gid[kEGWMax];
+  if (tid < EGW) s_gid[tid] = g * EGW + tid < HW ? groups[bj * HW + g * EGW + tid] : -1;
   epi_clear_words(L, epi_words(H, W));
   __syncthreads();
   // depth loads, then the reference tile's loads, all in flight together; the taps go into the
   // base bitmap of their box while the tile's LDS stores drain, and one barrier covers both
   const int pix = s_gid[i];  // -1: past the last pixel
   float dep[SPT];
-  epi_depths<SPT>(HW, D, depth_per_pixel, b, d0, pix, depth, dep);
-  epi_aref<NK>(L, HW, b, s_gid, ref_hwc);
+  epi_depths<SPT, PXB>(HW, D, depth_per_pixel, b, d0, pix, depth, dep);
+  epi_aref<NK, EGW>(L, HW, b, s_gid, ref_hwc);
   const EpiRay ry = epi_ray(geom + bj * 12, pix >= 0 ? (float)(pix % W) : 0.f, pix >= 0 ? (float)(pix / W) : 0.f);
   float sx[SPT], sy[SPT];
   int es[SPT];
-  epi_taps<SPT>(H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
+  epi_taps<SPT, PXB>(H, W, D, d0, pix, ry, dep, clampz, sx, sy, es);
   const EpiBox bx = epi_box<SPT>(L, es);
   epi_mark<SPT>(L, bx, es);
   __syncthreads();
   const int U = bx.nw ? epi_band(L, bx) : 0;
   const int Wx = bx.wb;
   // per sample: sum over its taps of grid_sample's weight x correlation, taps in a fixed order
-  // (a band of more than kEUMax positions takes several passes, each adding its taps)
+  // (a band of more than kEU positions takes several passes, each adding its taps)
   float* cb = cost + (size_t)b * D * HW;  // this scene's cost volume (< 2^32 elements)
   float acc[SPT], prev[SPT];
 #pragma unroll
@@ -946,40 +963,43 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
     int pc = max(pix, 0);
     asm volatile("" : "+v"(pc));  // addresses formed here, not hoisted (register pressure)
 #pragma unroll
-    for (int s = 0; s < SPT; ++s) prev[s] = cb[(uint32_t)(min(d0 + dl + 16 * s, D - 1) * HW + pc)];
+    for (int s = 0; s < SPT; ++s) prev[s] = cb[(uint32_t)(min(d0 + dl + DSL * s, D - 1) * HW + pc)];
   };
   const float* tg = tgt_hwc + bj * (size_t)(HW + 1) * C;
-  for (int r0 = 0; r0 < U; r0 += kEUMax) {
-    const int n = min(kEUMax, U - r0);
+  for (int r0 = 0; r0 < U; r0 += kEU) {
+    const int n = min(kEU, U - r0);
     epi_list(L, H, W, bx, r0, n);
     __syncthreads();
-    // corr[16 x n] = aref[16 x C] . tgt[n x C]^T; per 16-channel step lane l feeds channels
+    // corr[EGW x n] = aref[EGW x C] . tgt[n x C]^T; per 16-channel step lane l feeds channels
     // cb + 4 (l >> 4) + s to MFMA s (A and B permuted alike). The C / 16 row loads of a
-    // block are issued together.
+    // block are issued together and feed all MB row blocks.
     for (int blk = wv; blk * 16 < n; blk += 4) {
       const int u = blk * 16 + (lane & 15);
       const float* brow = tg + (size_t)L.list[u] * C + 4 * (lane >> 4);
       float4 bv[NK / 4];
 #pragma unroll
       for (int t = 0; t < NK / 4; ++t) bv[t] = *reinterpret_cast<const float4*>(brow + 16 * t);
-      const float* arow = L.aref + (lane & 15) * (C + 4) + 4 * (lane >> 4);
-      f32x4 c4[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int t = 0; t < NK / 4; ++t) {
-        const float4 av = *reinterpret_cast<const float4*>(arow + 16 * t);
-        f32x4& a4 = c4[t & 1];  // two independent accumulation chains
-        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[t].x, a4, 0, 0, 0);
-        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[t].y, a4, 0, 0, 0);
-        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[t].z, a4, 0, 0, 0);
-        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[t].w, a4, 0, 0, 0);
+      for (int mb = 0; mb < MB; ++mb) {
+        const float* arow = L.aref + (mb * 16 + (lane & 15)) * (C + 4) + 4 * (lane >> 4);
+        f32x4 c4[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int t = 0; t < NK / 4; ++t) {
+          const float4 av = *reinterpret_cast<const float4*>(arow + 16 * t);
+          f32x4& a4 = c4[t & 1];  // two independent accumulation chains
+          a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[t].x, a4, 0, 0, 0);
+          a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[t].y, a4, 0, 0, 0);
+          a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[t].z, a4, 0, 0, 0);
+          a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[t].w, a4, 0, 0, 0);
+        }
+        // D[row][col]: col = lane & 15 (band position u), row = 4 (lane >> 4) + r (pixel)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) L.corr[(mb * 16 + 4 * (lane >> 4) + r) * kEC + u] = c4[0][r] + c4[1][r];
       }
-      // D[row][col]: col = lane & 15 (band position u), row = 4 (lane >> 4) + r (reference pixel)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) L.corr[(4 * (lane >> 4) + r) * kECorr + u] = c4[0][r] + c4[1][r];
     }
     __syncthreads();
     if (r0 == 0 && accumulate) load_prev();  // the earlier views' sum, in flight across the gather
-    const float* crow = L.corr + i * kECorr;
+    const float* crow = L.corr + i * kEC;
     if (n == U) {
       // the one pass holds every tap: straight-line gather; a zero sample reads ranks 0 / 1
       // (written: the first 16 columns always are) with zero weights
@@ -1020,7 +1040,7 @@ __global__ __launch_bounds__(256, 4) void k_cost_epi(int B, int j, int J, int H,
   if (U == 0 && accumulate) load_prev();  // no pass ran: no tap of this group is inside view j
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
-    const int d = d0 + dl + 16 * s;
+    const int d = d0 + dl + DSL * s;
     if (d < D) cb[(uint32_t)(d * HW + pix)] = accumulate ? prev[s] + acc[s] * scale : acc[s] * scale;
   }
 }
@@ -1116,34 +1136,6 @@ __device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, floa
 // work over the union band and fewer workgroups (bwd_pxb picks the width per shape).
 // dref_hwc [B][HW][C] is written (view 0) or added to (views after it, in launch order): each
 // pixel is in exactly one group per view. cvmax: k_cv_absmax's per-block maxima (dcost, ref).
-constexpr int kEGWMax = 64;             // widest backward group
-template <int PXB>
-constexpr int bwd_band() { return PXB == 6 ? 128 : 256; }  // band positions per pass (LDS)
-static_assert(bwd_band<4>() <= kEUMax && bwd_band<6>() <= kEUMax, "the band list holds a pass");
-template <int PXB>
-__device__ __forceinline__ EpiLds epi_lds_wide(float* p, int C, int NWx) {
-  constexpr int EGW = 1 << PXB, kECorrB = bwd_band<PXB>() + 1;
-  EpiLds L;
-  L.aref = p;
-  p += EGW * (C + 4);
-  L.corr = p;
-  p += EGW * kECorrB;
-  L.list = reinterpret_cast<int*>(p);
-  p += kEUMax;
-  L.base = reinterpret_cast<uint32_t*>(p);
-  p += NWx;
-  p += (NWx & 1);
-  L.wb = reinterpret_cast<uint2*>(p);
-  p += 2 * NWx;
-  L.nzw = reinterpret_cast<int*>(p);
-  p += NWx;
-  L.misc = reinterpret_cast<uint32_t*>(p);
-  return L;
-}
-size_t epi_lds_bytes_wide(int pxb, int C, int H, int W) {
-  const size_t egw = (size_t)1 << pxb, corr = (pxb == 6 ? 128 : 256) + 1;
-  return sizeof(float) * (egw * (C + 4) + egw * corr + kEUMax + 4 * epi_words(H, W) + 1 + 32);
-}
 template <int NK, int PXB, int SPT>
 __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
                                                       int accumulate, const float* __restrict__ ref_hwc,
@@ -1679,10 +1671,17 @@ size_t dcv_cost_volume_bwd_workspace_size(int B, int J, int C, int H, int W) {
          2 * kCvMaxBlocks * sizeof(float);
 }
 
-// backward group width (log2 pixels) and samples per thread (depth chunk = (256 >> pxb) spt)
+// group width (log2 pixels) and samples per thread (depth chunk = (256 >> pxb) spt) of the
+// epipolar kernels
 struct BwdShape {
   int pxb, spt;
 };
+// The forward keeps 16-pixel groups: wider ones lost at every shape (same-box A/B,
+// profiles/r05r_ab_cvfwd_width.log, fwd ms at widths 16 / 32 / 64: config D scale 1
+// 0.855 / 1.11 / 1.12, scale 0 0.437 / 0.64 / 0.955): neighbouring groups' windows sit at
+// different places along their line, so the union band is close to the sum of the bands and
+// the GEMM and gather grow with it, while the set-up it saves is a small part of a workgroup.
+static BwdShape fwd_shape(int D) { return {4, D <= 32 ? 2 : 8}; }
 // Same-box A/B (profiles/r05n_ab_cvbwd_width.log, fwd + bwd ms, widths 16 / 32 / 64):
 // config D scale 1 (per-pixel candidates, D = 32) 3.38 / 3.15 / 3.00; scale 0 (per-image,
 // D = 128: every group's band is a long stretch of its line, the union grows almost as fast as
@@ -1694,7 +1693,8 @@ static BwdShape bwd_shape(int B, int H, int W, int D, int depth_per_pixel) {
   return {depth_per_pixel ? 6 : 5, 8};
 }
 static bool epi_path(int C, int H, int W, bool bwd) {
-  return C % 16 == 0 && C <= 128 && (bwd ? epi_lds_bytes_wide(6, C, H, W) : epi_lds_bytes(C, H, W)) <= 160 * 1024;
+  (void)bwd;  // (both directions fit the widest group's layout)
+  return C % 16 == 0 && C <= 128 && epi_lds_bytes_wide(6, C, H, W) <= 160 * 1024;
 }
 
 // Small grids take the band kernel for the forward: one launch with no channel-last copies
@@ -1790,27 +1790,30 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
   float* geom = reinterpret_cast<float*>(groups + (size_t)B * J * HW);
   const float scale = 1.0f / (sqrtf((float)C) * (float)J);
   if (path == DCV_PATH_EPI) {
-    const size_t lds = epi_lds_bytes(C, H, W);
-#define DCV_ATTR(NK, SPT)                                                                                       \
-  if (int e = dsplat::ensure_dyn_lds((const void*)k_cost_epi<NK, SPT>, lds, "hipFuncSetAttribute(k_cost_epi)")) return e;
-    DCV_ATTR(4, 2) DCV_ATTR(8, 2) DCV_ATTR(16, 2) DCV_ATTR(32, 2)
-    DCV_ATTR(4, 8) DCV_ATTR(8, 8) DCV_ATTR(16, 8) DCV_ATTR(32, 8)
-#undef DCV_ATTR
-    const int ngroups = (HW + EG - 1) / EG;
-    const int spt = D <= 32 ? 2 : 8;
-    const dim3 grid(8u * (unsigned)((B * ngroups + 7) / 8), (unsigned)((D + 16 * spt - 1) / (16 * spt)));
+    const BwdShape fs = fwd_shape(D);
+    const size_t lds = epi_lds_bytes_wide(fs.pxb, C, H, W);
+    const int ngw = (HW + (1 << fs.pxb) - 1) >> fs.pxb, chunk = (256 >> fs.pxb) * fs.spt;
+    const dim3 grid(8u * (unsigned)((B * ngw + 7) / 8), (unsigned)((D + chunk - 1) / chunk));
+    // one instance per (C, samples per thread)
+    auto kern = [&](auto nk) -> const void* {
+      constexpr int NK = decltype(nk)::value;
+      return fs.spt == 2 ? (const void*)k_cost_epi<NK, 2, 4> : (const void*)k_cost_epi<NK, 8, 4>;
+    };
+    const void* f = C == 16 ? kern(std::integral_constant<int, 4>{})
+                  : C == 32 ? kern(std::integral_constant<int, 8>{})
+                  : C == 64 ? kern(std::integral_constant<int, 16>{})
+                            : kern(std::integral_constant<int, 32>{});
+    if (int e = dsplat::ensure_dyn_lds(f, lds, "hipFuncSetAttribute(k_cost_epi)")) return e;
     for (int j = 0; j < J; ++j) {  // views in order: the sum over views is deterministic
-#define DCV_EPI(NK)                                                                                           \
-  (spt == 2 ? k_cost_epi<NK, 2> : k_cost_epi<NK, 8>)<<<grid, 256, lds, st>>>(B, j, J, H, W, D, depth_per_pixel, j > 0, ref_hwc, tgt_hwc, groups, geom, \
-                                         depth, clamp_min_depth, scale, cost)
-      switch (C) {
-        case 16: DCV_EPI(4); break;
-        case 32: DCV_EPI(8); break;
-        case 64: DCV_EPI(16); break;
-        default: DCV_EPI(32); break;
-      }
-#undef DCV_EPI
-      if (int e = dsplat::check_launch("k_cost_epi")) return e;
+      int a_B = B, a_j = j, a_J = J, a_H = H, a_W = W, a_D = D, a_dpp = depth_per_pixel, a_acc = j > 0;
+      float a_clamp = clamp_min_depth, a_scale = scale;
+      const float* a_ref = ref_hwc;
+      const float* a_tgt = tgt_hwc;
+      const int* a_groups = groups;
+      const float* a_geom = geom;
+      void* args[] = {&a_B, &a_j, &a_J, &a_H, &a_W, &a_D, &a_dpp, &a_acc, (void*)&a_ref, (void*)&a_tgt,
+                      (void*)&a_groups, (void*)&a_geom, (void*)&depth, &a_clamp, &a_scale, (void*)&cost};
+      if (int e = dsplat::check_hip(hipLaunchKernel(f, grid, dim3(256), args, lds, st), "k_cost_epi")) return e;
     }
     return 0;
   }
