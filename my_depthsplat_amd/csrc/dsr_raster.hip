@@ -1003,8 +1003,15 @@ __global__ __launch_bounds__(1024) void k_scan(int n, const uint32_t* __restrict
 // dsr_bin_scatter_cut). Depth bucket = 16 per octave of the view-space depth (in near units)
 // from 0.25, read off the float bits; monotone in the depth, so a bucket range is a depth range.
 constexpr int kCutBuckets = DSR_CUT_BUCKETS;
-constexpr int kCutLdsWords = 24576;  // count histogram + super-block depth histograms (96 KiB)
-constexpr int kCutMaxSB = kCutLdsWords / kCutBuckets;
+// count histogram + super-block depth histograms: 26 KiB, so that with k_preprocess_cut's 14 KiB
+// of static LDS four 512-thread workgroups fit a CU (32 waves; its deferred-geometry instances
+// use 60 VGPRs). Round 5: the budget was 96 KiB, which picked 4 x 4-tile super-blocks at
+// 512 x 960 (69 KiB of histograms: ONE workgroup per CU, 8 waves, while the host sized the
+// persistent grid for two); 8 x 8-tile super-blocks there took config E from 40.1 to 31.5 ms
+// per scene and config D from 1.24 to 1.09 ms per step (same box, profiles/r05s_ab_cut_lds.log)
+constexpr int kCutLdsWords = 6656;
+constexpr int kCutLdsWordsMax = 24576;  // larger images: fewer resident workgroups, still a cut
+constexpr int kCutMaxSB = kCutLdsWordsMax / kCutBuckets;
 __device__ __forceinline__ int depth_bucket(uint32_t zbits) {
   return min(kCutBuckets - 1, max(0, (int)(zbits >> 19) - (125 << 4)));
 }
@@ -1012,6 +1019,10 @@ __host__ __device__ inline int cut_superblock(int gx, int gy) {
   for (int sb = 4; sb <= 64; sb *= 2) {
     const int nsb = ((gx + sb - 1) / sb) * ((gy + sb - 1) / sb);
     if ((gx + 1) * (gy + 1) + nsb * kCutBuckets <= kCutLdsWords) return sb;
+  }
+  for (int sb = 4; sb <= 64; sb *= 2) {
+    const int nsb = ((gx + sb - 1) / sb) * ((gy + sb - 1) / sb);
+    if ((gx + 1) * (gy + 1) + nsb * kCutBuckets <= kCutLdsWordsMax) return sb;
   }
   return 0;
 }
@@ -3900,14 +3911,16 @@ int dsr_preprocess_cut(int S, int G, int V, int H, int W, int sh_degree, int M, 
   if (int e = dsplat::zero_async(depth_hist, (size_t)V * nsb * kCutBuckets * 4, st, "zero depth_hist")) return e;
   constexpr int kNTH = 512;
   const size_t lds = (size_t)((gx + 1) * (gy + 1) + nsb * kCutBuckets) * 4;
-  // persistent grid: about the resident workgroup count (LDS-limited), split evenly over views
-  const int per_cu = max(1, min(4, (int)((160 * 1024) / (lds + 8 * 1024))));
+  // persistent grid: about the resident workgroup count (LDS-limited: the histograms plus the
+  // kernel's static arrays), split evenly over views
+  constexpr size_t kStatic = (size_t)(kNTH / 64) * (sizeof(WaveRects) + 3 * 64 * sizeof(uint32_t));
+  const int per_cu = max(1, min(4, (int)((160 * 1024) / (lds + kStatic))));
   const int nblk = (G + kNTH - 1) / kNTH;
   const int per_view = max(1, min(nblk, (256 * per_cu) / V));
   const int deg = shs ? sh_degree : -1;
 #define DSR_PC(D, L)                                                                                         \
   do {                                                                                                       \
-    if (int e = dsplat::ensure_dyn_lds((const void*)k_preprocess_cut<D, kNTH, L>, kCutLdsWords * 4,           \
+    if (int e = dsplat::ensure_dyn_lds((const void*)k_preprocess_cut<D, kNTH, L>, kCutLdsWordsMax * 4,           \
                                        "hipFuncSetAttribute(k_preprocess_cut)"))                             \
       return e;                                                                                              \
     k_preprocess_cut<D, kNTH, L><<<xcd_grid(per_view, V), kNTH, lds, st>>>(                                  \
