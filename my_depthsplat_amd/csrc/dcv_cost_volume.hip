@@ -881,13 +881,19 @@ __device__ __forceinline__ int epi_rank(const EpiLds& L, int e) {
 // overlap), their samples' bands merged into one. The band set-up (bitmap, box, word pass,
 // list), the target rows' loads and the barriers are then paid once per 2^PXB pixels; the
 // GEMM covers the union band.
-constexpr int kEGWMax = 64;             // widest backward group
-template <int PXB>
-constexpr int bwd_band() { return PXB == 6 ? 128 : 256; }  // band positions per pass (LDS)
-static_assert(bwd_band<4>() <= kEUMax && bwd_band<6>() <= kEUMax, "the band list holds a pass");
-template <int PXB>
+constexpr int kEGWMax = 64;             // widest group
+// Band positions per GEMM pass (the [2^PXB][band + 1] LDS tile). 128 for the widest groups
+// and for the per-pixel-candidate shapes (SPT = 2: short bands; the smaller tile lets 6
+// instead of 4 workgroups share a CU: config D scale 1 forward 0.852 -> 0.761 ms, same box,
+// profiles/r05t_ab_cv_pass128.log), 256 otherwise (per-image candidates: long bands, a second
+// pass cost more there: scale 0 0.436 -> 0.474 ms at 128).
+__host__ __device__ constexpr int epi_pass(int pxb, int spt) { return (pxb == 6 || spt == 2) ? 128 : 256; }
+template <int PXB, int SPT>
+constexpr int bwd_band() { return epi_pass(PXB, SPT); }
+static_assert(epi_pass(4, 8) <= kEUMax && epi_pass(6, 8) <= kEUMax, "the band list holds a pass");
+template <int PXB, int SPT>
 __device__ __forceinline__ EpiLds epi_lds_wide(float* p, int C, int NWx) {
-  constexpr int EGW = 1 << PXB, kECorrB = bwd_band<PXB>() + 1;
+  constexpr int EGW = 1 << PXB, kECorrB = bwd_band<PXB, SPT>() + 1;
   EpiLds L;
   L.aref = p;
   p += EGW * (C + 4);
@@ -905,8 +911,8 @@ __device__ __forceinline__ EpiLds epi_lds_wide(float* p, int C, int NWx) {
   L.misc = reinterpret_cast<uint32_t*>(p);
   return L;
 }
-size_t epi_lds_bytes_wide(int pxb, int C, int H, int W) {
-  const size_t egw = (size_t)1 << pxb, corr = (pxb == 6 ? 128 : 256) + 1;
+size_t epi_lds_bytes_wide(int pxb, int spt, int C, int H, int W) {
+  const size_t egw = (size_t)1 << pxb, corr = (size_t)epi_pass(pxb, spt) + 1;
   return sizeof(float) * (egw * (C + 4) + egw * corr + kEUMax + 4 * epi_words(H, W) + 1 + 32);
 }
 // Forward, view j: grid.x = 8 * ceil(B * ngroups / 8) (XCD-contiguous, ngroups of 2^PXB
@@ -925,12 +931,12 @@ __global__ __launch_bounds__(256, PXB == 4 ? 4 : 2) void k_cost_epi(int B, int j
                                                                   const float* __restrict__ depth, float clampz,
                                                                   float scale, float* __restrict__ cost) {
   constexpr int C = 4 * NK, EGW = 1 << PXB, MB = EGW / 16, DSL = 256 >> PXB;
-  constexpr int kEU = bwd_band<PXB>(), kEC = kEU + 1;
+  constexpr int kEU = bwd_band<PXB, SPT>(), kEC = kEU + 1;
   extern __shared__ __attribute__((aligned(16))) float cv_lds[];
   const int HW = H * W, ngw = (HW + EGW - 1) / EGW;
   int b, g;
   if (!epi_item(B, ngw, b, g)) return;
-  const EpiLds L = epi_lds_wide<PXB>(cv_lds, C, epi_words(H, W));
+  const EpiLds L = epi_lds_wide<PXB, SPT>(cv_lds, C, epi_words(H, W));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int i = tid & (EGW - 1), dl = tid >> PXB, d0 = blockIdx.y * DSL * SPT;
   const size_t bj = (size_t)b * J + j;
@@ -1147,12 +1153,12 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
                                                       float* __restrict__ dref_hwc, long long* __restrict__ dtgt_fx) {
   constexpr int C = 4 * NK, NCB = (C / 16 + 3) / 4;  // channel blocks per wave (dref)
   constexpr int EGW = 1 << PXB, MB = EGW / 16, DSL = 256 >> PXB;  // pixels, row blocks, depth slots
-  constexpr int kEUMaxB = bwd_band<PXB>(), kECorrB = kEUMaxB + 1;
+  constexpr int kEUMaxB = bwd_band<PXB, SPT>(), kECorrB = kEUMaxB + 1;
   extern __shared__ __attribute__((aligned(16))) float cv_lds[];
   const int HW = H * W, ngw = (HW + EGW - 1) / EGW;
   int b, g;
   if (!epi_item(B, ngw, b, g)) return;
-  const EpiLds L = epi_lds_wide<PXB>(cv_lds, C, epi_words(H, W));
+  const EpiLds L = epi_lds_wide<PXB, SPT>(cv_lds, C, epi_words(H, W));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const size_t bj = (size_t)b * J + j;
   const float unit_t = cv_dtgt_unit(cvmax, scale, SPT);
@@ -1694,7 +1700,8 @@ static BwdShape bwd_shape(int B, int H, int W, int D, int depth_per_pixel) {
 }
 static bool epi_path(int C, int H, int W, bool bwd) {
   (void)bwd;  // (both directions fit the widest group's layout)
-  return C % 16 == 0 && C <= 128 && epi_lds_bytes_wide(6, C, H, W) <= 160 * 1024;
+  return C % 16 == 0 && C <= 128 && epi_lds_bytes_wide(6, 8, C, H, W) <= 160 * 1024 &&
+         epi_lds_bytes_wide(5, 8, C, H, W) <= 160 * 1024;
 }
 
 // Small grids take the band kernel for the forward: one launch with no channel-last copies
@@ -1791,7 +1798,7 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
   const float scale = 1.0f / (sqrtf((float)C) * (float)J);
   if (path == DCV_PATH_EPI) {
     const BwdShape fs = fwd_shape(D);
-    const size_t lds = epi_lds_bytes_wide(fs.pxb, C, H, W);
+    const size_t lds = epi_lds_bytes_wide(fs.pxb, fs.spt, C, H, W);
     const int ngw = (HW + (1 << fs.pxb) - 1) >> fs.pxb, chunk = (256 >> fs.pxb) * fs.spt;
     const dim3 grid(8u * (unsigned)((B * ngw + 7) / 8), (unsigned)((D + chunk - 1) / chunk));
     // one instance per (C, samples per thread)
@@ -1851,7 +1858,7 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
     k_cv_absmax<<<kCvMaxBlocks, 256, 0, st>>>((size_t)B * D * HW, dcost, (size_t)B * C * HW, ref, cvmax);
     if (int e = dsplat::check_launch("k_cv_absmax")) return e;
     const BwdShape bs = bwd_shape(B, H, W, D, depth_per_pixel);
-    const size_t lds = epi_lds_bytes_wide(bs.pxb, C, H, W);
+    const size_t lds = epi_lds_bytes_wide(bs.pxb, bs.spt, C, H, W);
     const int ngw = (HW + (1 << bs.pxb) - 1) >> bs.pxb;
     const dim3 grid(8u * (unsigned)((B * ngw + 7) / 8));
     // one instance per (C, width, samples per thread)
