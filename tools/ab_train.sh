@@ -15,7 +15,9 @@ import json, sys
 for l in open(sys.argv[2]):
     if l.startswith('{'):
         d = json.loads(l)
-        print(sys.argv[1], 'train_config_c ms', d['train_config_c']['ms_per_step'])
+        t = d['train_config_c']
+        k = (t.get('roofline') or {}).get('per_step_ms_by_kernel') or {}
+        print(sys.argv[1], 'train_config_c ms', t['ms_per_step'], ' '.join(f'{n}={v}' for n, v in k.items()))
 PY
   done
 done
