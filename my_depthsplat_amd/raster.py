@@ -242,7 +242,10 @@ SORT_PREFIX = int(os.environ.get("DSPLAT_SORT_PREFIX", "4096"))
 # entries per tile, the nearest depth buckets, are written and sorted; tiles whose pixels do
 # not all saturate within them get the rest appended, sorted and rendered again. 0 = off.
 CUT_PREFIX = int(os.environ.get("DSPLAT_CUT_PREFIX", "2048"))
-CUT_SORT_HINT = 4096  # LDS sort size for the written parts (larger ones sort through HBM)
+# LDS sort class for the written parts (larger ones sort through HBM). 3072 keys (4 workgroups
+# per CU) beat 4096 (3) and 2048 (heads above it go through HBM): config D 1.095 / 1.075 /
+# 1.34 ms, config E 31.8 / 31.0 / 34.6 ms per scene (round 5, profiles/r05w_ab_cut_sort_hint.log)
+CUT_SORT_HINT = 3072
 # Depth cut (need_state False or True): the count pass writes no geometry record and evaluates
 # no colour; each scatter pass lists the Gaussians that may emit and dsr_project_survivors
 # projects only those (~3 % of the (view, Gaussian) pairs at 12x512x960). Off only where the
