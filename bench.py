@@ -379,6 +379,7 @@ def main():
     ev = raster.KernelTimer(only=[dominant])
     raster.set_timer(ev)
     elapsed_eager = timed(step, args.steps)
+    gstate = gpu_state(dev) if rank == 0 else None  # clocks / power right after a loaded region
     raster.set_timer(None)
     ktimes = ev.summary()  # name -> (launches, avg_ms)
     elapsed, elapsed_eager, elapsed_ref = max_over_ranks(elapsed, elapsed_eager, elapsed_ref)
@@ -433,12 +434,54 @@ def main():
                        "parallelism": f"dp{world} (per-scene, no collective)", "ranks": world,
                        "scenes_in_flight_per_gpu": B * lanes_used, "distinct_scenes_per_gpu": B * lanes_used},
             "parity_vs_oracle": psnr,
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "gpu_state": gstate,
             **extra,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def gpu_state(dev) -> dict:
+    """Clock and power of the benched GPU from amdgpu sysfs (best effort, read right after the
+    timed region): current / top shader-clock level (pp_dpm_sclk), memory clock, power cap and
+    average power (hwmon, microwatts) — so box-to-box gaps of the same build can be read
+    (VERDICT r4). The device is matched by its PCI address from torch's device properties."""
+    import glob
+
+    import torch
+
+    out = {"source": "/sys/bus/pci/devices/<pci>/ (amdgpu)"}
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        dom, bus, slot = (getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+        out["pci"] = None if bus is None else f"{dom or 0:04x}:{bus:02x}:{slot or 0:02x}"
+        paths = glob.glob(f"/sys/bus/pci/devices/{out['pci']}.*") if bus is not None else []
+        if not paths:
+            out["error"] = "device not matched in sysfs"
+            return out
+        d = paths[0]
+
+        def levels(name):
+            with open(f"{d}/{name}") as f:
+                rows = [ln.split() for ln in f if ln.strip()]
+            mhz = [int(r[1].lower().rstrip("mhz")) for r in rows]
+            cur = [int(r[1].lower().rstrip("mhz")) for r in rows if r[-1] == "*"]
+            return (cur[0] if cur else None), max(mhz)
+
+        out["sclk_mhz"], out["sclk_max_mhz"] = levels("pp_dpm_sclk")
+        out["mclk_mhz"], out["mclk_max_mhz"] = levels("pp_dpm_mclk")
+        for hw in glob.glob(f"{d}/hwmon/hwmon*"):
+            for key, name in (("power_cap_w", "power1_cap"), ("power_avg_w", "power1_average"),
+                              ("power_now_w", "power1_input")):
+                try:
+                    with open(f"{hw}/{name}") as f:
+                        out[key] = round(int(f.read()) / 1e6, 1)
+                except OSError:
+                    pass
+    except Exception as e:  # noqa: BLE001 - diagnostics only, never fails the bench
+        out["error"] = f"{type(e).__name__}: {e}"
+    return out
 
 
 def measured_copy_gbs(dev, nbytes=1 << 30, reps=10) -> dict:
