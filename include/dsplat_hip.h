@@ -391,8 +391,7 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
  * SAME value to the forward and to the backward (which must know what the forward left in the
  * workspace); a path the shape cannot take is an error.
  * workspace: dcv_cost_volume_workspace_size bytes (channel-last copies of tgt and ref with a
- * zero padding row per image, the epipolar groups and, since round 5, each pixel's line id and
- * sort key (8 bytes per (batch, view, pixel)), filled here (or, after a band-kernel
+ * zero padding row per image, and the epipolar groups), filled here (or, after a band-kernel
  * forward, by dcv_cost_volume_bwd itself) and read by dcv_cost_volume_bwd. */
 #define DCV_PATH_BAND 0
 #define DCV_PATH_EPI 1
