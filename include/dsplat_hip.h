@@ -261,7 +261,9 @@ int dsr_project_survivors(int S, int G, int V, int H, int W, int sh_degree, int 
  * compositor needs little more than a few hundred entries per tile, so the rest of a
  * 30-40K entry list is never put in order; dsr_render_fwd checks the tail and flags the
  * rare tile that does need it. seg_filter (non-NULL, needs scratch): sort in full only
- * the segments with seg_filter[s] != 0 (the flagged tiles), leaving the others as they are.
+ * the segments with seg_filter[s] != 0 (the flagged tiles), leaving the others as they are;
+ * seg_filter[nseg] is the any-flag word (as dsr_render_fwd / dsr_sort_render write it: 0 =
+ * nothing flagged, the launch does nothing).
  * The reference sorts every key (cuda_rasterizer/rasterizer_impl.cu, SortPairs). */
 int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const uint32_t* seg_count,
                  uint32_t seg_stride, uint64_t* keys, uint64_t* scratch, uint32_t max_count,

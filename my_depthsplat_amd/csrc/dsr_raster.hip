@@ -1648,6 +1648,34 @@ __device__ void sort_segment(uint64_t* A, uint64_t* B, uint32_t n, int id_bits, 
     for (uint32_t i = threadIdx.x; i < n; i += NTH) home[i] = src[i];
 }
 
+// The tail pass's sort (dsr_bin_sort with seg_filter): the flagged tiles are few (0-21 of
+// 19,200 per config-E launch) and each is a whole list of 10-30 K keys. A persistent grid of
+// 1024-thread workgroups walks the segments and sorts the flagged ones through HBM with 16
+// waves each (sort_segment<1024>: 4x the threads of the LDS-sort workgroup); when no tile is
+// flagged (the any-flag word filter[nseg] is 0) every workgroup leaves at once. It replaces one
+// LDS-heavy workgroup per segment, whose dispatch alone took ~0.3 ms per config-E launch
+// (round 5).
+template <int NTH>
+__global__ __launch_bounds__(NTH) void k_sort_flagged(int nseg, const uint32_t* __restrict__ seg_start,
+                                                      const uint32_t* __restrict__ seg_count, uint32_t stride,
+                                                      uint64_t* __restrict__ keys, uint64_t* __restrict__ scratch,
+                                                      int id_bits, const uint32_t* __restrict__ filter,
+                                                      uint32_t* __restrict__ seg_sorted) {
+  __shared__ uint32_t hist[(NTH / kWave) * 256];
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t flag[4];
+  if (filter[nseg] == 0u) return;  // no tile flagged (uniform)
+  for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    if (filter[seg] == 0u) continue;  // uniform
+    uint32_t b, e;
+    seg_bounds(seg_start, seg_count, stride, seg, b, e);
+    const uint32_t n = e - b;
+    if (seg_sorted && threadIdx.x == 0) seg_sorted[seg] = n;
+    if (n > 1) sort_segment<NTH>(keys + b, scratch + b, n, id_bits, hist, wsum, flag, keys + b);
+    __syncthreads();  // LDS reused by the next flagged segment
+  }
+}
+
 // ---- in-LDS segment sort (n <= 256 * KMAX) -------------------------------------------
 // Keys live in LDS; each pass every thread loads its KMAX contiguous keys into registers,
 // ranks them with per-thread packed 8-bit counters for a 4-bit digit (no ballots, no
@@ -4102,8 +4130,14 @@ int dsr_bin_sort(int G, int V, int H, int W, const uint32_t* seg_start, const ui
                                                                           keys, scratch, id_bits, big_here, \
                                                                           FILT, seg_sorted);                \
   } while (0)
-  if (big_known || seg_filter) {  // small segments in LDS now, the rest split below (or through HBM)
-    DSR_SORT_LDS(16, NT, seg_filter);
+  if (seg_filter) {  // the tail pass: the few flagged segments, in full (k_sort_flagged)
+    constexpr int kFlagNT = 1024;
+    k_sort_flagged<kFlagNT><<<(unsigned)min(nseg, 512), kFlagNT, 0, st>>>(nseg, seg_start, seg_count, seg_stride, keys,
+                                                                       scratch, id_bits, seg_filter, seg_sorted);
+    return dsplat::check_launch("k_sort_flagged");
+  }
+  if (big_known) {  // small segments in LDS now, the rest split below
+    DSR_SORT_LDS(16, NT, nullptr);
   } else if (want <= kSortNT * 4) {
     DSR_SORT_LDS(4, kSortNT, nullptr);
   } else if (want <= kSortNT * 8) {
