@@ -2788,27 +2788,22 @@ __device__ __forceinline__ int tile_xcd(int gx, int gy, int& tx, int& ty) {
 // wave w owns the 8x8 sub-tile (w & 1, w >> 1) of the tile (composite_tile). There is no
 // workgroup barrier; the waves of a workgroup share the tile's keys/records through L1. A
 // stopped pixel keeps its final T (alive is a lane mask).
-__global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, int T,
-                                                   const dsr_camera* __restrict__ cams,
-                                                   const float* __restrict__ geom,
-                                                   const uint32_t* __restrict__ seg_start,
-                                                   const uint32_t* __restrict__ seg_count, uint32_t stride,
-                                                   const uint64_t* __restrict__ keys,
-                                                   const uint32_t* __restrict__ seg_sorted,
-                                                   uint32_t* __restrict__ seg_overflow,
-                                                   const uint32_t* __restrict__ seg_filter,
-                                                   float* __restrict__ out, float* __restrict__ finalT,
-                                                   uint32_t* __restrict__ ncontrib) {
-  __shared__ WaveList l_pair[4];
+// One tile of K6 (k_render_fwd's body; also run by k_render_flagged). V: the launch's views.
+__device__ __forceinline__ void render_fwd_tile(int v, int tx, int ty, int V, int G, int H, int W, int gx, int T,
+                                                const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
+                                                const uint32_t* __restrict__ seg_start,
+                                                const uint32_t* __restrict__ seg_count, uint32_t stride,
+                                                const uint64_t* __restrict__ keys,
+                                                const uint32_t* __restrict__ seg_sorted,
+                                                uint32_t* __restrict__ seg_overflow, float* __restrict__ out,
+                                                float* __restrict__ finalT, uint32_t* __restrict__ ncontrib,
+                                                WaveList* l_pair) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  int tx, ty;
-  const int v = tile_xcd(gx, T / gx, tx, ty);  // kbench: 3 views -4..-6 %, 64 views level
   const int sx0 = tx * BX + (w & 1) * SUB, sy0 = ty * BY + (w >> 1) * SUB;
   const int px = sx0 + (lane & (SUB - 1));
   const int py = sy0 + (lane >> 3);
   const bool inside = px < W && py < H;
   const int seg = v * T + ty * gx + tx;
-  if (seg_filter && !seg_filter[seg]) return;
   uint32_t start, end;
   seg_bounds(seg_start, seg_count, stride, seg, start, end);
   const uint32_t tail_end = end;  // [end, tail_end): unsorted tail (prefix-sorted segments)
@@ -2834,14 +2829,55 @@ __global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, 
     void_tile = tail_reaches_live(gv, keys, end, tail_end, fx0, fy0, pp, alive, plist, lt, lane, gmax);
   if (void_tile && lane == 0) {  // the tile's output is void: completed, sorted and re-rendered by the caller
     seg_overflow[seg] = 1u;
-    seg_overflow[(size_t)gridDim.z * T] = 1u;  // any-flag
+    seg_overflow[(size_t)V * T] = 1u;  // any-flag
     if (absent_tail) {  // depth cut: also flag the tile's super-block (the tail scatter's pre-test)
       const int sb = cut_superblock(gx, T / gx), sbl = __builtin_ctz((unsigned)sb);
       const int nsx = (gx + sb - 1) / sb, nsb = nsx * ((T / gx + sb - 1) / sb);
-      seg_overflow[(size_t)gridDim.z * T + 1 + (size_t)v * nsb + (ty >> sbl) * nsx + (tx >> sbl)] = 1u;
+      seg_overflow[(size_t)V * T + 1 + (size_t)v * nsb + (ty >> sbl) * nsx + (tx >> sbl)] = 1u;
     }
   }
   if (inside) store_pixel(out, finalT, ncontrib, cams[v].bg, v, H, W, px, py, Tr, C01, C2, last);
+}
+
+__global__ __launch_bounds__(NT) void k_render_fwd(int G, int H, int W, int gx, int T,
+                                                   const dsr_camera* __restrict__ cams,
+                                                   const float* __restrict__ geom,
+                                                   const uint32_t* __restrict__ seg_start,
+                                                   const uint32_t* __restrict__ seg_count, uint32_t stride,
+                                                   const uint64_t* __restrict__ keys,
+                                                   const uint32_t* __restrict__ seg_sorted,
+                                                   uint32_t* __restrict__ seg_overflow,
+                                                   float* __restrict__ out, float* __restrict__ finalT,
+                                                   uint32_t* __restrict__ ncontrib) {
+  __shared__ WaveList l_pair[4];
+  int tx, ty;
+  const int v = tile_xcd(gx, T / gx, tx, ty);  // kbench: 3 views -4..-6 %, 64 views level
+  render_fwd_tile(v, tx, ty, gridDim.z, G, H, W, gx, T, cams, geom, seg_start, seg_count, stride, keys, seg_sorted,
+                  seg_overflow, out, finalT, ncontrib, l_pair);
+}
+// The tail pass's re-render (dsr_render_fwd with seg_filter): a persistent grid walks the
+// (view, tile) segments and renders the flagged ones; with nothing flagged (any-flag word
+// seg_filter[V T] = 0) it leaves at once instead of dispatching a workgroup per tile (~49 us
+// per config-E launch, round 5).
+__global__ __launch_bounds__(NT) void k_render_flagged(int V, int G, int H, int W, int gx, int T,
+                                                       const dsr_camera* __restrict__ cams,
+                                                       const float* __restrict__ geom,
+                                                       const uint32_t* __restrict__ seg_start,
+                                                       const uint32_t* __restrict__ seg_count, uint32_t stride,
+                                                       const uint64_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ seg_filter,
+                                                       float* __restrict__ out, float* __restrict__ finalT,
+                                                       uint32_t* __restrict__ ncontrib) {
+  __shared__ WaveList l_pair[4];
+  const int nseg = V * T;
+  if (seg_filter[nseg] == 0u) return;  // uniform
+  for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    if (seg_filter[seg] == 0u) continue;  // uniform
+    const int v = seg / T, t = seg - v * T, ty = t / gx, tx = t - ty * gx;
+    render_fwd_tile(v, tx, ty, V, G, H, W, gx, T, cams, geom, seg_start, seg_count, stride, keys, nullptr, nullptr,
+                    out, finalT, ncontrib, l_pair);
+    __syncthreads();  // the wave lists are reused by the next flagged tile
+  }
 }
 
 // K4 + K6 fused: one workgroup per tile sorts the tile's keys in LDS (count_sort) and its 4
@@ -4177,10 +4213,19 @@ int dsr_render_fwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
                      n_contrib,
                  "dsr_render_fwd: null pointer");
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
+  if (seg_filter) {  // the tail pass: only the flagged tiles (their lists complete and sorted)
+    DSPLAT_REQUIRE(seg_sorted == nullptr && seg_overflow == nullptr,
+                   "dsr_render_fwd: seg_filter goes without seg_sorted / seg_overflow");
+    const int nseg = V * gx * gy;
+    k_render_flagged<<<(unsigned)min(nseg, 2048), NT, 0, (hipStream_t)stream>>>(
+        V, G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count, seg_stride, keys, seg_filter, out_color, final_T,
+        n_contrib);
+    return dsplat::check_launch("k_render_flagged");
+  }
   dim3 grid(gx, gy, V);
   k_render_fwd<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count,
-                                                     seg_stride, keys, seg_sorted, seg_overflow, seg_filter,
-                                                     out_color, final_T, n_contrib);
+                                                     seg_stride, keys, seg_sorted, seg_overflow, out_color, final_T,
+                                                     n_contrib);
   return dsplat::check_launch("k_render_fwd");
 }
 
