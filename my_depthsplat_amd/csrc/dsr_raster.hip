@@ -3551,18 +3551,20 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
   }
   float dm0 = 0.f, dm1 = 0.f, dm2 = 0.f, dop = 0.f, dcol0 = 0.f, dcol1 = 0.f, dcol2 = 0.f;
   float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int vb = valid ? scene_view_start[s] : 0, ve = valid ? scene_view_start[s + 1] : 0;
+  // the view loop is workgroup-uniform (scene = blockIdx.y), so the view ids and every camera
+  // field below are scalar loads; lanes past the scene's last Gaussian ride along masked off
+  const int vb = scene_view_start[s], ve = scene_view_start[s + 1];
   for (int k = vb; k < ve; ++k) {
     const int v = scene_views[k];
     const size_t vg = (size_t)v * G + g;
     // deferred geometry (depth cut): only the rows of the Gaussians some written list refers to
     // have a record and a zeroed accumulator (row_live); the others are skipped unread
-    const bool live = row_live == nullptr || row_live[vg] != 0u;
+    const bool live = valid && (row_live == nullptr || row_live[vg] != 0u);
     const float4 rec2 = live ? reinterpret_cast<const float4*>(geom + vg * GS)[2]  // depth, radius, clamp bits
                              : make_float4(0.f, 0.f, 0.f, 0.f);
     const int radius = __float_as_int(rec2.z);
     if (radius <= 0) {
-      if (dmean2D) {
+      if (dmean2D && valid) {
         dmean2D[3 * vg] = 0.f;
         dmean2D[3 * vg + 1] = 0.f;
         dmean2D[3 * vg + 2] = 0.f;

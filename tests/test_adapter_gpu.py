@@ -38,11 +38,17 @@ def _inputs(sh_degree, B=2, V=2, H=8, W=12, seed=0, dev="cuda"):
     return to(head), to(depths), to(images), to(ext), to(K), adapter.to(dev)
 
 
+# (8, 12): views split across workgroups (per-lane camera reads); (16, 32): every 256-row
+# workgroup inside one view (the workgroup-uniform camera path, dga_adapter.hip UNI)
+SIZES = [(8, 12), (16, 32)]
+
+
 @pytest.mark.parametrize("sh_degree", [0, 1, 2, 3])
-def test_fused_adapter_forward_matches_torch(gpu, sh_degree):
+@pytest.mark.parametrize("H,W", SIZES)
+def test_fused_adapter_forward_matches_torch(gpu, sh_degree, H, W):
     from my_depthsplat_amd.adapter_hip import fused_gaussians_from_head
     from my_depthsplat_amd.gaussian_adapter import gaussians_from_head_torch
-    head, depths, images, ext, K, adapter = _inputs(sh_degree, seed=sh_degree)
+    head, depths, images, ext, K, adapter = _inputs(sh_degree, H=H, W=W, seed=sh_degree)
     a = fused_gaussians_from_head(head, depths, images, ext, K, adapter)
     b = gaussians_from_head_torch(head, depths, images, ext, K, adapter)
     for name in ("means", "covariances", "harmonics", "opacities"):
@@ -52,10 +58,11 @@ def test_fused_adapter_forward_matches_torch(gpu, sh_degree):
 
 
 @pytest.mark.parametrize("sh_degree", [1, 2, 3])
-def test_fused_adapter_backward_matches_autograd(gpu, sh_degree):
+@pytest.mark.parametrize("H,W", SIZES)
+def test_fused_adapter_backward_matches_autograd(gpu, sh_degree, H, W):
     from my_depthsplat_amd.adapter_hip import fused_gaussians_from_head
     from my_depthsplat_amd.gaussian_adapter import gaussians_from_head_torch
-    head, depths, images, ext, K, adapter = _inputs(sh_degree, seed=10 + sh_degree)
+    head, depths, images, ext, K, adapter = _inputs(sh_degree, H=H, W=W, seed=10 + sh_degree)
     gen = torch.Generator(device=head.device).manual_seed(3)
     outs = []
     for fn in (fused_gaussians_from_head, gaussians_from_head_torch):

@@ -172,9 +172,6 @@ __device__ __forceinline__ void row_xy(const AdIn& a, const Pix& px, const float
   }
 }
 
-// UNI (host picks it when H W S % NT == 0): all rows of a workgroup belong to one view, so the
-// camera block address is workgroup-uniform and its ~55 reads per row are scalar loads instead
-// of per-lane vector loads (the per-lane form kept the adapter at ~3.6 TB/s in config C).
 template <int NSH, bool GLUE, bool UNI>
 __global__ __launch_bounds__(NT) void k_adapter_fwd(AdIn a, float* __restrict__ means, float* __restrict__ covs,
                                                     float* __restrict__ harm, float* __restrict__ opac,
