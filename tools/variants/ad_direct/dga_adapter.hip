@@ -189,12 +189,12 @@ __global__ __launch_bounds__(NT) void k_adapter_fwd(AdIn a, float* __restrict__ 
   Pix px{};
   const bool valid = pixel_of(n0 + tid, a, px);  // outputs share the row order
   const size_t HW = (size_t)a.H * a.W;
-  dsplat::stage_in<NT>(a.rows + n0 * C, (size_t)nrows * C, lds);
-  __syncthreads();
   float h[KH];
+  {
+    const float* row = a.rows + (valid ? (n0 + tid) * C : 0);
 #pragma unroll
-  for (int k = 0; k < KH; ++k) h[k] = valid ? lds[tid * C + k] : 0.f;
-  __syncthreads();
+    for (int k = 0; k < KH; ++k) h[k] = valid ? row[k] : 0.f;
+  }
   float mo[3], Cw[9], ho[3 * NSH], sc[3], q[4];
   if (valid) {
     const float* cam = a.cams + (UNI ? n0 / ((size_t)a.H * a.W * a.S) : px.bv) * kCamFloats;
@@ -249,24 +249,19 @@ __global__ __launch_bounds__(NT) void k_adapter_fwd(AdIn a, float* __restrict__ 
   // coalesced row writes through LDS: the three main outputs land in LDS together (harmonics,
   // covariances, means blocks back to back) and leave behind one barrier
   constexpr int kOC = NT * 3 * NSH, kOM = kOC + NT * 9;
+  (void)kOC; (void)kOM; (void)nrows;
   if (valid) {
+    const size_t n = n0 + tid;
 #pragma unroll
-    for (int k = 0; k < 3 * NSH; ++k) lds[tid * (3 * NSH) + k] = ho[k];
+    for (int k = 0; k < 3 * NSH; ++k) harm[n * (3 * NSH) + k] = ho[k];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) lds[kOC + tid * 9 + k] = Cw[k];
+    for (int k = 0; k < 9; ++k) covs[n * 9 + k] = Cw[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) lds[kOM + tid * 3 + k] = mo[k];
+    for (int k = 0; k < 3; ++k) means[n * 3 + k] = mo[k];
   }
-  __syncthreads();
-  dsplat::stage_out<NT>(harm + n0 * (3 * NSH), (size_t)nrows * (3 * NSH), lds);
-  dsplat::stage_out<NT>(covs + n0 * 9, (size_t)nrows * 9, lds + kOC);
-  dsplat::stage_out<NT>(means + n0 * 3, (size_t)nrows * 3, lds + kOM);
   const auto put = [&](float* dst, const float* v, int width) {
-    __syncthreads();
     if (valid)
-      for (int k = 0; k < width; ++k) lds[tid * width + k] = v[k];
-    __syncthreads();
-    dsplat::stage_out<NT>(dst + n0 * width, (size_t)nrows * width, lds);
+      for (int k = 0; k < width; ++k) dst[(n0 + tid) * width + k] = v[k];
   };
   if constexpr (!GLUE) {
     if (scales_out) put(scales_out, sc, 3);
@@ -572,7 +567,7 @@ template <int NS, bool GLUE>
 int launch_fwd(const AdIn& a, float* means, float* covs, float* harm, float* opac, float* scales, float* rots,
                hipStream_t st) {
   const size_t n = (size_t)a.BV * a.H * a.W * a.S;
-  const size_t lds = adapter_fwd_lds(a.C, NS);
+  const size_t lds = 0;
   if (lds > 64 * 1024 &&
       (hipFuncSetAttribute((const void*)k_adapter_fwd<NS, GLUE, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)lds) != hipSuccess ||

@@ -180,7 +180,7 @@ __global__ __launch_bounds__(NT) void k_adapter_fwd(AdIn a, float* __restrict__ 
                                                     float* __restrict__ harm, float* __restrict__ opac,
                                                     float* __restrict__ scales_out, float* __restrict__ rot_out) {
   constexpr int KH = Rows<NSH, GLUE>::kHead, O = Rows<NSH, GLUE>::kOff;
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // adapter_fwd_lds(): NT * max(C, 3 NSH + 12) floats
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // NT * max(C, 3 * NSH, 9) floats
   const size_t total = (size_t)a.BV * a.H * a.W * a.S;
   const size_t n0 = (size_t)blockIdx.x * NT;
   const int nrows = (int)min((size_t)NT, total - n0);
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(AdIn a, const float* __restr
                                                     const float* __restrict__ drot, float* __restrict__ drows,
                                                     float* __restrict__ ddepth, float* __restrict__ dcoords) {
   constexpr int KH = Rows<NSH, GLUE>::kHead, O = Rows<NSH, GLUE>::kOff;
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // adapter_lds(): NT * max(C, 3 NSH, 9) floats
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // NT * max(C, 3 * NSH, 9) floats
   const size_t total = (size_t)a.BV * a.H * a.W * a.S;
   const size_t n0 = (size_t)blockIdx.x * NT;
   const int nrows = (int)min((size_t)NT, total - n0);
