@@ -782,9 +782,22 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         if torch.cuda.is_current_stream_capturing():
             raise _lib.DsplatError(f"V*G*tiles = {V * G * T} key slots exceed the key budget: this size needs a "
                                    "host read-back and cannot be captured into a graph")
+        tot = totals[:3].cpu()  # one small read-back: N sizes the key buffer
+        N, maxc = int(tot[0]), int(tot[1])
+        if ctx.adapt_hints:
+            spec["two_phase_max"] = maxc
+        if int(tot[2]):
+            raise EntryOverflow(f"{V} views x {G} Gaussians produce >= 2^31 (view, tile, Gaussian) entries: "
+                                "render fewer views per call")
+        keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
+        if sb > 0 and maxc <= 2 * cut_prefix:  # short lists after all: write everything
+            sb = 0
+            if defer:  # the full scatter reads every record: project them all now
+                _project_all(lib, S, G, V, H, W, deg, M, means, shs_p, col_p, opacities, cov6, cams, geom, radii,
+                             layout, dev, st, dgeom_zero, row_live)
         if sb > 0:
-            # what does not depend on N is queued before the read-back, so the device has work
-            # while the host waits on it (the cut thresholds; the survivor counters)
+            # depth cut: write only each tile's nearest entries (cursor ends at their end)
+            scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev)  # only big segments touch it
             cut = torch.empty(V * nsb, dtype=torch.int32, device=dev)
             _lib.check(_timed("k_bin_cutoff", lib.dsr_bin_cutoff, V, H, W, hist.data_ptr(), cut_prefix,
                               cut.data_ptr(), st), "dsr_bin_cutoff")
@@ -796,23 +809,6 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                            "dsr_survivor_layout")
                 surv = torch.empty(slots.value, dtype=torch.int32, device=dev)
                 surv_n = torch.zeros(2 * ncnt.value, dtype=torch.int32, device=dev)
-        tot = totals[:3].cpu()  # one small read-back: N sizes the key buffer
-        N, maxc = int(tot[0]), int(tot[1])
-        if ctx.adapt_hints:
-            spec["two_phase_max"] = maxc
-        if int(tot[2]):
-            raise EntryOverflow(f"{V} views x {G} Gaussians produce >= 2^31 (view, tile, Gaussian) entries: "
-                                "render fewer views per call")
-        keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
-        if sb > 0 and maxc <= 2 * cut_prefix:  # short lists after all: write everything
-            sb = 0
-            surv = surv_n = None
-            if defer:  # the full scatter reads every record: project them all now
-                _project_all(lib, S, G, V, H, W, deg, M, means, shs_p, col_p, opacities, cov6, cams, geom, radii,
-                             layout, dev, st, dgeom_zero, row_live)
-        if sb > 0:
-            # depth cut: write only each tile's nearest entries (cursor ends at their end)
-            scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev)  # only big segments touch it
             proj = (S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                     cams.data_ptr())
             _lib.check(_timed("k_scatter_cut", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
