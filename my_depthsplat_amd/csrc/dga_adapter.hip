@@ -23,31 +23,6 @@ constexpr int kCamFloats = 104;  // R[9] t[3] Kinv[9] D1[9] D2[25] D3[49]
 constexpr int kOffR = 0, kOffT = 9, kOffKinv = 12, kOffD1 = 21, kOffD2 = 30, kOffD3 = 55;
 constexpr int NT = 256;
 
-// Register prefetch of one workgroup's contiguous row block (nfloat floats, 16-byte aligned):
-// P float4 per thread, issued together so every input of the workgroup is in flight at once;
-// pref_put then lands them in LDS for the row transpose (the tail past the last float4 is
-// read directly). P = ceil(width / 4) covers NT rows of `width` floats.
-template <int P>
-__device__ __forceinline__ void pref_get(const float* src, size_t nfloat, float4 (&v)[P]) {
-  const size_t n4 = nfloat / 4;
-  const float4* s4 = reinterpret_cast<const float4*>(src);
-#pragma unroll
-  for (int k = 0; k < P; ++k)
-    v[k] = n4 ? s4[min((size_t)threadIdx.x + (size_t)k * NT, n4 - 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-template <int P>
-__device__ __forceinline__ void pref_put(const float* src, size_t nfloat, const float4 (&v)[P], float* lds) {
-  const size_t n4 = nfloat / 4;
-  float4* l4 = reinterpret_cast<float4*>(lds);
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const size_t i = (size_t)threadIdx.x + (size_t)k * NT;
-    if (i < n4) l4[i] = v[k];
-  }
-  for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NT) lds[i] = src[i];
-}
-__device__ __forceinline__ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // torch.nn.functional.softplus (beta 1, threshold 20)
@@ -306,12 +281,13 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(AdIn a, const float* __restr
   // the three output-gradient row blocks are prefetched into registers with the head rows
   // (one round trip per workgroup instead of four) when all are present and 16-byte aligned
   constexpr int PH = (3 * NSH + 3) / 4;
-  const bool pf = NSH <= 9 && dharm && dcovs && dmeans && al16(dharm) && al16(dcovs) && al16(dmeans);
+  const bool pf = NSH <= 9 && dharm && dcovs && dmeans && dsplat::aligned16(dharm) && dsplat::aligned16(dcovs) &&
+                  dsplat::aligned16(dmeans);
   float4 vh[PH], vc[3], vm[1];
   if (pf) {
-    pref_get(dharm + n0 * (3 * NSH), (size_t)nrows * (3 * NSH), vh);
-    pref_get(dcovs + n0 * 9, (size_t)nrows * 9, vc);
-    pref_get(dmeans + n0 * 3, (size_t)nrows * 3, vm);
+    dsplat::pref_get<NT>(dharm + n0 * (3 * NSH), (size_t)nrows * (3 * NSH), vh);
+    dsplat::pref_get<NT>(dcovs + n0 * 9, (size_t)nrows * 9, vc);
+    dsplat::pref_get<NT>(dmeans + n0 * 3, (size_t)nrows * 3, vm);
   }
   const float z = valid ? a.depths[px.n] : 0.f;
   const float gop = (GLUE && valid && dopac) ? dopac[px.n] : 0.f;
@@ -322,7 +298,7 @@ __global__ __launch_bounds__(NT) void k_adapter_bwd(AdIn a, const float* __restr
   __syncthreads();
   if (pf) {
     const auto put_get = [&](const float* src, const auto& v, float* dst, int width) {
-      pref_put(src + n0 * width, (size_t)nrows * width, v, lds);
+      dsplat::pref_put<NT>(src + n0 * width, (size_t)nrows * width, v, lds);
       __syncthreads();
       for (int k = 0; k < width; ++k) dst[k] = valid ? lds[tid * width + k] : 0.f;
       __syncthreads();

@@ -137,6 +137,32 @@ __device__ __forceinline__ void stage_out(float* __restrict__ dst, size_t nfloat
   }
 }
 
+// Register prefetch of a workgroup's contiguous row block (nfloat floats, 16-byte aligned src):
+// P float4 per thread, issued together, so several row blocks of one workgroup are in flight
+// at once (stage_in waits for each block before the next one is requested); pref_put lands
+// them in LDS for the row transpose (the tail past the last float4 is read directly).
+// P >= ceil(width / 4) covers NTH rows of `width` floats.
+template <int NTH, int P>
+__device__ __forceinline__ void pref_get(const float* src, size_t nfloat, float4 (&v)[P]) {
+  const size_t n4 = nfloat / 4;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    v[k] = n4 ? s4[min((size_t)threadIdx.x + (size_t)k * NTH, n4 - 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+template <int NTH, int P>
+__device__ __forceinline__ void pref_put(const float* src, size_t nfloat, const float4 (&v)[P], float* lds) {
+  const size_t n4 = nfloat / 4;
+  float4* l4 = reinterpret_cast<float4*>(lds);
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const size_t i = (size_t)threadIdx.x + (size_t)k * NTH;
+    if (i < n4) l4[i] = v[k];
+  }
+  for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NTH) lds[i] = src[i];
+}
+__device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 inline int tiles_x(int W) { return (W + DSR_TILE - 1) / DSR_TILE; }
 inline int tiles_y(int H) { return (H + DSR_TILE - 1) / DSR_TILE; }
 

@@ -3494,7 +3494,7 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     const int32_t* __restrict__ scene_view_start, const int32_t* __restrict__ scene_views,
     const uint8_t* __restrict__ row_live,
     float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
-    float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D, int layout) {
+    float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D, int layout, int combine) {
   constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
   int fx_k = 0;  // fixed-point unit of dgeom (k_render_bwd); non-finite dL_dpix -> NaN gradients
   const float fx_unit = grad_fx_exp(gscale, threadIdx.x & 63, fx_k) ? ldexpf(1.f, fx_k - DSR_GRAD_FRAC_BITS)
@@ -3737,17 +3737,23 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     dm1 += e1 * gsc;
     dm2 += e2 * gsc;
   }
-  // outputs: coalesced through LDS
+  // outputs: coalesced through LDS. combine (the host's LDS allocation holds all three
+  // blocks): means, covariance and SH rows land in LDS together and leave behind one barrier
+  float* const lm = lds;
+  float* const lc = combine ? lds + 3 * NT : lds;
+  float* const lsh = combine ? lds + (3 + cw) * NT : lds;
   if (valid) {
-    lds[3 * tid] = dm0;
-    lds[3 * tid + 1] = dm1;
-    lds[3 * tid + 2] = dm2;
+    lm[3 * tid] = dm0;
+    lm[3 * tid + 1] = dm1;
+    lm[3 * tid + 2] = dm2;
   }
-  __syncthreads();
-  dsplat::stage_out<NT>(dmeans + 3 * sg0, (size_t)3 * nrows, lds);
-  __syncthreads();
+  if (!combine) {
+    __syncthreads();
+    dsplat::stage_out<NT>(dmeans + 3 * sg0, (size_t)3 * nrows, lm);
+    __syncthreads();
+  }
   if (valid) {
-    float* o = lds + tid * cw;
+    float* o = lc + tid * cw;
     if (cw == 9) {  // gradient lands on the upper triangle only (triu gather)
       o[0] = dc[0]; o[1] = dc[1]; o[2] = dc[2];
       o[3] = 0.f;   o[4] = dc[3]; o[5] = dc[4];
@@ -3757,8 +3763,10 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
       for (int k = 0; k < 6; ++k) o[k] = dc[k];
     }
   }
-  __syncthreads();
-  dsplat::stage_out<NT>(dcov6 + cw * sg0, (size_t)cw * nrows, lds);
+  if (!combine) {
+    __syncthreads();
+    dsplat::stage_out<NT>(dcov6 + cw * sg0, (size_t)cw * nrows, lc);
+  }
   if (valid) dopac[sg] = dop;
   if constexpr (DEG < 0) {
     if (valid) {
@@ -3766,11 +3774,15 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
       dcolors[3 * sg + 1] = dcol1;
       dcolors[3 * sg + 2] = dcol2;
     }
+    if (combine) {
+      __syncthreads();
+      dsplat::stage_out<NT>(dmeans + 3 * sg0, (size_t)3 * nrows, lm);
+      dsplat::stage_out<NT>(dcov6 + cw * sg0, (size_t)cw * nrows, lc);
+    }
   } else {
-    const int rw = 3 * M;
-    __syncthreads();
+    if (!combine) __syncthreads();
     if (valid) {
-      float* o = lds + tid * rw;
+      float* o = lsh + tid * rw;
       if (layout & kLayoutShChannelMajor) {
 #pragma unroll
         for (int k = 0; k < NC; ++k)
@@ -3785,7 +3797,11 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
       }
     }
     __syncthreads();
-    dsplat::stage_out<NT>(dshs + (size_t)rw * sg0, (size_t)rw * nrows, lds);
+    if (combine) {
+      dsplat::stage_out<NT>(dmeans + 3 * sg0, (size_t)3 * nrows, lm);
+      dsplat::stage_out<NT>(dcov6 + cw * sg0, (size_t)cw * nrows, lc);
+    }
+    dsplat::stage_out<NT>(dshs + (size_t)rw * sg0, (size_t)rw * nrows, lsh);
   }
 }
 
@@ -4384,13 +4400,17 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((G + NT - 1) / NT, S);
   const int deg = shs ? sh_degree : -1;
-  const size_t lds = (size_t)NT * (size_t)max(shs ? 3 * M : 0, 9) * sizeof(float);
-  DSPLAT_REQUIRE(lds <= 64 * 1024, "dsr_preprocess_bwd: M=%d SH coefficients exceed the LDS row staging", M);
+  const size_t lds_in = (size_t)NT * (size_t)max(shs ? 3 * M : 0, 9) * sizeof(float);
+  DSPLAT_REQUIRE(lds_in <= 64 * 1024, "dsr_preprocess_bwd: M=%d SH coefficients exceed the LDS row staging", M);
+  // all three output blocks at once when they fit the same 64 KiB (every M <= 17)
+  const size_t lds_all = (size_t)NT * (size_t)(3 + 9 + (shs ? 3 * M : 0)) * sizeof(float);
+  const int combine = lds_all <= 64 * 1024 ? 1 : 0;
+  const size_t lds = combine ? max(lds_all, lds_in) : lds_in;
 #define DSR_PREB(D)                                                                                              \
   k_preprocess_bwd<D><<<grid, NT, lds, st>>>(G, H, W, M, means, shs, cov6, cams, geom, dgeom, grad_scale,          \
                                            scene_view_start,                                                     \
                                            scene_views, row_live, dmeans, dshs, dcolors, dopac, dcov6, dmean2D,  \
-                                           layout)
+                                           layout, combine)
   switch (deg) {
     case -1: DSR_PREB(-1); break;
     case 0: DSR_PREB(0); break;
