@@ -92,31 +92,31 @@ int ensure_dyn_lds(const void* fn, size_t bytes, const char* what);
 // its store (one memory round trip per iteration: ~10 serial round trips for a block's
 // 37-float head rows).
 constexpr int kStageBatch = 8;
-template <int NTH>
+template <int NTH, int BATCH = kStageBatch>
 __device__ __forceinline__ void stage_in(const float* __restrict__ src, size_t nfloat, float* lds) {
   const uintptr_t addr = reinterpret_cast<uintptr_t>(src);
   if ((addr & 15) == 0) {
     const size_t n4 = nfloat / 4;
     const float4* s4 = reinterpret_cast<const float4*>(src);
     float4* l4 = reinterpret_cast<float4*>(lds);
-    for (size_t i0 = threadIdx.x; i0 < n4; i0 += (size_t)kStageBatch * NTH) {
-      float4 v[kStageBatch];  // unconditional loads (clamped index) keep v in registers
+    for (size_t i0 = threadIdx.x; i0 < n4; i0 += (size_t)BATCH * NTH) {
+      float4 v[BATCH];  // unconditional loads (clamped index) keep v in registers
 #pragma unroll
-      for (int k = 0; k < kStageBatch; ++k) v[k] = s4[min(i0 + (size_t)k * NTH, n4 - 1)];
+      for (int k = 0; k < BATCH; ++k) v[k] = s4[min(i0 + (size_t)k * NTH, n4 - 1)];
 #pragma unroll
-      for (int k = 0; k < kStageBatch; ++k) {
+      for (int k = 0; k < BATCH; ++k) {
         const size_t i = i0 + (size_t)k * NTH;
         if (i < n4) l4[i] = v[k];
       }
     }
     for (size_t i = 4 * n4 + threadIdx.x; i < nfloat; i += NTH) lds[i] = src[i];
   } else {
-    for (size_t i0 = threadIdx.x; i0 < nfloat; i0 += (size_t)kStageBatch * NTH) {
-      float v[kStageBatch];
+    for (size_t i0 = threadIdx.x; i0 < nfloat; i0 += (size_t)BATCH * NTH) {
+      float v[BATCH];
 #pragma unroll
-      for (int k = 0; k < kStageBatch; ++k) v[k] = src[min(i0 + (size_t)k * NTH, nfloat - 1)];
+      for (int k = 0; k < BATCH; ++k) v[k] = src[min(i0 + (size_t)k * NTH, nfloat - 1)];
 #pragma unroll
-      for (int k = 0; k < kStageBatch; ++k) {
+      for (int k = 0; k < BATCH; ++k) {
         const size_t i = i0 + (size_t)k * NTH;
         if (i < nfloat) lds[i] = v[k];
       }
