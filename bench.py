@@ -67,6 +67,8 @@ def parse():
                    help="config-E leg over N ranks: 'views' splits the 100 target views of ONE scene over the ranks "
                         "(Gaussians replicated, images all-gathered: per-scene latency, strong scaling); 'scenes': "
                         "every rank reconstructs its own scene (weak scaling)")
+    p.add_argument("--detail", default="gpurun_out/bench_detail.json",
+                   help="file for the full measurement record (the printed line is its summary); '' = none")
     p.add_argument("--skip-headline", action="store_true",
                    help="run only the --extra legs (profiling passes of one leg's kernels)")
     p.add_argument("--selftest", action="store_true",
@@ -405,7 +407,8 @@ def main():
                 "avg_ms": round(avg_ms, 5), "algorithmic_bytes_per_launch": alg,
                 "launches_timed": launches,
                 "per_kernel_avg_ms_probe": {k: round(v[1], 5) for k, v in sorted(all_kernels.items())},
-                "valu_issue": pmc_valu(name, workload_tag, avg_ms)}
+                "valu_issue": pmc_valu(name, workload_tag, avg_ms),
+                "traffic_tag": pmc_source_tag(workload_tag)}
         copy = measured_copy_gbs(dev)
         roof["peak_measured_copy"] = copy
         roof["frac_of_measured_copy"] = round(achieved / copy["value"], 5)
@@ -433,13 +436,79 @@ def main():
                        "gaussians": sc.gaussians.means.shape[1], "num_rendered_per_step": n_rendered,
                        "parallelism": f"dp{world} (per-scene, no collective)", "ranks": world,
                        "scenes_in_flight_per_gpu": B * lanes_used, "distinct_scenes_per_gpu": B * lanes_used},
-            "parity_vs_oracle": psnr,
+            "parity_vs_oracle": psnr, "_size": f"{H}x{W}",
             "roofline": roof, "cpu_baseline": cpu, "gpu_state": gstate,
             **extra,
         }
-        print(json.dumps(line), flush=True)
+        detail = write_detail(line, args.detail)
+        print(json.dumps(compact_line(line, detail)), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def write_detail(line: dict, path: str) -> str | None:
+    """The whole measurement record (every leg's roofline, the launch calibration, per-kernel
+    probes, the cost-volume shapes) as JSON beside the run: the printed line keeps one summary
+    number per leg so that it fits the driver's record."""
+    if not path:
+        return None
+    try:
+        Path(path).parent.mkdir(parents=True, exist_ok=True)
+        Path(path).write_text(json.dumps(line, indent=1) + "\n")
+        return path
+    except OSError:
+        return None
+
+
+def compact_line(line: dict, detail: str | None) -> dict:
+    """The printed bench line (< 2 KB): the contract keys, the headline's roofline (scalars, VALU
+    issue included) and CPU baseline, and one or two numbers per secondary leg."""
+    def g(d, *keys):
+        for k in keys:
+            if not isinstance(d, dict):
+                return None
+            d = d.get(k)
+        return d
+
+    out = {k: line.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                     "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    cfg = line.get("config") or {}
+    out["config"] = {"workload": f"2-view {line.get('_size')} RE10K render, G={cfg.get('gaussians')}, "
+                                 f"{cfg.get('views_per_scene')} target views/scene, fp32",
+                     "global_batch": cfg.get("global_batch"), "scenes_per_step_per_gpu": cfg.get("scenes_per_step_per_gpu"),
+                     "parallelism": cfg.get("parallelism")}
+    out["world_size_seen"] = line.get("world_size_seen")
+    out["launch_mode"] = line.get("launch_mode")
+    out["ms_per_step_eager"] = line.get("ms_per_step_eager")
+    r = line.get("roofline") or {}
+    out["roofline"] = {k: r.get(k) for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "avg_ms")}
+    if r:
+        out["roofline"]["algorithmic_bytes"] = r.get("algorithmic_bytes_per_launch")
+        out["roofline"]["traffic_source"] = r.get("traffic_tag")
+        out["roofline"]["valu_issue"] = g(r, "valu_issue", "frac")
+    c = line.get("cpu_baseline") or {}
+    out["cpu_baseline"] = {k: c.get(k) for k in ("value", "unit", "cores", "kind")} if c else None
+    if c:
+        out["cpu_baseline"]["sample"] = c.get("sample")
+        out["cpu_baseline"]["single_thread"] = c.get("single_thread_views_per_s")
+    out["parity_max_l1"] = g(line, "parity_vs_oracle", "max_l1")
+    legs = {"ref_binning_views_s": g(line, "reference_binning", "value"),
+            "train_c_ms": g(line, "train_config_c", "ms_per_step"),
+            "train_c_frac": g(line, "train_config_c", "roofline", "frac"),
+            "render_d_ms": g(line, "render_config_d", "ms_per_step"),
+            "render_d_frac": g(line, "render_config_d", "roofline", "frac"),
+            "recon_e_ms_scene": g(line, "recon_config_e", "ms_per_scene"),
+            "recon_e_frac": g(line, "recon_config_e", "roofline", "frac"),
+            "train_d_dp_ms": g(line, "train_config_d_dp", "ms_per_step")}
+    cv = line.get("cost_volume") or {}
+    for tag, key in (("cv_a", "config_a_32x32"), ("cv_b0", "config_b_scale0_64x64"),
+                     ("cv_d0", "config_d_scale0_56x96"), ("cv_d1", "config_d_scale1_112x192")):
+        if key in cv:
+            legs[tag + "_ms"] = [g(cv, key, "ms_per_call"), g(cv, key, "ms_fwd_bwd")]
+            legs[tag + "_frac"] = g(cv, key, "frac")
+    out["legs"] = {k: v for k, v in legs.items() if v is not None}
+    out["detail"] = detail
+    return out
 
 
 def gpu_state(dev) -> dict:
@@ -531,6 +600,17 @@ def _pmc_file(workload):
             if d.get("workload") == workload:
                 return d
     return None
+
+
+def pmc_source_tag(workload):
+    """Which profiling run the workload's committed PMC summary came from (its round tag, e.g.
+    "profiles/pmc_traffic_2v256x256x3b16.json r06a")."""
+    import re
+    d = _pmc_file(workload)
+    if d is None:
+        return None
+    m = re.findall(r"\b(r\d\d[a-z0-9]*)\b", d.get("source", ""))
+    return f"pmc_traffic_{workload}.json {m[-1] if m else ''}".strip()
 
 
 def pmc_traffic(kernel, workload):

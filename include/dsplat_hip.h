@@ -410,11 +410,20 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
  * (overwritten). fwd_path: the forward's path argument; ref / tgt: the forward's inputs;
  * workspace: the forward's (completed here when the forward ran the band kernel);
  * dcv_cost_volume_bwd_workspace_size bytes of scratch (channel-last gradient accumulators).
- * On the matrix-core paths both gradients are bit-identical run to run: reference gradients
- * are summed in a fixed order, the shared sums (the gradient weights in LDS, the target
- * gradients in HBM) in integer fixed point (units from the largest |dcost| and |ref|). The
- * direct kernel (C not a multiple of 16) adds target gradients with float atomics. */
+ * On the matrix-core paths both gradients are bit-identical run to run at every image size
+ * (the epipolar grouping is a function of the inputs, never of atomic arrival): reference
+ * gradients are summed in a fixed order, the shared sums in integer fixed point — the gradient
+ * weights in LDS with a unit per reference pixel and depth chunk (from that pixel's largest
+ * |dcost|), the target gradients in HBM with the finest unit the int64 range allows for the
+ * shape (from the largest |dcost| and |ref| and the number of partial sums per element). A
+ * non-finite dcost or ref makes dtgt NaN. The direct kernel (C not a multiple of 16) adds target
+ * gradients with float atomics. */
 size_t dcv_cost_volume_bwd_workspace_size(int B, int J, int C, int H, int W);
+/* The matrix-core backward's workgroup shape for these sizes (what dcv_cost_volume_bwd
+ * launches when C is a multiple of 16): 2^pxb reference pixels per workgroup (4: 16, 5: 32,
+ * 6: 64 — consecutive epipolar groups sharing one union band) and spt samples per thread
+ * (depth chunk (256 >> pxb) * spt). Returns 1 (no matrix-core backward) otherwise. */
+int dcv_cost_volume_bwd_shape(int B, int C, int H, int W, int D, int depth_per_pixel, int* pxb, int* spt);
 int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_pixel, int fwd_path,
                         const float* ref, const float* tgt, void* workspace, const float* intr,
                         const float* pose, const float* depth, float clamp_min_depth,

@@ -51,6 +51,7 @@ SIGNATURES: dict[str, tuple] = {
     "dcv_cost_volume_workspace_size": (ctypes.c_size_t, [_I, _I, _I, _I, _I]),
     "dcv_cost_volume_bwd_workspace_size": (ctypes.c_size_t, [_I, _I, _I, _I, _I]),
     "dcv_cost_volume_path": (_I, [_I, _I, _I, _I, _I]),
+    "dcv_cost_volume_bwd_shape": (_I, [_I, _I, _I, _I, _I, _I, _P, _P]),
     "dcv_cost_volume_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P, _P]),
     "dcv_cost_volume_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, c_float, _P, _P,
                                  _P, _P, _P]),

@@ -17,6 +17,7 @@
 
 #include "dsplat_common.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -316,9 +317,7 @@ constexpr int EG = 16;                       // reference pixels per group (MFMA
 // for D <= 32: the per-pixel candidate windows of the finer scale); 16 depth lanes x SPT
 constexpr int kEUMax = 256;                  // band pixels per GEMM pass (LDS)
 constexpr int kECorr = kEUMax + 1;           // odd row stride: the gather's lanes spread over banks
-constexpr int kEpiBuckets = 8192;            // epipolar-line buckets per (batch, view)
-
-// Line key of reference pixel (px, py) w.r.t. one source view (see k_epi_groups).
+// Line key of reference pixel (px, py) w.r.t. one source view (see the grouping passes below).
 struct EpiKey {
   int mode;        // 0: by row (no baseline), 1: angle about a finite epipole, 2: offset across parallel lines
   float ex, ey;    // epipole (mode 1)
@@ -326,6 +325,7 @@ struct EpiKey {
   float o0, inv;   // bucket = floor((value - o0) * inv)
   int nb;
 };
+static_assert(sizeof(EpiKey) == 32, "EpiKey is 8 words in the workspace");
 __device__ __forceinline__ int epi_bucket(const EpiKey& k, float px, float py) {
   float v;
   if (k.mode == 0) return min((int)py, k.nb - 1);
@@ -338,259 +338,354 @@ __device__ __forceinline__ int epi_bucket(const EpiKey& k, float px, float py) {
   return min(max((int)((v - k.o0) * k.inv), 0), k.nb - 1);
 }
 
-// One workgroup per (batch, source view j): groups[b, j, :] = the reference pixel ids
-// ordered by the epipolar line (w.r.t. view j) they lie on. The epipole e = K c, c = -R^T t
-// the source camera centre in reference camera coordinates (pose = [R | t] maps reference
-// to source coordinates). Finite epipole: lines are buckets of the angle about e, 1 / dmax
-// radians wide (dmax: farthest pixel from e), so neighbouring buckets are <= 1 px apart
-// anywhere in the image; epipole far outside the image (sideways baseline): parallel lines,
-// 1-px buckets of the offset across them; no baseline: rows. Inside a line (round 5) the
-// pixels are ordered by where their middle depth candidate lands along the target line: each
-// line's key range is cut into ceil(n / 16) segments (about one 16-pixel group each), the
-// pixels are counting-sorted by (line, segment) and, inside a segment, by pixel id. With
-// per-pixel candidate windows (scale > 0) a group's 16 pixels then tap nearby stretches of the
-// line and its band is their windows' union, not the whole line. The order is a function of
-// the inputs only (never of atomic arrival), so the groups, and with them the backward's MFMA
-// blocking and bits, are the same in every run. (Results of the forward do not depend on the
-// grouping at all: each output is computed from its own correlations.)
-// Also writes geom[b, j] = {M = K R K^-1 (row-major), K t} (double, rounded once): the
-// projection of reference pixel p at depth d is M [px, py, 1] d + K t (see epi_ray).
-// larger images (pixel id in 15 bits, keys in registers, the scattered pixels staged in LDS
-// with the two line tables: 160 KB): lines only
-constexpr int kEpiPool = 3 * kEpiBuckets - 32;
-constexpr int kEpiKeyMaxPixels = kEpiPool;
-__global__ __launch_bounds__(1024) void k_epi_groups(int J, int H, int W, int D, int depth_per_pixel,
-                                                     const float* __restrict__ intr, const float* __restrict__ pose,
-                                                     const float* __restrict__ depth, int* __restrict__ groups,
-                                                     float* __restrict__ geom) {
-  __shared__ uint32_t hist[kEpiBuckets];  // line counts, then segment-bin counters
-  __shared__ uint32_t lmin[kEpiBuckets];  // per line: key minimum (orderable bits), then the bins' starts
-  // bst (first segment bin of each line) and lmax (per line: key maximum), then the pixels
-  // scattered by bin (read back by the in-bin ranking: LDS instead of a global round trip per
-  // comparison, which made this kernel 204 us at config D scale 1)
-  __shared__ uint32_t pool[kEpiPool];
-  uint32_t* const bst = pool;
-  uint32_t* const lmax = pool + kEpiBuckets;
-  __shared__ float s_geom[12];
-  __shared__ uint32_t wsum[16];
-  const int b = blockIdx.x, j = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int HW = H * W;
-  const size_t bj = (size_t)b * J + j;
+// ---- epipolar grouping (round 6: a grid-wide pass pipeline) --------------------------------
+// groups[b, j, :] = the reference pixel ids ordered by the epipolar line (w.r.t. view j) they lie
+// on. The epipole e = K c, c = -R^T t the source camera centre in reference camera coordinates
+// (pose = [R | t] maps reference to source coordinates). Finite epipole: lines are buckets of the
+// angle about e, 1 / dmax radians wide (dmax: farthest pixel from e), so neighbouring buckets are
+// <= 1 px apart anywhere in the image; epipole far outside the image (sideways baseline): parallel
+// lines, 1-px buckets of the offset across them; no baseline: rows. Inside a line the pixels are
+// ordered by where their middle depth candidate lands along the target line: each line's key
+// range is cut into ceil(n / 16) segments (about one 16-pixel group each), the pixels are
+// counting-sorted by (line, segment) and, inside a segment, by pixel id. With per-pixel candidate
+// windows (scale > 0) a group's 16 pixels then tap nearby stretches of the line and its band is
+// their windows' union, not the whole line. The order is a function of the inputs only (never of
+// atomic arrival), so the groups, and with them the backward's MFMA blocking and bits, are the
+// same in every run, at every image size. (Results of the forward do not depend on the grouping
+// at all: each output is computed from its own correlations.)
+// Round 5 did this in ONE workgroup per (scene, view) (48 workgroups at config D: 129 us at
+// scale 1, and above 24,544 pixels it fell back to an arrival-ordered line sort). Here every step
+// that touches pixels is a grid over the pixels:
+//   k_epi_init     per image: line-key parameters + geom; clears the line / bin tables
+//   k_epi_count    per pixel: line, sort key; per line: count, key min / max (wave-run atomics)
+//   k_epi_segs     per image: first segment bin of each line (scan of ceil(n / 16))
+//   k_epi_bin      per pixel: its segment bin; per bin: count
+//   k_epi_binscan  per image: bin starts (scan)
+//   k_epi_scatter  per pixel: into its bin (arrival order)
+//   k_epi_rank     per position: the bin's pixels re-ordered by id (the arrival order is erased)
+// geom[b, j] = {M = K R K^-1 (row-major), K t} (double, rounded once): the projection of
+// reference pixel p at depth d is M [px, py, 1] d + K t (see epi_ray).
+constexpr int kEpiBuckets = 8192;  // epipolar-line buckets per (batch, view)
+__host__ __device__ constexpr int epi_bin_stride(int HW) { return (HW + 15) / 16 + kEpiBuckets + 1; }
+// grouping scratch inside the forward workspace, after geom
+struct EpiScratch {
+  EpiKey* keys;                             // [BJ]
+  uint32_t *hist, *lmin, *lmax, *bst;       // [BJ][kEpiBuckets]
+  uint32_t *bcount, *bstart;                // [BJ][epi_bin_stride]
+  uint32_t *pl, *pkv;                       // [BJ][HW]: line (then bin), sort-key bits
+  int* stage;                               // [BJ][HW]: pixels by bin, arrival order
+};
+__host__ __device__ inline size_t epi_scratch_words(int BJ, int HW) {
+  return (size_t)BJ * (8 + 4 * (size_t)kEpiBuckets + 2 * (size_t)epi_bin_stride(HW) + 3 * (size_t)HW);
+}
+__host__ __device__ inline EpiScratch epi_scratch(void* base, int BJ, int HW) {
+  uint32_t* p = static_cast<uint32_t*>(base);
+  EpiScratch s;
+  s.keys = reinterpret_cast<EpiKey*>(p);
+  p += (size_t)BJ * 8;
+  s.hist = p;
+  p += (size_t)BJ * kEpiBuckets;
+  s.lmin = p;
+  p += (size_t)BJ * kEpiBuckets;
+  s.lmax = p;
+  p += (size_t)BJ * kEpiBuckets;
+  s.bst = p;
+  p += (size_t)BJ * kEpiBuckets;
+  const size_t bsz = (size_t)BJ * epi_bin_stride(HW);
+  s.bcount = p;
+  p += bsz;
+  s.bstart = p;
+  p += bsz;
+  s.pl = p;
+  p += (size_t)BJ * HW;
+  s.pkv = p;
+  p += (size_t)BJ * HW;
+  s.stage = reinterpret_cast<int*>(p);
+  return s;
+}
+// orderable bits of a float (monotone as unsigned) and back
+__device__ __forceinline__ uint32_t epi_obits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float epi_ofloat(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+
+// The line-key parameters of one (scene, view) from its K and pose (double).
+__device__ EpiKey epi_key_of(const float* __restrict__ k, const float* __restrict__ P, int H, int W) {
   EpiKey key;
-  {
-    const float* k = intr + bj * 9;
-    const float* P = pose + bj * 16;
-    const double tx = P[3], ty = P[7], tz = P[11];
-    if (tid < 12) {
-      // Kinv by the adjugate, M = K R Kinv, bt = K t
-      const double a = k[0], bb = k[1], c = k[2], d = k[3], e = k[4], f = k[5], g = k[6], h = k[7], i = k[8];
-      const double A = e * i - f * h, Bc = -(d * i - f * g), Cc = d * h - e * g;
-      const double id = 1.0 / (a * A + bb * Bc + c * Cc);
-      const double Ki[9] = {A * id, -(bb * i - c * h) * id, (bb * f - c * e) * id,
-                            Bc * id, (a * i - c * g) * id, -(a * f - c * d) * id,
-                            Cc * id, -(a * h - bb * g) * id, (a * e - bb * d) * id};
-      const int r = tid / 3, q = tid % 3;
-      double v = 0.0;
-      if (tid < 9) {
-        for (int m = 0; m < 3; ++m) {
-          double rk = 0.0;  // (R Kinv)[m][q]
-          for (int n = 0; n < 3; ++n) rk += (double)P[m * 4 + n] * Ki[n * 3 + q];
-          v += (double)k[r * 3 + m] * rk;
-        }
-      } else {
-        const int rr = tid - 9;
-        v = k[rr * 3 + 0] * tx + k[rr * 3 + 1] * ty + k[rr * 3 + 2] * tz;
-      }
-      geom[bj * 12 + tid] = (float)v;
-      s_geom[tid] = (float)v;
+  const double tx = P[3], ty = P[7], tz = P[11];
+  const double cx = -(P[0] * tx + P[4] * ty + P[8] * tz);
+  const double cy = -(P[1] * tx + P[5] * ty + P[9] * tz);
+  const double cz = -(P[2] * tx + P[6] * ty + P[10] * tz);
+  const double exh = k[0] * cx + k[1] * cy + k[2] * cz;
+  const double eyh = k[3] * cx + k[4] * cy + k[5] * cz;
+  const double ezh = k[6] * cx + k[7] * cy + k[8] * cz;
+  const double diag = sqrt((double)W * W + (double)H * H);
+  const double mx = 0.5 * (W - 1), my = 0.5 * (H - 1);
+  key.ex = key.ey = key.nx = key.ny = key.o0 = 0.f;
+  key.inv = 1.f;
+  if (fabs(exh) + fabs(eyh) + fabs(ezh) < 1e-12) {
+    key.mode = 0;
+    key.nb = min(H, kEpiBuckets);
+  } else if (fabs(ezh) > 1e-12 && hypot(exh / ezh - mx, eyh / ezh - my) < 64.0 * diag) {
+    key.mode = 1;
+    key.ex = (float)(exh / ezh);
+    key.ey = (float)(eyh / ezh);
+    double dmax = 1.0;
+    for (int c = 0; c < 4; ++c)
+      dmax = fmax(dmax, hypot((c & 1) * (W - 1) - (double)key.ex, (c >> 1) * (H - 1) - (double)key.ey));
+    const double nb = ceil(3.14159265358979 * dmax) + 1;
+    key.nb = (int)fmin(nb, (double)kEpiBuckets);
+    key.inv = (float)(key.nb / 3.14159265358979);
+  } else {
+    key.mode = 2;
+    const double n = hypot(exh, eyh);
+    key.nx = (float)(-eyh / n);
+    key.ny = (float)(exh / n);
+    float lo = 3.4e38f, hi = -3.4e38f;
+    for (int c = 0; c < 4; ++c) {
+      const float v = key.nx * (float)((c & 1) * (W - 1)) + key.ny * (float)((c >> 1) * (H - 1));
+      lo = fminf(lo, v);
+      hi = fmaxf(hi, v);
     }
-    const double cx = -(P[0] * tx + P[4] * ty + P[8] * tz);
-    const double cy = -(P[1] * tx + P[5] * ty + P[9] * tz);
-    const double cz = -(P[2] * tx + P[6] * ty + P[10] * tz);
-    const double exh = k[0] * cx + k[1] * cy + k[2] * cz;
-    const double eyh = k[3] * cx + k[4] * cy + k[5] * cz;
-    const double ezh = k[6] * cx + k[7] * cy + k[8] * cz;
-    const double diag = sqrt((double)W * W + (double)H * H);
-    const double mx = 0.5 * (W - 1), my = 0.5 * (H - 1);
-    key.ex = key.ey = key.nx = key.ny = key.o0 = 0.f;
-    key.inv = 1.f;
-    if (fabs(exh) + fabs(eyh) + fabs(ezh) < 1e-12) {
-      key.mode = 0;
-      key.nb = H;
-    } else if (fabs(ezh) > 1e-12 && hypot(exh / ezh - mx, eyh / ezh - my) < 64.0 * diag) {
-      key.mode = 1;
-      key.ex = (float)(exh / ezh);
-      key.ey = (float)(eyh / ezh);
-      double dmax = 1.0;
-      for (int c = 0; c < 4; ++c)
-        dmax = fmax(dmax, hypot((c & 1) * (W - 1) - (double)key.ex, (c >> 1) * (H - 1) - (double)key.ey));
-      const double nb = ceil(3.14159265358979 * dmax) + 1;
-      key.nb = (int)fmin(nb, (double)kEpiBuckets);
-      key.inv = (float)(key.nb / 3.14159265358979);
-    } else {
-      key.mode = 2;
-      const double n = hypot(exh, eyh);
-      key.nx = (float)(-eyh / n);
-      key.ny = (float)(exh / n);
-      float lo = 3.4e38f, hi = -3.4e38f;
-      for (int c = 0; c < 4; ++c) {
-        const float v = key.nx * (float)((c & 1) * (W - 1)) + key.ny * (float)((c >> 1) * (H - 1));
-        lo = fminf(lo, v);
-        hi = fmaxf(hi, v);
+    key.o0 = lo;
+    key.nb = min(kEpiBuckets, (int)ceilf(hi - lo) + 1);
+    key.inv = (float)key.nb / fmaxf(hi - lo + 1.f, 1.f);
+  }
+  return key;
+}
+
+// grid (ceil(max(kEpiBuckets, bin stride) / 256), B * J), 256 threads. Block 0 of each image
+// writes its key and geom; every block clears its share of the tables.
+__global__ __launch_bounds__(256) void k_epi_init(int J, int H, int W, const float* __restrict__ intr,
+                                                  const float* __restrict__ pose, float* __restrict__ geom,
+                                                  EpiScratch s) {
+  const int bj = blockIdx.y, tid = threadIdx.x, HW = H * W, nbs = epi_bin_stride(HW);
+  const float* k = intr + (size_t)bj * 9;
+  const float* P = pose + (size_t)bj * 16;
+  if (blockIdx.x == 0 && tid < 12) {
+    // Kinv by the adjugate, M = K R Kinv, bt = K t
+    const double a = k[0], bb = k[1], c = k[2], d = k[3], e = k[4], f = k[5], g = k[6], h = k[7], i = k[8];
+    const double A = e * i - f * h, Bc = -(d * i - f * g), Cc = d * h - e * g;
+    const double id = 1.0 / (a * A + bb * Bc + c * Cc);
+    const double Ki[9] = {A * id, -(bb * i - c * h) * id, (bb * f - c * e) * id,
+                          Bc * id, (a * i - c * g) * id, -(a * f - c * d) * id,
+                          Cc * id, -(a * h - bb * g) * id, (a * e - bb * d) * id};
+    const int r = tid / 3, q = tid % 3;
+    double v = 0.0;
+    if (tid < 9) {
+      for (int m = 0; m < 3; ++m) {
+        double rk = 0.0;  // (R Kinv)[m][q]
+        for (int n = 0; n < 3; ++n) rk += (double)P[m * 4 + n] * Ki[n * 3 + q];
+        v += (double)k[r * 3 + m] * rk;
       }
-      key.o0 = lo;
-      key.nb = min(kEpiBuckets, (int)ceilf(hi - lo) + 1);
-      key.inv = (float)key.nb / fmaxf(hi - lo + 1.f, 1.f);
+    } else {
+      const int rr = tid - 9;
+      v = k[rr * 3 + 0] * (double)P[3] + k[rr * 3 + 1] * (double)P[7] + k[rr * 3 + 2] * (double)P[11];
+    }
+    geom[(size_t)bj * 12 + tid] = (float)v;
+  }
+  if (blockIdx.x == 0 && tid == 32) s.keys[bj] = epi_key_of(k, P, H, W);
+  const int i = blockIdx.x * 256 + tid;
+  if (i < kEpiBuckets) {
+    s.hist[(size_t)bj * kEpiBuckets + i] = 0u;
+    s.lmin[(size_t)bj * kEpiBuckets + i] = 0xFFFFFFFFu;
+    s.lmax[(size_t)bj * kEpiBuckets + i] = 0u;
+  }
+  if (i < nbs) s.bcount[(size_t)bj * nbs + i] = 0u;
+}
+
+// Runs of equal keys in a wave (lanes with the key of their left neighbour; consecutive pixels of
+// a row mostly share their line and bin): inclusive segmented scans of a count, a minimum and a
+// maximum, so only the run's last lane issues the global atomics. All 64 lanes must be active
+// (callers pass key 0xFFFFFFFF for lanes without an item).
+struct EpiRun {
+  uint32_t cnt, mn, mx;
+  int head;  // the run's first lane
+  bool tail;
+};
+__device__ __forceinline__ EpiRun epi_run(uint32_t key, uint32_t cnt, uint32_t mn, uint32_t mx) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t left = __shfl_up(key, 1, 64), right = __shfl_down(key, 1, 64);
+  const bool head = lane == 0 || left != key;
+  const int hd = (int)dsplat::wave_incl_max_dpp(head ? (uint32_t)lane : 0u);  // this run's first lane
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t c2 = __shfl_up(cnt, off, 64), n2 = __shfl_up(mn, off, 64), x2 = __shfl_up(mx, off, 64);
+    if (lane - off >= hd) {
+      cnt += c2;
+      mn = min(mn, n2);
+      mx = max(mx, x2);
     }
   }
-  int* out = groups + bj * HW;
-  // each pixel's sort key: where its middle candidate lands, projected on the direction of its
-  // own near-to-far step (canonically oriented: x > 0, or y > 0 on vertical lines), so the
-  // pixels of one target line, whose directions agree to a fraction of a degree, order along it
+  return {cnt, mn, mx, hd, lane == 63 || right != key};
+}
+
+// grid (ceil(HW / 256), B * J), 256 threads: each pixel's line and sort key (where its middle
+// candidate lands, projected on the direction of its own near-to-far step, canonically oriented:
+// x > 0, or y > 0 on vertical lines, so the pixels of one target line, whose directions agree to
+// a fraction of a degree, order along it); per line the count and the key range.
+__global__ __launch_bounds__(256) void k_epi_count(int H, int W, int D, int depth_per_pixel,
+                                                   const float* __restrict__ depth, const float* __restrict__ geom,
+                                                   int J, EpiScratch s) {
+  const int bj = blockIdx.y, HW = H * W, b = bj / J;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const EpiKey key = s.keys[bj];
+  const float* gm = geom + (size_t)bj * 12;
+  const bool valid = p < HW;
+  const int pc = valid ? p : 0;
   const float* dp = depth + (size_t)b * D * (depth_per_pixel ? HW : 1);
   const int dm = D / 2, d1 = D > 1 ? D - 1 : 0;
-  auto target = [&](int p, float d, float& u, float& v) {
-    const float px = (float)(p % W), py = (float)(p / W);
-    const float x = fmaf(fmaf(s_geom[0], px, fmaf(s_geom[1], py, s_geom[2])), d, s_geom[9]);
-    const float y = fmaf(fmaf(s_geom[3], px, fmaf(s_geom[4], py, s_geom[5])), d, s_geom[10]);
-    const float z = fmaxf(fmaf(fmaf(s_geom[6], px, fmaf(s_geom[7], py, s_geom[8])), d, s_geom[11]), 1e-3f);
+  const float dmid = depth_per_pixel ? dp[(size_t)dm * HW + pc] : dp[dm];
+  const float dfar = depth_per_pixel ? dp[(size_t)d1 * HW + pc] : dp[d1];
+  const float px = (float)(pc % W), py = (float)(pc / W);
+  auto target = [&](float d, float& u, float& v) {
+    const float x = fmaf(fmaf(gm[0], px, fmaf(gm[1], py, gm[2])), d, gm[9]);
+    const float y = fmaf(fmaf(gm[3], px, fmaf(gm[4], py, gm[5])), d, gm[10]);
+    const float z = fmaxf(fmaf(fmaf(gm[6], px, fmaf(gm[7], py, gm[8])), d, gm[11]), 1e-3f);
     u = x / z;
     v = y / z;
   };
-  auto sort_key = [&](int p) -> float {
-    const float dmid = depth_per_pixel ? dp[(size_t)dm * HW + p] : dp[dm];
-    const float dfar = depth_per_pixel ? dp[(size_t)d1 * HW + p] : dp[d1];
-    float u0, v0, u1, v1;
-    target(p, dmid, u0, v0);
-    target(p, dfar, u1, v1);
-    float dx = u1 - u0, dy = v1 - v0;
-    const float l = sqrtf(dx * dx + dy * dy);
-    if (l > 1e-6f && l < 3.0e38f) {
-      dx /= l;
-      dy /= l;
-    } else {
-      dx = 1.f;
-      dy = 0.f;
-    }
-    if (dx < -1e-3f || (!(dx > 1e-3f) && dy < 0.f)) {
-      dx = -dx;
-      dy = -dy;
-    }
-    const float kv = fmaf(u0, dx, v0 * dy);
-    return (kv == kv && fabsf(kv) < 1e30f) ? kv : 1e30f;  // NaN / inf: last
-  };
-  // exclusive scan of 8192 words in place (8 per thread); returns the total
-  auto scan8k = [&](uint32_t* a, uint32_t* copy) -> uint32_t {
-    constexpr int PT = kEpiBuckets / 1024;
+  float u0, v0, u1, v1;
+  target(dmid, u0, v0);
+  target(dfar, u1, v1);
+  float dx = u1 - u0, dy = v1 - v0;
+  const float l = sqrtf(dx * dx + dy * dy);
+  if (l > 1e-6f && l < 3.0e38f) {
+    dx /= l;
+    dy /= l;
+  } else {
+    dx = 1.f;
+    dy = 0.f;
+  }
+  if (dx < -1e-3f || (!(dx > 1e-3f) && dy < 0.f)) {
+    dx = -dx;
+    dy = -dy;
+  }
+  float kv = fmaf(u0, dx, v0 * dy);
+  kv = (kv == kv && fabsf(kv) < 1e30f) ? kv : 1e30f;  // NaN / inf: last
+  const uint32_t line = valid ? (uint32_t)epi_bucket(key, px, py) : 0xFFFFFFFFu;
+  const uint32_t ob = epi_obits(kv);
+  if (valid) {
+    s.pl[(size_t)bj * HW + p] = line;
+    s.pkv[(size_t)bj * HW + p] = ob;
+  }
+  const EpiRun r = epi_run(line, valid ? 1u : 0u, ob, ob);
+  if (r.tail && valid) {
+    const size_t o = (size_t)bj * kEpiBuckets + line;
+    atomicAdd(&s.hist[o], r.cnt);
+    atomicMin(&s.lmin[o], r.mn);
+    atomicMax(&s.lmax[o], r.mx);
+  }
+}
+
+// Exclusive scan of n words by one 1024-thread workgroup (chunks of 8192, carried): out[i] =
+// sum of load(k) for k < i; out2 (optional) gets a copy. Returns the total.
+template <typename Load>
+__device__ uint32_t epi_block_scan(int n, Load load, uint32_t* __restrict__ out, uint32_t* __restrict__ out2,
+                                   uint32_t* wsum) {
+  constexpr int PT = 8;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint32_t carry = 0;
+  for (int base = 0; base < n; base += 1024 * PT) {
     uint32_t v[PT], tot = 0;
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
-      v[i] = a[tid * PT + i];
+      const int k = base + tid * PT + i;
+      v[i] = k < n ? load(k) : 0u;
       tot += v[i];
     }
     const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    uint32_t off = incl - tot;
-    for (int k = 0; k < wv; ++k) off += wsum[k];
-    uint32_t total = 0;
-    for (int k = 0; k < 16; ++k) total += wsum[k];
+    uint32_t off = carry + incl - tot, total = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < wv) off += wsum[k];
+      total += wsum[k];
+    }
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
-      a[tid * PT + i] = off;
-      if (copy) copy[tid * PT + i] = off;
+      const int k = base + tid * PT + i;
+      if (k < n) {
+        out[k] = off;
+        if (out2) out2[k] = off;
+      }
       off += v[i];
     }
-    __syncthreads();
-    return total;
-  };
-  // orderable bits of a float (monotone as unsigned)
-  auto obits = [](float f) -> uint32_t {
-    const uint32_t u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-  };
-  auto ofloat = [](uint32_t o) -> float { return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o); };
-  // 1) per line: count, key min / max (the keys are kept in registers)
-  constexpr int PER = (kEpiKeyMaxPixels + 1023) / 1024;
-  const bool sorted = HW <= kEpiKeyMaxPixels;  // uniform
-  for (int i = tid; i < kEpiBuckets; i += 1024) {
-    hist[i] = 0u;
-    lmin[i] = 0xFFFFFFFFu;
-    lmax[i] = 0u;
+    carry += total;
+    __syncthreads();  // wsum reused by the next chunk
   }
-  __syncthreads();
-  if (!sorted) {  // large images: lines only, arrival order inside them
-    for (int p = tid; p < HW; p += 1024) atomicAdd(&hist[epi_bucket(key, (float)(p % W), (float)(p / W))], 1u);
-    __syncthreads();
-    scan8k(hist, nullptr);
-    for (int p = tid; p < HW; p += 1024) out[atomicAdd(&hist[epi_bucket(key, (float)(p % W), (float)(p / W))], 1u)] = p;
-    return;
+  return carry;
+}
+
+// grid B * J, 1024 threads: bst[line] = the line's first segment bin.
+__global__ __launch_bounds__(1024) void k_epi_segs(EpiScratch s) {
+  __shared__ uint32_t wsum[16];
+  const size_t o = (size_t)blockIdx.x * kEpiBuckets;
+  const uint32_t* hist = s.hist + o;
+  epi_block_scan(kEpiBuckets, [&](int k) { return (hist[k] + 15u) / 16u; }, s.bst + o, nullptr, wsum);
+}
+
+// grid (ceil(HW / 256), B * J): each pixel's segment bin (its line's key range cut into
+// ceil(n / 16) equal parts); per bin the count.
+__global__ __launch_bounds__(256) void k_epi_bin(int HW, EpiScratch s) {
+  const int bj = blockIdx.y, p = blockIdx.x * 256 + threadIdx.x;
+  const bool valid = p < HW;
+  uint32_t bin = 0xFFFFFFFFu;
+  if (valid) {
+    const int l = (int)s.pl[(size_t)bj * HW + p];
+    const size_t o = (size_t)bj * kEpiBuckets + l;
+    const uint32_t nseg = (s.hist[o] + 15u) / 16u;
+    const float lo = epi_ofloat(s.lmin[o]), hi = epi_ofloat(s.lmax[o]);
+    const float kv = epi_ofloat(s.pkv[(size_t)bj * HW + p]);
+    const float f = hi > lo ? (kv - lo) / (hi - lo) : 0.f;
+    bin = s.bst[o] + (uint32_t)min((int)nseg - 1, max(0, (int)(f * (float)nseg)));
+    s.pl[(size_t)bj * HW + p] = bin;
   }
-  // (the line of pixel p is recomputed where needed instead of kept: registers)
-  auto line_of = [&](int p) { return epi_bucket(key, (float)(p % W), (float)(p / W)); };
-  float kv[PER];
-#pragma unroll
-  for (int t = 0; t < PER; ++t) kv[t] = tid + 1024 * t < HW ? sort_key(tid + 1024 * t) : 0.f;
-#pragma unroll
-  for (int t = 0; t < PER; ++t)
-    if (tid + 1024 * t < HW) {
-      const int l = line_of(tid + 1024 * t);
-      atomicAdd(&hist[l], 1u);
-      atomicMin(&lmin[l], obits(kv[t]));
-      atomicMax(&lmax[l], obits(kv[t]));
-    }
-  __syncthreads();
-  // 2) each line cut into ceil(n / 16) segments of its key range (about one 16-pixel group per
-  //    segment); segment bins numbered line by line: bst[line] = the line's first bin
-  for (int i = tid; i < kEpiBuckets; i += 1024) bst[i] = (hist[i] + 15u) / 16u;
-  __syncthreads();
-  const uint32_t nbins = scan8k(bst, nullptr);
-  if (nbins > (uint32_t)kEpiBuckets) {  // (more bins than counters: lines only, as above; uniform)
-    scan8k(hist, nullptr);
-#pragma unroll
-    for (int t = 0; t < PER; ++t)
-      if (tid + 1024 * t < HW) out[atomicAdd(&hist[line_of(tid + 1024 * t)], 1u)] = tid + 1024 * t;
-    return;
-  }
-  int bin[PER];
-#pragma unroll
-  for (int t = 0; t < PER; ++t) {
-    bin[t] = 0;
-    if (tid + 1024 * t < HW) {
-      const int l = line_of(tid + 1024 * t);
-      const uint32_t nseg = (hist[l] + 15u) / 16u;
-      const float lo = ofloat(lmin[l]), hi = ofloat(lmax[l]);
-      const float f = hi > lo ? (kv[t] - lo) / (hi - lo) : 0.f;
-      bin[t] = (int)bst[l] + min((int)nseg - 1, max(0, (int)(f * (float)nseg)));
-    }
-  }
-  __syncthreads();  // hist / bst reads above before they are reused
-  // 3) counting sort by bin (pixel and bin packed into one word: bin << 15 | p)
-  for (int i = tid; i < kEpiBuckets; i += 1024) hist[i] = 0u;
-  __syncthreads();
-#pragma unroll
-  for (int t = 0; t < PER; ++t)
-    if (tid + 1024 * t < HW) atomicAdd(&hist[bin[t]], 1u);
-  __syncthreads();
-  scan8k(hist, lmin);  // lmin: the bins' starts (hist: their ends after the scatter)
-#pragma unroll
-  for (int t = 0; t < PER; ++t)
-    if (tid + 1024 * t < HW) pool[atomicAdd(&hist[bin[t]], 1u)] = (bin[t] << 15) | (tid + 1024 * t);
-  __syncthreads();
-  // 4) inside each bin (~16 pixels) the pixels in id order, so the groups never depend on the
-  //    scatter's arrival order (the backward's MFMA blocking, hence its bits, are the same
-  //    every run)
-#pragma unroll 4
-  for (int t = 0; t < PER; ++t) {
-    const int pos = tid + 1024 * t;
-    if (pos < HW) {
-      const int v = (int)pool[pos], bn = v >> 15, pp = v & 0x7FFF;
-      const int st = (int)lmin[bn], en = (int)hist[bn];
-      int r = 0;
-      for (int q = st; q < en; ++q) r += (int)(pool[q] & 0x7FFFu) < pp ? 1 : 0;
-      out[st + r] = pp;
-    }
-  }
+  const EpiRun r = epi_run(bin, valid ? 1u : 0u, 0u, 0u);
+  if (r.tail && valid) atomicAdd(&s.bcount[(size_t)bj * epi_bin_stride(HW) + bin], r.cnt);
+}
+
+// grid B * J, 1024 threads: bin starts (bstart; bcount becomes the scatter's cursor).
+__global__ __launch_bounds__(1024) void k_epi_binscan(int HW, EpiScratch s) {
+  __shared__ uint32_t wsum[16];
+  const int nbs = epi_bin_stride(HW);
+  const size_t o = (size_t)blockIdx.x * nbs;
+  uint32_t* bc = s.bcount + o;
+  epi_block_scan(nbs, [&](int k) { return bc[k]; }, s.bstart + o, bc, wsum);
+}
+
+// grid (ceil(HW / 256), B * J): every pixel into its bin, in arrival order (one returning atomic
+// per wave run of equal bins).
+__global__ __launch_bounds__(256) void k_epi_scatter(int HW, EpiScratch s) {
+  const int bj = blockIdx.y, p = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63;
+  const bool valid = p < HW;
+  const uint32_t bin = valid ? s.pl[(size_t)bj * HW + p] : 0xFFFFFFFFu;
+  const EpiRun r = epi_run(bin, valid ? 1u : 0u, 0u, 0u);
+  uint32_t base = 0;
+  if (r.tail && valid) base = atomicAdd(&s.bcount[(size_t)bj * epi_bin_stride(HW) + bin], r.cnt);
+  // the run's base from its tail lane: lanes of a run are contiguous, the tail is the run's last
+  const int hd = r.head;
+  const uint64_t tails = __ballot(r.tail);
+  const int tl = hd + __builtin_ctzll(tails >> hd);  // first tail at or after the head
+  base = __shfl(base, tl, 64);
+  if (valid) s.stage[(size_t)bj * HW + base + (uint32_t)(lane - hd)] = p;
+}
+
+// grid (ceil(HW / 256), B * J): output position -> the pixel of that rank (by id) in its bin.
+__global__ __launch_bounds__(256) void k_epi_rank(int HW, EpiScratch s, int* __restrict__ groups) {
+  const int bj = blockIdx.y, pos = blockIdx.x * 256 + threadIdx.x;
+  if (pos >= HW) return;
+  const int* st = s.stage + (size_t)bj * HW;
+  const int p = st[pos];
+  const uint32_t bin = s.pl[(size_t)bj * HW + p];
+  const uint32_t* bs = s.bstart + (size_t)bj * epi_bin_stride(HW);
+  const int b0 = (int)bs[bin], b1 = (int)bs[bin + 1];
+  int r = 0;
+  for (int q = b0; q < b1; ++q) r += st[q] < p ? 1 : 0;
+  groups[(size_t)bj * HW + b0 + r] = p;
 }
 
 // Shared set-up of the forward and backward group kernels: the workgroup's (b, group) with
@@ -1106,9 +1201,15 @@ __global__ __launch_bounds__(256) void k_cv_absmax(size_t n1, const float* __res
     out[kCvMaxBlocks + blockIdx.x] = fmaxf(fmaxf(s2[0], s2[1]), fmaxf(s2[2], s2[3]));
   }
 }
-// the dtgt unit 2^(kt - 40) from the per-block maxima (every caller reads the same values; a
-// non-finite maximum gives a unit of 0: the sums stay 0 and the conversion yields NaN below)
-__device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, float scale, int spt) {
+// The dtgt unit from the per-block maxima (every caller reads the same values). One partial is
+// bounded by 2^lgS max|dcost| scale max|ref| (2^lgS = 256 SPT samples of a workgroup's chunk)
+// and an element takes at most 2^lgP partials (one per workgroup and depth chunk of its image:
+// host-computed), so unit = 2^(e1 + e2 + es + lgS + lgP - 62) keeps every sum below 2^62: the
+// finest unit the int64 range allows for this shape (round 5 used 2^(kt - 40) whatever the shape:
+// 12+ bits coarser at config D). The exponents are added as integers, so no intermediate product
+// overflows; a non-finite maximum, or a unit beyond float range (where the float gradients
+// themselves overflow), gives 0: the conversion below then writes NaN.
+__device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, float scale, int lgps) {
   const int lane = threadIdx.x & 63;
   float m1 = 0.f, m2 = 0.f;
 #pragma unroll
@@ -1121,11 +1222,14 @@ __device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, floa
     m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
     m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
   }
-  const float bound = 256.f * (float)spt * m1 * scale * m2;
-  if (!(bound <= 3.0e38f)) return 0.f;
-  int e = 0;
-  frexpf(bound, &e);  // bound < 2^e
-  return ldexpf(1.f, max(e, -80) - 40);
+  if (!(m1 <= 3.4e38f) || !(m2 <= 3.4e38f)) return 0.f;
+  if (m1 == 0.f || m2 == 0.f) return 1.f;  // every partial is 0
+  int e1 = 0, e2 = 0, es = 0;
+  frexpf(m1, &e1);  // m1 < 2^e1
+  frexpf(m2, &e2);
+  frexpf(scale, &es);
+  const int ue = e1 + e2 + es + lgps - 62;
+  return ue > 127 ? 0.f : ldexpf(1.f, max(ue, -126));
 }
 
 // Backward, view j, on groups of 2^PXB reference pixels (round 5): 16 (a group of
@@ -1149,7 +1253,7 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
                                                       const int* __restrict__ groups, const float* __restrict__ geom,
                                                       const float* __restrict__ depth,
                                                       float clampz, float scale, const float* __restrict__ dcost,
-                                                      const float* __restrict__ cvmax,
+                                                      const float* __restrict__ cvmax, int lgps,
                                                       float* __restrict__ dref_hwc, long long* __restrict__ dtgt_fx) {
   constexpr int C = 4 * NK, NCB = (C / 16 + 3) / 4;  // channel blocks per wave (dref)
   constexpr int EGW = 1 << PXB, MB = EGW / 16, DSL = 256 >> PXB;  // pixels, row blocks, depth slots
@@ -1161,12 +1265,29 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
   const EpiLds L = epi_lds_wide<PXB, SPT>(cv_lds, C, epi_words(H, W));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const size_t bj = (size_t)b * J + j;
-  const float unit_t = cv_dtgt_unit(cvmax, scale, SPT);
+  const float unit_t = cv_dtgt_unit(cvmax, scale, lgps);
   const float unit_t_inv = unit_t > 0.f ? 1.f / unit_t : 0.f;  // exact: a power of 2
   __shared__ int s_gid[kEGWMax];
-  __shared__ float s_gmax[4];
-  if (tid < EGW) s_gid[tid] = g * EGW + tid < HW ? groups[bj * HW + g * EGW + tid] : -1;
+  // per pixel of the group: the largest |dcost scale| of its samples in the current chunk (float
+  // bits; LDS atomicMax), whose exponent sets that pixel's fixed-point unit for G (round 6: the
+  // unit was per workgroup, so a pixel next to one with a 1e4x larger gradient kept ~4 bits)
+  __shared__ uint32_t s_pmax[kEGWMax];
+  if (tid < EGW) {
+    s_gid[tid] = g * EGW + tid < HW ? groups[bj * HW + g * EGW + tid] : -1;
+    s_pmax[tid] = 0u;
+  }
   __syncthreads();
+  // unit 2^(E - 149) and its inverse for a pixel whose bound has float exponent field E (every
+  // |G| add then is < 2^23 units, at most DSL SPT <= 128 of them per element: int32 holds the
+  // sum); E = 255 (inf / NaN gradient): unit 0, the pixel adds nothing
+  auto unit_of = [&](int p) -> float {
+    const uint32_t E = s_pmax[p] >> 23;
+    return E == 255u ? 0.f : __uint_as_float((max(E, 23u) - 22u) << 23);
+  };
+  auto uinv_of = [&](int p) -> float {
+    const uint32_t E = s_pmax[p] >> 23;
+    return E == 255u ? 0.f : __uint_as_float((276u - max(E, 23u)) << 23);
+  };
   epi_aref<NK, EGW>(L, HW, b, s_gid, ref_hwc);
   const int i = tid & (EGW - 1), dl = tid >> PXB;
   const int pix = s_gid[i];
@@ -1194,27 +1315,20 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
                                       nw_prev);
     nw_prev = bx.nw;
     const int Wx = bx.wb;
-    // the chunk's fixed-point unit: 2^(kg - 23), |dcost scale| <= 2^kg over its samples; an
-    // element of G takes at most DSL SPT <= 128 adds of <= 2^23 units
+    // the pixel's fixed-point unit for this chunk (unit_of): from its samples' largest |dcost scale|
     float gm = 0.f;
 #pragma unroll
     for (int s = 0; s < SPT; ++s) {
       gs[s] = es[s] >= 0 ? gs[s] * scale : 0.f;
       gm = fmaxf(gm, fabsf(gs[s]));
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) gm = fmaxf(gm, __shfl_xor(gm, off, 64));
-    if (lane == 0) s_gmax[wv] = gm;
+    if (gm != 0.f) atomicMax(&s_pmax[i], __float_as_uint(gm));  // (non-negative: orderable as uint)
     for (int r0 = 0; r0 < U; r0 += kEUMaxB) {
       const int n = min(kEUMaxB, U - r0), np = epi_padded(n);
       for (int k = tid; k < EGW * np; k += 256) gi[(k & (EGW - 1)) * kECorrB + (k >> PXB)] = 0;
       epi_list(L, H, W, bx, r0, n);
       __syncthreads();
-      gm = fmaxf(fmaxf(s_gmax[0], s_gmax[1]), fmaxf(s_gmax[2], s_gmax[3]));
-      int ke = 0;
-      frexpf(gm, &ke);
-      const float unit_g = (gm > 0.f && gm <= 3.0e38f) ? ldexpf(1.f, max(ke, -100) - 23) : 0.f;
-      const float unit_g_inv = unit_g > 0.f ? 1.f / unit_g : 0.f;
+      const float unit_g_inv = uinv_of(i);
       int* grow = gi + i * kECorrB;
 #pragma unroll
       for (int s = 0; s < SPT; ++s) {
@@ -1234,6 +1348,9 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
       __syncthreads();
       // dref[EGW x C] += G[EGW x np] . tgt[np x C]: wave wv owns channel blocks wv, wv + 4, ...
       // for all MB row blocks (one target load feeds MB MFMAs); 32 band positions per batch
+      float urow[MB];  // the units of this lane's A rows (pixel mb 16 + (lane & 15))
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) urow[mb] = unit_of(mb * 16 + (lane & 15));
 #pragma unroll
       for (int q = 0; q < NCB; ++q) {
         const int cbk = wv + 4 * q;
@@ -1248,7 +1365,7 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
             const int u = u0 + 4 * t + (lane >> 4);
 #pragma unroll
             for (int mb = 0; mb < MB; ++mb)
-              dacc[q][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[(mb * 16 + (lane & 15)) * kECorrB + u] * unit_g,
+              dacc[q][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[(mb * 16 + (lane & 15)) * kECorrB + u] * urow[mb],
                                                                  bv[t], dacc[q][mb], 0, 0, 0);
           }
         }
@@ -1261,7 +1378,7 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
 #pragma unroll
         for (int k0 = 0; k0 < EGW; k0 += 4) {
           const int u = ub * 16 + (lane & 15), p = k0 + (lane >> 4);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[p * kECorrB + u] * unit_g,
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[p * kECorrB + u] * unit_of(p),
                                                      L.aref[p * (C + 4) + cbk * 16 + (lane & 15)], acc, 0, 0, 0);
         }
 #pragma unroll
@@ -1277,7 +1394,9 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
       }
       __syncthreads();  // G / list reused by the next pass
     }
-    if (U == 0) __syncthreads();  // s_gmax of this chunk read by every wave before the next writes it
+    // every read of this chunk's units is behind the last barrier above (no pass: none); the next
+    // chunk's atomicMax is behind epi_front's barriers
+    if (tid < EGW) s_pmax[tid] = 0u;
   }
   // the group's reference-gradient rows, channel-last: dacc[q][mb][r] is row
   // 16 mb + 4 (lane >> 4) + r, channel 16 (wv + 4 q) + (lane & 15)
@@ -1300,10 +1419,10 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
 // [n][rows][C] int64 fixed point (the first HW rows) -> [n][C][HW] float, times the unit of
 // k_cost_epi_bwd (cv_dtgt_unit, recomputed from the same maxima)
 __global__ __launch_bounds__(256) void k_fx_to_chw(int C, int HW, int rows, const long long* __restrict__ src,
-                                                   const float* __restrict__ cvmax, float scale, int spt,
+                                                   const float* __restrict__ cvmax, float scale, int lgps,
                                                    float* __restrict__ dst) {
   __shared__ float tile[64][65];
-  const float unit = cv_dtgt_unit(cvmax, scale, spt);
+  const float unit = cv_dtgt_unit(cvmax, scale, lgps);
   const bool ok = unit > 0.f;
   const int bj = blockIdx.z;
   const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
@@ -1315,7 +1434,8 @@ __global__ __launch_bounds__(256) void k_fx_to_chw(int C, int HW, int rows, cons
     const long long q = (p < HW && c < C) ? s[(size_t)p * C + c] : 0ll;
     const int hi = (int)(q >> 32);
     const unsigned lo = (unsigned)(q & 0xffffffffll);
-    tile[r][tx] = ok ? fmaf((float)hi, 4294967296.0f * unit, (float)lo * unit) : __builtin_nanf("");
+    // (hi unit first: 2^32 unit may exceed float range where the value itself does not)
+    tile[r][tx] = ok ? fmaf((float)hi * unit, 4294967296.0f, (float)lo * unit) : __builtin_nanf("");
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
@@ -1663,11 +1783,12 @@ int dcv_warp_bwd(int B, int C, int H, int W, int D, const float* dout, const flo
 }
 
 // forward workspace: tgt_hwc [B][J][HW + 1][C] | ref_hwc [B][HW + 1][C] | groups [B][J][HW] | geom [B][J][12]
+// | the grouping passes' scratch (EpiScratch)
 size_t dcv_cost_volume_workspace_size(int B, int J, int C, int H, int W) {
   if (B <= 0 || J <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
   const size_t rows = (size_t)H * W + 1;
   return ((size_t)B * J * rows * C + (size_t)B * rows * C + (size_t)B * J * 12) * sizeof(float) +
-         (size_t)B * J * H * W * sizeof(int32_t);
+         (size_t)B * J * H * W * sizeof(int32_t) + epi_scratch_words(B * J, H * W) * sizeof(uint32_t);
 }
 // backward workspace: dtgt [B][J][HW + 1][C] (int64 fixed point on the matrix-core path, float
 // on the direct one) | dref_hwc [B][HW][C] float | per-block maxima of |dcost| and |ref|
@@ -1744,8 +1865,22 @@ static int epi_setup(int B, int J, int C, int H, int W, int D, int depth_per_pix
     }
   }
   if (!epi) return 0;
-  k_epi_groups<<<dim3(B, J), 1024, 0, st>>>(J, H, W, D, depth_per_pixel, intr, pose, depth, groups, geom);
-  return dsplat::check_launch("k_epi_groups");
+  const int BJ = B * J, nbs = epi_bin_stride(HW), pg = (HW + 255) / 256;
+  const EpiScratch sc = epi_scratch(geom + (size_t)BJ * 12, BJ, HW);
+  k_epi_init<<<dim3((std::max(kEpiBuckets, nbs) + 255) / 256, BJ), 256, 0, st>>>(J, H, W, intr, pose, geom, sc);
+  if (int e = dsplat::check_launch("k_epi_init")) return e;
+  k_epi_count<<<dim3(pg, BJ), 256, 0, st>>>(H, W, D, depth_per_pixel, depth, geom, J, sc);
+  if (int e = dsplat::check_launch("k_epi_count")) return e;
+  k_epi_segs<<<BJ, 1024, 0, st>>>(sc);
+  if (int e = dsplat::check_launch("k_epi_segs")) return e;
+  k_epi_bin<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc);
+  if (int e = dsplat::check_launch("k_epi_bin")) return e;
+  k_epi_binscan<<<BJ, 1024, 0, st>>>(HW, sc);
+  if (int e = dsplat::check_launch("k_epi_binscan")) return e;
+  k_epi_scatter<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc);
+  if (int e = dsplat::check_launch("k_epi_scatter")) return e;
+  k_epi_rank<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc, groups);
+  return dsplat::check_launch("k_epi_rank");
 }
 
 int dcv_cost_volume_path(int B, int J, int C, int H, int W) {
@@ -1756,6 +1891,16 @@ int dcv_cost_volume_path(int B, int J, int C, int H, int W) {
   }
   if (band_ok(C) && (long)B * H * W <= kBandMaxPixels) return DCV_PATH_BAND;
   return epi_path(C, H, W, false) ? DCV_PATH_EPI : DCV_PATH_DIRECT;
+}
+
+int dcv_cost_volume_bwd_shape(int B, int C, int H, int W, int D, int depth_per_pixel, int* pxb, int* spt) {
+  DSPLAT_REQUIRE(B > 0 && C > 0 && H > 1 && W > 1 && D > 0 && pxb && spt, "dcv_cost_volume_bwd_shape: bad arguments");
+  DSPLAT_REQUIRE(epi_path(C, H, W, true), "dcv_cost_volume_bwd_shape: C=%d H=%d W=%d has no matrix-core backward", C,
+                 H, W);
+  const BwdShape bs = bwd_shape(B, H, W, D, depth_per_pixel);
+  *pxb = bs.pxb;
+  *spt = bs.spt;
+  return 0;
 }
 
 static bool path_ok(int path, int C, int H, int W) {
@@ -1861,6 +2006,13 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
     const size_t lds = epi_lds_bytes_wide(bs.pxb, bs.spt, C, H, W);
     const int ngw = (HW + (1 << bs.pxb) - 1) >> bs.pxb;
     const dim3 grid(8u * (unsigned)((B * ngw + 7) / 8));
+    // dtgt unit (cv_dtgt_unit): 2^lgS bounds a partial over |dcost| scale |ref|, 2^lgP the partials
+    // per element (one per workgroup of the image and depth chunk)
+    const int chunk = (256 >> bs.pxb) * bs.spt;
+    const long long nparts = (long long)ngw * ((D + chunk - 1) / chunk);
+    int lgp = 0;
+    while ((1ll << lgp) < nparts) ++lgp;
+    const int lgps = 8 + (bs.spt == 8 ? 3 : 1) + lgp;
     // one instance per (C, width, samples per thread)
     auto kern = [&](auto nk) -> const void* {
       constexpr int NK = decltype(nk)::value;
@@ -1877,16 +2029,17 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
       int a_j = j, a_acc = j > 0;
       int a_B = B, a_J = J, a_H = H, a_W = W, a_D = D, a_dpp = depth_per_pixel;
       float a_clamp = clamp_min_depth, a_scale = scale;
+      int a_lgps = lgps;
       void* args[] = {&a_B, &a_j, &a_J, &a_H, &a_W, &a_D, &a_dpp, &a_acc, (void*)&ref_hwc, (void*)&tgt_hwc,
                       (void*)&groups, (void*)&geom, (void*)&depth, &a_clamp, &a_scale, (void*)&dcost, (void*)&cvmax,
-                      (void*)&dref_hwc, (void*)&dtgt_fx};
+                      &a_lgps, (void*)&dref_hwc, (void*)&dtgt_fx};
       if (int e = dsplat::check_hip(hipLaunchKernel(f, grid, dim3(256), args, lds, st), "k_cost_epi_bwd")) return e;
     }
     (C % 4 == 0 && HW % 4 == 0 && aligned16(dref) && aligned16(bwd_workspace) ? k_to_chw4 : k_to_chw)<<<
         dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW, dref_hwc, dref);
     if (int e = dsplat::check_launch("k_to_chw(dref)")) return e;
     k_fx_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_fx, cvmax, scale,
-                                                                          bs.spt, dtgt);
+                                                                          lgps, dtgt);
     return dsplat::check_launch("k_fx_to_chw");
   }
   float* dtgt_hwc = reinterpret_cast<float*>(dtgt_fx);

@@ -1341,13 +1341,17 @@ __global__ __launch_bounds__(NT) void k_project_survivors(int G, int V, int H, i
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x138, 0xf, 0xf, false);  // wave_shr:1
 }
+// Lanes outside the exec mask (a divergent caller) neither extend nor end a run:
+// the lane after an inactive lane is a run head, the lane before it a run end.
 __device__ __forceinline__ void lds_add_runs(uint32_t* lds, uint32_t addr, uint32_t val, bool act, int lane) {
-  const uint32_t a = act ? addr : 0xFFFFFFFFu - (uint32_t)lane;  // inactive lanes start runs of their own
+  const uint32_t a = act ? addr : 0xFFFFFFFFu - (uint32_t)lane;  // !act lanes start runs of their own
   const uint32_t v = act ? val : 0u;
   const uint32_t pa = wave_shr1(a), pv = wave_shr1(v);
-  const bool head = lane == 0 || a != pa || v != pv;
+  const uint64_t on = __ballot(true);  // the exec mask
+  const bool prev_on = lane > 0 && ((on >> (lane - 1)) & 1ull);
+  const bool head = !prev_on || a != pa || v != pv;
   const uint64_t hm = __ballot(head);
-  const bool last = lane == 63 || ((hm >> (lane + 1)) & 1ull);
+  const bool last = lane == 63 || !((on >> (lane + 1)) & 1ull) || ((hm >> (lane + 1)) & 1ull);
   if (act && last) {
     const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
     const int start = 63 - __clzll(hm & upto);
