@@ -16,6 +16,7 @@
 // All floating-point expressions feeding the bit-exact outputs (depth, radius, xy, tile
 // rect, sort keys) keep the evaluation order of oracle/dsr_oracle.cpp (-ffp-contract=off).
 
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -4301,7 +4302,22 @@ int dsr_sort_render(int G, int V, int H, int W, const dsr_camera* cams, const fl
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
   const int T = gx * gy;
-  const size_t lds = cls[ci].lds;
+  size_t lds = cls[ci].lds;
+  // A/B timing knob (DSPLAT_SR_LDS: dynamic LDS bytes of the launch, at least the class's): a
+  // larger request caps the resident sort workgroups per CU and leaves room for another
+  // kernel's workgroups (round-6 overlap experiment)
+  static const size_t lds_req = [] {
+    const char* e = getenv("DSPLAT_SR_LDS");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
+  }();
+  if (lds_req > lds && lds_req <= 64 * 1024) {
+    lds = lds_req;
+    for (const Cls& c : cls)
+      for (const void* f : c.k)
+        if (int e = dsplat::ensure_dyn_lds(f, lds, "hipFuncSetAttribute(k_sort_render)")) return e;
+    for (const void* f : k8w5)
+      if (int e = dsplat::ensure_dyn_lds(f, lds, "hipFuncSetAttribute(k_sort_render)")) return e;
+  }
   hipStream_t st = (hipStream_t)stream;
 #define DSR_SR_LAUNCH(K, L, NB, WP)                                                                          \
   k_sort_render<K, L, NB, WP><<<grid, NT, lds, st>>>(G, H, W, gx, T, cams, geom, seg_start, seg_count, seg_stride, \
