@@ -910,6 +910,12 @@ def _costvol_case(tag, dev, rank):
             depth = (1.0 / torch.linspace(1 / 0.5, 1 / 100.0, D, device=dev)).expand(BV, D)
         depth = depth.contiguous()
     ref = torch.randn(BV, C, Hc, Wc, generator=g, device=dev)
+    if tag.startswith("config_d"):
+        # config D: the features of every view once + each view's neighbour indices (the
+        # reference's nn_matrix, flattened over the batch); tgt = ref[nn] is what the reference's
+        # batch_features_camera_parameters stacks
+        nn_g = (torch.arange(B, device=dev)[:, None, None] * V + nn[None]).reshape(BV, J)
+        return ref, nn_g, K.contiguous(), pose, depth, (BV, J, C, Hc, Wc, D)
     tgt = torch.randn(BV, J, C, Hc, Wc, generator=g, device=dev)
     return ref, tgt, K.contiguous(), pose, depth, (BV, J, C, Hc, Wc, D)
 
@@ -926,15 +932,22 @@ def costvol_leg(args, dev, rank, world, max_over_ranks):
     backward computes both feature gradients: 2x that)."""
     import torch
 
-    from my_depthsplat_amd.matching import plane_sweep_cost_volume
+    from my_depthsplat_amd.matching import plane_sweep_cost_volume, plane_sweep_cost_volume_views
 
     res = {}
     for tag in ("config_a_32x32", "config_b_scale0_64x64", "config_d_scale0_56x96", "config_d_scale1_112x192",
                 "config_d_scale1_112x192_rand"):
         ref, tgt, K, pose, depth, (BV, J, C, Hc, Wc, D) = _costvol_case(tag, dev, rank)
+        views = tag.startswith("config_d")  # tgt is the neighbour index [BV, J] there
+        fanin = J  # the rig: each view is the neighbour of exactly J views
+
+        def op(r, t):
+            if views:
+                return plane_sweep_cost_volume_views(r, t, K, pose, depth, max_fanin=fanin)
+            return plane_sweep_cost_volume(r, t, K, pose, depth)
 
         def call():
-            return plane_sweep_cost_volume(ref, tgt, K, pose, depth)
+            return op(ref, tgt)
 
         def timed_ms(fn, n):
             for _ in range(3):
@@ -949,16 +962,33 @@ def costvol_leg(args, dev, rank, world, max_over_ranks):
             return e0.elapsed_time(e1) / n
 
         (ms,) = max_over_ranks(timed_ms(call, 50))
-        rg, tg_ = ref.clone().requires_grad_(True), tgt.clone().requires_grad_(True)
+        rg = ref.clone().requires_grad_(True)
+        tg_ = tgt if views else tgt.clone().requires_grad_(True)
         dcost = torch.randn(BV, D, Hc, Wc, generator=torch.Generator(device=dev).manual_seed(9), device=dev)
 
         def fwd_bwd():
-            rg.grad = tg_.grad = None
-            (plane_sweep_cost_volume(rg, tg_, K, pose, depth) * dcost).sum().backward()
+            rg.grad = None
+            if not views:
+                tg_.grad = None
+            (op(rg, tg_) * dcost).sum().backward()
 
         (ms_fb,) = max_over_ranks(timed_ms(fwd_bwd, 20))
+        stacked = None
+        if views:  # the same shape through the stacked API (tgt = features[nn] materialised)
+            tst = ref[tgt.long()].contiguous()
+            rs, ts = ref.clone().requires_grad_(True), tst.clone().requires_grad_(True)
+
+            def st_fb():
+                rs.grad = ts.grad = None
+                (plane_sweep_cost_volume(rs, ts, K, pose, depth) * dcost).sum().backward()
+
+            (st_f,) = max_over_ranks(timed_ms(lambda: plane_sweep_cost_volume(ref, tst, K, pose, depth), 50))
+            (st_fb_ms,) = max_over_ranks(timed_ms(st_fb, 20))
+            stacked = {"ms_per_call": round(st_f, 5), "ms_fwd_bwd": round(st_fb_ms, 5),
+                       "note": "plane_sweep_cost_volume(features, features[nn]): the stacked tgt input"}
+            del tst, rs, ts
         flops = 2.0 * BV * J * C * D * Hc * Wc
-        nbytes = 4.0 * (BV * C * Hc * Wc * (1 + J) + BV * D * Hc * Wc * (2 if depth.dim() == 4 else 1))
+        nbytes = 4.0 * (BV * C * Hc * Wc * (1 if views else 1 + J) + BV * D * Hc * Wc * (2 if depth.dim() == 4 else 1))
         tf = flops / (ms * 1e-3) / 1e12
         tf_fb = 3 * flops / (ms_fb * 1e-3) / 1e12
         ent = {"shape": {"BV": BV, "J": J, "C": C, "H": Hc, "W": Wc, "D": D,
@@ -967,7 +997,9 @@ def costvol_leg(args, dev, rank, world, max_over_ranks):
                "frac": round(tf / FP32_MATRIX_PEAK_TFLOPS, 4), "gbps": round(nbytes / (ms * 1e-3) / 1e9, 1),
                "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                "ms_fwd_bwd": round(ms_fb, 5), "tflops_fwd_bwd": round(tf_fb, 3),
-               "frac_fwd_bwd": round(tf_fb / FP32_MATRIX_PEAK_TFLOPS, 4), "mfma_busy": pmc_mfma(tag)}
+               "frac_fwd_bwd": round(tf_fb / FP32_MATRIX_PEAK_TFLOPS, 4), "mfma_busy": pmc_mfma(tag),
+               "api": "plane_sweep_cost_volume_views (features once + nn)" if views else "plane_sweep_cost_volume",
+               "stacked": stacked}
         if rank == 0 and not args.no_cpu_baseline and tag.startswith(("config_a", "config_b")):
             ent["cpu"] = costvol_cpu(ref, tgt, K, pose, depth)
         res[tag] = ent

@@ -430,6 +430,28 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
                         const float* dcost, float* dref, float* dtgt, void* bwd_workspace,
                         void* stream);
 
+/* Views mode: the same cost volume from per-view features and a neighbour index instead of
+ * the stacked tgt the reference builds with batch_features_camera_parameters
+ * (mv_transformer.py:653-747, a gather copying every feature map J more times):
+ *   features [BV,C,H,W]; nn [BV,J] int32 view indices in [0, BV) (tgt[b, j] = features[nn[b J
+ *   + j]]; out-of-range indices are clamped); intr / pose / depth as dcv_cost_volume_fwd.
+ * ONE channel-last copy of the features serves every role. Matrix-core shapes only (C a
+ * multiple of 16, dcv_cost_volume_path(...) == DCV_PATH_EPI sizes); else status 1.
+ * The backward writes dfeatures [BV,C,H,W] = the gradient through both roles (reference and
+ * target), bit-identical run to run; max_fanin: an upper bound on how many (b, j) pairs name one
+ * view (<= 0: BV J), which sets the int64 fixed-point unit of the target sums. */
+size_t dcv_cost_volume_views_workspace_size(int BV, int J, int C, int H, int W);
+size_t dcv_cost_volume_views_bwd_workspace_size(int BV, int J, int C, int H, int W);
+int dcv_cost_volume_views_fwd(int BV, int J, int C, int H, int W, int D, int depth_per_pixel,
+                              const float* features, const int32_t* nn, const float* intr,
+                              const float* pose, const float* depth, float clamp_min_depth,
+                              void* workspace, float* cost, void* stream);
+int dcv_cost_volume_views_bwd(int BV, int J, int C, int H, int W, int D, int depth_per_pixel,
+                              int max_fanin, const float* features, const int32_t* nn,
+                              void* workspace, const float* intr, const float* pose,
+                              const float* depth, float clamp_min_depth, const float* dcost,
+                              float* dfeatures, void* bwd_workspace, void* stream);
+
 /* Materialising warp with the exact matching.py:24-90 signature semantics:
  * feature [B,C,H,W], intr [B,3,3], pose [B,4,4], depth [B,D,H,W] -> out [B,C,D,H,W]. */
 int dcv_warp_fwd(int B, int C, int H, int W, int D, const float* feature, const float* intr,

@@ -55,6 +55,11 @@ SIGNATURES: dict[str, tuple] = {
     "dcv_cost_volume_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P, _P]),
     "dcv_cost_volume_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, c_float, _P, _P,
                                  _P, _P, _P]),
+    "dcv_cost_volume_views_workspace_size": (ctypes.c_size_t, [_I, _I, _I, _I, _I]),
+    "dcv_cost_volume_views_bwd_workspace_size": (ctypes.c_size_t, [_I, _I, _I, _I, _I]),
+    "dcv_cost_volume_views_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, c_float, _P, _P, _P]),
+    "dcv_cost_volume_views_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, c_float, _P, _P, _P,
+                                       _P]),
     "dcv_warp_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, _P, _P]),
     "dcv_warp_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, _P, _P]),
     "dga_adapter_cameras": (_I, [_I, _P, _P, _I, _P, _P, _P]),

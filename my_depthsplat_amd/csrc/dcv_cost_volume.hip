@@ -688,6 +688,12 @@ __global__ __launch_bounds__(256) void k_epi_rank(int HW, EpiScratch s, int* __r
   groups[(size_t)bj * HW + b0 + r] = p;
 }
 
+// The target image of (b, j): its own copy, or view tmap[bj] of the per-view copy (views mode;
+// the index is clamped to the B views: a bad caller index must not reach past the buffer).
+__device__ __forceinline__ size_t cv_target(const int* __restrict__ tmap, size_t bj, int B) {
+  return tmap ? (size_t)min(max(tmap[bj], 0), B - 1) : bj;
+}
+
 // Shared set-up of the forward and backward group kernels: the workgroup's (b, group) with
 // a given view's groups on a contiguous range of one XCD (their target bands overlap: L2).
 __device__ __forceinline__ bool epi_item(int B, int ngroups, int& b, int& g) {
@@ -1015,12 +1021,14 @@ size_t epi_lds_bytes_wide(int pxb, int spt, int C, int H, int W) {
 // depths d0 + (t >> PXB) + (256 >> PXB) s. Writes (accumulate = 0) or adds (accumulate = 1:
 // views after the first, launched in view order, so the sum over views is deterministic)
 // scale * sum_taps w * corr. ref_hwc [B][HW + 1][C], tgt_hwc [B][J][HW + 1][C]: channel-last
-// copies, row HW zero.
+// copies, row HW zero. tmap (views mode, round 6): tgt_hwc is the per-view copy [BV][HW + 1][C]
+// (the same buffer as ref_hwc) and (b, j)'s target image is view tmap[b J + j].
 template <int NK, int SPT, int PXB>
 __global__ __launch_bounds__(256, PXB == 4 ? 4 : 2) void k_cost_epi(int B, int j, int J, int H, int W, int D,
                                                                   int depth_per_pixel, int accumulate,
                                                                   const float* __restrict__ ref_hwc,
                                                                   const float* __restrict__ tgt_hwc,
+                                                                  const int* __restrict__ tmap,
                                                                   const int* __restrict__ groups,
                                                                   const float* __restrict__ geom,
                                                                   const float* __restrict__ depth, float clampz,
@@ -1066,7 +1074,7 @@ __global__ __launch_bounds__(256, PXB == 4 ? 4 : 2) void k_cost_epi(int B, int j
 #pragma unroll
     for (int s = 0; s < SPT; ++s) prev[s] = cb[(uint32_t)(min(d0 + dl + DSL * s, D - 1) * HW + pc)];
   };
-  const float* tg = tgt_hwc + bj * (size_t)(HW + 1) * C;
+  const float* tg = tgt_hwc + cv_target(tmap, bj, B) * (size_t)(HW + 1) * C;
   for (int r0 = 0; r0 < U; r0 += kEU) {
     const int n = min(kEU, U - r0);
     epi_list(L, H, W, bx, r0, n);
@@ -1249,7 +1257,7 @@ __device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, floa
 template <int NK, int PXB, int SPT>
 __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
                                                       int accumulate, const float* __restrict__ ref_hwc,
-                                                      const float* __restrict__ tgt_hwc,
+                                                      const float* __restrict__ tgt_hwc, const int* __restrict__ tmap,
                                                       const int* __restrict__ groups, const float* __restrict__ geom,
                                                       const float* __restrict__ depth,
                                                       float clampz, float scale, const float* __restrict__ dcost,
@@ -1292,8 +1300,11 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
   const int i = tid & (EGW - 1), dl = tid >> PXB;
   const int pix = s_gid[i];
   const EpiRay ry = epi_ray(geom + bj * 12, pix >= 0 ? (float)(pix % W) : 0.f, pix >= 0 ? (float)(pix / W) : 0.f);
-  const float* tg = tgt_hwc + bj * (size_t)(HW + 1) * C;
-  long long* dtg = dtgt_fx + bj * (size_t)(HW + 1) * C;
+  // views mode: (b, j)'s target view; its gradient accumulates in that view's rows (int64 sums:
+  // the order of the (b, j) pairs sharing a view does not matter)
+  const size_t tb = cv_target(tmap, bj, B);
+  const float* tg = tgt_hwc + tb * (size_t)(HW + 1) * C;
+  long long* dtg = dtgt_fx + tb * (size_t)(HW + 1) * C;
   int* gi = reinterpret_cast<int*>(L.corr);  // G in fixed point, [EGW][kECorrB]
   f32x4 dacc[NCB][MB];
 #pragma unroll
@@ -1417,10 +1428,11 @@ __global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, i
 }
 
 // [n][rows][C] int64 fixed point (the first HW rows) -> [n][C][HW] float, times the unit of
-// k_cost_epi_bwd (cv_dtgt_unit, recomputed from the same maxima)
+// k_cost_epi_bwd (cv_dtgt_unit, recomputed from the same maxima); add (views mode: the reference
+// gradient [n][HW][C], float) is added to each element (one fixed-order add: deterministic)
 __global__ __launch_bounds__(256) void k_fx_to_chw(int C, int HW, int rows, const long long* __restrict__ src,
                                                    const float* __restrict__ cvmax, float scale, int lgps,
-                                                   float* __restrict__ dst) {
+                                                   const float* __restrict__ add, float* __restrict__ dst) {
   __shared__ float tile[64][65];
   const float unit = cv_dtgt_unit(cvmax, scale, lgps);
   const bool ok = unit > 0.f;
@@ -1435,7 +1447,9 @@ __global__ __launch_bounds__(256) void k_fx_to_chw(int C, int HW, int rows, cons
     const int hi = (int)(q >> 32);
     const unsigned lo = (unsigned)(q & 0xffffffffll);
     // (hi unit first: 2^32 unit may exceed float range where the value itself does not)
-    tile[r][tx] = ok ? fmaf((float)hi * unit, 4294967296.0f, (float)lo * unit) : __builtin_nanf("");
+    float v = ok ? fmaf((float)hi * unit, 4294967296.0f, (float)lo * unit) : __builtin_nanf("");
+    if (add && p < HW && c < C) v += add[((size_t)bj * HW + p) * C + c];
+    tile[r][tx] = v;
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
@@ -1838,6 +1852,28 @@ static bool band_ok(int C) { return C == 16 || C == 32 || C == 64 || C == 128; }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// The epipolar grouping passes (k_epi_init .. k_epi_rank) of B x J (reference, source view)
+// pairs into groups [B J][HW] and geom [B J][12], scratch after geom.
+static int epi_group(int B, int J, int H, int W, int D, int depth_per_pixel, const float* intr, const float* pose,
+                     const float* depth, int* groups, float* geom, hipStream_t st) {
+  const int HW = H * W, BJ = B * J, nbs = epi_bin_stride(HW), pg = (HW + 255) / 256;
+  const EpiScratch sc = epi_scratch(geom + (size_t)BJ * 12, BJ, HW);
+  k_epi_init<<<dim3((std::max(kEpiBuckets, nbs) + 255) / 256, BJ), 256, 0, st>>>(J, H, W, intr, pose, geom, sc);
+  if (int e = dsplat::check_launch("k_epi_init")) return e;
+  k_epi_count<<<dim3(pg, BJ), 256, 0, st>>>(H, W, D, depth_per_pixel, depth, geom, J, sc);
+  if (int e = dsplat::check_launch("k_epi_count")) return e;
+  k_epi_segs<<<BJ, 1024, 0, st>>>(sc);
+  if (int e = dsplat::check_launch("k_epi_segs")) return e;
+  k_epi_bin<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc);
+  if (int e = dsplat::check_launch("k_epi_bin")) return e;
+  k_epi_binscan<<<BJ, 1024, 0, st>>>(HW, sc);
+  if (int e = dsplat::check_launch("k_epi_binscan")) return e;
+  k_epi_scatter<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc);
+  if (int e = dsplat::check_launch("k_epi_scatter")) return e;
+  k_epi_rank<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc, groups);
+  return dsplat::check_launch("k_epi_rank");
+}
+
 // Channel-last copies (+ the epipolar groups when the epipolar kernels run): the forward's
 // set-up on the epipolar / generic paths, and the backward's when the forward took the band
 // kernel (which needs none of it).
@@ -1865,22 +1901,86 @@ static int epi_setup(int B, int J, int C, int H, int W, int D, int depth_per_pix
     }
   }
   if (!epi) return 0;
-  const int BJ = B * J, nbs = epi_bin_stride(HW), pg = (HW + 255) / 256;
-  const EpiScratch sc = epi_scratch(geom + (size_t)BJ * 12, BJ, HW);
-  k_epi_init<<<dim3((std::max(kEpiBuckets, nbs) + 255) / 256, BJ), 256, 0, st>>>(J, H, W, intr, pose, geom, sc);
-  if (int e = dsplat::check_launch("k_epi_init")) return e;
-  k_epi_count<<<dim3(pg, BJ), 256, 0, st>>>(H, W, D, depth_per_pixel, depth, geom, J, sc);
-  if (int e = dsplat::check_launch("k_epi_count")) return e;
-  k_epi_segs<<<BJ, 1024, 0, st>>>(sc);
-  if (int e = dsplat::check_launch("k_epi_segs")) return e;
-  k_epi_bin<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc);
-  if (int e = dsplat::check_launch("k_epi_bin")) return e;
-  k_epi_binscan<<<BJ, 1024, 0, st>>>(HW, sc);
-  if (int e = dsplat::check_launch("k_epi_binscan")) return e;
-  k_epi_scatter<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc);
-  if (int e = dsplat::check_launch("k_epi_scatter")) return e;
-  k_epi_rank<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc, groups);
-  return dsplat::check_launch("k_epi_rank");
+  return epi_group(B, J, H, W, D, depth_per_pixel, intr, pose, depth, groups, geom, st);
+}
+
+// The epipolar forward launches (one per source view, in view order). tmap: views mode.
+static int epi_fwd_launch(int B, int J, int C, int H, int W, int D, int depth_per_pixel, const float* ref_hwc,
+                          const float* tgt_hwc, const int* tmap, const int* groups, const float* geom,
+                          const float* depth, float clamp_min_depth, float* cost, hipStream_t st) {
+  const int HW = H * W;
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  const BwdShape fs = fwd_shape(D);
+  const size_t lds = epi_lds_bytes_wide(fs.pxb, fs.spt, C, H, W);
+  const int ngw = (HW + (1 << fs.pxb) - 1) >> fs.pxb, chunk = (256 >> fs.pxb) * fs.spt;
+  const dim3 grid(8u * (unsigned)((B * ngw + 7) / 8), (unsigned)((D + chunk - 1) / chunk));
+  // one instance per (C, samples per thread)
+  auto kern = [&](auto nk) -> const void* {
+    constexpr int NK = decltype(nk)::value;
+    return fs.spt == 2 ? (const void*)k_cost_epi<NK, 2, 4> : (const void*)k_cost_epi<NK, 8, 4>;
+  };
+  const void* f = C == 16 ? kern(std::integral_constant<int, 4>{})
+                : C == 32 ? kern(std::integral_constant<int, 8>{})
+                : C == 64 ? kern(std::integral_constant<int, 16>{})
+                          : kern(std::integral_constant<int, 32>{});
+  if (int e = dsplat::ensure_dyn_lds(f, lds, "hipFuncSetAttribute(k_cost_epi)")) return e;
+  for (int j = 0; j < J; ++j) {  // views in order: the sum over views is deterministic
+    int a_B = B, a_j = j, a_J = J, a_H = H, a_W = W, a_D = D, a_dpp = depth_per_pixel, a_acc = j > 0;
+    float a_clamp = clamp_min_depth, a_scale = scale;
+    void* args[] = {&a_B, &a_j, &a_J, &a_H, &a_W, &a_D, &a_dpp, &a_acc, (void*)&ref_hwc, (void*)&tgt_hwc,
+                    (void*)&tmap, (void*)&groups, (void*)&geom, (void*)&depth, &a_clamp, &a_scale, (void*)&cost};
+    if (int e = dsplat::check_hip(hipLaunchKernel(f, grid, dim3(256), args, lds, st), "k_cost_epi")) return e;
+  }
+  return 0;
+}
+
+// The epipolar backward launches: |dcost|, |ref| maxima, then one launch per source view.
+// fanin: an upper bound on the (b, j) pairs whose gradient lands on one target image (1: own
+// copies; views mode: how often a view is a neighbour). Returns the dtgt unit's lgps via *lgps.
+static int epi_bwd_launch(int B, int J, int C, int H, int W, int D, int depth_per_pixel, int fanin,
+                          const float* ref_for_max, const float* ref_hwc, const float* tgt_hwc, const int* tmap,
+                          const int* groups, const float* geom, const float* depth, float clamp_min_depth,
+                          const float* dcost, float* cvmax, float* dref_hwc, long long* dtgt_fx, int* lgps_out,
+                          hipStream_t st) {
+  const int HW = H * W;
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  k_cv_absmax<<<kCvMaxBlocks, 256, 0, st>>>((size_t)B * D * HW, dcost, (size_t)B * C * HW, ref_for_max, cvmax);
+  if (int e = dsplat::check_launch("k_cv_absmax")) return e;
+  const BwdShape bs = bwd_shape(B, H, W, D, depth_per_pixel);
+  const size_t lds = epi_lds_bytes_wide(bs.pxb, bs.spt, C, H, W);
+  const int ngw = (HW + (1 << bs.pxb) - 1) >> bs.pxb;
+  const dim3 grid(8u * (unsigned)((B * ngw + 7) / 8));
+  // dtgt unit (cv_dtgt_unit): 2^lgS bounds a partial over |dcost| scale |ref|, 2^lgP the partials
+  // per element (one per workgroup of the image and depth chunk, times the fan-in)
+  const int chunk = (256 >> bs.pxb) * bs.spt;
+  const long long nparts = (long long)ngw * ((D + chunk - 1) / chunk) * std::max(fanin, 1);
+  int lgp = 0;
+  while ((1ll << lgp) < nparts) ++lgp;
+  const int lgps = 8 + (bs.spt == 8 ? 3 : 1) + lgp;
+  *lgps_out = lgps;
+  // one instance per (C, width, samples per thread)
+  auto kern = [&](auto nk) -> const void* {
+    constexpr int NK = decltype(nk)::value;
+    if (bs.pxb == 6) return (const void*)k_cost_epi_bwd<NK, 6, 8>;
+    if (bs.pxb == 5) return (const void*)k_cost_epi_bwd<NK, 5, 8>;
+    return bs.spt == 2 ? (const void*)k_cost_epi_bwd<NK, 4, 2> : (const void*)k_cost_epi_bwd<NK, 4, 8>;
+  };
+  const void* f = C == 16 ? kern(std::integral_constant<int, 4>{})
+                : C == 32 ? kern(std::integral_constant<int, 8>{})
+                : C == 64 ? kern(std::integral_constant<int, 16>{})
+                          : kern(std::integral_constant<int, 32>{});
+  if (int e = dsplat::ensure_dyn_lds(f, lds, "hipFuncSetAttribute(k_cost_epi_bwd)")) return e;
+  for (int j = 0; j < J; ++j) {
+    int a_j = j, a_acc = j > 0;
+    int a_B = B, a_J = J, a_H = H, a_W = W, a_D = D, a_dpp = depth_per_pixel;
+    float a_clamp = clamp_min_depth, a_scale = scale;
+    int a_lgps = lgps;
+    void* args[] = {&a_B, &a_j, &a_J, &a_H, &a_W, &a_D, &a_dpp, &a_acc, (void*)&ref_hwc, (void*)&tgt_hwc,
+                    (void*)&tmap, (void*)&groups, (void*)&geom, (void*)&depth, &a_clamp, &a_scale, (void*)&dcost,
+                    (void*)&cvmax, &a_lgps, (void*)&dref_hwc, (void*)&dtgt_fx};
+    if (int e = dsplat::check_hip(hipLaunchKernel(f, grid, dim3(256), args, lds, st), "k_cost_epi_bwd")) return e;
+  }
+  return 0;
 }
 
 int dcv_cost_volume_path(int B, int J, int C, int H, int W) {
@@ -1940,35 +2040,9 @@ int dcv_cost_volume_fwd(int B, int J, int C, int H, int W, int D, int depth_per_
   float* ref_hwc = tgt_hwc + (size_t)B * J * (HW + 1) * C;
   int* groups = reinterpret_cast<int*>(ref_hwc + (size_t)B * (HW + 1) * C);
   float* geom = reinterpret_cast<float*>(groups + (size_t)B * J * HW);
-  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-  if (path == DCV_PATH_EPI) {
-    const BwdShape fs = fwd_shape(D);
-    const size_t lds = epi_lds_bytes_wide(fs.pxb, fs.spt, C, H, W);
-    const int ngw = (HW + (1 << fs.pxb) - 1) >> fs.pxb, chunk = (256 >> fs.pxb) * fs.spt;
-    const dim3 grid(8u * (unsigned)((B * ngw + 7) / 8), (unsigned)((D + chunk - 1) / chunk));
-    // one instance per (C, samples per thread)
-    auto kern = [&](auto nk) -> const void* {
-      constexpr int NK = decltype(nk)::value;
-      return fs.spt == 2 ? (const void*)k_cost_epi<NK, 2, 4> : (const void*)k_cost_epi<NK, 8, 4>;
-    };
-    const void* f = C == 16 ? kern(std::integral_constant<int, 4>{})
-                  : C == 32 ? kern(std::integral_constant<int, 8>{})
-                  : C == 64 ? kern(std::integral_constant<int, 16>{})
-                            : kern(std::integral_constant<int, 32>{});
-    if (int e = dsplat::ensure_dyn_lds(f, lds, "hipFuncSetAttribute(k_cost_epi)")) return e;
-    for (int j = 0; j < J; ++j) {  // views in order: the sum over views is deterministic
-      int a_B = B, a_j = j, a_J = J, a_H = H, a_W = W, a_D = D, a_dpp = depth_per_pixel, a_acc = j > 0;
-      float a_clamp = clamp_min_depth, a_scale = scale;
-      const float* a_ref = ref_hwc;
-      const float* a_tgt = tgt_hwc;
-      const int* a_groups = groups;
-      const float* a_geom = geom;
-      void* args[] = {&a_B, &a_j, &a_J, &a_H, &a_W, &a_D, &a_dpp, &a_acc, (void*)&a_ref, (void*)&a_tgt,
-                      (void*)&a_groups, (void*)&a_geom, (void*)&depth, &a_clamp, &a_scale, (void*)&cost};
-      if (int e = dsplat::check_hip(hipLaunchKernel(f, grid, dim3(256), args, lds, st), "k_cost_epi")) return e;
-    }
-    return 0;
-  }
+  if (path == DCV_PATH_EPI)
+    return epi_fwd_launch(B, J, C, H, W, D, depth_per_pixel, ref_hwc, tgt_hwc, nullptr, groups, geom, depth,
+                          clamp_min_depth, cost, st);
   k_cost_fwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
                                                    depth, clamp_min_depth, cost);
   return dsplat::check_launch("k_cost_fwd");
@@ -1998,48 +2072,17 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
   float* cvmax = dref_hwc + (size_t)B * HW * C;
   const bool epi = epi_path(C, H, W, true) && epi_path(C, H, W, false);
   if (int e = dsplat::zero_async(dtgt_fx, ntg * (epi ? sizeof(long long) : sizeof(float)), st, "zero dtgt")) return e;
-  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
   if (epi) {
-    k_cv_absmax<<<kCvMaxBlocks, 256, 0, st>>>((size_t)B * D * HW, dcost, (size_t)B * C * HW, ref, cvmax);
-    if (int e = dsplat::check_launch("k_cv_absmax")) return e;
-    const BwdShape bs = bwd_shape(B, H, W, D, depth_per_pixel);
-    const size_t lds = epi_lds_bytes_wide(bs.pxb, bs.spt, C, H, W);
-    const int ngw = (HW + (1 << bs.pxb) - 1) >> bs.pxb;
-    const dim3 grid(8u * (unsigned)((B * ngw + 7) / 8));
-    // dtgt unit (cv_dtgt_unit): 2^lgS bounds a partial over |dcost| scale |ref|, 2^lgP the partials
-    // per element (one per workgroup of the image and depth chunk)
-    const int chunk = (256 >> bs.pxb) * bs.spt;
-    const long long nparts = (long long)ngw * ((D + chunk - 1) / chunk);
-    int lgp = 0;
-    while ((1ll << lgp) < nparts) ++lgp;
-    const int lgps = 8 + (bs.spt == 8 ? 3 : 1) + lgp;
-    // one instance per (C, width, samples per thread)
-    auto kern = [&](auto nk) -> const void* {
-      constexpr int NK = decltype(nk)::value;
-      if (bs.pxb == 6) return (const void*)k_cost_epi_bwd<NK, 6, 8>;
-      if (bs.pxb == 5) return (const void*)k_cost_epi_bwd<NK, 5, 8>;
-      return bs.spt == 2 ? (const void*)k_cost_epi_bwd<NK, 4, 2> : (const void*)k_cost_epi_bwd<NK, 4, 8>;
-    };
-    const void* f = C == 16 ? kern(std::integral_constant<int, 4>{})
-                  : C == 32 ? kern(std::integral_constant<int, 8>{})
-                  : C == 64 ? kern(std::integral_constant<int, 16>{})
-                            : kern(std::integral_constant<int, 32>{});
-    if (int e = dsplat::ensure_dyn_lds(f, lds, "hipFuncSetAttribute(k_cost_epi_bwd)")) return e;
-    for (int j = 0; j < J; ++j) {
-      int a_j = j, a_acc = j > 0;
-      int a_B = B, a_J = J, a_H = H, a_W = W, a_D = D, a_dpp = depth_per_pixel;
-      float a_clamp = clamp_min_depth, a_scale = scale;
-      int a_lgps = lgps;
-      void* args[] = {&a_B, &a_j, &a_J, &a_H, &a_W, &a_D, &a_dpp, &a_acc, (void*)&ref_hwc, (void*)&tgt_hwc,
-                      (void*)&groups, (void*)&geom, (void*)&depth, &a_clamp, &a_scale, (void*)&dcost, (void*)&cvmax,
-                      &a_lgps, (void*)&dref_hwc, (void*)&dtgt_fx};
-      if (int e = dsplat::check_hip(hipLaunchKernel(f, grid, dim3(256), args, lds, st), "k_cost_epi_bwd")) return e;
-    }
+    int lgps = 0;
+    if (int e = epi_bwd_launch(B, J, C, H, W, D, depth_per_pixel, 1, ref, ref_hwc, tgt_hwc, nullptr, groups, geom,
+                               depth, clamp_min_depth, dcost, cvmax, dref_hwc, dtgt_fx, &lgps, st))
+      return e;
     (C % 4 == 0 && HW % 4 == 0 && aligned16(dref) && aligned16(bwd_workspace) ? k_to_chw4 : k_to_chw)<<<
         dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW, dref_hwc, dref);
     if (int e = dsplat::check_launch("k_to_chw(dref)")) return e;
+    const float scale = 1.0f / (sqrtf((float)C) * (float)J);
     k_fx_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_fx, cvmax, scale,
-                                                                          lgps, dtgt);
+                                                                          lgps, nullptr, dtgt);
     return dsplat::check_launch("k_fx_to_chw");
   }
   float* dtgt_hwc = reinterpret_cast<float*>(dtgt_fx);
@@ -2049,6 +2092,83 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
   (C % 4 == 0 && HW % 4 == 0 && aligned16(dtgt) && aligned16(bwd_workspace) ? k_to_chw4 : k_to_chw)<<<
       dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_hwc, dtgt);
   return dsplat::check_launch("k_to_chw");
+}
+
+// ---- views mode (round 6) -----------------------------------------------------------------
+// The reference stacks each view's neighbours' features into tgt [BV, J, C, H, W]
+// (batch_features_camera_parameters, mv_transformer.py:653-747: a gather that copies every
+// feature map J more times) and differentiates back through that gather. Here the features are
+// read once: ONE channel-last copy [BV][HW + 1][C] serves as the reference tile of view b and as
+// the target band rows of every (b, j) whose neighbour it is (nn[b J + j]); in the backward the
+// target gradients accumulate straight into the neighbour view's int64 rows (order-independent)
+// and one conversion adds the reference gradient: dfeatures in one pass.
+// workspace: fhwc [BV][HW + 1][C] | groups [BV][J][HW] | geom [BV][J][12] | grouping scratch
+size_t dcv_cost_volume_views_workspace_size(int BV, int J, int C, int H, int W) {
+  if (BV <= 0 || J <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  const size_t rows = (size_t)H * W + 1;
+  return ((size_t)BV * rows * C + (size_t)BV * J * 12) * sizeof(float) + (size_t)BV * J * H * W * sizeof(int32_t) +
+         epi_scratch_words(BV * J, H * W) * sizeof(uint32_t);
+}
+// backward workspace: dfeat_fx [BV][HW + 1][C] int64 | dref_hwc [BV][HW][C] | maxima
+size_t dcv_cost_volume_views_bwd_workspace_size(int BV, int J, int C, int H, int W) {
+  if (BV <= 0 || J <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  return (size_t)BV * ((size_t)H * W + 1) * C * sizeof(long long) + (size_t)BV * H * W * C * sizeof(float) +
+         2 * kCvMaxBlocks * sizeof(float);
+}
+
+int dcv_cost_volume_views_fwd(int BV, int J, int C, int H, int W, int D, int depth_per_pixel, const float* features,
+                              const int32_t* nn, const float* intr, const float* pose, const float* depth,
+                              float clamp_min_depth, void* workspace, float* cost, void* stream) {
+  DSPLAT_REQUIRE(BV > 0 && J > 0 && C > 0 && H > 1 && W > 1 && D > 0,
+                 "dcv_cost_volume_views_fwd: bad sizes BV=%d J=%d C=%d H=%d W=%d D=%d", BV, J, C, H, W, D);
+  DSPLAT_REQUIRE(features && nn && intr && pose && depth && workspace && cost, "dcv_cost_volume_views_fwd: null pointer");
+  DSPLAT_REQUIRE(epi_path(C, H, W, false), "dcv_cost_volume_views_fwd: C=%d H=%d W=%d needs the matrix-core path", C, H,
+                 W);
+  hipStream_t st = (hipStream_t)stream;
+  const int HW = H * W;
+  float* fhwc = static_cast<float*>(workspace);
+  int* groups = reinterpret_cast<int*>(fhwc + (size_t)BV * (HW + 1) * C);
+  float* geom = reinterpret_cast<float*>(groups + (size_t)BV * J * HW);
+  if (C % 4 == 0 && HW % 4 == 0 && aligned16(features) && aligned16(workspace))
+    k_to_hwc4<<<dim3((HW + 63) / 64, (C + 63) / 64, BV), 256, 0, st>>>(C, HW, HW + 1, features, fhwc, BV, nullptr,
+                                                                      nullptr);
+  else
+    k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, BV), 256, 0, st>>>(C, HW, HW + 1, features, fhwc);
+  if (int e = dsplat::check_launch("k_to_hwc(features)")) return e;
+  if (int e = epi_group(BV, J, H, W, D, depth_per_pixel, intr, pose, depth, groups, geom, st)) return e;
+  return epi_fwd_launch(BV, J, C, H, W, D, depth_per_pixel, fhwc, fhwc, nn, groups, geom, depth, clamp_min_depth, cost,
+                        st);
+}
+
+int dcv_cost_volume_views_bwd(int BV, int J, int C, int H, int W, int D, int depth_per_pixel, int max_fanin,
+                              const float* features, const int32_t* nn, void* workspace, const float* intr,
+                              const float* pose, const float* depth, float clamp_min_depth, const float* dcost,
+                              float* dfeatures, void* bwd_workspace, void* stream) {
+  DSPLAT_REQUIRE(BV > 0 && J > 0 && C > 0 && H > 1 && W > 1 && D > 0, "dcv_cost_volume_views_bwd: bad sizes");
+  DSPLAT_REQUIRE(features && nn && workspace && intr && pose && depth && dcost && dfeatures && bwd_workspace,
+                 "dcv_cost_volume_views_bwd: null pointer");
+  DSPLAT_REQUIRE(epi_path(C, H, W, true), "dcv_cost_volume_views_bwd: C=%d H=%d W=%d needs the matrix-core path", C, H,
+                 W);
+  hipStream_t st = (hipStream_t)stream;
+  const int HW = H * W;
+  const float* fhwc = static_cast<const float*>(workspace);
+  const int* groups = reinterpret_cast<const int*>(fhwc + (size_t)BV * (HW + 1) * C);
+  const float* geom = reinterpret_cast<const float*>(groups + (size_t)BV * J * HW);
+  const size_t nfx = (size_t)BV * (HW + 1) * C;
+  long long* dfx = static_cast<long long*>(bwd_workspace);
+  float* dref_hwc = reinterpret_cast<float*>(dfx + nfx);
+  float* cvmax = dref_hwc + (size_t)BV * HW * C;
+  if (int e = dsplat::zero_async(dfx, nfx * sizeof(long long), st, "zero dfeatures")) return e;
+  // a view is the neighbour of at most BV J (b, j) pairs; the caller may know a smaller bound
+  const int fanin = max_fanin > 0 ? std::min(max_fanin, BV * J) : BV * J;
+  int lgps = 0;
+  if (int e = epi_bwd_launch(BV, J, C, H, W, D, depth_per_pixel, fanin, features, fhwc, fhwc, nn, groups, geom, depth,
+                             clamp_min_depth, dcost, cvmax, dref_hwc, dfx, &lgps, st))
+    return e;
+  const float scale = 1.0f / (sqrtf((float)C) * (float)J);
+  k_fx_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, BV), 256, 0, st>>>(C, HW, HW + 1, dfx, cvmax, scale, lgps,
+                                                                      dref_hwc, dfeatures);
+  return dsplat::check_launch("k_fx_to_chw(dfeatures)");
 }
 
 int dcv_warp_fwd(int B, int C, int H, int W, int D, const float* feature, const float* intr, const float* pose,

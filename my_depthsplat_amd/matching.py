@@ -139,6 +139,76 @@ def plane_sweep_cost_volume(ref: torch.Tensor, tgt: torch.Tensor, intrinsics: to
     return _cost_volume_fwd(*args)[0]
 
 
+class _CostVolumeViews(torch.autograd.Function):
+    """dcv_cost_volume_views_fwd / _bwd (include/dsplat_hip.h): features read once."""
+
+    @staticmethod
+    def forward(ctx, features, nn, intrinsics, pose, depth, per_pixel, clamp, fanin):
+        lib = _lib.load()
+        BV, C, H, W = features.shape
+        J, D = nn.shape[1], depth.shape[1]
+        dev = features.device
+        ws = torch.empty(lib.dcv_cost_volume_views_workspace_size(BV, J, C, H, W), dtype=torch.uint8, device=dev)
+        cost = torch.empty((BV, D, H, W), dtype=torch.float32, device=dev)
+        _lib.check(lib.dcv_cost_volume_views_fwd(BV, J, C, H, W, D, int(per_pixel), features.data_ptr(), nn.data_ptr(),
+                                                 intrinsics.data_ptr(), pose.data_ptr(), depth.data_ptr(), clamp,
+                                                 ws.data_ptr(), cost.data_ptr(), _lib.stream_of(dev)),
+                   "dcv_cost_volume_views_fwd")
+        ctx.save_for_backward(features, nn, ws, intrinsics, pose, depth)
+        ctx.meta = (BV, J, C, H, W, D, per_pixel, clamp, fanin)
+        return cost
+
+    @staticmethod
+    def backward(ctx, dcost):
+        features, nn, ws, intrinsics, pose, depth = ctx.saved_tensors
+        BV, J, C, H, W, D, per_pixel, clamp, fanin = ctx.meta
+        dev = features.device
+        dcost = _f(dcost)
+        lib = _lib.load()
+        dfeat = torch.empty_like(features)
+        scratch = torch.empty(lib.dcv_cost_volume_views_bwd_workspace_size(BV, J, C, H, W), dtype=torch.uint8,
+                              device=dev)
+        _lib.check(lib.dcv_cost_volume_views_bwd(
+            BV, J, C, H, W, D, int(per_pixel), fanin, features.data_ptr(), nn.data_ptr(), ws.data_ptr(),
+            intrinsics.data_ptr(), pose.data_ptr(), depth.data_ptr(), clamp, dcost.data_ptr(), dfeat.data_ptr(),
+            scratch.data_ptr(), _lib.stream_of(dev)), "dcv_cost_volume_views_bwd")
+        return dfeat, None, None, None, None, None, None, None
+
+
+def plane_sweep_cost_volume_views(features: torch.Tensor, nn: torch.Tensor, intrinsics: torch.Tensor,
+                                  pose: torch.Tensor, depth: torch.Tensor, clamp_min_depth: float = 1e-3,
+                                  max_fanin: int | None = None) -> torch.Tensor:
+    """plane_sweep_cost_volume(features, features[nn], ...) without the stacked copy:
+    features [BV,C,H,W] (every view's features, once), nn [BV,J] integer indices into BV (view
+    b's J source views: the reference's nn_matrix gather, mv_transformer.py:653-747, flattened
+    over the batch), intrinsics [BV,3,3] or [BV,J,3,3], pose [BV,J,4,4], depth [BV,D] or
+    [BV,D,H,W] -> cost [BV,D,H,W]; the gradient reaches `features` through both roles.
+    Matrix-core sizes (dcv_cost_volume_path == epipolar groups) run the views kernels; other
+    sizes gather tgt and take plane_sweep_cost_volume (both HIP). max_fanin: an upper bound on
+    how often one view appears in nn (taken from nn when it is a CPU tensor)."""
+    BV, C, H, W = features.shape
+    if nn.dim() != 2 or nn.shape[0] != BV:
+        raise ValueError(f"nn must be [BV={BV}, J], got {tuple(nn.shape)}")
+    J = nn.shape[1]
+    if not nn.is_cuda:
+        if nn.numel() and (int(nn.min()) < 0 or int(nn.max()) >= BV):
+            raise ValueError(f"nn indices must lie in [0, {BV})")
+        if max_fanin is None and nn.numel():
+            max_fanin = int(torch.bincount(nn.flatten().long(), minlength=BV).max())
+    lib = _lib.load()
+    if lib.dcv_cost_volume_path(BV, J, C, H, W) != 1:  # band / direct sizes: the stacked path
+        nn_d = nn.to(features.device).long()
+        return plane_sweep_cost_volume(features, features[nn_d], intrinsics, pose, depth, clamp_min_depth)
+    if intrinsics.dim() == 3:
+        intrinsics = intrinsics[:, None].expand(BV, J, 3, 3)
+    if depth.dim() not in (2, 4):
+        raise ValueError("depth must be [B, D] or [B, D, H, W]")
+    _lib.require_gpu(features, intrinsics, pose, depth)
+    nn32 = nn.to(device=features.device, dtype=torch.int32).contiguous()
+    return _CostVolumeViews.apply(_f(features), nn32, _f(intrinsics).detach(), _f(pose).detach(), _f(depth).detach(),
+                                  depth.dim() == 4, float(clamp_min_depth), int(max_fanin or 0))
+
+
 def batch_features_camera_parameters(features, intrinsics, extrinsics, nn_matrix=None, no_batch=False):
     """Reference view + its source views for every view (mv_transformer.py:653-747).
     features/intrinsics/extrinsics: lists over views of [B,C,H,W] / [B,3,3] / [B,4,4].

@@ -445,3 +445,90 @@ def test_hip_cost_volume_skewed_gradient_precision(gpu, cv_path, wide):
     for got, want, keep in ((dref, wref, keep_r), (dtgt, wtgt, keep_t)):
         err = (got.double() - want).abs()[keep].max() / want.abs()[keep].max()
         assert err < 1e-4, float(err)
+
+
+def _views_case(per_pixel, C=32, H=64, W=96, D=32, seed=41, nn_mode="rig"):
+    """Views mode: 6 views of the circle rig, each against its 2 nearest views (nn_mode "rig"),
+    or views 2-5 against views 0 and 1 ("hub": view 0 is the neighbour of five views, the largest
+    fan-in of the int64 target sums)."""
+    from my_depthsplat_amd.matching import depth_candidates
+    from my_depthsplat_amd.synthetic import context_cameras
+    g = torch.Generator().manual_seed(seed)
+    V, J = 6, 2
+    c2w = context_cameras(V)
+    centres = c2w[:, :3, 3]
+    dist = (centres[:, None] - centres[None]).norm(dim=-1) + torch.eye(V) * 1e9
+    if nn_mode == "rig":
+        nn = dist.argsort(dim=1)[:, :J]
+    else:
+        nn = torch.tensor([[1, 2], [0, 2]] + [[0, 1]] * (V - 2))
+    pose = (torch.linalg.inv(c2w[nn]) @ c2w[:, None]).contiguous()
+    K = torch.tensor([[W * 1.0, 0, W / 2], [0, H * 1.0, H / 2], [0, 0, 1]]).expand(V, J, 3, 3).contiguous()
+    feats = torch.randn(V, C, H, W, generator=g)
+    inv_min, inv_max = torch.full((V,), 1 / 100.0), torch.full((V,), 1 / 0.5)
+    if per_pixel:
+        prior = inv_min.view(-1, 1, 1, 1) + torch.rand(V, 1, H, W, generator=g) * 0.5
+        depth = (1.0 / depth_candidates(inv_min, inv_max, 4 * D, 1, prior)).contiguous()
+    else:
+        depth = (1.0 / torch.linspace(1 / 0.5, 1 / 100.0, D)).expand(V, D).contiguous()
+    return feats, nn, K, pose, depth
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("per_pixel", [False, True])
+@pytest.mark.parametrize("nn_mode", ["rig", "hub"])
+def test_hip_cost_volume_views_vs_stacked_and_oracle(gpu, monkeypatch, per_pixel, nn_mode):
+    """Round 6 views mode (dcv_cost_volume_views_*: features read once, neighbours by index):
+    the cost is bit-identical to the stacked call on features[nn] (same kernels, same groups);
+    dfeatures (both roles summed in-kernel) matches the oracle's autograd through the gather
+    within 1e-4, and is bit-identical run to run."""
+    from my_depthsplat_amd.matching import plane_sweep_cost_volume, plane_sweep_cost_volume_views
+    monkeypatch.setenv("DSPLAT_CV_PATH", "epi")
+    feats, nn, K, pose, depth = _views_case(per_pixel, nn_mode=nn_mode)
+    fg = feats.to(gpu).requires_grad_(True)
+    cost = plane_sweep_cost_volume_views(fg, nn, K.to(gpu), pose.to(gpu), depth.to(gpu))
+    stacked = plane_sweep_cost_volume(feats.to(gpu), feats.to(gpu)[nn.to(gpu)], K.to(gpu), pose.to(gpu),
+                                      depth.to(gpu))
+    assert torch.equal(cost.detach(), stacked)
+    dcost = torch.randn(cost.shape, generator=torch.Generator().manual_seed(12))
+    (cost * dcost.to(gpu)).sum().backward()
+    f2 = feats.clone().requires_grad_(True)
+    want = ocv.cost_volume(f2, f2[nn], K, pose, depth)
+    (want * dcost).sum().backward()
+    rel_close(cost.detach().cpu(), want.detach(), 1e-4)
+    rel_close(fg.grad.cpu(), f2.grad, 1e-4)
+    g1 = fg.grad.clone()
+    fg.grad = None
+    (plane_sweep_cost_volume_views(fg, nn, K.to(gpu), pose.to(gpu), depth.to(gpu)) * dcost.to(gpu)).sum().backward()
+    assert torch.equal(fg.grad, g1)
+
+
+@pytest.mark.gpu
+def test_hip_cost_volume_views_wide_shape_vs_oracle(gpu):
+    """Views mode at a config-D-sized grid (k_cost_epi_bwd<., 6, 8>: 6 views x 112 x 192,
+    per-pixel candidates, each view against its 2 nearest) vs the oracle through the gather."""
+    from my_depthsplat_amd.matching import plane_sweep_cost_volume_views
+    feats, nn, K, pose, depth = _views_case(True, C=16, H=112, W=192, D=32, seed=43)
+    assert bwd_shape(6, 16, 112, 192, 32, True) == (6, 8)
+    fg = feats.to(gpu).requires_grad_(True)
+    cost = plane_sweep_cost_volume_views(fg, nn, K.to(gpu), pose.to(gpu), depth.to(gpu))
+    dcost = torch.randn(cost.shape, generator=torch.Generator().manual_seed(13))
+    (cost * dcost.to(gpu)).sum().backward()
+    f2 = feats.clone().requires_grad_(True)
+    want = ocv.cost_volume(f2, f2[nn], K, pose, depth)
+    (want * dcost).sum().backward()
+    rel_close(cost.detach().cpu(), want.detach(), 1e-4)
+    rel_close(fg.grad.cpu(), f2.grad, 1e-4)
+
+
+def test_cost_volume_views_rejects_bad_nn_without_gpu():
+    """nn is checked on the host when it lives there: out-of-range view indices never reach the
+    kernels (which also clamp device-side indices)."""
+    from my_depthsplat_amd.matching import plane_sweep_cost_volume_views
+    feats = torch.zeros(3, 16, 8, 8)
+    with pytest.raises(ValueError, match="nn indices"):
+        plane_sweep_cost_volume_views(feats, torch.tensor([[1], [2], [3]]), torch.eye(3).expand(3, 3, 3),
+                                      torch.eye(4).expand(3, 1, 4, 4), torch.ones(3, 4))
+    with pytest.raises(ValueError, match="nn must be"):
+        plane_sweep_cost_volume_views(feats, torch.tensor([1, 2, 0]), torch.eye(3).expand(3, 3, 3),
+                                      torch.eye(4).expand(3, 1, 4, 4), torch.ones(3, 4))
