@@ -706,7 +706,8 @@ def train_leg(args, dev, rank, world, timed, max_over_ranks):
     import torch
 
     from my_depthsplat_amd.decoder import DecoderSplattingCUDA, DecoderSplattingCUDACfg
-    from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg, gaussians_from_head
+    from my_depthsplat_amd.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg
+    from my_depthsplat_amd.head_render import render_from_head
     from my_depthsplat_amd.loss import l1_mse_loss
     from my_depthsplat_amd.synthetic import context_cameras, target_cameras
 
@@ -727,8 +728,9 @@ def train_leg(args, dev, rank, world, timed, max_over_ranks):
     dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
 
     def step():
-        gs = gaussians_from_head(head, depths, images, ctx, ctx_k, adapter)
-        color = dec(gs, tgt, tgt_k, near, far, (H, W)).color
+        # adapter + rasterizer as one autograd node (head_render.py: the Gaussians' backward is one
+        # fused kernel, dsr_head_bwd; bit-identical to gaussians_from_head -> dec)
+        color = render_from_head(dec, head, depths, images, ctx, ctx_k, adapter, tgt, tgt_k, near, far, (H, W))
         loss = l1_mse_loss(color, gt, 1.0, 1.0)  # fused loss + gradient (dls_l1_mse_psnr)
         loss.backward()
         with torch.no_grad():
@@ -1095,7 +1097,7 @@ def train_d_leg(args, dev, rank, world, timed, max_over_ranks):
     head = GaussianHead(3 + adapter.d_in).to(dev)
     dec = DecoderSplattingCUDA(DecoderSplattingCUDACfg("splatting_cuda"), {"background_color": [0.0, 0.0, 0.0]}).to(dev)
     step = TrainStep(head, adapter, lambda gs, e, k, n, f, hw: dec(gs, e, k, n, f, hw).color,
-                     lambda p, t: l1_mse_loss(p, t, 1.0, 1.0), world=world)
+                     lambda p, t: l1_mse_loss(p, t, 1.0, 1.0), world=world, decoder=dec)
     for _ in range(2):
         step(batch)
     n_steps = max(3, args.extra_steps // 2)

@@ -217,7 +217,11 @@ int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t pre
 int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor,
                         uint64_t* keys, const uint32_t* cut, int tail, const uint32_t* seg_overflow,
                         const uint32_t* cut_rec, uint32_t* survivors, uint32_t* survivor_count,
-                        void* stream);
+                        const uint32_t* totals, uint64_t keys_capacity, void* stream);
+/* totals (dsr_bin_scan's, or NULL) and keys_capacity (entries `keys` holds): with totals given,
+ * the launch does nothing when totals[0] > keys_capacity (or totals[2] flags an offset overflow) —
+ * so the pass can be queued before the
+ * host has read N, into a buffer sized from an earlier call, and re-run if it was too small. */
 /* cut_rec: dsr_preprocess_cut's compact records (or NULL: the pre-test reads geom).
  * survivors / survivor_count (sizes from dsr_survivor_layout; the counters zeroed by the
  * caller; both NULL: none): the Gaussians that may emit in this pass are listed, per view and
@@ -370,6 +374,21 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M,
                        const float* grad_scale, const int32_t* scene_view_start, const int32_t* scene_views,
                        const uint8_t* row_live, float* dmeans, float* dshs, float* dcolors, float* dopac,
                        float* dcov6, float* dmean2D, int layout, void* stream);
+
+/* Fused head backward (round 6): dsr_preprocess_bwd + dga_adapter_bwd in one pass for
+ * Gaussians made by dga_adapter_fwd from head rows (the training step). Arguments: those of
+ * dga_adapter_bwd for the head side (head [B,V,H*W,C], depths [B,V,H*W], images [B,V,3,H,W]
+ * (the adapter's forward is re-evaluated), adapter_cams [B*V,104], scale range, sh_mask [d_sh]) and those of dsr_preprocess_bwd for the raster side
+ * (target size Ht x Wt, cams, geom, dgeom_fx, grad_scale, scene_view_start / scene_views,
+ * row_live; the Gaussians of scene b are rows [b G, (b + 1) G), G = V H W, and the SH degree is
+ * sqrt(d_sh) - 1). Writes dhead [B,V,H*W,C] (channels past 10 + 3 d_sh: 0) and, when
+ * non-NULL, ddepths [B,V,H*W]: bit-identical to dsr_preprocess_bwd followed by
+ * dga_adapter_bwd, without the Gaussian gradients' round trip through HBM. Needs H*W % 256 == 0. */
+int dsr_head_bwd(int B, int V, int H, int W, int d_sh, int C, const float* head, const float* depths,
+                 const float* images, const float* adapter_cams, float scale_min, float scale_max, const float* sh_mask, int Ht, int Wt,
+                 const dsr_camera* cams, const float* geom, const int64_t* dgeom_fx, const float* grad_scale,
+                 const int32_t* scene_view_start, const int32_t* scene_views, const uint8_t* row_live, float* dhead,
+                 float* ddepths, void* stream);
 
 /* ---- plane-sweep cost volume -------------------------------------------------------
  * Fused warp_with_pose_depth_candidates (matching.py:24-90) + correlation

@@ -30,7 +30,7 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_preprocess_cut": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I,
                                 _P]),
     "dsr_bin_cutoff": (_I, [_I, _I, _I, _P, c_uint32, _P, _P]),
-    "dsr_bin_scatter_cut": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P]),
+    "dsr_bin_scatter_cut": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, ctypes.c_uint64, _P]),
     "dsr_survivor_layout": (_I, [_I, _I, _P, _P]),
     "dsr_project_survivors": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I,
                                    _P]),
@@ -48,6 +48,8 @@ SIGNATURES: dict[str, tuple] = {
     "dsr_dgeom_to_float": (_I, [_I, _I, _P, _P, _P, _P, _P, _P]),
     "dsr_preprocess_bwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                 _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "dsr_head_bwd": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, c_float, c_float, _P, _I, _I, _P, _P, _P, _P, _P,
+                          _P, _P, _P, _P, _P]),
     "dcv_cost_volume_workspace_size": (ctypes.c_size_t, [_I, _I, _I, _I, _I]),
     "dcv_cost_volume_bwd_workspace_size": (ctypes.c_size_t, [_I, _I, _I, _I, _I]),
     "dcv_cost_volume_path": (_I, [_I, _I, _I, _I, _I]),

@@ -52,5 +52,5 @@ int ensure_dyn_lds(const void* fn, size_t bytes, const char* what) {
 
 extern "C" {
 const char* dsplat_last_error(void) { return g_err; }
-int dsplat_abi_version(void) { return 18; }
+int dsplat_abi_version(void) { return 20; }
 }

@@ -21,6 +21,7 @@
 #include <utility>
 
 #include "dsplat_common.h"
+#include "dga_math.h"
 
 namespace {
 
@@ -950,56 +951,76 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kProjectWPE)
 
 // ------------------------------------------------------------------------------------
 // Single-workgroup exclusive scan of the per-(view, tile) counts (V*T is small: 768 at
-// 2x256^2 x 3 views, ~20K at 12x512x960 x 10 views).
+// 2x256^2 x 3 views, ~20K at 12x512x960 x 10 views). Each thread scans 16 consecutive counts
+// (their loads issued together), so 16K counts take ONE pass of 3 barriers: round 5 walked
+// 1024 per pass (config D's 10,752 counts: 11 dependent passes, ~20 us).
 __global__ __launch_bounds__(1024) void k_scan(int n, const uint32_t* __restrict__ cnt,
                                                uint32_t* __restrict__ start,
                                                uint32_t* __restrict__ cursor,
                                                uint32_t* __restrict__ totals) {
+  constexpr int PT = 16;
   __shared__ uint32_t s_w[16];
-  __shared__ uint32_t s_carry, s_max, s_big;
+  __shared__ uint32_t s_max[16];
+  __shared__ uint32_t s_carry, s_big;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid == 0) {
     s_carry = 0;
-    s_max = 0;
     s_big = 0;
   }
   __syncthreads();
   uint32_t my_max = 0;
-  for (int base = 0; base < n; base += 1024) {
-    const int i = base + tid;
-    const uint32_t x = i < n ? cnt[i] : 0u;
-    my_max = max(my_max, x);
-    const uint32_t incl = dsplat::wave_incl_scan(x, lane);
+  for (int base = 0; base < n; base += 1024 * PT) {
+    uint32_t x[PT], tot = 0;
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int k = base + tid * PT + i;
+      x[i] = k < n ? cnt[k] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      tot += x[i];
+      my_max = max(my_max, x[i]);
+    }
+    const uint32_t incl = dsplat::wave_incl_scan(tot, lane);
     if (lane == 63) s_w[w] = incl;
     __syncthreads();
-    uint32_t off = s_carry;
-    for (int k = 0; k < w; ++k) off += s_w[k];
-    const uint32_t ex = off + incl - x;
-    if (i < n) {
-      start[i] = ex;
-      cursor[i] = ex;
+    uint64_t chunk = 0;
+    uint32_t off = s_carry + incl - tot;
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) off += s_w[k];
+      chunk += s_w[k];
     }
-    __syncthreads();
-    if (tid == 1023) {
-      const uint64_t c = (uint64_t)s_carry + (s_w[0] + s_w[1] + s_w[2] + s_w[3] + s_w[4] + s_w[5] + s_w[6] + s_w[7] +
-                                              s_w[8] + s_w[9] + s_w[10] + s_w[11] + s_w[12] + s_w[13] + s_w[14] +
-                                              (uint64_t)s_w[15]);
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int k = base + tid * PT + i;
+      if (k < n) {
+        start[k] = off;
+        cursor[k] = off;
+      }
+      off += x[i];
+    }
+    __syncthreads();  // every thread has read s_carry / s_w
+    if (tid == 0) {
+      const uint64_t c = (uint64_t)s_carry + chunk;
       if (c >> 31) s_big = 1u;  // offsets past 2^31: the caller must split the batch
-      s_carry = ex + x;
+      s_carry = (uint32_t)c;
     }
     __syncthreads();
   }
-  atomicMax(&s_max, my_max);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) my_max = max(my_max, (uint32_t)__shfl_xor((int)my_max, off, 64));
+  if (lane == 0) s_max[w] = my_max;
   __syncthreads();
   if (tid == 0) {
+    uint32_t m = 0;
+    for (int k = 0; k < 16; ++k) m = max(m, s_max[k]);
     start[n] = s_carry;
     totals[0] = s_carry;
-    totals[1] = s_max;
+    totals[1] = m;
     totals[2] = s_big;
   }
 }
 
-// ------------------------------------------------------------------------------------
 // ---- depth-cut binning (include/dsplat_hip.h: dsr_preprocess_cut / dsr_bin_cutoff /
 // dsr_bin_scatter_cut). Depth bucket = 16 per octave of the view-space depth (in near units)
 // from 0.25, read off the float bits; monotone in the depth, so a bucket range is a depth range.
@@ -1124,8 +1145,12 @@ __global__ __launch_bounds__(NTH) void k_scatter_cut(int G, int V, int gx, int g
                                                      const uint32_t* __restrict__ cut, int tail,
                                                      const uint32_t* __restrict__ seg_overflow,
                                                      const uint2* __restrict__ cut_rec, int per_view,
-                                                     uint32_t* __restrict__ surv, uint32_t* __restrict__ surv_count) {
+                                                     uint32_t* __restrict__ surv, uint32_t* __restrict__ surv_count,
+                                                     const uint32_t* __restrict__ totals, uint64_t keys_cap) {
   constexpr int NW = NTH / 64;
+  // launched before the host has read N (round 6): a key buffer smaller than N entries leaves
+  // everything untouched (uniform early exit before any side effect) and the host re-runs the pass
+  if (totals != nullptr && ((uint64_t)totals[0] > keys_cap || totals[2] != 0u)) return;  // (totals[2]: N >= 2^31)
   __shared__ uint32_t s_cut[kCutMaxSB];
   __shared__ WaveRects s_wr[NW];
   __shared__ uint64_t s_key[NTH];
@@ -3489,90 +3514,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
 }
 
-// ------------------------------------------------------------------------------------
-// K8 + K9: per (scene, Gaussian), summed over the scene's views in a fixed order.
+// K8 + K9's per-Gaussian work: Gaussian g of scene s (valid: g < G), its view-independent
+// inputs m0 (mean), c60 (covariance triu) and sh (coefficient-major), summed over the scene's
+// views in view order from the fixed-point rows dgeom -> the gradients of the mean (dm), the
+// covariance triu (dc), the opacity (dop), the SH (dsh) or precomputed colours (dcol).
+// Shared by k_preprocess_bwd and the fused head backward (k_head_bwd): the same operations.
 template <int DEG>
-__global__ __launch_bounds__(NT) void k_preprocess_bwd(
-    int G, int H, int W, int M, const float* __restrict__ means, const float* __restrict__ shs,
-    const float* __restrict__ cov6, const dsr_camera* __restrict__ cams,
-    const float* __restrict__ geom, const long long* __restrict__ dgeom, const float* __restrict__ gscale,
-    const int32_t* __restrict__ scene_view_start, const int32_t* __restrict__ scene_views,
-    const uint8_t* __restrict__ row_live,
-    float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
-    float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D, int layout) {
-  constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
-  int fx_k = 0;  // fixed-point unit of dgeom (k_render_bwd); non-finite dL_dpix -> NaN gradients
-  const float fx_unit = grad_fx_exp(gscale, threadIdx.x & 63, fx_k) ? ldexpf(1.f, fx_k - DSR_GRAD_FRAC_BITS)
-                                                                     : __builtin_nanf("");
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // NT * max(3 M, 9) floats: row staging
-  const int s = blockIdx.y;
-  const int tid = threadIdx.x;
-  const int g0 = blockIdx.x * NT;
-  const int nrows = min(NT, G - g0);
-  const int g = g0 + tid;
-  const bool valid = tid < nrows;
-  const size_t sg0 = (size_t)s * G + g0;
-  const size_t sg = sg0 + tid;
-  const int cw = (layout & kLayoutCovFull) ? 9 : 6;
-  // scene inputs of the block's Gaussians: coalesced through LDS
-  F3 m0 = {0.f, 0.f, 0.f};
-  float c60[6];
-  float sh[NC * 3];
-  float dsh[NC * 3];
-#pragma unroll
-  for (int k = 0; k < NC * 3; ++k) {
-    sh[k] = 0.f;
-    dsh[k] = 0.f;
-  }
-  // the covariance and SH row blocks are requested into registers together with the means
-  // (one memory round trip per workgroup instead of three) when the blocks are 16-byte aligned
-  // and the SH rows hold exactly the evaluated coefficients; else staged one after the other
-  constexpr int PS = DEG >= 0 ? (3 * NC + 3) / 4 : 1;
-  const int rw = DEG >= 0 ? 3 * M : 0;
-  const bool pf = dsplat::aligned16(cov6 + cw * sg0) &&
-                  (DEG < 0 || (rw <= 4 * PS && dsplat::aligned16(shs + (size_t)rw * sg0)));
-  float4 vc[3], vs[PS];
-  if (pf) {
-    dsplat::pref_get<NT>(cov6 + cw * sg0, (size_t)cw * nrows, vc);
-    if constexpr (DEG >= 0) dsplat::pref_get<NT>(shs + (size_t)rw * sg0, (size_t)rw * nrows, vs);
-  }
-  dsplat::stage_in<NT>(means + 3 * sg0, (size_t)3 * nrows, lds);
-  __syncthreads();
-  if (valid) m0 = {lds[3 * tid], lds[3 * tid + 1], lds[3 * tid + 2]};
-  __syncthreads();
-  if (pf)
-    dsplat::pref_put<NT>(cov6 + cw * sg0, (size_t)cw * nrows, vc, lds);
-  else
-    dsplat::stage_in<NT>(cov6 + cw * sg0, (size_t)cw * nrows, lds);
-  __syncthreads();
-  {
-    constexpr int full_idx[6] = {0, 1, 2, 4, 5, 8};
-#pragma unroll
-    for (int k = 0; k < 6; ++k) c60[k] = valid ? lds[tid * cw + (cw == 9 ? full_idx[k] : k)] : 0.f;
-  }
-  __syncthreads();
-  if constexpr (DEG >= 0) {
-    if (pf)
-      dsplat::pref_put<NT>(shs + (size_t)rw * sg0, (size_t)rw * nrows, vs, lds);
-    else
-      dsplat::stage_in<NT>(shs + (size_t)rw * sg0, (size_t)rw * nrows, lds);
-    __syncthreads();
-    if (valid) {
-      const float* p = lds + tid * rw;
-      if (layout & kLayoutShChannelMajor) {
-#pragma unroll
-        for (int k = 0; k < NC; ++k)
-#pragma unroll
-          for (int ch = 0; ch < 3; ++ch) sh[k * 3 + ch] = p[ch * M + k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < NC * 3; ++k) sh[k] = p[k];
-      }
-    }
-    __syncthreads();
-  }
-  float dm0 = 0.f, dm1 = 0.f, dm2 = 0.f, dop = 0.f, dcol0 = 0.f, dcol1 = 0.f, dcol2 = 0.f;
-  float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+__device__ __forceinline__ void pbwd_views(int s, int g, bool valid, int G, int H, int W, F3 m0,
+                                           const float (&c60)[6], const float* sh, const dsr_camera* __restrict__ cams,
+                                           const float* __restrict__ geom, const long long* __restrict__ dgeom,
+                                           float fx_unit, const int32_t* __restrict__ scene_view_start,
+                                           const int32_t* __restrict__ scene_views,
+                                           const uint8_t* __restrict__ row_live, float* __restrict__ dmean2D,
+                                           float& dm0, float& dm1, float& dm2, float& dop, float (&dc)[6],
+                                           float* dsh, float& dcol0, float& dcol1, float& dcol2) {
   // the view loop is workgroup-uniform (scene = blockIdx.y), so the view ids and every camera
   // field below are scalar loads; lanes past the scene's last Gaussian ride along masked off
   const int vb = scene_view_start[s], ve = scene_view_start[s + 1];
@@ -3742,6 +3697,94 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     dm1 += e1 * gsc;
     dm2 += e2 * gsc;
   }
+}
+
+// ------------------------------------------------------------------------------------
+// K8 + K9: per (scene, Gaussian), summed over the scene's views in a fixed order.
+template <int DEG>
+__global__ __launch_bounds__(NT) void k_preprocess_bwd(
+    int G, int H, int W, int M, const float* __restrict__ means, const float* __restrict__ shs,
+    const float* __restrict__ cov6, const dsr_camera* __restrict__ cams,
+    const float* __restrict__ geom, const long long* __restrict__ dgeom, const float* __restrict__ gscale,
+    const int32_t* __restrict__ scene_view_start, const int32_t* __restrict__ scene_views,
+    const uint8_t* __restrict__ row_live,
+    float* __restrict__ dmeans, float* __restrict__ dshs, float* __restrict__ dcolors,
+    float* __restrict__ dopac, float* __restrict__ dcov6, float* __restrict__ dmean2D, int layout) {
+  constexpr int NC = DEG >= 0 ? (DEG + 1) * (DEG + 1) : 1;
+  int fx_k = 0;  // fixed-point unit of dgeom (k_render_bwd); non-finite dL_dpix -> NaN gradients
+  const float fx_unit = grad_fx_exp(gscale, threadIdx.x & 63, fx_k) ? ldexpf(1.f, fx_k - DSR_GRAD_FRAC_BITS)
+                                                                     : __builtin_nanf("");
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // NT * max(3 M, 9) floats: row staging
+  const int s = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int g0 = blockIdx.x * NT;
+  const int nrows = min(NT, G - g0);
+  const int g = g0 + tid;
+  const bool valid = tid < nrows;
+  const size_t sg0 = (size_t)s * G + g0;
+  const size_t sg = sg0 + tid;
+  const int cw = (layout & kLayoutCovFull) ? 9 : 6;
+  // scene inputs of the block's Gaussians: coalesced through LDS
+  F3 m0 = {0.f, 0.f, 0.f};
+  float c60[6];
+  float sh[NC * 3];
+  float dsh[NC * 3];
+#pragma unroll
+  for (int k = 0; k < NC * 3; ++k) {
+    sh[k] = 0.f;
+    dsh[k] = 0.f;
+  }
+  // the covariance and SH row blocks are requested into registers together with the means
+  // (one memory round trip per workgroup instead of three) when the blocks are 16-byte aligned
+  // and the SH rows hold exactly the evaluated coefficients; else staged one after the other
+  constexpr int PS = DEG >= 0 ? (3 * NC + 3) / 4 : 1;
+  const int rw = DEG >= 0 ? 3 * M : 0;
+  const bool pf = dsplat::aligned16(cov6 + cw * sg0) &&
+                  (DEG < 0 || (rw <= 4 * PS && dsplat::aligned16(shs + (size_t)rw * sg0)));
+  float4 vc[3], vs[PS];
+  if (pf) {
+    dsplat::pref_get<NT>(cov6 + cw * sg0, (size_t)cw * nrows, vc);
+    if constexpr (DEG >= 0) dsplat::pref_get<NT>(shs + (size_t)rw * sg0, (size_t)rw * nrows, vs);
+  }
+  dsplat::stage_in<NT>(means + 3 * sg0, (size_t)3 * nrows, lds);
+  __syncthreads();
+  if (valid) m0 = {lds[3 * tid], lds[3 * tid + 1], lds[3 * tid + 2]};
+  __syncthreads();
+  if (pf)
+    dsplat::pref_put<NT>(cov6 + cw * sg0, (size_t)cw * nrows, vc, lds);
+  else
+    dsplat::stage_in<NT>(cov6 + cw * sg0, (size_t)cw * nrows, lds);
+  __syncthreads();
+  {
+    constexpr int full_idx[6] = {0, 1, 2, 4, 5, 8};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) c60[k] = valid ? lds[tid * cw + (cw == 9 ? full_idx[k] : k)] : 0.f;
+  }
+  __syncthreads();
+  if constexpr (DEG >= 0) {
+    if (pf)
+      dsplat::pref_put<NT>(shs + (size_t)rw * sg0, (size_t)rw * nrows, vs, lds);
+    else
+      dsplat::stage_in<NT>(shs + (size_t)rw * sg0, (size_t)rw * nrows, lds);
+    __syncthreads();
+    if (valid) {
+      const float* p = lds + tid * rw;
+      if (layout & kLayoutShChannelMajor) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch) sh[k * 3 + ch] = p[ch * M + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < NC * 3; ++k) sh[k] = p[k];
+      }
+    }
+    __syncthreads();
+  }
+  float dm0 = 0.f, dm1 = 0.f, dm2 = 0.f, dop = 0.f, dcol0 = 0.f, dcol1 = 0.f, dcol2 = 0.f;
+  float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  pbwd_views<DEG>(s, g, valid, G, H, W, m0, c60, sh, cams, geom, dgeom, fx_unit, scene_view_start, scene_views,
+                  row_live, dmean2D, dm0, dm1, dm2, dop, dc, dsh, dcol0, dcol1, dcol2);
   // outputs: coalesced through LDS
   if (valid) {
     lds[3 * tid] = dm0;
@@ -3792,6 +3835,105 @@ __global__ __launch_bounds__(NT) void k_preprocess_bwd(
     __syncthreads();
     dsplat::stage_out<NT>(dshs + (size_t)rw * sg0, (size_t)rw * nrows, lds);
   }
+}
+
+// ------------------------------------------------------------------------------------
+// Fused head backward (round 6; dsr_head_bwd): K8 + K9 and the adapter's backward in ONE pass
+// per (scene, Gaussian) = adapter row. The training step's Gaussians come from the head through
+// the fused adapter (dga_adapter_fwd), so the Gaussian gradients K8 + K9 produce are consumed
+// by exactly one reader, the adapter's backward; written to HBM and read back they were ~320 B
+// per Gaussian (config C: 2.1 M Gaussians, ~0.67 GB). Here the adapter's forward is re-evaluated
+// from the head row (dga::adapter_row_fwd: the same float operations, so mean, covariance and
+// harmonics are the values the rasterizer's forward read), K8 + K9 run on them (pbwd_views: the
+// same operations as k_preprocess_bwd), and their gradients feed dga::adapter_row_bwd in
+// registers: dhead is bit-identical to the two-kernel path. The head rows stay staged in LDS
+// across the view loop (re-read for the adapter's backward instead of held in registers).
+// Rows are view-major inside a scene (G = V_ctx H W), and H W % NT == 0 (host check), so a
+// workgroup's rows share one context view and one scene: camera blocks and the view loop are
+// workgroup-uniform.
+template <int DEG, int NSH>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(DEG <= 2 ? 4 : 1))) void k_head_bwd(dga::AdIn a, int G, int Ht, int Wt, const dsr_camera* __restrict__ cams,
+                                                 const float* __restrict__ geom, const long long* __restrict__ dgeom,
+                                                 const float* __restrict__ gscale,
+                                                 const int32_t* __restrict__ scene_view_start,
+                                                 const int32_t* __restrict__ scene_views,
+                                                 const uint8_t* __restrict__ row_live, float* __restrict__ drows,
+                                                 float* __restrict__ ddepth) {
+  constexpr int NC = (DEG + 1) * (DEG + 1);
+  static_assert(NC <= NSH, "the harmonics hold the evaluated coefficients");
+  constexpr int KH = dga::Rows<NSH, true>::kHead;
+  int fx_k = 0;
+  const float fx_unit = grad_fx_exp(gscale, threadIdx.x & 63, fx_k) ? ldexpf(1.f, fx_k - DSR_GRAD_FRAC_BITS)
+                                                                     : __builtin_nanf("");
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // NT * C floats: the head rows
+  const size_t total = (size_t)a.BV * a.H * a.W;
+  const size_t n0 = (size_t)blockIdx.x * NT;
+  const int nrows = (int)min((size_t)NT, total - n0);
+  const int tid = threadIdx.x, C = a.C;
+  dga::Pix px{};
+  const bool valid = dga::pixel_of(n0 + tid, a, px);
+  const int s = (int)(n0 / (size_t)G);  // workgroup-uniform
+  const int g = (int)(n0 + tid - (size_t)s * G);
+  const float* cam = a.cams + n0 / ((size_t)a.H * a.W) * dga::kCamFloats;
+  dsplat::stage_in<NT>(a.rows + n0 * C, (size_t)nrows * C, lds);
+  __syncthreads();
+  float mo[3], Cw[9], ho[3 * NSH], sc[3], q[4];
+  {
+    float h[KH];
+#pragma unroll
+    for (int k = 0; k < KH; ++k) h[k] = valid ? lds[tid * C + k] : 0.f;
+    if (valid) dga::adapter_row_fwd<NSH, true>(a, px, cam, h, nullptr, mo, Cw, ho, sc, q);
+  }
+  // the rasterizer's inputs as it read them: mean, covariance triu, SH coefficient-major
+  const F3 m0 = valid ? F3{mo[0], mo[1], mo[2]} : F3{0.f, 0.f, 0.f};
+  float c60[6];
+  float sh[NC * 3], dsh[NC * 3];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    constexpr int full_idx[6] = {0, 1, 2, 4, 5, 8};
+    c60[k] = valid ? Cw[full_idx[k]] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      sh[k * 3 + ch] = valid ? ho[ch * NSH + k] : 0.f;
+      dsh[k * 3 + ch] = 0.f;
+    }
+  float dm0 = 0.f, dm1 = 0.f, dm2 = 0.f, dop = 0.f, dcol0 = 0.f, dcol1 = 0.f, dcol2 = 0.f;
+  float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  pbwd_views<DEG>(s, g, valid, G, Ht, Wt, m0, c60, sh, cams, geom, dgeom, fx_unit, scene_view_start, scene_views,
+                  row_live, nullptr, dm0, dm1, dm2, dop, dc, dsh, dcol0, dcol1, dcol2);
+  // the adapter's backward from those gradients (the values k_preprocess_bwd would have stored:
+  // covariance gradient on the upper triangle, harmonics channel-major, zeros past NC)
+  const float gm[3] = {dm0, dm1, dm2};
+  const float gCw[9] = {dc[0], dc[1], dc[2], 0.f, dc[3], dc[4], 0.f, 0.f, dc[5]};
+  float gh[3 * NSH];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+    for (int k = 0; k < NSH; ++k) gh[ch * NSH + k] = k < NC ? dsh[k * 3 + ch] : 0.f;
+  const float z0[3] = {0.f, 0.f, 0.f}, z1[4] = {0.f, 0.f, 0.f, 0.f};
+  float dh[KH];
+#pragma unroll
+  for (int k = 0; k < KH; ++k) dh[k] = 0.f;
+  float gxy[2] = {0.f, 0.f};
+  __syncthreads();  // (the head rows are read again below, not kept live across the view loop)
+  if (valid) {
+    float h[KH];
+#pragma unroll
+    for (int k = 0; k < KH; ++k) h[k] = lds[tid * C + k];
+    const float z = a.depths[px.n];
+    dga::adapter_row_bwd<NSH, true>(a, px, cam, h, z, gm, gCw, gh, dop, true, z0, z1, dh, gxy, ddepth);
+  }
+  __syncthreads();
+  if (valid) {
+#pragma unroll
+    for (int k = 0; k < KH; ++k) lds[tid * C + k] = dh[k];
+    for (int k = KH; k < C; ++k) lds[tid * C + k] = 0.f;
+  }
+  __syncthreads();
+  dsplat::stage_out<NT>(drows + n0 * C, (size_t)nrows * C, lds);
 }
 
 // dgeom_fx -> float [rows, GS] (diagnostics / tests): the values k_preprocess_bwd consumes
@@ -4048,7 +4190,8 @@ int dsr_bin_cutoff(int V, int H, int W, const uint32_t* depth_hist, uint32_t pre
 
 int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t* seg_cursor, uint64_t* keys,
                         const uint32_t* cut, int tail, const uint32_t* seg_overflow, const uint32_t* cut_rec,
-                        uint32_t* survivors, uint32_t* survivor_count, void* stream) {
+                        uint32_t* survivors, uint32_t* survivor_count, const uint32_t* totals, uint64_t keys_capacity,
+                        void* stream) {
   DSPLAT_REQUIRE(G > 0 && V > 0 && H > 0 && W > 0, "dsr_bin_scatter_cut: bad sizes");
   DSPLAT_REQUIRE(geom && seg_cursor && keys && cut && (!tail || seg_overflow), "dsr_bin_scatter_cut: null pointer");
   DSPLAT_REQUIRE((survivors == nullptr) == (survivor_count == nullptr) && (survivors == nullptr || cut_rec),
@@ -4060,7 +4203,8 @@ int dsr_bin_scatter_cut(int G, int V, int H, int W, const float* geom, uint32_t*
   k_scatter_cut<kNTH><<<xcd_grid(per_view, V), kNTH, 0, (hipStream_t)stream>>>(G, V, gx, gy, geom, seg_cursor,
                                                                                   keys, cut, tail, seg_overflow,
                                                                                   reinterpret_cast<const uint2*>(cut_rec),
-                                                                                  per_view, survivors, survivor_count);
+                                                                                  per_view, survivors, survivor_count,
+                                                                                  totals, keys_capacity);
   return dsplat::check_launch("k_scatter_cut");
 }
 
@@ -4420,6 +4564,43 @@ int dsr_preprocess_bwd(int S, int G, int V, int H, int W, int sh_degree, int M, 
   }
 #undef DSR_PREB
   return dsplat::check_launch("k_preprocess_bwd");
+}
+
+int dsr_head_bwd(int B, int V, int H, int W, int d_sh, int C, const float* head, const float* depths,
+                 const float* images, const float* adapter_cams, float scale_min, float scale_max, const float* sh_mask, int Ht, int Wt,
+                 const dsr_camera* cams, const float* geom, const int64_t* dgeom_fx, const float* grad_scale,
+                 const int32_t* scene_view_start, const int32_t* scene_views, const uint8_t* row_live, float* dhead,
+                 float* ddepths, void* stream) {
+  DSPLAT_REQUIRE(B > 0 && V > 0 && H > 0 && W > 0 && Ht > 0 && Wt > 0, "dsr_head_bwd: bad sizes");
+  DSPLAT_REQUIRE(d_sh == 1 || d_sh == 4 || d_sh == 9 || d_sh == 16, "dsr_head_bwd: d_sh=%d (1, 4, 9, 16)", d_sh);
+  DSPLAT_REQUIRE(C >= 10 + 3 * d_sh, "dsr_head_bwd: %d head channels < 10 + 3*d_sh", C);
+  DSPLAT_REQUIRE((size_t)H * W % NT == 0, "dsr_head_bwd: H*W=%d must be a multiple of %d (use dsr_preprocess_bwd + "
+                 "dga_adapter_bwd)", H * W, NT);
+  DSPLAT_REQUIRE(head && depths && images && adapter_cams && sh_mask && cams && geom && dgeom_fx && grad_scale &&
+                     scene_view_start && scene_views && dhead,
+                 "dsr_head_bwd: null pointer");
+  const size_t lds = (size_t)NT * C * sizeof(float);
+  DSPLAT_REQUIRE(lds <= 160 * 1024, "dsr_head_bwd: %d head channels exceed the LDS row staging", C);
+  const dga::AdIn a{head, nullptr, depths, images, adapter_cams, sh_mask, scale_min, scale_max, 1e-8f, C, B * V, H, W, 1};
+  const int G = V * H * W;
+  const long long* dgeom = reinterpret_cast<const long long*>(dgeom_fx);
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned grid = (unsigned)(((size_t)B * G + NT - 1) / NT);
+#define DSR_HEADB(D, NS)                                                                                          \
+  do {                                                                                                            \
+    if (int e = dsplat::ensure_dyn_lds((const void*)k_head_bwd<D, NS>, lds, "hipFuncSetAttribute(k_head_bwd)"))  \
+      return e;                                                                                                   \
+    k_head_bwd<D, NS><<<grid, NT, lds, st>>>(a, G, Ht, Wt, cams, geom, dgeom, grad_scale, scene_view_start,       \
+                                             scene_views, row_live, dhead, ddepths);                               \
+  } while (0)
+  switch (d_sh) {  // the rasterizer's SH degree follows the harmonics: (degree + 1)^2 = d_sh
+    case 1: DSR_HEADB(0, 1); break;
+    case 4: DSR_HEADB(1, 4); break;
+    case 9: DSR_HEADB(2, 9); break;
+    default: DSR_HEADB(3, 16); break;
+  }
+#undef DSR_HEADB
+  return dsplat::check_launch("k_head_bwd");
 }
 
 }  // extern "C"

@@ -127,6 +127,8 @@ def algorithmic_bytes(kernel: str, *, G: int, V: int, N: int, HW: int, T: int | 
         return 8 * N + 36 * V * G + 20 * V * HW + 72 * V * G  # rendered (view, Gaussian) out
     if kernel == "k_preprocess_bwd":  # params + per-view records and sums in; param grads out
         return S * G * (148 + 148) + V * G * (48 + 72)
+    if kernel == "k_head_bwd":  # head row (148) + depth + pixel colour in, dhead (148) out per Gaussian;
+        return S * G * (148 + 4 + 12 + 148) + V * G * (36 + 72)  # per view the record's 36 B, the 72-B sums
     raise KeyError(kernel)
 
 
@@ -782,6 +784,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         if torch.cuda.is_current_stream_capturing():
             raise _lib.DsplatError(f"V*G*tiles = {V * G * T} key slots exceed the key budget: this size needs a "
                                    "host read-back and cannot be captured into a graph")
+        early = None  # capacity of the depth-cut scatter queued before the read-back
         if sb > 0:
             # what does not depend on N is queued before the read-back, so the device has work
             # while the host waits on it (the cut thresholds; the survivor counters)
@@ -796,6 +799,25 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                            "dsr_survivor_layout")
                 surv = torch.empty(slots.value, dtype=torch.int32, device=dev)
                 surv_n = torch.zeros(2 * ncnt.value, dtype=torch.int32, device=dev)
+            proj = (S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
+                    cams.data_ptr())
+            prev_n = spec.get("two_phase_n")
+            if prev_n:
+                # round 6: the scatter (and its survivor projection) queued BEFORE the read-back,
+                # into keys sized from the previous call's N: the device runs it while the host
+                # waits, instead of idling from the cut thresholds to the host's next launch. The
+                # launch checks N on the device and does nothing when the buffer is too small
+                # (then it is re-run below with the exact size)
+                early = int(prev_n * 1.25) + (1 << 16)
+                keys = torch.empty(early, dtype=torch.int64, device=dev)
+                scratch = torch.empty(early, dtype=torch.int64, device=dev)  # only big segments touch it
+                _lib.check(_timed("k_scatter_cut", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(),
+                                  cursor.data_ptr(), keys.data_ptr(), cut.data_ptr(), 0, None, _ptr(cut_rec),
+                                  _ptr(surv), _ptr(surv_n), totals.data_ptr(), early, st), "dsr_bin_scatter_cut")
+                if defer:
+                    _lib.check(_timed("k_project_survivors", lib.dsr_project_survivors, *proj, surv.data_ptr(),
+                                      surv_n.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero),
+                                      _ptr(row_live), layout, st), "dsr_project_survivors")
         tot = totals[:3].cpu()  # one small read-back: N sizes the key buffer
         N, maxc = int(tot[0]), int(tot[1])
         if ctx.adapt_hints:
@@ -803,7 +825,15 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
         if int(tot[2]):
             raise EntryOverflow(f"{V} views x {G} Gaussians produce >= 2^31 (view, tile, Gaussian) entries: "
                                 "render fewer views per call")
-        keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
+        spec["two_phase_n"] = N
+        if early is not None and (N > early or maxc <= 2 * cut_prefix):
+            if N <= early:  # it ran, but the lists are short after all: cursors and counters back
+                cursor.copy_(seg_start[:-1])
+                if surv_n is not None:
+                    surv_n.zero_()
+            early = None
+        if early is None:
+            keys = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
         if sb > 0 and maxc <= 2 * cut_prefix:  # short lists after all: write everything
             sb = 0
             surv = surv_n = None
@@ -812,16 +842,15 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
                              layout, dev, st, dgeom_zero, row_live)
         if sb > 0:
             # depth cut: write only each tile's nearest entries (cursor ends at their end)
-            scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev)  # only big segments touch it
-            proj = (S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
-                    cams.data_ptr())
-            _lib.check(_timed("k_scatter_cut", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(), cursor.data_ptr(),
-                              keys.data_ptr(), cut.data_ptr(), 0, None, _ptr(cut_rec), _ptr(surv), _ptr(surv_n), st),
-                       "dsr_bin_scatter_cut")
-            if defer:
-                _lib.check(_timed("k_project_survivors", lib.dsr_project_survivors, *proj, surv.data_ptr(),
-                                  surv_n.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero),
-                                  _ptr(row_live), layout, st), "dsr_project_survivors")
+            if early is None:
+                scratch = torch.empty(max(N, 1), dtype=torch.int64, device=dev)  # only big segments touch it
+                _lib.check(_timed("k_scatter_cut", lib.dsr_bin_scatter_cut, G, V, H, W, geom.data_ptr(),
+                                  cursor.data_ptr(), keys.data_ptr(), cut.data_ptr(), 0, None, _ptr(cut_rec),
+                                  _ptr(surv), _ptr(surv_n), None, 0, st), "dsr_bin_scatter_cut")
+                if defer:
+                    _lib.check(_timed("k_project_survivors", lib.dsr_project_survivors, *proj, surv.data_ptr(),
+                                      surv_n.data_ptr(), geom.data_ptr(), radii.data_ptr(), _ptr(dgeom_zero),
+                                      _ptr(row_live), layout, st), "dsr_project_survivors")
             tile_count, seg_count, stride = seg_count, cursor, SEG_ENDS
             # no backward: the written heads are sorted and composited in one launch below
             # (dsr_sort_render, flags as dsr_render_fwd); the keys stay unsorted in HBM unless a
@@ -890,7 +919,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             tail_n = None if surv is None else surv_n[surv_n.numel() // 2:]
             _lib.check(lib.dsr_bin_scatter_cut(G, V, H, W, geom.data_ptr(), seg_count.data_ptr(), keys.data_ptr(),
                                                cut.data_ptr(), 1, overflow.data_ptr(), _ptr(cut_rec), _ptr(surv),
-                                               _ptr(tail_n), st), "dsr_bin_scatter_cut(tail)")
+                                               _ptr(tail_n), None, 0, st), "dsr_bin_scatter_cut(tail)")
             if surv is not None:
                 _lib.check(lib.dsr_project_survivors(*proj, surv.data_ptr(), tail_n.data_ptr(), geom.data_ptr(),
                                                      radii.data_ptr(), _ptr(dgeom_zero), _ptr(row_live), layout, st),
@@ -962,6 +991,41 @@ GRAD_SCALE_BLOCKS = 512   # DSR_GRAD_SCALE_BLOCKS
 
 
 
+def render_bwd_raw(state: RasterState, cams, dcolor: torch.Tensor, G: int):
+    """K7 of a forward's state: dsr_grad_scale + dsr_render_bwd into the 64-bit fixed-point rows
+    (the forward's zeroed accumulator when it made one). Returns (dgeom_fx [V,G,DGEOM_WORDS],
+    grad_scale)."""
+    lib = _lib.load()
+    V, _, H, W = dcolor.shape
+    dev = dcolor.device
+    st = _lib.stream_of(dev)
+    dcolor = dcolor.contiguous().float()
+    if state.dgeom is not None:  # rendered rows zeroed by the forward's projection kernel
+        dgeom_fx, state.dgeom = state.dgeom, None
+    else:
+        dgeom_fx = torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev)
+    gscale = torch.empty(GRAD_SCALE_BLOCKS, dtype=torch.float32, device=dev)
+    _lib.check(lib.dsr_grad_scale(V, H, W, dcolor.data_ptr(), gscale.data_ptr(), st), "dsr_grad_scale")
+    _lib.check(_timed("k_render_bwd", lib.dsr_render_bwd, G, V, H, W, cams.data_ptr(), state.geom.data_ptr(),
+                      _ptr(state.seg_start), state.seg_count.data_ptr(), state.seg_stride, state.keys.data_ptr(),
+                      _ptr(state.spill), state.final_T.data_ptr(), state.n_contrib.data_ptr(), dcolor.data_ptr(),
+                      gscale.data_ptr(), dgeom_fx.data_ptr(), st), "dsr_render_bwd")
+    return dgeom_fx, gscale
+
+
+def scene_view_index(view_scene, S: int, dev) -> torch.Tensor:
+    """[scene_view_start (S + 1), scene_views (V)] int32 on the device: the views of each scene in
+    view order (the fixed summation order of the preprocess backward)."""
+    V = len(view_scene)
+    order = sorted(range(V), key=lambda v: (view_scene[v], v))
+    starts = [0] * (S + 1)
+    for v in range(V):
+        starts[view_scene[v] + 1] += 1
+    for s in range(S):
+        starts[s + 1] += starts[s]
+    return device_index(starts + order, dev)
+
+
 def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_scene, state: RasterState,
                  dcolor, want_mean2d: bool, layout=0, want_dgeom: bool = False):
     """Rasterizer backward (K7 -> K8 + K9). Deterministic: the per-Gaussian sums are 64-bit
@@ -974,30 +1038,13 @@ def backward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, view_sc
     M = (feats.shape[3] if layout & LAYOUT_SH_CHANNEL_MAJOR else feats.shape[2]) if use_sh else 0
     dev = means.device
     st = _lib.stream_of(dev)
-    dcolor = dcolor.contiguous().float()
-    if state.dgeom is not None:  # rendered rows zeroed by the forward's projection kernel
-        dgeom_fx, state.dgeom = state.dgeom, None
-    else:
-        dgeom_fx = torch.zeros((V, G, DGEOM_WORDS), dtype=torch.int64, device=dev)
-    gscale = torch.empty(GRAD_SCALE_BLOCKS, dtype=torch.float32, device=dev)
-    _lib.check(lib.dsr_grad_scale(V, H, W, dcolor.data_ptr(), gscale.data_ptr(), st), "dsr_grad_scale")
-    _lib.check(_timed("k_render_bwd", lib.dsr_render_bwd, G, V, H, W, cams.data_ptr(), state.geom.data_ptr(), _ptr(state.seg_start),
-                                  state.seg_count.data_ptr(), state.seg_stride, state.keys.data_ptr(),
-                                  _ptr(state.spill), state.final_T.data_ptr(), state.n_contrib.data_ptr(), dcolor.data_ptr(),
-                                  gscale.data_ptr(), dgeom_fx.data_ptr(), st), "dsr_render_bwd")
+    dgeom_fx, gscale = render_bwd_raw(state, cams, dcolor, G)
     dgeom = None
     if want_dgeom:
         dgeom = torch.empty((V, G, GEOM_STRIDE), dtype=torch.float32, device=dev)
         _lib.check(lib.dsr_dgeom_to_float(G, V, state.geom.data_ptr(), dgeom_fx.data_ptr(), gscale.data_ptr(),
                                           _ptr(state.row_live), dgeom.data_ptr(), st), "dsr_dgeom_to_float")
-    # views of each scene, in view order (fixed summation order -> deterministic reduce)
-    order = sorted(range(V), key=lambda v: (view_scene[v], v))
-    starts = [0] * (S + 1)
-    for v in range(V):
-        starts[view_scene[v] + 1] += 1
-    for s in range(S):
-        starts[s + 1] += starts[s]
-    idx = device_index(starts + order, dev)
+    idx = scene_view_index(view_scene, S, dev)
     dmeans = torch.empty((S, G, 3), dtype=torch.float32, device=dev)
     dfeat = torch.empty_like(feats, dtype=torch.float32)
     dopac = torch.empty((S, G), dtype=torch.float32, device=dev)

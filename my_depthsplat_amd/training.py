@@ -168,8 +168,13 @@ class TrainStep:
     0.5 (config/main.yaml:92). max_steps defaults to 150,000 (scripts/re10k_depthsplat_train.sh:9)."""
 
     def __init__(self, head: GaussianHead, adapter, render: Callable, loss: Callable, lr: float = 2e-4,
-                 clip: float = 0.5, world: int = 1, weight_decay: float = 0.01, max_steps: int = 150_000):
+                 clip: float = 0.5, world: int = 1, weight_decay: float = 0.01, max_steps: int = 150_000,
+                 decoder=None):
         self.head, self.adapter, self.render, self.loss = head, adapter, render, loss
+        # decoder (a DecoderSplattingCUDA): adapter + rasterizer as one autograd node
+        # (head_render.render_from_head: one fused kernel for the Gaussians' backward); `render`
+        # is then unused
+        self.decoder = decoder
         self.clip, self.world = clip, world
         self.opt = torch.optim.AdamW(head.parameters(), lr=lr, weight_decay=weight_decay)
         self.sched = torch.optim.lr_scheduler.OneCycleLR(self.opt, lr, max_steps + 10, pct_start=0.01,
@@ -180,8 +185,13 @@ class TrainStep:
         from .gaussian_adapter import gaussians_from_head
         H, W = batch.images.shape[-2:]
         raw = self.head(batch.images, batch.depths)
-        gs = gaussians_from_head(raw, batch.depths, batch.images, batch.ctx_ext, batch.ctx_k, self.adapter)
-        color = self.render(gs, batch.tgt_ext, batch.tgt_k, batch.near, batch.far, (H, W))
+        if self.decoder is not None:
+            from .head_render import render_from_head
+            color = render_from_head(self.decoder, raw, batch.depths, batch.images, batch.ctx_ext, batch.ctx_k,
+                                     self.adapter, batch.tgt_ext, batch.tgt_k, batch.near, batch.far, (H, W))
+        else:
+            gs = gaussians_from_head(raw, batch.depths, batch.images, batch.ctx_ext, batch.ctx_k, self.adapter)
+            color = self.render(gs, batch.tgt_ext, batch.tgt_k, batch.near, batch.far, (H, W))
         loss = self.loss(color, batch.target)
         loss.backward()
         return loss.detach()

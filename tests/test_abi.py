@@ -53,7 +53,7 @@ def test_load_without_gpu_and_error_channel():
     if not _lib.LIB_PATH.exists():
         pytest.skip("extension not built")
     lib = _lib.load()
-    assert lib.dsplat_abi_version() == 18
+    assert lib.dsplat_abi_version() == 20
     assert lib.dsr_sort_lds_capacity() >= 256
     # argument validation happens before any HIP call -> works on a GPU-less host
     rc = lib.dsr_render_fwd(0, 1, 8, 8, None, None, None, None, 0, None, None, None, None, None, None, None, None)
