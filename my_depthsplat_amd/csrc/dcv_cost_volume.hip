@@ -497,87 +497,86 @@ __global__ __launch_bounds__(256) void k_epi_init(int J, int H, int W, const flo
   if (i < nbs) s.bcount[(size_t)bj * nbs + i] = 0u;
 }
 
-// Runs of equal keys in a wave (lanes with the key of their left neighbour; consecutive pixels of
-// a row mostly share their line and bin): inclusive segmented scans of a count, a minimum and a
-// maximum, so only the run's last lane issues the global atomics. All 64 lanes must be active
-// (callers pass key 0xFFFFFFFF for lanes without an item).
-struct EpiRun {
-  uint32_t cnt, mn, mx;
-  int head;  // the run's first lane
-  bool tail;
-};
-__device__ __forceinline__ EpiRun epi_run(uint32_t key, uint32_t cnt, uint32_t mn, uint32_t mx) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t left = __shfl_up(key, 1, 64), right = __shfl_down(key, 1, 64);
-  const bool head = lane == 0 || left != key;
-  const int hd = (int)dsplat::wave_incl_max_dpp(head ? (uint32_t)lane : 0u);  // this run's first lane
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t c2 = __shfl_up(cnt, off, 64), n2 = __shfl_up(mn, off, 64), x2 = __shfl_up(mx, off, 64);
-    if (lane - off >= hd) {
-      cnt += c2;
-      mn = min(mn, n2);
-      mx = max(mx, x2);
-    }
-  }
-  return {cnt, mn, mx, hd, lane == 63 || right != key};
-}
+// The pixel passes run 1024-thread workgroups over kEpiPix = 4096 pixels (4 per thread, each
+// step coalesced) and combine their per-line / per-bin updates in LDS first: on the diagonal
+// epipolar lines of the config-D rig neighbouring pixels of a row lie on different lines, so
+// per-pixel (or per-wave-run) global atomics were the passes' cost (round-6 first version,
+// 256-pixel workgroups: 21 / 24 / 34 us for count / bin / scatter at 24 x 2 x 112 x 192).
+constexpr int kEpiPix = 4096;
 
-// grid (ceil(HW / 256), B * J), 256 threads: each pixel's line and sort key (where its middle
-// candidate lands, projected on the direction of its own near-to-far step, canonically oriented:
-// x > 0, or y > 0 on vertical lines, so the pixels of one target line, whose directions agree to
-// a fraction of a degree, order along it); per line the count and the key range.
-__global__ __launch_bounds__(256) void k_epi_count(int H, int W, int D, int depth_per_pixel,
-                                                   const float* __restrict__ depth, const float* __restrict__ geom,
-                                                   int J, EpiScratch s) {
-  const int bj = blockIdx.y, HW = H * W, b = bj / J;
-  const int p = blockIdx.x * 256 + threadIdx.x;
+// grid (ceil(HW / kEpiPix), B * J), 1024 threads, dynamic LDS 3 kEpiBuckets words: each pixel's
+// line and sort key (where its middle candidate lands, projected on the direction of its own
+// near-to-far step, canonically oriented: x > 0, or y > 0 on vertical lines, so the pixels of one
+// target line, whose directions agree to a fraction of a degree, order along it); per line the
+// count and the key range.
+__global__ __launch_bounds__(1024) void k_epi_count(int H, int W, int D, int depth_per_pixel,
+                                                    const float* __restrict__ depth, const float* __restrict__ geom,
+                                                    int J, EpiScratch s) {
+  extern __shared__ uint32_t epi_lds[];
+  uint32_t* l_cnt = epi_lds;
+  uint32_t* l_min = epi_lds + kEpiBuckets;
+  uint32_t* l_max = epi_lds + 2 * kEpiBuckets;
+  const int bj = blockIdx.y, HW = H * W, b = bj / J, tid = threadIdx.x;
   const EpiKey key = s.keys[bj];
+  const int nb = key.nb;
+  for (int l = tid; l < nb; l += 1024) {
+    l_cnt[l] = 0u;
+    l_min[l] = 0xFFFFFFFFu;
+    l_max[l] = 0u;
+  }
+  __syncthreads();
   const float* gm = geom + (size_t)bj * 12;
-  const bool valid = p < HW;
-  const int pc = valid ? p : 0;
   const float* dp = depth + (size_t)b * D * (depth_per_pixel ? HW : 1);
   const int dm = D / 2, d1 = D > 1 ? D - 1 : 0;
-  const float dmid = depth_per_pixel ? dp[(size_t)dm * HW + pc] : dp[dm];
-  const float dfar = depth_per_pixel ? dp[(size_t)d1 * HW + pc] : dp[d1];
-  const float px = (float)(pc % W), py = (float)(pc / W);
-  auto target = [&](float d, float& u, float& v) {
-    const float x = fmaf(fmaf(gm[0], px, fmaf(gm[1], py, gm[2])), d, gm[9]);
-    const float y = fmaf(fmaf(gm[3], px, fmaf(gm[4], py, gm[5])), d, gm[10]);
-    const float z = fmaxf(fmaf(fmaf(gm[6], px, fmaf(gm[7], py, gm[8])), d, gm[11]), 1e-3f);
-    u = x / z;
-    v = y / z;
-  };
-  float u0, v0, u1, v1;
-  target(dmid, u0, v0);
-  target(dfar, u1, v1);
-  float dx = u1 - u0, dy = v1 - v0;
-  const float l = sqrtf(dx * dx + dy * dy);
-  if (l > 1e-6f && l < 3.0e38f) {
-    dx /= l;
-    dy /= l;
-  } else {
-    dx = 1.f;
-    dy = 0.f;
-  }
-  if (dx < -1e-3f || (!(dx > 1e-3f) && dy < 0.f)) {
-    dx = -dx;
-    dy = -dy;
-  }
-  float kv = fmaf(u0, dx, v0 * dy);
-  kv = (kv == kv && fabsf(kv) < 1e30f) ? kv : 1e30f;  // NaN / inf: last
-  const uint32_t line = valid ? (uint32_t)epi_bucket(key, px, py) : 0xFFFFFFFFu;
-  const uint32_t ob = epi_obits(kv);
-  if (valid) {
+#pragma unroll
+  for (int k = 0; k < kEpiPix / 1024; ++k) {
+    const int p = blockIdx.x * kEpiPix + k * 1024 + tid;
+    if (p >= HW) break;
+    const float dmid = depth_per_pixel ? dp[(size_t)dm * HW + p] : dp[dm];
+    const float dfar = depth_per_pixel ? dp[(size_t)d1 * HW + p] : dp[d1];
+    const float px = (float)(p % W), py = (float)(p / W);
+    auto target = [&](float d, float& u, float& v) {
+      const float x = fmaf(fmaf(gm[0], px, fmaf(gm[1], py, gm[2])), d, gm[9]);
+      const float y = fmaf(fmaf(gm[3], px, fmaf(gm[4], py, gm[5])), d, gm[10]);
+      const float z = fmaxf(fmaf(fmaf(gm[6], px, fmaf(gm[7], py, gm[8])), d, gm[11]), 1e-3f);
+      u = x / z;
+      v = y / z;
+    };
+    float u0, v0, u1, v1;
+    target(dmid, u0, v0);
+    target(dfar, u1, v1);
+    float dx = u1 - u0, dy = v1 - v0;
+    const float l = sqrtf(dx * dx + dy * dy);
+    if (l > 1e-6f && l < 3.0e38f) {
+      dx /= l;
+      dy /= l;
+    } else {
+      dx = 1.f;
+      dy = 0.f;
+    }
+    if (dx < -1e-3f || (!(dx > 1e-3f) && dy < 0.f)) {
+      dx = -dx;
+      dy = -dy;
+    }
+    float kv = fmaf(u0, dx, v0 * dy);
+    kv = (kv == kv && fabsf(kv) < 1e30f) ? kv : 1e30f;  // NaN / inf: last
+    const uint32_t line = (uint32_t)epi_bucket(key, px, py);
+    const uint32_t ob = epi_obits(kv);
     s.pl[(size_t)bj * HW + p] = line;
     s.pkv[(size_t)bj * HW + p] = ob;
+    atomicAdd(&l_cnt[line], 1u);
+    atomicMin(&l_min[line], ob);
+    atomicMax(&l_max[line], ob);
   }
-  const EpiRun r = epi_run(line, valid ? 1u : 0u, ob, ob);
-  if (r.tail && valid) {
-    const size_t o = (size_t)bj * kEpiBuckets + line;
-    atomicAdd(&s.hist[o], r.cnt);
-    atomicMin(&s.lmin[o], r.mn);
-    atomicMax(&s.lmax[o], r.mx);
+  __syncthreads();
+  for (int l = tid; l < nb; l += 1024) {
+    const uint32_t c = l_cnt[l];
+    if (c) {
+      const size_t o = (size_t)bj * kEpiBuckets + l;
+      atomicAdd(&s.hist[o], c);
+      atomicMin(&s.lmin[o], l_min[l]);
+      atomicMax(&s.lmax[o], l_max[l]);
+    }
   }
 }
 
@@ -628,24 +627,32 @@ __global__ __launch_bounds__(1024) void k_epi_segs(EpiScratch s) {
   epi_block_scan(kEpiBuckets, [&](int k) { return (hist[k] + 15u) / 16u; }, s.bst + o, nullptr, wsum);
 }
 
-// grid (ceil(HW / 256), B * J): each pixel's segment bin (its line's key range cut into
-// ceil(n / 16) equal parts); per bin the count.
-__global__ __launch_bounds__(256) void k_epi_bin(int HW, EpiScratch s) {
-  const int bj = blockIdx.y, p = blockIdx.x * 256 + threadIdx.x;
-  const bool valid = p < HW;
-  uint32_t bin = 0xFFFFFFFFu;
-  if (valid) {
+// grid (ceil(HW / kEpiPix), B * J), 1024 threads, dynamic LDS epi_bin_stride(HW) words: each
+// pixel's segment bin (its line's key range cut into ceil(n / 16) equal parts); per bin the count.
+__global__ __launch_bounds__(1024) void k_epi_bin(int HW, EpiScratch s) {
+  extern __shared__ uint32_t epi_lds[];
+  const int bj = blockIdx.y, tid = threadIdx.x, nbs = epi_bin_stride(HW);
+  for (int i = tid; i < nbs; i += 1024) epi_lds[i] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kEpiPix / 1024; ++k) {
+    const int p = blockIdx.x * kEpiPix + k * 1024 + tid;
+    if (p >= HW) break;
     const int l = (int)s.pl[(size_t)bj * HW + p];
     const size_t o = (size_t)bj * kEpiBuckets + l;
     const uint32_t nseg = (s.hist[o] + 15u) / 16u;
     const float lo = epi_ofloat(s.lmin[o]), hi = epi_ofloat(s.lmax[o]);
     const float kv = epi_ofloat(s.pkv[(size_t)bj * HW + p]);
     const float f = hi > lo ? (kv - lo) / (hi - lo) : 0.f;
-    bin = s.bst[o] + (uint32_t)min((int)nseg - 1, max(0, (int)(f * (float)nseg)));
+    const uint32_t bin = s.bst[o] + (uint32_t)min((int)nseg - 1, max(0, (int)(f * (float)nseg)));
     s.pl[(size_t)bj * HW + p] = bin;
+    atomicAdd(&epi_lds[bin], 1u);
   }
-  const EpiRun r = epi_run(bin, valid ? 1u : 0u, 0u, 0u);
-  if (r.tail && valid) atomicAdd(&s.bcount[(size_t)bj * epi_bin_stride(HW) + bin], r.cnt);
+  __syncthreads();
+  for (int i = tid; i < nbs; i += 1024) {
+    const uint32_t c = epi_lds[i];
+    if (c) atomicAdd(&s.bcount[(size_t)bj * nbs + i], c);
+  }
 }
 
 // grid B * J, 1024 threads: bin starts (bstart; bcount becomes the scatter's cursor).
@@ -657,21 +664,33 @@ __global__ __launch_bounds__(1024) void k_epi_binscan(int HW, EpiScratch s) {
   epi_block_scan(nbs, [&](int k) { return bc[k]; }, s.bstart + o, bc, wsum);
 }
 
-// grid (ceil(HW / 256), B * J): every pixel into its bin, in arrival order (one returning atomic
-// per wave run of equal bins).
-__global__ __launch_bounds__(256) void k_epi_scatter(int HW, EpiScratch s) {
-  const int bj = blockIdx.y, p = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63;
-  const bool valid = p < HW;
-  const uint32_t bin = valid ? s.pl[(size_t)bj * HW + p] : 0xFFFFFFFFu;
-  const EpiRun r = epi_run(bin, valid ? 1u : 0u, 0u, 0u);
-  uint32_t base = 0;
-  if (r.tail && valid) base = atomicAdd(&s.bcount[(size_t)bj * epi_bin_stride(HW) + bin], r.cnt);
-  // the run's base from its tail lane: lanes of a run are contiguous, the tail is the run's last
-  const int hd = r.head;
-  const uint64_t tails = __ballot(r.tail);
-  const int tl = hd + __builtin_ctzll(tails >> hd);  // first tail at or after the head
-  base = __shfl(base, tl, 64);
-  if (valid) s.stage[(size_t)bj * HW + base + (uint32_t)(lane - hd)] = p;
+// grid (ceil(HW / kEpiPix), B * J), 1024 threads, dynamic LDS epi_bin_stride(HW) words: every
+// pixel into its bin, in arrival order: local ranks from LDS counters, then one global
+// reservation per (workgroup, bin).
+__global__ __launch_bounds__(1024) void k_epi_scatter(int HW, EpiScratch s) {
+  extern __shared__ uint32_t epi_lds[];
+  const int bj = blockIdx.y, tid = threadIdx.x, nbs = epi_bin_stride(HW);
+  for (int i = tid; i < nbs; i += 1024) epi_lds[i] = 0u;
+  __syncthreads();
+  uint32_t bin[kEpiPix / 1024], rank[kEpiPix / 1024];
+#pragma unroll
+  for (int k = 0; k < kEpiPix / 1024; ++k) {
+    const int p = blockIdx.x * kEpiPix + k * 1024 + tid;
+    bin[k] = p < HW ? s.pl[(size_t)bj * HW + p] : 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (int k = 0; k < kEpiPix / 1024; ++k)
+    if (bin[k] != 0xFFFFFFFFu) rank[k] = atomicAdd(&epi_lds[bin[k]], 1u);
+  __syncthreads();
+  for (int i = tid; i < nbs; i += 1024) {  // count -> this workgroup's base in the bin
+    const uint32_t c = epi_lds[i];
+    if (c) epi_lds[i] = atomicAdd(&s.bcount[(size_t)bj * nbs + i], c);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kEpiPix / 1024; ++k)
+    if (bin[k] != 0xFFFFFFFFu)
+      s.stage[(size_t)bj * HW + epi_lds[bin[k]] + rank[k]] = blockIdx.x * kEpiPix + k * 1024 + tid;
 }
 
 // grid (ceil(HW / 256), B * J): output position -> the pixel of that rank (by id) in its bin.
@@ -1836,7 +1855,8 @@ static BwdShape bwd_shape(int B, int H, int W, int D, int depth_per_pixel) {
 static bool epi_path(int C, int H, int W, bool bwd) {
   (void)bwd;  // (both directions fit the widest group's layout)
   return C % 16 == 0 && C <= 128 && epi_lds_bytes_wide(6, 8, C, H, W) <= 160 * 1024 &&
-         epi_lds_bytes_wide(5, 8, C, H, W) <= 160 * 1024;
+         epi_lds_bytes_wide(5, 8, C, H, W) <= 160 * 1024 &&
+         (size_t)epi_bin_stride(H * W) * sizeof(uint32_t) <= 160 * 1024;  // grouping's LDS bin counters
 }
 
 // Small grids take the band kernel for the forward: one launch with no channel-last copies
@@ -1860,15 +1880,22 @@ static int epi_group(int B, int J, int H, int W, int D, int depth_per_pixel, con
   const EpiScratch sc = epi_scratch(geom + (size_t)BJ * 12, BJ, HW);
   k_epi_init<<<dim3((std::max(kEpiBuckets, nbs) + 255) / 256, BJ), 256, 0, st>>>(J, H, W, intr, pose, geom, sc);
   if (int e = dsplat::check_launch("k_epi_init")) return e;
-  k_epi_count<<<dim3(pg, BJ), 256, 0, st>>>(H, W, D, depth_per_pixel, depth, geom, J, sc);
+  const int pb = (HW + kEpiPix - 1) / kEpiPix;
+  const size_t lds_count = 3 * kEpiBuckets * sizeof(uint32_t), lds_bins = (size_t)nbs * sizeof(uint32_t);
+  DSPLAT_REQUIRE(lds_bins <= 160 * 1024, "cost volume: %d pixels exceed the grouping's LDS bin counters", HW);
+  if (int e = dsplat::ensure_dyn_lds((const void*)k_epi_count, lds_count, "hipFuncSetAttribute(k_epi_count)")) return e;
+  if (int e = dsplat::ensure_dyn_lds((const void*)k_epi_bin, lds_bins, "hipFuncSetAttribute(k_epi_bin)")) return e;
+  if (int e = dsplat::ensure_dyn_lds((const void*)k_epi_scatter, lds_bins, "hipFuncSetAttribute(k_epi_scatter)"))
+    return e;
+  k_epi_count<<<dim3(pb, BJ), 1024, lds_count, st>>>(H, W, D, depth_per_pixel, depth, geom, J, sc);
   if (int e = dsplat::check_launch("k_epi_count")) return e;
   k_epi_segs<<<BJ, 1024, 0, st>>>(sc);
   if (int e = dsplat::check_launch("k_epi_segs")) return e;
-  k_epi_bin<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc);
+  k_epi_bin<<<dim3(pb, BJ), 1024, lds_bins, st>>>(HW, sc);
   if (int e = dsplat::check_launch("k_epi_bin")) return e;
   k_epi_binscan<<<BJ, 1024, 0, st>>>(HW, sc);
   if (int e = dsplat::check_launch("k_epi_binscan")) return e;
-  k_epi_scatter<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc);
+  k_epi_scatter<<<dim3(pb, BJ), 1024, lds_bins, st>>>(HW, sc);
   if (int e = dsplat::check_launch("k_epi_scatter")) return e;
   k_epi_rank<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc, groups);
   return dsplat::check_launch("k_epi_rank");

@@ -288,6 +288,9 @@ BOUNDED_TRAIN_SEGMENTS = True
 # copy and the key stores; the product never sets it.
 DEBUG_KEEP_FAST_LISTS = False
 SEG_ENDS = 0xFFFFFFFF  # DSR_SEG_ENDS
+# Depth cut: queue the scatter before the N read-back, into keys sized from the previous call
+# (round 6; DSPLAT_EARLY_CUT_SCATTER=0 restores the synchronous order for A/B timing)
+EARLY_CUT_SCATTER = os.environ.get("DSPLAT_EARLY_CUT_SCATTER", "1") != "0"
 _HIST_LDS_MAX = 32768  # tiles per view binned in k_project_emit's LDS histogram (kHistLdsMax)
 
 
@@ -802,7 +805,7 @@ def forward_raw(means, feats, use_sh, sh_degree, opacities, cov6, cams, V, H, W,
             proj = (S, G, V, H, W, deg, M, means.data_ptr(), shs_p, col_p, opacities.data_ptr(), cov6.data_ptr(),
                     cams.data_ptr())
             prev_n = spec.get("two_phase_n")
-            if prev_n:
+            if prev_n and EARLY_CUT_SCATTER:
                 # round 6: the scatter (and its survivor projection) queued BEFORE the read-back,
                 # into keys sized from the previous call's N: the device runs it while the host
                 # waits, instead of idling from the cut thresholds to the host's next launch. The

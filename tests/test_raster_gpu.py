@@ -470,6 +470,33 @@ def test_depth_cut_matches_full_scatter(gpu, opacity, monkeypatch):
         o.close()
 
 
+@pytest.mark.parametrize("case", ["too_small", "fits", "short_lists"])
+def test_depth_cut_early_scatter(gpu, case, monkeypatch):
+    """Round 6: the depth-cut scatter is queued before the host reads N, into keys sized from the
+    previous call's N (hint two_phase_n). too_small: the buffer cannot hold N, the queued launch
+    does nothing and the pass is re-run at the exact size; fits: the queued pass is the pass;
+    short_lists: the cut was planned (long lists last call) but this call's lists are short, so
+    the queued pass ran and its cursors / survivor counters are rewound before the full scatter.
+    Every case: forward and gradients bit-identical to the synchronous order (no hint)."""
+    from my_depthsplat_amd import raster
+    monkeypatch.setattr(raster, "KEY_BUDGET_BYTES", 0)
+    monkeypatch.setattr(raster, "SORT_PREFIX", 0)
+    monkeypatch.setattr(raster, "CUT_PREFIX", 1 << 20 if case == "short_lists" else 1024)
+    sc = _large_tile_scene(opacity_scale=1.0)
+    st = settings_for(sc)
+    hints = raster.default_context(gpu).hints
+    out = {}
+    for mode in ("sync", case):
+        monkeypatch.setitem(hints, "two_phase_max", 1 << 30 if case == "short_lists" else None)
+        monkeypatch.setitem(hints, "two_phase_n",
+                            {"sync": None, "too_small": 1, "fits": 1 << 26, "short_lists": 1 << 26}[mode])
+        state, res = _forward_backward(sc, st, gpu)
+        out[mode] = (state.seg_stride, res)
+    assert out["sync"][0] == out[case][0] == (0 if case == "short_lists" else raster.SEG_ENDS)
+    for a, b in zip(out["sync"][1], out[case][1]):
+        assert torch.equal(a, b)
+
+
 def test_depth_cut_multiview_scene_vs_oracle(gpu, monkeypatch):
     """A scaled-down 6-view scene (6 x 128x224 context -> G = 172K, ~5K entries per tile):
     the two-phase path with the depth cut writes a fraction of the entries, and the images,
