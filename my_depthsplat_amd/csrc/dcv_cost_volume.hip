@@ -1186,11 +1186,13 @@ __global__ __launch_bounds__(256, PXB == 4 ? 4 : 2) void k_cost_epi(int B, int j
 //     the per-block maxima of k_cv_absmax, the same in every workgroup), added as int64: 2^23
 //     partials of the bound fit. k_fx_to_chw converts the sum back to float while transposing.
 // dref needs none of this: each element has one writer (its pixel's group, views in launch order).
+// 256 workgroups of 1024 threads (16 waves per CU: the pass reads dcost and ref at HBM rate;
+// 256 threads per workgroup ran at ~3.5 TB/s, 57 us at config D scale 1)
 constexpr int kCvMaxBlocks = 256;
-__global__ __launch_bounds__(256) void k_cv_absmax(size_t n1, const float* __restrict__ a1, size_t n2,
+__global__ __launch_bounds__(1024) void k_cv_absmax(size_t n1, const float* __restrict__ a1, size_t n2,
                                                    const float* __restrict__ a2, float* __restrict__ out) {
   float m1 = 0.f, m2 = 0.f;
-  const size_t stride = (size_t)256 * gridDim.x, i0 = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t stride = (size_t)1024 * gridDim.x, i0 = (size_t)blockIdx.x * 1024 + threadIdx.x;
   // 16-byte loads, 4 in flight per thread, then the scalar tail (an unaligned array: all scalar)
   auto vmax = [&](size_t n, const float* __restrict__ a, float& m) {
     const float4* a4 = reinterpret_cast<const float4*>(a);
@@ -1217,15 +1219,21 @@ __global__ __launch_bounds__(256) void k_cv_absmax(size_t n1, const float* __res
     m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
     m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
   }
-  __shared__ float s1[4], s2[4];
+  __shared__ float s1[16], s2[16];
   if ((threadIdx.x & 63) == 0) {
     s1[threadIdx.x >> 6] = m1;
     s2[threadIdx.x >> 6] = m2;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    out[blockIdx.x] = fmaxf(fmaxf(s1[0], s1[1]), fmaxf(s1[2], s1[3]));
-    out[kCvMaxBlocks + blockIdx.x] = fmaxf(fmaxf(s2[0], s2[1]), fmaxf(s2[2], s2[3]));
+    float a = 0.f, c = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      a = fmaxf(a, s1[k]);
+      c = fmaxf(c, s2[k]);
+    }
+    out[blockIdx.x] = a;
+    out[kCvMaxBlocks + blockIdx.x] = c;
   }
 }
 // The dtgt unit from the per-block maxima (every caller reads the same values). One partial is
@@ -1475,6 +1483,70 @@ __global__ __launch_bounds__(256) void k_fx_to_chw(int C, int HW, int rows, cons
     const int c = c0 + r, p = p0 + tx;
     if (c < C && p < HW) d[(size_t)c * HW + p] = tile[tx][r];
   }
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// k_fx_to_chw with 16-byte accesses (C % 4 == 0, HW % 4 == 0, 16-byte aligned arrays): each
+// thread reads 4 consecutive channels of one pixel (2 x 16 B of int64, + 16 B of add) and
+// writes 4 consecutive pixels of one channel (the 4-byte form moved ~4.7 TB/s).
+__global__ __launch_bounds__(256) void k_fx_to_chw4(int C, int HW, int rows, const long long* __restrict__ src,
+                                                    const float* __restrict__ cvmax, float scale, int lgps,
+                                                    const float* __restrict__ add, float* __restrict__ dst) {
+  __shared__ float tile[64][65];
+  const float unit = cv_dtgt_unit(cvmax, scale, lgps);
+  const bool ok = unit > 0.f;
+  const int bj = blockIdx.z;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const long long* s = src + (size_t)bj * rows * C;
+  float* d = dst + (size_t)bj * C * HW;
+  const int q = threadIdx.x & 15, rr = threadIdx.x >> 4;
+  auto cvt = [&](long long v) {
+    return ok ? fmaf((float)(int)(v >> 32) * unit, 4294967296.0f, (float)(unsigned)(v & 0xffffffffll) * unit)
+              : __builtin_nanf("");
+  };
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = p0 + rr + 16 * k, c = c0 + 4 * q;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p < HW && c < C) {
+      const longlong2* sp = reinterpret_cast<const longlong2*>(s + (size_t)p * C + c);
+      const longlong2 a01 = sp[0], a23 = sp[1];
+      v = make_float4(cvt(a01.x), cvt(a01.y), cvt(a23.x), cvt(a23.y));
+      if (add) {
+        const float4 w = *reinterpret_cast<const float4*>(add + ((size_t)bj * HW + p) * C + c);
+        v.x += w.x;
+        v.y += w.y;
+        v.z += w.z;
+        v.w += w.w;
+      }
+    }
+    float* t = &tile[rr + 16 * k][4 * q];  // tile[p - p0][c - c0]
+    t[0] = v.x;
+    t[1] = v.y;
+    t[2] = v.z;
+    t[3] = v.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = c0 + rr + 16 * k, p = p0 + 4 * q;
+    if (c < C && p < HW)
+      *reinterpret_cast<float4*>(d + (size_t)c * HW + p) =
+          make_float4(tile[4 * q][rr + 16 * k], tile[4 * q + 1][rr + 16 * k], tile[4 * q + 2][rr + 16 * k],
+                      tile[4 * q + 3][rr + 16 * k]);
+  }
+}
+
+// [n][rows][C] int64 -> [n][C][HW] float (+ add): the 16-byte form where the shape allows
+static int fx_to_chw(int n, int C, int HW, const long long* src, const float* cvmax, float scale, int lgps,
+                     const float* add, float* dst, hipStream_t st) {
+  const dim3 grid((HW + 63) / 64, (C + 63) / 64, n);
+  if (C % 4 == 0 && HW % 4 == 0 && aligned16(src) && aligned16(dst) && (!add || aligned16(add)))
+    k_fx_to_chw4<<<grid, 256, 0, st>>>(C, HW, HW + 1, src, cvmax, scale, lgps, add, dst);
+  else
+    k_fx_to_chw<<<grid, 256, 0, st>>>(C, HW, HW + 1, src, cvmax, scale, lgps, add, dst);
+  return dsplat::check_launch("k_fx_to_chw");
 }
 
 // ---- forward on the matrix cores, band form (small grids: configs A / B) ---------------
@@ -1870,7 +1942,6 @@ static bool epi_path(int C, int H, int W, bool bwd) {
 constexpr long kBandMaxPixels = 32768;  // B * H * W
 static bool band_ok(int C) { return C == 16 || C == 32 || C == 64 || C == 128; }
 
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // The epipolar grouping passes (k_epi_init .. k_epi_rank) of B x J (reference, source view)
 // pairs into groups [B J][HW] and geom [B J][12], scratch after geom.
@@ -1971,7 +2042,7 @@ static int epi_bwd_launch(int B, int J, int C, int H, int W, int D, int depth_pe
                           hipStream_t st) {
   const int HW = H * W;
   const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-  k_cv_absmax<<<kCvMaxBlocks, 256, 0, st>>>((size_t)B * D * HW, dcost, (size_t)B * C * HW, ref_for_max, cvmax);
+  k_cv_absmax<<<kCvMaxBlocks, 1024, 0, st>>>((size_t)B * D * HW, dcost, (size_t)B * C * HW, ref_for_max, cvmax);
   if (int e = dsplat::check_launch("k_cv_absmax")) return e;
   const BwdShape bs = bwd_shape(B, H, W, D, depth_per_pixel);
   const size_t lds = epi_lds_bytes_wide(bs.pxb, bs.spt, C, H, W);
@@ -2108,9 +2179,7 @@ int dcv_cost_volume_bwd(int B, int J, int C, int H, int W, int D, int depth_per_
         dim3((HW + 63) / 64, (C + 63) / 64, B), 256, 0, st>>>(C, HW, HW, dref_hwc, dref);
     if (int e = dsplat::check_launch("k_to_chw(dref)")) return e;
     const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-    k_fx_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, dtgt_fx, cvmax, scale,
-                                                                          lgps, nullptr, dtgt);
-    return dsplat::check_launch("k_fx_to_chw");
+    return fx_to_chw(B * J, C, HW, dtgt_fx, cvmax, scale, lgps, nullptr, dtgt, st);
   }
   float* dtgt_hwc = reinterpret_cast<float*>(dtgt_fx);
   k_cost_bwd<<<dim3((HW + 3) / 4, B), 256, 0, st>>>(J, C, H, W, D, depth_per_pixel, ref, tgt_hwc, intr, pose,
@@ -2193,9 +2262,7 @@ int dcv_cost_volume_views_bwd(int BV, int J, int C, int H, int W, int D, int dep
                              clamp_min_depth, dcost, cvmax, dref_hwc, dfx, &lgps, st))
     return e;
   const float scale = 1.0f / (sqrtf((float)C) * (float)J);
-  k_fx_to_chw<<<dim3((HW + 63) / 64, (C + 63) / 64, BV), 256, 0, st>>>(C, HW, HW + 1, dfx, cvmax, scale, lgps,
-                                                                      dref_hwc, dfeatures);
-  return dsplat::check_launch("k_fx_to_chw(dfeatures)");
+  return fx_to_chw(BV, C, HW, dfx, cvmax, scale, lgps, dref_hwc, dfeatures, st);
 }
 
 int dcv_warp_fwd(int B, int C, int H, int W, int D, const float* feature, const float* intr, const float* pose,
