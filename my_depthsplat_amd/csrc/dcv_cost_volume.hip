@@ -1002,12 +1002,20 @@ __device__ __forceinline__ int epi_rank(const EpiLds& L, int e) {
 // list), the target rows' loads and the barriers are then paid once per 2^PXB pixels; the
 // GEMM covers the union band.
 constexpr int kEGWMax = 64;             // widest group
-// Band positions per GEMM pass (the [2^PXB][band + 1] LDS tile). 128 for the widest groups
-// and for the per-pixel-candidate shapes (SPT = 2: short bands; the smaller tile lets 6
+// Band positions per GEMM pass (the [2^PXB][band + 1] LDS tile). Forward (16-pixel groups):
+// 128 for the per-pixel-candidate shapes (SPT = 2: short bands; the smaller tile lets 6
 // instead of 4 workgroups share a CU: config D scale 1 forward 0.852 -> 0.761 ms, same box,
 // profiles/r05t_ab_cv_pass128.log), 256 otherwise (per-image candidates: long bands, a second
-// pass cost more there: scale 0 0.436 -> 0.474 ms at 128).
-__host__ __device__ constexpr int epi_pass(int pxb, int spt) { return (pxb == 6 || spt == 2) ? 128 : 256; }
+// pass cost more there: scale 0 0.436 -> 0.474 ms at 128). Backward (round 6): the backward is
+// latency-bound (MFMA busy 0.22, more wait than issue cycles), so the tile is sized for
+// occupancy: 64 positions at 64-pixel groups (3 workgroups per CU instead of 2), 128 at 32 (4
+// instead of 2): config D fwd + bwd scale 1 2.50 -> 2.27 ms, scale 0 2.01 -> 1.97 ms (same box,
+// profiles/r06s_ab_cv_bwd_occupancy.log); 32 / 64 (4 / 5 per CU) lost (r06t: 2.37 / 2.14).
+__host__ __device__ constexpr int epi_pass(int pxb, int spt) {
+  return pxb == 6 ? 64 : pxb == 5 ? 128 : spt == 2 ? 128 : 256;
+}
+// workgroups per CU the backward's LDS allows (launch bounds: the VGPR budget to match)
+__host__ __device__ constexpr int bwd_occ(int pxb) { return pxb == 4 ? 3 : pxb == 6 ? 3 : 4; }
 template <int PXB, int SPT>
 constexpr int bwd_band() { return epi_pass(PXB, SPT); }
 static_assert(epi_pass(4, 8) <= kEUMax && epi_pass(6, 8) <= kEUMax, "the band list holds a pass");
@@ -1282,7 +1290,7 @@ __device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, floa
 // dref_hwc [B][HW][C] is written (view 0) or added to (views after it, in launch order): each
 // pixel is in exactly one group per view. cvmax: k_cv_absmax's per-block maxima (dcost, ref).
 template <int NK, int PXB, int SPT>
-__global__ __launch_bounds__(256, PXB == 4 ? 3 : 2) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
+__global__ __launch_bounds__(256, bwd_occ(PXB)) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
                                                       int accumulate, const float* __restrict__ ref_hwc,
                                                       const float* __restrict__ tgt_hwc, const int* __restrict__ tmap,
                                                       const int* __restrict__ groups, const float* __restrict__ geom,
