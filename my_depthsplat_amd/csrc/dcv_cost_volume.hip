@@ -528,12 +528,19 @@ __global__ __launch_bounds__(1024) void k_epi_count(int H, int W, int D, int dep
   const float* gm = geom + (size_t)bj * 12;
   const float* dp = depth + (size_t)b * D * (depth_per_pixel ? HW : 1);
   const int dm = D / 2, d1 = D > 1 ? D - 1 : 0;
+  constexpr int PPT = kEpiPix / 1024;
+  float dmids[PPT], dfars[PPT];  // every pixel's two depth loads in flight together
 #pragma unroll
-  for (int k = 0; k < kEpiPix / 1024; ++k) {
+  for (int k = 0; k < PPT; ++k) {
+    const int p = min(blockIdx.x * kEpiPix + k * 1024 + tid, HW - 1);
+    dmids[k] = depth_per_pixel ? dp[(size_t)dm * HW + p] : dp[dm];
+    dfars[k] = depth_per_pixel ? dp[(size_t)d1 * HW + p] : dp[d1];
+  }
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
     const int p = blockIdx.x * kEpiPix + k * 1024 + tid;
     if (p >= HW) break;
-    const float dmid = depth_per_pixel ? dp[(size_t)dm * HW + p] : dp[dm];
-    const float dfar = depth_per_pixel ? dp[(size_t)d1 * HW + p] : dp[d1];
+    const float dmid = dmids[k], dfar = dfars[k];
     const float px = (float)(p % W), py = (float)(p / W);
     auto target = [&](float d, float& u, float& v) {
       const float x = fmaf(fmaf(gm[0], px, fmaf(gm[1], py, gm[2])), d, gm[9]);
@@ -661,7 +668,11 @@ __global__ __launch_bounds__(1024) void k_epi_binscan(int HW, EpiScratch s) {
   const int nbs = epi_bin_stride(HW);
   const size_t o = (size_t)blockIdx.x * nbs;
   uint32_t* bc = s.bcount + o;
-  epi_block_scan(nbs, [&](int k) { return bc[k]; }, s.bstart + o, bc, wsum);
+  // the image's bins end where its last line's segments end; bstart of that end is read too
+  const int nb = s.keys[blockIdx.x].nb;
+  const size_t ol = (size_t)blockIdx.x * kEpiBuckets + (nb - 1);
+  const int nbins = nb > 0 ? (int)(s.bst[ol] + (s.hist[ol] + 15u) / 16u) : 0;
+  epi_block_scan(min(nbins + 1, nbs), [&](int k) { return bc[k]; }, s.bstart + o, bc, wsum);
 }
 
 // grid (ceil(HW / kEpiPix), B * J), 1024 threads, dynamic LDS epi_bin_stride(HW) words: every

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Cost-volume tests (main library), then a same-box A/B of the cost-volume leg: main vs
 # lib/variants/libdsplat_NAME.so, 3 rounds.
-# usage: bash tools/r06_abcv.sh TAG NAME
+# usage: bash tools/r06_abcv.sh TAG NAME...
 set -u
-tag=${1:?tag}; var=${2:?variant}
+tag=${1:?tag}; shift; vars="$*"
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_cost_volume.py -x -q --timeout 120 --timeout-method thread -m gpu \
   > gpurun_out/abcvtest_$tag.log 2>&1
@@ -11,7 +11,7 @@ rc=$?
 tail -2 gpurun_out/abcvtest_$tag.log
 if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" gpurun_out/abcvtest_$tag.log | head -20; exit $rc; fi
 for r in 1 2 3; do
-  for n in main $var; do
+  for n in main $vars; do
     lib=""; [ "$n" != main ] && lib=my_depthsplat_amd/lib/variants/libdsplat_$n.so
     DSPLAT_LIB=$lib timeout -k 10 300 python3 bench.py --skip-headline --no-cpu-baseline --extra costvol --detail= \
       > gpurun_out/abcv_${tag}_${n}_$r.log 2>&1 || { echo "$n failed"; tail -3 gpurun_out/abcv_${tag}_${n}_$r.log; exit 1; }
