@@ -124,21 +124,28 @@ __global__ __launch_bounds__(256) void k_to_hwc(int C, int HW, int rows, const f
 // consecutive pixels of one channel and writes 4 consecutive channels of one pixel (the
 // 4-byte version moved ~4.2 TB/s at config D's 24 x 2 x 128 x 5376 floats).
 // Two copies in one launch: planes z < nz1 from (src, dst), the rest from (src2, dst2).
-__global__ __launch_bounds__(256) void k_to_hwc4(int C, int HW, int rows, const float* __restrict__ src,
-                                                 float* __restrict__ dst, int nz1, const float* __restrict__ src2,
-                                                 float* __restrict__ dst2) {
-  __shared__ float tile[64][65];
-  int bj = blockIdx.z;
-  if (bj >= nz1) {
-    bj -= nz1;
-    src = src2;
-    dst = dst2;
+struct HwcJob {
+  int C, HW, rows, nz1;
+  const float* src;
+  float* dst;
+  const float* src2;
+  float* dst2;
+};
+__device__ __forceinline__ void hwc4_tile(const HwcJob& jb, int bx, int by, int bz, float (*tile)[65]) {
+  const int C = jb.C, HW = jb.HW;
+  const float* src = jb.src;
+  float* dst = jb.dst;
+  int bj = bz;
+  if (bj >= jb.nz1) {
+    bj -= jb.nz1;
+    src = jb.src2;
+    dst = jb.dst2;
   }
-  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int p0 = bx * 64, c0 = by * 64;
   const float* s = src + (size_t)bj * C * HW;
-  float* d = dst + (size_t)bj * rows * C;
-  if (blockIdx.x == 0 && (int)threadIdx.x < 64 && c0 + (int)threadIdx.x < C)
-    for (int p = HW; p < rows; ++p) d[(size_t)p * C + c0 + threadIdx.x] = 0.f;
+  float* d = dst + (size_t)bj * jb.rows * C;
+  if (bx == 0 && (int)threadIdx.x < 64 && c0 + (int)threadIdx.x < C)
+    for (int p = HW; p < jb.rows; ++p) d[(size_t)p * C + c0 + threadIdx.x] = 0.f;
   const int q = threadIdx.x & 15, rr = threadIdx.x >> 4;  // 16 float4 per 64-float run, 16 runs per pass
   float4 v[4];
 #pragma unroll
@@ -163,6 +170,13 @@ __global__ __launch_bounds__(256) void k_to_hwc4(int C, int HW, int rows, const 
           make_float4(tile[4 * q][rr + 16 * k], tile[4 * q + 1][rr + 16 * k], tile[4 * q + 2][rr + 16 * k],
                       tile[4 * q + 3][rr + 16 * k]);
   }
+}
+__global__ __launch_bounds__(256) void k_to_hwc4(HwcJob jb) {
+  __shared__ float tile[64][65];
+  hwc4_tile(jb, blockIdx.x, blockIdx.y, blockIdx.z, tile);
+}
+__host__ __device__ inline int hwc4_blocks(const HwcJob& jb, int nz) {
+  return ((jb.HW + 63) / 64) * ((jb.C + 63) / 64) * nz;
 }
 
 // [n][rows][C] (the first HW rows) -> [n][C][HW]
@@ -705,8 +719,7 @@ __global__ __launch_bounds__(1024) void k_epi_scatter(int HW, EpiScratch s) {
 }
 
 // grid (ceil(HW / 256), B * J): output position -> the pixel of that rank (by id) in its bin.
-__global__ __launch_bounds__(256) void k_epi_rank(int HW, EpiScratch s, int* __restrict__ groups) {
-  const int bj = blockIdx.y, pos = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void epi_rank_one(int HW, const EpiScratch& s, int* __restrict__ groups, int bj, int pos) {
   if (pos >= HW) return;
   const int* st = s.stage + (size_t)bj * HW;
   const int p = st[pos];
@@ -716,6 +729,26 @@ __global__ __launch_bounds__(256) void k_epi_rank(int HW, EpiScratch s, int* __r
   int r = 0;
   for (int q = b0; q < b1; ++q) r += st[q] < p ? 1 : 0;
   groups[(size_t)bj * HW + b0 + r] = p;
+}
+__global__ __launch_bounds__(256) void k_epi_rank(int HW, EpiScratch s, int* __restrict__ groups) {
+  epi_rank_one(HW, s, groups, blockIdx.y, blockIdx.x * 256 + threadIdx.x);
+}
+
+// k_epi_rank with the forward's channel-last copies (hwc4_tile) as extra workgroups after its
+// own (round 6): the copy is HBM-bound and the rank pass latency-bound, so the two overlap
+// instead of running back to back. Workgroups [0, pg BJ) rank, the rest copy tiles.
+__global__ __launch_bounds__(256) void k_epi_rank_hwc(int HW, EpiScratch s, int* __restrict__ groups, int pg, int BJ,
+                                                      HwcJob jb) {
+  __shared__ float tile[64][65];
+  const int nrank = pg * BJ;
+  if ((int)blockIdx.x < nrank) {
+    const int bj = blockIdx.x / pg, pos = (blockIdx.x - bj * pg) * 256 + threadIdx.x;
+    epi_rank_one(HW, s, groups, bj, pos);
+    return;
+  }
+  const int t = blockIdx.x - nrank, nx = (jb.HW + 63) / 64, ny = (jb.C + 63) / 64;
+  const int bz = t / (nx * ny), r = t - bz * nx * ny, by = r / nx, bx = r - by * nx;
+  hwc4_tile(jb, bx, by, bz, tile);
 }
 
 // The target image of (b, j): its own copy, or view tmap[bj] of the per-view copy (views mode;
@@ -1965,7 +1998,8 @@ static bool band_ok(int C) { return C == 16 || C == 32 || C == 64 || C == 128; }
 // The epipolar grouping passes (k_epi_init .. k_epi_rank) of B x J (reference, source view)
 // pairs into groups [B J][HW] and geom [B J][12], scratch after geom.
 static int epi_group(int B, int J, int H, int W, int D, int depth_per_pixel, const float* intr, const float* pose,
-                     const float* depth, int* groups, float* geom, hipStream_t st) {
+                     const float* depth, int* groups, float* geom, hipStream_t st, const HwcJob* hwc = nullptr,
+                     int hwc_planes = 0) {
   const int HW = H * W, BJ = B * J, nbs = epi_bin_stride(HW), pg = (HW + 255) / 256;
   const EpiScratch sc = epi_scratch(geom + (size_t)BJ * 12, BJ, HW);
   k_epi_init<<<dim3((std::max(kEpiBuckets, nbs) + 255) / 256, BJ), 256, 0, st>>>(J, H, W, intr, pose, geom, sc);
@@ -1987,6 +2021,11 @@ static int epi_group(int B, int J, int H, int W, int D, int depth_per_pixel, con
   if (int e = dsplat::check_launch("k_epi_binscan")) return e;
   k_epi_scatter<<<dim3(pb, BJ), 1024, lds_bins, st>>>(HW, sc);
   if (int e = dsplat::check_launch("k_epi_scatter")) return e;
+  if (hwc) {  // the channel-last copies as extra workgroups of the last grouping launch
+    const unsigned nblk = (unsigned)pg * BJ + (unsigned)hwc4_blocks(*hwc, hwc_planes);
+    k_epi_rank_hwc<<<nblk, 256, 0, st>>>(HW, sc, groups, pg, BJ, *hwc);
+    return dsplat::check_launch("k_epi_rank_hwc");
+  }
   k_epi_rank<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc, groups);
   return dsplat::check_launch("k_epi_rank");
 }
@@ -2006,8 +2045,10 @@ static int epi_setup(int B, int J, int C, int H, int W, int D, int depth_per_pix
   const bool v4 = C % 4 == 0 && HW % 4 == 0 && aligned16(tgt) && aligned16(ref) && aligned16(workspace);
   const bool epi = epi_path(C, H, W, false);
   if (v4) {  // tgt (and, for the epipolar kernels, ref) in one launch
-    k_to_hwc4<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J + (epi ? B : 0)), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc,
-                                                                                       B * J, ref, ref_hwc);
+    const HwcJob jb{C, HW, HW + 1, B * J, tgt, tgt_hwc, ref, ref_hwc};
+    if (epi)  // the copies ride along the grouping's last launch (k_epi_rank_hwc)
+      return epi_group(B, J, H, W, D, depth_per_pixel, intr, pose, depth, groups, geom, st, &jb, B * J + B);
+    k_to_hwc4<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(jb);
     if (int e = dsplat::check_launch("k_to_hwc4")) return e;
   } else {
     k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, B * J), 256, 0, st>>>(C, HW, HW + 1, tgt, tgt_hwc);
@@ -2244,13 +2285,14 @@ int dcv_cost_volume_views_fwd(int BV, int J, int C, int H, int W, int D, int dep
   float* fhwc = static_cast<float*>(workspace);
   int* groups = reinterpret_cast<int*>(fhwc + (size_t)BV * (HW + 1) * C);
   float* geom = reinterpret_cast<float*>(groups + (size_t)BV * J * HW);
-  if (C % 4 == 0 && HW % 4 == 0 && aligned16(features) && aligned16(workspace))
-    k_to_hwc4<<<dim3((HW + 63) / 64, (C + 63) / 64, BV), 256, 0, st>>>(C, HW, HW + 1, features, fhwc, BV, nullptr,
-                                                                      nullptr);
-  else
+  if (C % 4 == 0 && HW % 4 == 0 && aligned16(features) && aligned16(workspace)) {
+    const HwcJob jb{C, HW, HW + 1, BV, features, fhwc, nullptr, nullptr};
+    if (int e = epi_group(BV, J, H, W, D, depth_per_pixel, intr, pose, depth, groups, geom, st, &jb, BV)) return e;
+  } else {
     k_to_hwc<<<dim3((HW + 63) / 64, (C + 63) / 64, BV), 256, 0, st>>>(C, HW, HW + 1, features, fhwc);
-  if (int e = dsplat::check_launch("k_to_hwc(features)")) return e;
-  if (int e = epi_group(BV, J, H, W, D, depth_per_pixel, intr, pose, depth, groups, geom, st)) return e;
+    if (int e = dsplat::check_launch("k_to_hwc(features)")) return e;
+    if (int e = epi_group(BV, J, H, W, D, depth_per_pixel, intr, pose, depth, groups, geom, st)) return e;
+  }
   return epi_fwd_launch(BV, J, C, H, W, D, depth_per_pixel, fhwc, fhwc, nn, groups, geom, depth, clamp_min_depth, cost,
                         st);
 }
