@@ -131,8 +131,11 @@ struct HwcJob {
   const float* src2;
   float* dst2;
 };
-__device__ __forceinline__ void hwc4_tile(const HwcJob& jb, int bx, int by, int bz, float (*tile)[65]) {
-  const int C = jb.C, HW = jb.HW;
+// (tid: the thread's index among the tile's 256; every thread of the workgroup reaches the one
+// barrier, valid or not)
+__device__ __forceinline__ void hwc4_tile(const HwcJob& jb, int bx, int by, int bz, float (*tile)[65], int tid,
+                                          bool valid = true) {
+  const int C = valid ? jb.C : 0, HW = jb.HW;
   const float* src = jb.src;
   float* dst = jb.dst;
   int bj = bz;
@@ -144,9 +147,9 @@ __device__ __forceinline__ void hwc4_tile(const HwcJob& jb, int bx, int by, int 
   const int p0 = bx * 64, c0 = by * 64;
   const float* s = src + (size_t)bj * C * HW;
   float* d = dst + (size_t)bj * jb.rows * C;
-  if (bx == 0 && (int)threadIdx.x < 64 && c0 + (int)threadIdx.x < C)
-    for (int p = HW; p < jb.rows; ++p) d[(size_t)p * C + c0 + threadIdx.x] = 0.f;
-  const int q = threadIdx.x & 15, rr = threadIdx.x >> 4;  // 16 float4 per 64-float run, 16 runs per pass
+  if (bx == 0 && tid < 64 && c0 + tid < C)
+    for (int p = HW; p < jb.rows; ++p) d[(size_t)p * C + c0 + tid] = 0.f;
+  const int q = tid & 15, rr = tid >> 4;  // 16 float4 per 64-float run, 16 runs per pass
   float4 v[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -173,7 +176,7 @@ __device__ __forceinline__ void hwc4_tile(const HwcJob& jb, int bx, int by, int 
 }
 __global__ __launch_bounds__(256) void k_to_hwc4(HwcJob jb) {
   __shared__ float tile[64][65];
-  hwc4_tile(jb, blockIdx.x, blockIdx.y, blockIdx.z, tile);
+  hwc4_tile(jb, blockIdx.x, blockIdx.y, blockIdx.z, tile, threadIdx.x);
 }
 __host__ __device__ inline int hwc4_blocks(const HwcJob& jb, int nz) {
   return ((jb.HW + 63) / 64) * ((jb.C + 63) / 64) * nz;
@@ -523,14 +526,32 @@ constexpr int kEpiPix = 4096;
 // near-to-far step, canonically oriented: x > 0, or y > 0 on vertical lines, so the pixels of one
 // target line, whose directions agree to a fraction of a degree, order along it); per line the
 // count and the key range.
+// HWC: the first half of the forward's channel-last copies ride along as extra workgroups (a
+// 1-D grid: pb B J counting workgroups, then 4 copy tiles of 256 threads per workgroup, tiles
+// [0, t1); the rest go with the rank pass): the copy is HBM-bound, this pass latency-bound.
+template <bool HWC>
 __global__ __launch_bounds__(1024) void k_epi_count(int H, int W, int D, int depth_per_pixel,
                                                     const float* __restrict__ depth, const float* __restrict__ geom,
-                                                    int J, EpiScratch s) {
+                                                    int J, EpiScratch s, int pb, int BJ, HwcJob jb, int t1) {
   extern __shared__ uint32_t epi_lds[];
   uint32_t* l_cnt = epi_lds;
   uint32_t* l_min = epi_lds + kEpiBuckets;
   uint32_t* l_max = epi_lds + 2 * kEpiBuckets;
-  const int bj = blockIdx.y, HW = H * W, b = bj / J, tid = threadIdx.x;
+  int bx_ = blockIdx.x, bj_ = blockIdx.y;
+  if (HWC) {
+    const int ncount = pb * BJ;
+    if ((int)blockIdx.x >= ncount) {
+      const int t = ((int)blockIdx.x - ncount) * 4 + (int)(threadIdx.x >> 8);
+      const int nx = (jb.HW + 63) / 64, ny = (jb.C + 63) / 64;
+      const int bz = t / (nx * ny), r = t - bz * nx * ny, by = r / nx, bx = r - by * nx;
+      hwc4_tile(jb, bx, by, bz, reinterpret_cast<float(*)[65]>(epi_lds) + (threadIdx.x >> 8) * 64, threadIdx.x & 255,
+                t < t1);
+      return;
+    }
+    bj_ = (int)blockIdx.x / pb;
+    bx_ = (int)blockIdx.x - bj_ * pb;
+  }
+  const int bj = bj_, HW = H * W, b = bj / J, tid = threadIdx.x;
   const EpiKey key = s.keys[bj];
   const int nb = key.nb;
   for (int l = tid; l < nb; l += 1024) {
@@ -546,13 +567,13 @@ __global__ __launch_bounds__(1024) void k_epi_count(int H, int W, int D, int dep
   float dmids[PPT], dfars[PPT];  // every pixel's two depth loads in flight together
 #pragma unroll
   for (int k = 0; k < PPT; ++k) {
-    const int p = min(blockIdx.x * kEpiPix + k * 1024 + tid, HW - 1);
+    const int p = min(bx_ * kEpiPix + k * 1024 + tid, HW - 1);
     dmids[k] = depth_per_pixel ? dp[(size_t)dm * HW + p] : dp[dm];
     dfars[k] = depth_per_pixel ? dp[(size_t)d1 * HW + p] : dp[d1];
   }
 #pragma unroll
   for (int k = 0; k < PPT; ++k) {
-    const int p = blockIdx.x * kEpiPix + k * 1024 + tid;
+    const int p = bx_ * kEpiPix + k * 1024 + tid;
     if (p >= HW) break;
     const float dmid = dmids[k], dfar = dfars[k];
     const float px = (float)(p % W), py = (float)(p / W);
@@ -736,9 +757,10 @@ __global__ __launch_bounds__(256) void k_epi_rank(int HW, EpiScratch s, int* __r
 
 // k_epi_rank with the forward's channel-last copies (hwc4_tile) as extra workgroups after its
 // own (round 6): the copy is HBM-bound and the rank pass latency-bound, so the two overlap
-// instead of running back to back. Workgroups [0, pg BJ) rank, the rest copy tiles.
+// instead of running back to back. Workgroups [0, pg BJ) rank, the rest copy tiles [t0, ...)
+// (k_epi_count<true> took the tiles before t0).
 __global__ __launch_bounds__(256) void k_epi_rank_hwc(int HW, EpiScratch s, int* __restrict__ groups, int pg, int BJ,
-                                                      HwcJob jb) {
+                                                      HwcJob jb, int t0) {
   __shared__ float tile[64][65];
   const int nrank = pg * BJ;
   if ((int)blockIdx.x < nrank) {
@@ -747,8 +769,9 @@ __global__ __launch_bounds__(256) void k_epi_rank_hwc(int HW, EpiScratch s, int*
     return;
   }
   const int t = blockIdx.x - nrank, nx = (jb.HW + 63) / 64, ny = (jb.C + 63) / 64;
-  const int bz = t / (nx * ny), r = t - bz * nx * ny, by = r / nx, bx = r - by * nx;
-  hwc4_tile(jb, bx, by, bz, tile);
+  const int tt = t + t0;
+  const int bz = tt / (nx * ny), r = tt - bz * nx * ny, by = r / nx, bx = r - by * nx;
+  hwc4_tile(jb, bx, by, bz, tile, threadIdx.x);
 }
 
 // The target image of (b, j): its own copy, or view tmap[bj] of the per-view copy (views mode;
@@ -2007,11 +2030,20 @@ static int epi_group(int B, int J, int H, int W, int D, int depth_per_pixel, con
   const int pb = (HW + kEpiPix - 1) / kEpiPix;
   const size_t lds_count = 3 * kEpiBuckets * sizeof(uint32_t), lds_bins = (size_t)nbs * sizeof(uint32_t);
   DSPLAT_REQUIRE(lds_bins <= 160 * 1024, "cost volume: %d pixels exceed the grouping's LDS bin counters", HW);
-  if (int e = dsplat::ensure_dyn_lds((const void*)k_epi_count, lds_count, "hipFuncSetAttribute(k_epi_count)")) return e;
+  if (int e = dsplat::ensure_dyn_lds((const void*)(hwc ? k_epi_count<true> : k_epi_count<false>), lds_count,
+                                     "hipFuncSetAttribute(k_epi_count)"))
+    return e;
   if (int e = dsplat::ensure_dyn_lds((const void*)k_epi_bin, lds_bins, "hipFuncSetAttribute(k_epi_bin)")) return e;
   if (int e = dsplat::ensure_dyn_lds((const void*)k_epi_scatter, lds_bins, "hipFuncSetAttribute(k_epi_scatter)"))
     return e;
-  k_epi_count<<<dim3(pb, BJ), 1024, lds_count, st>>>(H, W, D, depth_per_pixel, depth, geom, J, sc);
+  // the channel-last copy tiles: the first half with the counting pass, the rest with the rank pass
+  const int ntiles = hwc ? hwc4_blocks(*hwc, hwc_planes) : 0, t1 = ntiles / 2;
+  if (hwc)
+    k_epi_count<true><<<(unsigned)(pb * BJ + (t1 + 3) / 4), 1024, lds_count, st>>>(H, W, D, depth_per_pixel, depth,
+                                                                                    geom, J, sc, pb, BJ, *hwc, t1);
+  else
+    k_epi_count<false><<<dim3(pb, BJ), 1024, lds_count, st>>>(H, W, D, depth_per_pixel, depth, geom, J, sc, pb, BJ,
+                                                              HwcJob{}, 0);
   if (int e = dsplat::check_launch("k_epi_count")) return e;
   k_epi_segs<<<BJ, 1024, 0, st>>>(sc);
   if (int e = dsplat::check_launch("k_epi_segs")) return e;
@@ -2022,8 +2054,8 @@ static int epi_group(int B, int J, int H, int W, int D, int depth_per_pixel, con
   k_epi_scatter<<<dim3(pb, BJ), 1024, lds_bins, st>>>(HW, sc);
   if (int e = dsplat::check_launch("k_epi_scatter")) return e;
   if (hwc) {  // the channel-last copies as extra workgroups of the last grouping launch
-    const unsigned nblk = (unsigned)pg * BJ + (unsigned)hwc4_blocks(*hwc, hwc_planes);
-    k_epi_rank_hwc<<<nblk, 256, 0, st>>>(HW, sc, groups, pg, BJ, *hwc);
+    const unsigned nblk = (unsigned)pg * BJ + (unsigned)(ntiles - t1);
+    k_epi_rank_hwc<<<nblk, 256, 0, st>>>(HW, sc, groups, pg, BJ, *hwc, t1);
     return dsplat::check_launch("k_epi_rank_hwc");
   }
   k_epi_rank<<<dim3(pg, BJ), 256, 0, st>>>(HW, sc, groups);
