@@ -2001,7 +2001,9 @@ static BwdShape bwd_shape(int B, int H, int W, int D, int depth_per_pixel) {
 }
 static bool epi_path(int C, int H, int W, bool bwd) {
   (void)bwd;  // (both directions fit the widest group's layout)
-  return C % 16 == 0 && C <= 128 && epi_lds_bytes_wide(6, 8, C, H, W) <= 160 * 1024 &&
+  // the channel counts the epipolar kernels are instantiated for (C = 48, 80, ... take the
+  // direct kernels: the dispatch below has no instance for them)
+  return (C == 16 || C == 32 || C == 64 || C == 128) && epi_lds_bytes_wide(6, 8, C, H, W) <= 160 * 1024 &&
          epi_lds_bytes_wide(5, 8, C, H, W) <= 160 * 1024 &&
          (size_t)epi_bin_stride(H * W) * sizeof(uint32_t) <= 160 * 1024;  // grouping's LDS bin counters
 }

@@ -532,3 +532,35 @@ def test_cost_volume_views_rejects_bad_nn_without_gpu():
     with pytest.raises(ValueError, match="nn must be"):
         plane_sweep_cost_volume_views(feats, torch.tensor([1, 2, 0]), torch.eye(3).expand(3, 3, 3),
                                       torch.eye(4).expand(3, 1, 4, 4), torch.ones(3, 4))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,C", [(29, 47, 32), (30, 44, 48), (36, 70, 16)])
+def test_hip_cost_volume_copy_paths_vs_oracle(gpu, monkeypatch, H, W, C):
+    """The epipolar path's channel-last copies: H*W % 4 != 0 (29 x 47: the scalar copies, then
+    the grouping) and the 16-byte copies that ride along the grouping's counting and rank
+    launches (round 6; C = 48 / 16: a partial 64-channel tile), in stacked and views mode, vs
+    the oracle within 1e-4 (forward and feature gradients)."""
+    from my_depthsplat_amd.matching import plane_sweep_cost_volume, plane_sweep_cost_volume_views
+    monkeypatch.setenv("DSPLAT_CV_PATH", "epi")
+    feats, nn, K, pose, depth = _views_case(False, C=C, H=H, W=W, D=16, seed=47)
+    dcost = torch.randn(feats.shape[0], depth.shape[1], H, W, generator=torch.Generator().manual_seed(14))
+    # views mode
+    fg = feats.to(gpu).requires_grad_(True)
+    cost = plane_sweep_cost_volume_views(fg, nn, K.to(gpu), pose.to(gpu), depth.to(gpu))
+    (cost * dcost.to(gpu)).sum().backward()
+    f2 = feats.clone().requires_grad_(True)
+    want = ocv.cost_volume(f2, f2[nn], K, pose, depth)
+    (want * dcost).sum().backward()
+    rel_close(cost.detach().cpu(), want.detach(), 1e-4)
+    rel_close(fg.grad.cpu(), f2.grad, 1e-4)
+    # stacked
+    tgt = feats[nn].contiguous()
+    rg, tg_ = feats.to(gpu).requires_grad_(True), tgt.to(gpu).requires_grad_(True)
+    cost_s = plane_sweep_cost_volume(rg, tg_, K.to(gpu), pose.to(gpu), depth.to(gpu))
+    assert torch.equal(cost_s.detach(), cost.detach())
+    (cost_s * dcost.to(gpu)).sum().backward()
+    r3, t3 = feats.clone().requires_grad_(True), tgt.clone().requires_grad_(True)
+    (ocv.cost_volume(r3, t3, K, pose, depth) * dcost).sum().backward()
+    rel_close(rg.grad.cpu(), r3.grad, 1e-4)
+    rel_close(tg_.grad.cpu(), t3.grad, 1e-4)
