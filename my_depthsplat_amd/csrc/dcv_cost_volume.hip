@@ -4,9 +4,9 @@
 //   warp_with_pose_depth_candidates   src/model/encoder/unimatch/matching.py:24-90
 //   cost = mean_j(sum_c ref * warped_j) / sqrt(C)   src/model/encoder/unimatch/mv_unimatch.py:494-505
 //
-// Channel counts that are multiples of 16 run on the matrix cores: reference pixels grouped by
-// epipolar line, each group correlated with the band of target pixels its samples tap as one
-// exact-f32 GEMM (k_epi_groups + k_cost_epi / k_cost_epi_bwd below). Other channel counts: the
+// C = 16 / 32 / 64 / 128 run on the matrix cores: reference pixels grouped by epipolar line,
+// each group correlated with the band of target pixels its samples tap as one exact-f32 GEMM
+// (the k_epi_* grouping passes + k_cost_epi / k_cost_epi_bwd below). Other channel counts: the
 // target features are copied channel-last ([B,J,H,W,C]) so every bilinear tap is one
 // contiguous C-float row; a wave owns one reference pixel with its 64 lanes over channels
 // and finishes 64 depths' partial dot products with a transpose reduction (k_cost_fwd).
@@ -322,7 +322,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // target pixels it taps. All depth samples of pixel p lie on p's epipolar line in target
 // view j, and reference pixels on ONE epipolar line of the reference image map to ONE
 // epipolar line of the target image. So the reference pixels are grouped by the epipolar
-// line they lie on (k_epi_groups: a counting sort by line, per (batch, view)); 16 pixels of
+// line they lie on (the k_epi_* passes: a counting sort by line, per (batch, view)); 16 pixels of
 // a group tap a thin band around a single target line, and their correlations with the
 // band's U distinct pixels are one [16 x U x C] GEMM on the matrix cores
 // (v_mfma_f32_16x16x4_f32, exact f32), finished by the 4-tap bilinear gather from LDS. With
@@ -829,7 +829,7 @@ __device__ __forceinline__ void epi_aref(const EpiLds& L, int HW, int b, const i
 }
 
 // Per-pixel ray terms: the projection of depth d is (ax d + bx, ay d + by, az d + bz) with
-// a = M [px, py, 1], M = K R K^-1 and b = K t (from k_epi_groups' geom; matching.py:47-65
+// a = M [px, py, 1], M = K R K^-1 and b = K t (from k_epi_init's geom; matching.py:47-65
 // regrouped, each coefficient rounded once from double: within a few ulp of the reference's
 // K (R K^-1 p d + t); the parity bar is 1e-4).
 struct EpiRay {
@@ -1063,7 +1063,7 @@ __device__ __forceinline__ int epi_rank(const EpiLds& L, int e) {
   return (int)(w.y + __popc(w.x & ((1u << (e & 31)) - 1u)));
 }
 
-// Workgroups of 2^PXB reference pixels (round 5): 16 (one group of k_epi_groups' order) or
+// Workgroups of 2^PXB reference pixels (round 5): 16 (one group of the grouping's order) or
 // 32 / 64 (2 / 4 consecutive groups: neighbours along one epipolar line, whose target bands
 // overlap), their samples' bands merged into one. The band set-up (bitmap, box, word pass,
 // list), the target rows' loads and the barriers are then paid once per 2^PXB pixels; the
@@ -1343,7 +1343,7 @@ __device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, floa
 }
 
 // Backward, view j, on groups of 2^PXB reference pixels (round 5): 16 (a group of
-// k_epi_groups' order), or 32 / 64 = 2 / 4 consecutive groups (neighbours along one epipolar
+// the grouping's order), or 32 / 64 = 2 / 4 consecutive groups (neighbours along one epipolar
 // line, whose target bands overlap), depth chunks of (256 >> PXB) x SPT looped inside. Thread t
 // has pixel t & (2^PXB - 1) and depths d0 + (t >> PXB) + (256 >> PXB) s. Per chunk the gradient
 // weights G[p][u] = sum over p's samples' taps of dcost * scale * w (LDS, fixed point) over the
