@@ -13,7 +13,8 @@ if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" gpurun_out/k7test_$tag.log | 
 for r in 1 2 3; do
   for n in main $vars; do
     lib=""; [ "$n" != main ] && lib=my_depthsplat_amd/lib/variants/libdsplat_$n.so
-    DSPLAT_LIB=$lib timeout -k 10 200 python3 bench.py --skip-headline --no-cpu-baseline --extra train --extra-steps 20 \
+    ag=""; [ "$n" = bwdrec ] && ag=1  # (that variant takes the geometry records: the pre-ABI-21 backward)
+    DSPLAT_AB_GEOM=$ag DSPLAT_LIB=$lib timeout -k 10 200 python3 bench.py --skip-headline --no-cpu-baseline --extra train --extra-steps 20 \
       --detail= > gpurun_out/abk7_${tag}_${n}_$r.log 2>&1 || { echo "$n failed"; tail -3 gpurun_out/abk7_${tag}_${n}_$r.log; exit 1; }
     python3 -c "import json,sys; t=json.loads(open(sys.argv[1]).read().splitlines()[-1])['train_config_c']; print(sys.argv[2], 'C ms', t['ms_per_step'], json.dumps(t['roofline']['per_step_ms_by_kernel']))" gpurun_out/abk7_${tag}_${n}_$r.log $n
   done
