@@ -3291,6 +3291,9 @@ struct __align__(16) BwdRec {
 // lane 63 parks the sums in LDS; at the end of the chunk the wave adds them to dgeom with
 // one 64-bit fixed-point atomic per non-zero (entry, component): order-independent sums.
 constexpr int BCH = 64;
+#ifndef DSR_K7TW_WPE
+#define DSR_K7TW_WPE 3
+#endif
 // WPE = 5 (96 VGPRs, small spills) pays only on wide grids (kbench at 64 views: -3 %; 16:
 // level; 3: +12 %), so dsr_render_bwd picks it from the number of tiles.
 template <int WPE>
@@ -3464,6 +3467,238 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             a9[3] = -0.5f * R[3];
             a9[4] = -0.5f * R[4];
             a9[5] = R[5] * __uint_as_float(list[kk].pad[1]);
+#pragma unroll
+            for (int c = 6; c < 9; ++c) a9[c] = R[c];
+          }
+        }
+      } else if ((lane & 15) == 15) {
+        const int row = lane >> 4;
+        const int kk = k - ((row & 1) * 2 + (row >> 1));
+        if (kk >= 0) {
+          float* a9 = acc + kk * 9;
+#pragma unroll
+          for (int c = 0; c < 9; ++c) a9[c] = 0.f;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < cnt * 9; i += 64) {
+      const float a = acc[i];
+      const int k = i / 9;
+      if (a != 0.f)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&dgv[(size_t)list[k].id * DSR_DGEOM_WORDS + (i - k * 9)]),
+                  (unsigned long long)to_fx(a, fx_unit_inv));
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  uint32_t ids[PD];
+  float4 q[PD], r[PD];
+  float bl[PD];
+#pragma unroll
+  for (int c = 0; c < PD; ++c) ids[c] = id_at(c);
+#pragma unroll
+  for (int c = 0; c < PD; ++c) {
+    const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)ids[c] * GS);
+    q[c] = rec[0];
+    r[c] = rec[1];
+    bl[c] = rec[2].x;
+  }
+  uint32_t nid = id_at(PD);
+#pragma unroll
+  for (int c = 0; c < PD; ++c)
+    if (c < nch) chunk(c, ids[c], q[c], r[c], bl[c]);
+  for (int c = PD; c < nch; ++c) {
+    const uint32_t id = nid;
+    const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
+    const float4 cq = rec[0], cr = rec[1];
+    const float cb = rec[2].x;
+    nid = id_at(c + 1);
+    chunk(c, id, cq, cr, cb);
+  }
+}
+
+// K7, tile-wave form (round 6): ONE wave per 16x16 tile; lane l holds the pixel (l & 7, l >> 3)
+// of each of the four 8x8 sub-tiles (all four share the sub-tile offset (u, v), so the falloff
+// polynomial of an entry differs between them only in its constant terms F, D, E, staged per
+// sub-tile exactly as the sub-tile waves of k_render_bwd stage theirs: the same alpha, the same
+// skip decisions). Per entry the four pixels' gradient terms are added in the lane, then over
+// the wave (reduce36): one dgeom row per (tile, entry) instead of one per (sub-tile, entry),
+// and four independent transmittance chains per lane.
+struct __align__(16) BwdRec4 {
+  float4 q;        // x, y, A, C (scaled conic)
+  float4 r;        // B, opacity, red, green
+  float4 s;        // blue, conic a, b, c
+  float4 F, D, E;  // per sub-tile falloff constants (F includes lo = log2 o)
+  uint32_t id, pos, mask;  // mask: the sub-tiles the entry reaches (rect_hit on their live pixels)
+  float thr, rcp_o;        // power-test threshold, 1 / o
+  uint32_t pad[3];
+};
+template <int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_render_bwd_tw(
+    int G, int H, int W, int gx, int T, const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
+    const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ seg_count, uint32_t stride,
+    const uint64_t* __restrict__ keys, const uint64_t* __restrict__ spill_keys, const float* __restrict__ finalT,
+    const uint32_t* __restrict__ ncontrib, const float* __restrict__ dpix, const float* __restrict__ gscale,
+    long long* __restrict__ dgeom) {
+  __shared__ BwdRec4 list[BCH + 1];
+  __shared__ float acc[BCH * 9];
+  const int lane = threadIdx.x;
+  int tx, ty;
+  const int v = tile_xcd(gx, T / gx, tx, ty);
+  const int sxl = lane & (SUB - 1), syl = lane >> 3;
+  const float tfx0 = (float)(tx * BX), tfy0 = (float)(ty * BY);
+  const int seg = v * T + ty * gx + tx;
+  uint32_t start, end;
+  seg_bounds(seg_start, seg_count, stride, seg, start, end);
+  const bool spilled = spill_keys != nullptr && stride != 0u && stride != kSegEnds && end - start > stride;
+  const uint64_t* __restrict__ kseg = spilled ? spill_keys + (size_t)seg * G : keys + start;
+  const size_t HW = (size_t)H * W;
+  const float* gv = geom + (size_t)v * G * GS;
+  long long* dgv = dgeom + (size_t)v * G * DSR_DGEOM_WORDS;
+  int fx_k = 0;
+  const bool fx_ok = grad_fx_exp(gscale, lane, fx_k);
+  const float fx_unit_inv = fx_ok ? ldexpf(1.f, DSR_GRAD_FRAC_BITS - fx_k) : 0.f;
+  const float* bg = cams[v].bg;
+  const uint64_t lt = dsplat::lanemask_lt(lane);
+  // the lane's pixel in each sub-tile k = (k & 1, k >> 1); the same (u, v) offsets for all four
+  const PixUV puv = pix_uv(sxl, syl, 0.f, 0.f);
+  bool inside[4];
+  float Tfin[4], dp0[4], dp1[4], dp2[4], bgd[4], Tr[4], a0[4], a1[4], a2[4], l0[4], l1[4], l2[4], la[4];
+  uint32_t lastc[4];
+  uint32_t wmax = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int px = tx * BX + (k & 1) * SUB + sxl, py = ty * BY + (k >> 1) * SUB + syl;
+    inside[k] = px < W && py < H;
+    const size_t pix = (size_t)py * W + px;
+    Tfin[k] = inside[k] ? finalT[v * HW + pix] : 0.f;
+    lastc[k] = inside[k] ? ncontrib[v * HW + pix] : 0u;
+    dp0[k] = inside[k] ? dpix[(size_t)v * 3 * HW + pix] : 0.f;
+    dp1[k] = inside[k] ? dpix[(size_t)v * 3 * HW + HW + pix] : 0.f;
+    dp2[k] = inside[k] ? dpix[(size_t)v * 3 * HW + 2 * HW + pix] : 0.f;
+    bgd[k] = bg[0] * dp0[k] + bg[1] * dp1[k] + bg[2] * dp2[k];
+    Tr[k] = Tfin[k];
+    a0[k] = a1[k] = a2[k] = l0[k] = l1[k] = l2[k] = la[k] = 0.f;
+    wmax = max(wmax, lastc[k]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, off, 64));
+  const uint32_t nproc = min(end - start, wmax);
+  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+  const int nch = (int)((nproc + BCH - 1) / BCH);
+  auto id_at = [&](int c) -> uint32_t {
+    const int pos = (int)nproc - (c + 1) * BCH + lane;
+    const uint32_t kk = min((uint32_t)kseg[(uint32_t)min(max(pos, 0), max((int)nproc - 1, 0))], (uint32_t)G - 1u);
+    return (pos >= 0 && c < nch) ? kk : 0u;
+  };
+  auto chunk = [&](int ch, uint32_t id, float4 q, float4 r, float bl) {
+    const int p = (int)nproc - (ch + 1) * BCH + lane;
+    const uint32_t plo = (uint32_t)max((int)nproc - (ch + 1) * BCH, 0);
+    uint32_t mk = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float fx0 = tfx0 + (float)((k & 1) * SUB), fy0 = tfy0 + (float)((k >> 1) * SUB);
+      const uint64_t act_px = __ballot(inside[k] && lastc[k] > plo);
+      float lx0 = fx0, ly0 = fy0, lx1 = fx0 + (SUB - 1), ly1 = fy0 + (SUB - 1);
+      if (act_px) live_rect(act_px, fx0, fy0, lx0, ly0, lx1, ly1);
+      if (p >= 0 && act_px != 0ull && rect_hit(q, r, lx0, ly0, lx1, ly1)) mk |= 1u << k;
+    }
+    const uint64_t bal = __ballot(mk != 0u);
+    if (mk) {
+      BwdRec4& d = list[__popcll(bal & lt)];
+      const float4 sq = scaled_conic_q(q);
+      d.q = make_float4(sq.x, sq.y, sq.z, -0.5f * kLog2e * r.x);
+      d.r = make_float4(sq.w, r.y, r.z, r.w);
+      d.s = make_float4(bl, q.z, q.w, r.x);
+      const float lo = fall_lo(r.y);
+      float Fk[4], Dk[4], Ek[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const FallPoly f = fall_poly(sq.x, sq.y, sq.z, sq.w, d.q.w, tfx0 + (float)((k & 1) * SUB),
+                                     tfy0 + (float)((k >> 1) * SUB));
+        Fk[k] = f.F + lo;
+        Dk[k] = f.D;
+        Ek[k] = f.E;
+      }
+      d.F = make_float4(Fk[0], Fk[1], Fk[2], Fk[3]);
+      d.D = make_float4(Dk[0], Dk[1], Dk[2], Dk[3]);
+      d.E = make_float4(Ek[0], Ek[1], Ek[2], Ek[3]);
+      d.id = id;
+      d.pos = (uint32_t)p;
+      d.mask = mk;
+      d.thr = conic_pd(d.q.z, d.r.x, d.q.w) ? __builtin_inff() : kP2Max + lo;
+      d.rcp_o = r.y >= 1.17549435e-38f ? __builtin_amdgcn_rcpf(r.y) : 0.f;
+    }
+    const int cnt = __popcll(bal);
+    __builtin_amdgcn_wave_barrier();
+    for (int k = cnt - 1; k >= 0; k -= 4) {
+      float g[4][9];
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k - j;
+        const BwdRec4 cur = list[max(kk, 0)];
+#pragma unroll
+        for (int c = 0; c < 9; ++c) g[j][c] = 0.f;
+        const float c0 = cur.r.z, c1 = cur.r.w, c2 = cur.s.x;
+        const float Fs[4] = {cur.F.x, cur.F.y, cur.F.z, cur.F.w};
+        const float Ds[4] = {cur.D.x, cur.D.y, cur.D.z, cur.D.w};
+        const float Es[4] = {cur.E.x, cur.E.y, cur.E.z, cur.E.w};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const float pfx = tfx0 + (float)((s4 & 1) * SUB + sxl), pfy = tfy0 + (float)((s4 >> 1) * SUB + syl);
+          const float dx = cur.q.x - pfx, dy = cur.q.y - pfy;
+          const float p2o = fall_p2(puv, Fs[s4], Ds[s4], Es[s4], cur.q.z, cur.r.x, cur.q.w);
+          const float oG = __builtin_amdgcn_exp2f(p2o);
+          const float alpha = fminf(0.99f, oG);
+          const bool act = kk >= 0 && ((cur.mask >> s4) & 1u) && cur.pos < lastc[s4] && p2o <= cur.thr &&
+                           alpha >= 1.0f / 255.0f;
+          any = any || act;
+          if (act) {
+            const float inv1ma = __builtin_amdgcn_rcpf(1.f - alpha);
+            Tr[s4] = Tr[s4] * inv1ma;
+            const float dchannel_dcolor = alpha * Tr[s4];
+            a0[s4] = la[s4] * l0[s4] + (1.f - la[s4]) * a0[s4];
+            a1[s4] = la[s4] * l1[s4] + (1.f - la[s4]) * a1[s4];
+            a2[s4] = la[s4] * l2[s4] + (1.f - la[s4]) * a2[s4];
+            l0[s4] = c0;
+            l1[s4] = c1;
+            l2[s4] = c2;
+            float dL_dalpha = (c0 - a0[s4]) * dp0[s4];
+            dL_dalpha += (c1 - a1[s4]) * dp1[s4];
+            dL_dalpha += (c2 - a2[s4]) * dp2[s4];
+            g[j][6] += dchannel_dcolor * dp0[s4];
+            g[j][7] += dchannel_dcolor * dp1[s4];
+            g[j][8] += dchannel_dcolor * dp2[s4];
+            dL_dalpha *= Tr[s4];
+            la[s4] = alpha;
+            dL_dalpha += (-Tfin[s4] * inv1ma) * bgd[s4];
+            const float h = oG * dL_dalpha;
+            const float hx = h * dx, hy = h * dy;
+            g[j][0] += hx;
+            g[j][1] += hy;
+            g[j][2] += hx * dx;
+            g[j][3] += hx * dy;
+            g[j][4] += hy * dy;
+            g[j][5] += h;
+          }
+        }
+      }
+      if (__ballot(any) != 0ull) {
+        float R[9];
+        reduce36(g, R);
+        if ((lane & 15) == 15) {
+          const int row = lane >> 4;
+          const int kk = k - ((row & 1) * 2 + (row >> 1));
+          if (kk >= 0) {
+            const float4 cs = list[kk].s;
+            float* a9 = acc + kk * 9;
+            a9[0] = -(cs.y * R[0] + cs.z * R[1]) * ddelx_dx;
+            a9[1] = -(cs.w * R[1] + cs.z * R[0]) * ddely_dy;
+            a9[2] = -0.5f * R[2];
+            a9[3] = -0.5f * R[3];
+            a9[4] = -0.5f * R[4];
+            a9[5] = R[5] * list[kk].rcp_o;
 #pragma unroll
             for (int c = 6; c < 9; ++c) a9[c] = R[c];
           }
@@ -4514,6 +4749,17 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
   constexpr int64_t kWideBwd = 8192;  // (view, tile) segments from which WPE = 5 pays
+  // DSPLAT_K7_SUBTILE=1: the sub-tile-wave kernel (A/B timing)
+  static const bool tile_wave = [] {
+    const char* e = getenv("DSPLAT_K7_SUBTILE");
+    return !(e && e[0] && e[0] != '0');
+  }();
+  if (tile_wave) {
+    k_render_bwd_tw<DSR_K7TW_WPE><<<grid, 64, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start,
+                                                                         seg_count, seg_stride, keys, spill_keys,
+                                                                         final_T, n_contrib, dL_dpix, grad_scale, dgeom);
+    return dsplat::check_launch("k_render_bwd_tw");
+  }
   auto kern = (int64_t)V * gx * gy >= kWideBwd ? k_render_bwd<5> : k_render_bwd<1>;
   kern<<<grid, NT, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start, seg_count, seg_stride, keys,
                                              spill_keys, final_T, n_contrib, dL_dpix, grad_scale, dgeom);
