@@ -3294,6 +3294,9 @@ constexpr int BCH = 64;
 #ifndef DSR_K7TW_WPE
 #define DSR_K7TW_WPE 3
 #endif
+#ifndef DSR_K7TW_NS
+#define DSR_K7TW_NS 4
+#endif
 // WPE = 5 (96 VGPRs, small spills) pays only on wide grids (kbench at 64 views: -3 %; 16:
 // level; 3: +12 %), so dsr_render_bwd picks it from the number of tiles.
 template <int WPE>
@@ -3533,16 +3536,19 @@ struct __align__(16) BwdRec4 {
   float thr, rcp_o;        // power-test threshold, 1 / o
   uint32_t pad[3];
 };
-template <int WPE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_render_bwd_tw(
+// NS: sub-tiles per wave (4: one wave per tile; 2: two waves, the tile's top and bottom halves)
+template <int WPE, int NS>
+__global__ __launch_bounds__(64 * (4 / NS)) __attribute__((amdgpu_waves_per_eu(WPE))) void k_render_bwd_tw(
     int G, int H, int W, int gx, int T, const dsr_camera* __restrict__ cams, const float* __restrict__ geom,
     const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ seg_count, uint32_t stride,
     const uint64_t* __restrict__ keys, const uint64_t* __restrict__ spill_keys, const float* __restrict__ finalT,
     const uint32_t* __restrict__ ncontrib, const float* __restrict__ dpix, const float* __restrict__ gscale,
     long long* __restrict__ dgeom) {
-  __shared__ BwdRec4 list[BCH + 1];
-  __shared__ float acc[BCH * 9];
-  const int lane = threadIdx.x;
+  __shared__ BwdRec4 l_list[4 / NS][BCH + 1];
+  __shared__ float l_acc[4 / NS][BCH * 9];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, kb = wv * NS;  // this wave's first sub-tile
+  BwdRec4* list = l_list[wv];
+  float* acc = l_acc[wv];
   int tx, ty;
   const int v = tile_xcd(gx, T / gx, tx, ty);
   const int sxl = lane & (SUB - 1), syl = lane >> 3;
@@ -3562,22 +3568,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const uint64_t lt = dsplat::lanemask_lt(lane);
   // the lane's pixel in each sub-tile k = (k & 1, k >> 1); the same (u, v) offsets for all four
   const PixUV puv = pix_uv(sxl, syl, 0.f, 0.f);
-  bool inside[4];
-  float Tfin[4], dp0[4], dp1[4], dp2[4], bgd[4], Tr[4], a0[4], a1[4], a2[4], l0[4], l1[4], l2[4], la[4];
-  uint32_t lastc[4];
+  // per pixel (lastc = 0 off the image: no entry is active there), the background term
+  // -T_final (bg . dL/dpix) folded once
+  float dp0[NS], dp1[NS], dp2[NS], bgT[NS], Tr[NS], a0[NS], a1[NS], a2[NS], l0[NS], l1[NS], l2[NS], la[NS];
+  uint32_t lastc[NS];
   uint32_t wmax = 0u;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int px = tx * BX + (k & 1) * SUB + sxl, py = ty * BY + (k >> 1) * SUB + syl;
-    inside[k] = px < W && py < H;
+  for (int k = 0; k < NS; ++k) {
+    const int st = kb + k;
+    const int px = tx * BX + (st & 1) * SUB + sxl, py = ty * BY + (st >> 1) * SUB + syl;
+    const bool inside = px < W && py < H;
     const size_t pix = (size_t)py * W + px;
-    Tfin[k] = inside[k] ? finalT[v * HW + pix] : 0.f;
-    lastc[k] = inside[k] ? ncontrib[v * HW + pix] : 0u;
-    dp0[k] = inside[k] ? dpix[(size_t)v * 3 * HW + pix] : 0.f;
-    dp1[k] = inside[k] ? dpix[(size_t)v * 3 * HW + HW + pix] : 0.f;
-    dp2[k] = inside[k] ? dpix[(size_t)v * 3 * HW + 2 * HW + pix] : 0.f;
-    bgd[k] = bg[0] * dp0[k] + bg[1] * dp1[k] + bg[2] * dp2[k];
-    Tr[k] = Tfin[k];
+    const float tf = inside ? finalT[v * HW + pix] : 0.f;
+    lastc[k] = inside ? ncontrib[v * HW + pix] : 0u;
+    dp0[k] = inside ? dpix[(size_t)v * 3 * HW + pix] : 0.f;
+    dp1[k] = inside ? dpix[(size_t)v * 3 * HW + HW + pix] : 0.f;
+    dp2[k] = inside ? dpix[(size_t)v * 3 * HW + 2 * HW + pix] : 0.f;
+    bgT[k] = -tf * (bg[0] * dp0[k] + bg[1] * dp1[k] + bg[2] * dp2[k]);
+    Tr[k] = tf;
     a0[k] = a1[k] = a2[k] = l0[k] = l1[k] = l2[k] = la[k] = 0.f;
     wmax = max(wmax, lastc[k]);
   }
@@ -3596,9 +3604,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     const uint32_t plo = (uint32_t)max((int)nproc - (ch + 1) * BCH, 0);
     uint32_t mk = 0u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float fx0 = tfx0 + (float)((k & 1) * SUB), fy0 = tfy0 + (float)((k >> 1) * SUB);
-      const uint64_t act_px = __ballot(inside[k] && lastc[k] > plo);
+    for (int k = 0; k < NS; ++k) {
+      const float fx0 = tfx0 + (float)(((kb + k) & 1) * SUB), fy0 = tfy0 + (float)(((kb + k) >> 1) * SUB);
+      const uint64_t act_px = __ballot(lastc[k] > plo);
       float lx0 = fx0, ly0 = fy0, lx1 = fx0 + (SUB - 1), ly1 = fy0 + (SUB - 1);
       if (act_px) live_rect(act_px, fx0, fy0, lx0, ly0, lx1, ly1);
       if (p >= 0 && act_px != 0ull && rect_hit(q, r, lx0, ly0, lx1, ly1)) mk |= 1u << k;
@@ -3611,11 +3619,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       d.r = make_float4(sq.w, r.y, r.z, r.w);
       d.s = make_float4(bl, q.z, q.w, r.x);
       const float lo = fall_lo(r.y);
-      float Fk[4], Dk[4], Ek[4];
+      float Fk[4] = {0.f, 0.f, 0.f, 0.f}, Dk[4] = {0.f, 0.f, 0.f, 0.f}, Ek[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const FallPoly f = fall_poly(sq.x, sq.y, sq.z, sq.w, d.q.w, tfx0 + (float)((k & 1) * SUB),
-                                     tfy0 + (float)((k >> 1) * SUB));
+      for (int k = 0; k < NS; ++k) {
+        const FallPoly f = fall_poly(sq.x, sq.y, sq.z, sq.w, d.q.w, tfx0 + (float)(((kb + k) & 1) * SUB),
+                                     tfy0 + (float)(((kb + k) >> 1) * SUB));
         Fk[k] = f.F + lo;
         Dk[k] = f.D;
         Ek[k] = f.E;
@@ -3645,8 +3653,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const float Ds[4] = {cur.D.x, cur.D.y, cur.D.z, cur.D.w};
         const float Es[4] = {cur.E.x, cur.E.y, cur.E.z, cur.E.w};
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const float pfx = tfx0 + (float)((s4 & 1) * SUB + sxl), pfy = tfy0 + (float)((s4 >> 1) * SUB + syl);
+        for (int s4 = 0; s4 < NS; ++s4) {
+          const int st = kb + s4;
+          const float pfx = tfx0 + (float)((st & 1) * SUB + sxl), pfy = tfy0 + (float)((st >> 1) * SUB + syl);
           const float dx = cur.q.x - pfx, dy = cur.q.y - pfy;
           const float p2o = fall_p2(puv, Fs[s4], Ds[s4], Es[s4], cur.q.z, cur.r.x, cur.q.w);
           const float oG = __builtin_amdgcn_exp2f(p2o);
@@ -3672,7 +3681,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             g[j][8] += dchannel_dcolor * dp2[s4];
             dL_dalpha *= Tr[s4];
             la[s4] = alpha;
-            dL_dalpha += (-Tfin[s4] * inv1ma) * bgd[s4];
+            dL_dalpha += bgT[s4] * inv1ma;
             const float h = oG * dL_dalpha;
             const float hx = h * dx, hy = h * dy;
             g[j][0] += hx;
@@ -4755,7 +4764,7 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
     return !(e && e[0] && e[0] != '0');
   }();
   if (tile_wave) {
-    k_render_bwd_tw<DSR_K7TW_WPE><<<grid, 64, 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start,
+    k_render_bwd_tw<DSR_K7TW_WPE, DSR_K7TW_NS><<<grid, 64 * (4 / DSR_K7TW_NS), 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start,
                                                                          seg_count, seg_stride, keys, spill_keys,
                                                                          final_T, n_contrib, dL_dpix, grad_scale, dgeom);
     return dsplat::check_launch("k_render_bwd_tw");
