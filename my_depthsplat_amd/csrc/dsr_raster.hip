@@ -3297,6 +3297,10 @@ constexpr int BCH = 64;
 #ifndef DSR_K7TW_NS
 #define DSR_K7TW_NS 4
 #endif
+#ifndef DSR_K7TW_PD
+#define DSR_K7TW_PD 2
+#endif
+constexpr int kPDtw = DSR_K7TW_PD;  // chunks whose records the tile-wave K7 gathers up front
 // WPE = 5 (96 VGPRs, small spills) pays only on wide grids (kbench at 64 views: -3 %; 16:
 // level; 3: +12 %), so dsr_render_bwd picks it from the number of tiles.
 template <int WPE>
@@ -3732,23 +3736,23 @@ __global__ __launch_bounds__(64 * (4 / NS)) __attribute__((amdgpu_waves_per_eu(W
     }
     __builtin_amdgcn_wave_barrier();
   };
-  uint32_t ids[PD];
-  float4 q[PD], r[PD];
-  float bl[PD];
+  uint32_t ids[kPDtw];
+  float4 q[kPDtw], r[kPDtw];
+  float bl[kPDtw];
 #pragma unroll
-  for (int c = 0; c < PD; ++c) ids[c] = id_at(c);
+  for (int c = 0; c < kPDtw; ++c) ids[c] = id_at(c);
 #pragma unroll
-  for (int c = 0; c < PD; ++c) {
+  for (int c = 0; c < kPDtw; ++c) {
     const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)ids[c] * GS);
     q[c] = rec[0];
     r[c] = rec[1];
     bl[c] = rec[2].x;
   }
-  uint32_t nid = id_at(PD);
+  uint32_t nid = id_at(kPDtw);
 #pragma unroll
-  for (int c = 0; c < PD; ++c)
+  for (int c = 0; c < kPDtw; ++c)
     if (c < nch) chunk(c, ids[c], q[c], r[c], bl[c]);
-  for (int c = PD; c < nch; ++c) {
+  for (int c = kPDtw; c < nch; ++c) {
     const uint32_t id = nid;
     const float4* rec = reinterpret_cast<const float4*>(gv + (size_t)id * GS);
     const float4 cq = rec[0], cr = rec[1];
@@ -4758,11 +4762,10 @@ int dsr_render_bwd(int G, int V, int H, int W, const dsr_camera* cams, const flo
   const int gx = dsplat::tiles_x(W), gy = dsplat::tiles_y(H);
   dim3 grid(gx, gy, V);
   constexpr int64_t kWideBwd = 8192;  // (view, tile) segments from which WPE = 5 pays
-  // DSPLAT_K7_SUBTILE=1: the sub-tile-wave kernel (A/B timing)
-  static const bool tile_wave = [] {
-    const char* e = getenv("DSPLAT_K7_SUBTILE");
-    return !(e && e[0] && e[0] != '0');
-  }();
+  // DSPLAT_K7_SUBTILE=1: the sub-tile-wave kernel (A/B timing, and the test that checks the two
+  // forms against each other; read per call)
+  const char* e7 = getenv("DSPLAT_K7_SUBTILE");
+  const bool tile_wave = !(e7 && e7[0] && e7[0] != '0');
   if (tile_wave) {
     k_render_bwd_tw<DSR_K7TW_WPE, DSR_K7TW_NS><<<grid, 64 * (4 / DSR_K7TW_NS), 0, (hipStream_t)stream>>>(G, H, W, gx, gx * gy, cams, geom, seg_start,
                                                                          seg_count, seg_stride, keys, spill_keys,

@@ -219,6 +219,48 @@ def test_render_backward_matches_oracle(gpu):
     close(dopac[0].cpu().numpy(), acc["dopacity"], "opacity")
 
 
+@pytest.mark.parametrize("h,w,seed", [(48, 64, 4), (40, 72, 11)])
+def test_render_backward_tile_wave_and_subtile_forms(gpu, monkeypatch, h, w, seed):
+    """K7's two forms (round 6): the tile-wave kernel (default; one wave per 16x16 tile, four
+    pixels per lane, one dgeom row per (tile, entry)) and the sub-tile-wave kernel
+    (DSPLAT_K7_SUBTILE=1). Same skip decisions, different float summation groupings: the
+    per-(view, Gaussian) rows and the parameter gradients agree within 1e-4 of their scale, every gradient
+    matches the float64 oracle, and each form is bit-identical run to run. 40 x 72: partial
+    tiles at the right and bottom edges."""
+    from my_depthsplat_amd import raster
+    sc = scene_inputs(h=h, w=w, seed=seed, n_tgt=2)
+    st = settings_for(sc)
+    means, shs, opac, cov6 = flat_inputs(sc)
+    B, v = sc.target_extrinsics.shape[:2]
+    dpix = torch.randn(B * v, 3, h, w, generator=torch.Generator().manual_seed(9))
+    outs = {}
+    for form in ("tile", "sub", "tile_again"):
+        monkeypatch.setenv("DSPLAT_K7_SUBTILE", "1" if form == "sub" else "0")
+        _, state, cams = hip_forward(sc, st, gpu)
+        r = raster.backward_raw(means.to(gpu), shs.to(gpu), True, 2, opac.to(gpu), cov6.to(gpu), cams,
+                                [i // v for i in range(B * v)], state, dpix.to(gpu), False, want_dgeom=True)
+        outs[form] = [t.detach().cpu() for t in (r[0], r[1], r[2], r[3], r[5])]
+    for a, b in zip(outs["tile"], outs["tile_again"]):
+        assert torch.equal(a, b)
+    for a, b, name in zip(outs["tile"], outs["sub"], ("dmeans", "dshs", "dopac", "dcov6", "dgeom")):
+        err = float((a - b).abs().max() / (b.abs().max() + 1e-12))
+        assert err < 1e-4, (name, err)  # (dcov6: ~3e-5, the conic chain amplifies the regrouping)
+    orcs = oracle_views(sc, st)
+    acc = {k: 0 for k in ("dmean3D", "dcov6", "dsh", "dopacity")}
+    for i, o in enumerate(orcs):
+        gr = o.backward(dpix[i].numpy(), f64=True)
+        sc_i = float(st["scale"][i])
+        acc["dmean3D"] = acc["dmean3D"] + gr["dmean3D"] * sc_i
+        acc["dcov6"] = acc["dcov6"] + gr["dcov6"] * (sc_i * sc_i)
+        acc["dsh"] = acc["dsh"] + gr["dsh"]
+        acc["dopacity"] = acc["dopacity"] + gr["dopacity"]
+        o.close()
+    for hip, key in zip(outs["tile"][:4], ("dmean3D", "dsh", "dopacity", "dcov6")):
+        ref = acc[key]
+        err = np.abs(hip[0].numpy().reshape(ref.shape) - ref).max() / (np.abs(ref).max() + 1e-12)
+        assert err < 5e-4, (key, err)
+
+
 def _large_tile_scene(opacity_scale=0.05, constant_opacity=None):
     sc = scene_inputs(h=32, w=32, seed=5, n_ctx=2)
     g = sc.gaussians
