@@ -629,7 +629,12 @@ def _pmc_record(d, kernel):
     ks = d.get("kernels", {})
     if kernel in ks:
         return ks[kernel]
-    return next((v for k, v in ks.items() if k.startswith(kernel + "<")), None)
+    # (k_render_bwd's default form since round 6 is the tile-wave kernel k_render_bwd_tw<...>)
+    for pre in (kernel + "_tw<", kernel + "<"):
+        rec = next((v for k, v in ks.items() if k.startswith(pre)), None)
+        if rec is not None:
+            return rec
+    return None
 
 
 def pmc_valu(kernel, workload, avg_ms):
