@@ -1483,26 +1483,55 @@ __global__ __launch_bounds__(256, bwd_occ(PXB)) void k_cost_epi_bwd(int B, int j
           }
         }
       }
-      // dtgt[n x C] += G^T[n x EGW] . aref[EGW x C]: (band block, channel block) pairs over the waves
+      // dtgt[n x C] += G^T[n x EGW] . aref[EGW x C], added as int64 fixed point
       const int nub = np / 16;
-      for (int pr = wv; pr < nub * (C / 16); pr += 4) {
-        const int ub = pr / (C / 16), cbk = pr - ub * (C / 16);
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k0 = 0; k0 < EGW; k0 += 4) {
-          const int u = ub * 16 + (lane & 15), p = k0 + (lane >> 4);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[p * kECorrB + u] * unit_of(p),
-                                                     L.aref[p * (C + 4) + cbk * 16 + (lane & 15)], acc, 0, 0, 0);
+      auto add_dtgt = [&](const f32x4& acc, int q, int r, int cbk) {
+        if (q < HW && acc[r] != 0.f) {
+          const long long v = (long long)rintf(fminf(fmaxf(acc[r] * unit_t_inv, -4.0e18f), 4.0e18f));
+          if (v != 0ll)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&dtg[(size_t)q * C + cbk * 16 + (lane & 15)]),
+                      (unsigned long long)v);
         }
+      };
+      if constexpr (PXB == 6) {
+        // band blocks over the waves: a block's A fragments (G^T rows in float, times the
+        // pixels' units) loaded once and reused over every channel block (the same MFMA order:
+        // bit-identical; scale 1 fwd + bwd -1 %, profiles/r06at_ab_cvbwd_dtgt.txt; half the
+        // channel blocks per item was slower, and the 32-pixel instances, at 4 waves per SIMD,
+        // would spill)
+        for (int ub = wv; ub < nub; ub += 4) {
+          float af[EGW / 4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = L.list[ub * 16 + 4 * (lane >> 4) + r];
-          if (q < HW && acc[r] != 0.f) {
-            const long long v = (long long)rintf(fminf(fmaxf(acc[r] * unit_t_inv, -4.0e18f), 4.0e18f));
-            if (v != 0ll)
-              atomicAdd(reinterpret_cast<unsigned long long*>(&dtg[(size_t)q * C + cbk * 16 + (lane & 15)]),
-                        (unsigned long long)v);
+          for (int kk = 0; kk < EGW / 4; ++kk) {
+            const int p = 4 * kk + (lane >> 4);
+            af[kk] = (float)gi[p * kECorrB + ub * 16 + (lane & 15)] * unit_of(p);
           }
+          int qr[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) qr[r] = L.list[ub * 16 + 4 * (lane >> 4) + r];
+#pragma unroll 1
+          for (int cbk = 0; cbk < C / 16; ++cbk) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < EGW / 4; ++kk)
+              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                  af[kk], L.aref[(4 * kk + (lane >> 4)) * (C + 4) + cbk * 16 + (lane & 15)], acc, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) add_dtgt(acc, qr[r], r, cbk);
+          }
+        }
+      } else {  // (band block, channel block) pairs over the waves
+        for (int pr = wv; pr < nub * (C / 16); pr += 4) {
+          const int ub = pr / (C / 16), cbk = pr - ub * (C / 16);
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int k0 = 0; k0 < EGW; k0 += 4) {
+            const int u = ub * 16 + (lane & 15), p = k0 + (lane >> 4);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)gi[p * kECorrB + u] * unit_of(p),
+                                                       L.aref[p * (C + 4) + cbk * 16 + (lane & 15)], acc, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) add_dtgt(acc, L.list[ub * 16 + 4 * (lane >> 4) + r], r, cbk);
         }
       }
       __syncthreads();  // G / list reused by the next pass
