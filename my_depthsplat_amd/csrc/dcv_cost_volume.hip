@@ -1082,7 +1082,9 @@ __host__ __device__ constexpr int epi_pass(int pxb, int spt) {
   return pxb == 6 ? 64 : pxb == 5 ? 128 : spt == 2 ? 128 : 256;
 }
 // workgroups per CU the backward's LDS allows (launch bounds: the VGPR budget to match)
-__host__ __device__ constexpr int bwd_occ(int pxb) { return pxb == 4 ? 3 : pxb == 6 ? 3 : 4; }
+// (late round 6: the C = 128 32-pixel instance at 3, where it needs no scratch spills and both
+// GEMMs reuse their A fragments: scale 0 fwd + bwd -2.4 %, profiles/r06av_ab_cvbwd_scale0.txt)
+__host__ __device__ constexpr int bwd_occ(int pxb, int c) { return pxb == 4 ? 3 : pxb == 6 ? 3 : c == 128 ? 3 : 4; }
 template <int PXB, int SPT>
 constexpr int bwd_band() { return epi_pass(PXB, SPT); }
 static_assert(epi_pass(4, 8) <= kEUMax && epi_pass(6, 8) <= kEUMax, "the band list holds a pass");
@@ -1357,7 +1359,7 @@ __device__ __forceinline__ float cv_dtgt_unit(const float* __restrict__ bm, floa
 // dref_hwc [B][HW][C] is written (view 0) or added to (views after it, in launch order): each
 // pixel is in exactly one group per view. cvmax: k_cv_absmax's per-block maxima (dcost, ref).
 template <int NK, int PXB, int SPT>
-__global__ __launch_bounds__(256, bwd_occ(PXB)) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
+__global__ __launch_bounds__(256, bwd_occ(PXB, 4 * NK)) void k_cost_epi_bwd(int B, int j, int J, int H, int W, int D, int depth_per_pixel,
                                                       int accumulate, const float* __restrict__ ref_hwc,
                                                       const float* __restrict__ tgt_hwc, const int* __restrict__ tmap,
                                                       const int* __restrict__ groups, const float* __restrict__ geom,
@@ -1464,6 +1466,31 @@ __global__ __launch_bounds__(256, bwd_occ(PXB)) void k_cost_epi_bwd(int B, int j
       float urow[MB];  // the units of this lane's A rows (pixel mb 16 + (lane & 15))
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) urow[mb] = unit_of(mb * 16 + (lane & 15));
+      if constexpr (C == 128 && PXB == 5) {
+        // the wave's two channel blocks (wv, wv + 4) in one sweep: each A fragment loaded once
+        // for both (the same MFMA order per accumulator: bit-identical)
+        const float* tc0 = tg + wv * 16 + (lane & 15);
+        const float* tc1 = tc0 + 64;
+        for (int u0 = 0; u0 < np; u0 += kEPad) {
+          float b0[kEPad / 4], b1[kEPad / 4];
+#pragma unroll
+          for (int t = 0; t < kEPad / 4; ++t) {
+            const size_t o = (size_t)L.list[u0 + 4 * t + (lane >> 4)] * C;
+            b0[t] = tc0[o];
+            b1[t] = tc1[o];
+          }
+#pragma unroll
+          for (int t = 0; t < kEPad / 4; ++t) {
+            const int u = u0 + 4 * t + (lane >> 4);
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb) {
+              const float av = (float)gi[(mb * 16 + (lane & 15)) * kECorrB + u] * urow[mb];
+              dacc[0][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0[t], dacc[0][mb], 0, 0, 0);
+              dacc[1][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1[t], dacc[1][mb], 0, 0, 0);
+            }
+          }
+        }
+      } else
 #pragma unroll
       for (int q = 0; q < NCB; ++q) {
         const int cbk = wv + 4 * q;
@@ -1493,12 +1520,12 @@ __global__ __launch_bounds__(256, bwd_occ(PXB)) void k_cost_epi_bwd(int B, int j
                       (unsigned long long)v);
         }
       };
-      if constexpr (PXB == 6) {
+      if constexpr (PXB == 6 || (PXB == 5 && C == 128)) {
         // band blocks over the waves: a block's A fragments (G^T rows in float, times the
         // pixels' units) loaded once and reused over every channel block (the same MFMA order:
         // bit-identical; scale 1 fwd + bwd -1 %, profiles/r06at_ab_cvbwd_dtgt.txt; half the
-        // channel blocks per item was slower, and the 32-pixel instances, at 4 waves per SIMD,
-        // would spill)
+        // channel blocks per item was slower; the other 32-pixel instances, at 4 waves per
+        // SIMD, would spill)
         for (int ub = wv; ub < nub; ub += 4) {
           float af[EGW / 4];
 #pragma unroll
